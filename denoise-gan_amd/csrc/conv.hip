@@ -1,0 +1,957 @@
+// Convolution engine for the pix2pix training step on MI355X (gfx950).
+//
+// Replaces TF's Conv2D / Conv2DBackpropInput / Conv2DBackpropFilter, which
+// the reference dispatches for every Conv2D (pix2pix.py:115, :207, :217) and
+// Conv2DTranspose (pix2pix.py:130, :169).  All three are written as one
+// implicit GEMM on the fp32 matrix cores (v_mfma_f32_32x32x2_f32, exact fp32
+// FMA chains), over the *conv view* of a layer:
+//     x [N,H,W,Ci]  --conv(w HWIO [kh,kw,Ci,Co], stride, pad)-->  y [N,Ho,Wo,Co]
+//   FWD   : C[m=(n,ho,wo)][co]  = sum_k im2col(x)[m][k=(i,j,ci)] * w[k][co]
+//   DGRAD : per output phase (h%sh, w%sw) a dense GEMM over the Th*Tw taps
+//           that hit that phase (sub-pixel decomposition, no zero-stuffing):
+//           C[m=(n,hh,ww)][ci] = sum_{(a,b,co)} dy[n,ho,wo,co] * w[i,j,ci,co]
+//   WGRAD : C[k=(i,j,ci)][co]   = sum_{m=(n,ho,wo)} im2col(x)[m][k] * dy[m][co]
+//           split over m into fp32 partial slabs, reduced deterministically.
+// Conv2DTranspose fwd is DGRAD, its input-grad is FWD and its filter grad is
+// WGRAD with the roles of x and dy exchanged (Keras kernel [kh,kw,F,Cin] is
+// exactly the HWIO kernel of the equivalent conv).
+//
+// Tiling: 256 threads = 4 waves; block tile BM x BN x BK(32); each wave owns
+// a (BM/WGM) x (BN/WGN) sub-tile of 32x32 MFMA accumulators.  Operands are
+// staged global -> registers -> LDS (double buffered, one barrier per
+// K-tile), stored k-major ([k][m], [k][n]) so every MFMA operand fetch is a
+// conflict-free ds_read_b32 of 32 consecutive floats per half-wave.
+#include "common.h"
+#include <algorithm>
+#include <new>
+
+namespace dg {
+
+enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+
+struct ConvGeom {
+    int N, H, W, Ci;  // conv-view input
+    int Ho, Wo, Co;   // conv-view output
+    int kh, kw, sh, sw, pt, pl;
+    int Th, Tw;       // DGRAD taps per phase
+};
+
+struct GemmArgs {
+    ConvGeom g;
+    const float *A; int lda;
+    const float *B; int ldb;
+    float *C; int ldc;
+    const float *bias;
+    float beta; int act; float alpha;
+    int M, N, K;       // GEMM dims; DGRAD: M = max rows over phases
+    int kchunk;        // K per split (multiple of BK)
+    int splits;
+    int mtiles, ntiles;
+    int nphase;
+    float *slab;       // split-K partials [nphase*splits][M][N]
+};
+
+struct PhaseInfo {
+    int ph, pw, Hp, Wp, Mp, i0h, i0w;
+};
+
+__device__ __forceinline__ PhaseInfo phase_info(const ConvGeom &g, int phase, int N) {
+    PhaseInfo q;
+    q.ph = phase / g.sw;
+    q.pw = phase - q.ph * g.sw;
+    q.Hp = (g.H - q.ph + g.sh - 1) / g.sh;
+    q.Wp = (g.W - q.pw + g.sw - 1) / g.sw;
+    if (q.Hp < 0) q.Hp = 0;
+    if (q.Wp < 0) q.Wp = 0;
+    q.Mp = N * q.Hp * q.Wp;
+    q.i0h = ((q.ph + g.pt) % g.sh + g.sh) % g.sh;
+    q.i0w = ((q.pw + g.pl) % g.sw + g.sw) % g.sw;
+    return q;
+}
+
+// -------------------------------------------------------------------------
+// The MFMA implicit-GEMM kernel
+// -------------------------------------------------------------------------
+template <int MODE, int BM, int BN, int WGM, int WGN, bool VEC>
+__global__ void __launch_bounds__(256)
+k_conv_gemm(const GemmArgs p) {
+    constexpr int BK = 32;
+    constexpr bool A_KC = (MODE != MODE_WGRAD);  // A rows contiguous along k
+    constexpr bool B_KC = (MODE == MODE_DGRAD);  // B rows (n) contiguous along k
+    constexpr int LDA = A_KC ? BM + 1 : BM + 4;
+    constexpr int LDB = B_KC ? BN + 1 : BN + 4;
+    constexpr int ASZ = BK * LDA;
+    constexpr int BSZ = BK * LDB;
+    constexpr int WTM = BM / WGM, WTN = BN / WGN;
+    constexpr int TM = WTM / 32, TN = WTN / 32;
+    static_assert(WGM * WGN == 4, "4 waves");
+    static_assert(TM >= 1 && TN >= 1, "wave tile >= 32x32");
+
+    __shared__ __attribute__((aligned(16))) float smem[2 * (ASZ + BSZ)];
+
+    const ConvGeom &g = p.g;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = tid >> 6;
+    const int wm = wid / WGN, wn = wid % WGN;
+    const int l32 = lane & 31, h2 = lane >> 5;
+
+    const int zz = blockIdx.y;
+    const int phase = zz / p.splits;
+    const int split = zz - phase * p.splits;
+    const int tile = blockIdx.x;
+    const int mt = tile / p.ntiles;
+    const int nt = tile - mt * p.ntiles;
+    const int m0 = mt * BM, n0 = nt * BN;
+
+    int Mrows = p.M;
+    PhaseInfo ph{};
+    if constexpr (MODE == MODE_DGRAD) {
+        ph = phase_info(g, phase, g.N);
+        Mrows = ph.Mp;
+        if (m0 >= Mrows) return;
+    }
+    const int kbeg = split * p.kchunk;
+    const int kend = min(p.K, kbeg + p.kchunk);
+    if (kbeg >= kend) return;
+    const int nk = (kend - kbeg + BK - 1) / BK;
+
+    // ---------------- A operand -----------------
+    // KC (FWD / DGRAD): tile BM rows x BK, row r contiguous along k.
+    constexpr int A_NPV = BM / 32;          // vec rows per thread (8 threads per row)
+    constexpr int A_NES = BM * BK / 256;    // scalar elements per thread
+    // RC (WGRAD): tile BK k-rows x BM, contiguous along m.
+    constexpr int AR_TPR = BM / 4, AR_RPP = 256 / AR_TPR, AR_NP = BK / AR_RPP;
+    constexpr int AR_NES = BM * BK / 256;
+
+    // ---------------- B operand -----------------
+    constexpr int B_NPV = BN / 32;          // KC vec rows per thread (DGRAD)
+    constexpr int B_NES = BN * BK / 256;    // KC scalar elements per thread (DGRAD)
+    constexpr int BR_TPR = BN / 4, BR_RPP = 256 / BR_TPR, BR_NP = BK / BR_RPP;  // RC vec
+
+    // staging registers (sized for the largest variant used by this MODE)
+    constexpr int A_REGS = A_KC ? (VEC ? A_NPV * 4 : A_NES) : (VEC ? AR_NP * 4 : AR_NES);
+    constexpr int B_REGS = B_KC ? (VEC ? B_NPV * 4 : B_NES) : BR_NP * 4;
+    float ra[A_REGS];
+    float rb[B_REGS];
+
+    // ---- per-thread precomputation ----
+    // KC vec: thread -> (row rr + 32*ip, k-chunk c4)
+    const int kc_c4 = tid & 7, kc_rr = tid >> 3;
+    // KC scalar: thread -> (kk = tid % 32, rows r0 + 8*e)
+    const int ks_kk = tid & 31, ks_r0 = tid >> 5;
+
+    // row geometry for the A operand (FWD/DGRAD vec path), up to 4 rows
+    int arow_n[A_NPV > 0 ? A_NPV : 1], arow_h[A_NPV > 0 ? A_NPV : 1], arow_w[A_NPV > 0 ? A_NPV : 1];
+    if constexpr (A_KC && VEC) {
+#pragma unroll
+        for (int ip = 0; ip < A_NPV; ++ip) {
+            int m = m0 + kc_rr + 32 * ip;
+            if (m < Mrows) {
+                if constexpr (MODE == MODE_FWD) {
+                    int wo = m % g.Wo; int t = m / g.Wo; int ho = t % g.Ho; int n = t / g.Ho;
+                    arow_n[ip] = n; arow_h[ip] = ho * g.sh - g.pt; arow_w[ip] = wo * g.sw - g.pl;
+                } else {
+                    int ww = m % ph.Wp; int t = m / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
+                    arow_n[ip] = n; arow_h[ip] = hh * g.sh + ph.ph; arow_w[ip] = ww * g.sw + ph.pw;
+                }
+            } else {
+                arow_n[ip] = -1; arow_h[ip] = 0; arow_w[ip] = 0;
+            }
+        }
+    }
+    // WGRAD A (RC vec4): the thread's column chunk is fixed -> (i, j, ci) once
+    const int ar_c4 = tid % AR_TPR, ar_kr = tid / AR_TPR;
+    int wg_i = 0, wg_j = 0, wg_ci = 0; bool wg_colok = false;
+    if constexpr (MODE == MODE_WGRAD && VEC) {
+        int mc = m0 + 4 * ar_c4;
+        wg_colok = mc < p.M;
+        int tap = mc / g.Ci; wg_ci = mc - tap * g.Ci; wg_i = tap / g.kw; wg_j = tap - wg_i * g.kw;
+    }
+    // WGRAD A scalar: thread column c = tid % BM fixed
+    const int as_c = tid % BM, as_kr = tid / BM;
+    if constexpr (MODE == MODE_WGRAD && !VEC) {
+        int mc = m0 + as_c;
+        wg_colok = mc < p.M;
+        int tap = mc / g.Ci; wg_ci = mc - tap * g.Ci; wg_i = tap / g.kw; wg_j = tap - wg_i * g.kw;
+    }
+    const int br_c4 = tid % BR_TPR, br_kr = tid / BR_TPR;
+
+    // decode a DGRAD tap (k0 is a multiple of BK; VEC => whole tile inside one tap)
+    auto dgrad_tap = [&](int k, int &i, int &j, int &co) {
+        int tap = k / g.Co; co = k - tap * g.Co;
+        int a = tap / g.Tw; int b = tap - a * g.Tw;
+        i = ph.i0h + a * g.sh; j = ph.i0w + b * g.sw;
+    };
+
+    auto load_tiles = [&](int k0) {
+        // ----- A -----
+        if constexpr (MODE == MODE_FWD) {
+            if constexpr (VEC) {
+                int tap = k0 / g.Ci; int ci0 = k0 - tap * g.Ci;
+                int i = tap / g.kw; int j = tap - i * g.kw;
+#pragma unroll
+                for (int ip = 0; ip < A_NPV; ++ip) {
+                    int hi = arow_h[ip] + i, wi = arow_w[ip] + j;
+                    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+                    if (arow_n[ip] >= 0 && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W) {
+                        const float *ptr = p.A + ((long)(arow_n[ip] * g.H + hi) * g.W + wi) * p.lda + ci0 + 4 * kc_c4;
+                        v = *reinterpret_cast<const f32x4 *>(ptr);
+                    }
+                    ra[4 * ip + 0] = v[0]; ra[4 * ip + 1] = v[1]; ra[4 * ip + 2] = v[2]; ra[4 * ip + 3] = v[3];
+                }
+            } else {
+                int k = k0 + ks_kk;
+                int tap = k / g.Ci; int ci = k - tap * g.Ci;
+                int i = tap / g.kw; int j = tap - i * g.kw;
+                bool kok = k < kend;
+#pragma unroll
+                for (int e = 0; e < A_NES; ++e) {
+                    int m = m0 + ks_r0 + 8 * e;
+                    float v = 0.f;
+                    if (kok && m < Mrows) {
+                        int wo = m % g.Wo; int t = m / g.Wo; int ho = t % g.Ho; int n = t / g.Ho;
+                        int hi = ho * g.sh - g.pt + i, wi = wo * g.sw - g.pl + j;
+                        if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
+                            v = p.A[((long)(n * g.H + hi) * g.W + wi) * p.lda + ci];
+                    }
+                    ra[e] = v;
+                }
+            }
+        } else if constexpr (MODE == MODE_DGRAD) {
+            if constexpr (VEC) {
+                int i, j, co0; dgrad_tap(k0, i, j, co0);
+                bool tapok = (i < g.kh) && (j < g.kw);
+#pragma unroll
+                for (int ip = 0; ip < A_NPV; ++ip) {
+                    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+                    int th = arow_h[ip] + g.pt - i, tw = arow_w[ip] + g.pl - j;
+                    if (tapok && arow_n[ip] >= 0 && th >= 0 && tw >= 0) {
+                        int ho = th / g.sh, wo = tw / g.sw;
+                        if (ho < g.Ho && wo < g.Wo) {
+                            const float *ptr = p.A + ((long)(arow_n[ip] * g.Ho + ho) * g.Wo + wo) * p.lda + co0 + 4 * kc_c4;
+                            v = *reinterpret_cast<const f32x4 *>(ptr);
+                        }
+                    }
+                    ra[4 * ip + 0] = v[0]; ra[4 * ip + 1] = v[1]; ra[4 * ip + 2] = v[2]; ra[4 * ip + 3] = v[3];
+                }
+            } else {
+                int k = k0 + ks_kk;
+                int i, j, co; dgrad_tap(k, i, j, co);
+                bool kok = (k < kend) && (i < g.kh) && (j < g.kw);
+#pragma unroll
+                for (int e = 0; e < A_NES; ++e) {
+                    int m = m0 + ks_r0 + 8 * e;
+                    float v = 0.f;
+                    if (kok && m < Mrows) {
+                        int ww = m % ph.Wp; int t = m / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
+                        int th = hh * g.sh + ph.ph + g.pt - i, tw = ww * g.sw + ph.pw + g.pl - j;
+                        if (th >= 0 && tw >= 0) {
+                            int ho = th / g.sh, wo = tw / g.sw;
+                            if (ho < g.Ho && wo < g.Wo)
+                                v = p.A[((long)(n * g.Ho + ho) * g.Wo + wo) * p.lda + co];
+                        }
+                    }
+                    ra[e] = v;
+                }
+            }
+        } else {  // WGRAD: A k-rows are pixels, columns are (tap, ci)
+            if constexpr (VEC) {
+#pragma unroll
+                for (int ip = 0; ip < AR_NP; ++ip) {
+                    int pix = k0 + ar_kr + AR_RPP * ip;
+                    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+                    if (wg_colok && pix < kend) {
+                        int wo = pix % g.Wo; int t = pix / g.Wo; int ho = t % g.Ho; int n = t / g.Ho;
+                        int hi = ho * g.sh - g.pt + wg_i, wi = wo * g.sw - g.pl + wg_j;
+                        if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
+                            v = *reinterpret_cast<const f32x4 *>(p.A + ((long)(n * g.H + hi) * g.W + wi) * p.lda + wg_ci);
+                    }
+                    ra[4 * ip + 0] = v[0]; ra[4 * ip + 1] = v[1]; ra[4 * ip + 2] = v[2]; ra[4 * ip + 3] = v[3];
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < AR_NES; ++e) {
+                    int pix = k0 + as_kr + (256 / BM) * e;
+                    float v = 0.f;
+                    if (wg_colok && pix < kend) {
+                        int wo = pix % g.Wo; int t = pix / g.Wo; int ho = t % g.Ho; int n = t / g.Ho;
+                        int hi = ho * g.sh - g.pt + wg_i, wi = wo * g.sw - g.pl + wg_j;
+                        if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
+                            v = p.A[((long)(n * g.H + hi) * g.W + wi) * p.lda + wg_ci];
+                    }
+                    ra[e] = v;
+                }
+            }
+        }
+        // ----- B -----
+        if constexpr (MODE == MODE_FWD) {  // w rows k contiguous along co
+#pragma unroll
+            for (int ip = 0; ip < BR_NP; ++ip) {
+                int k = k0 + br_kr + BR_RPP * ip;
+                int col = n0 + 4 * br_c4;
+                f32x4 v = {0.f, 0.f, 0.f, 0.f};
+                if (k < kend && col < p.N) v = *reinterpret_cast<const f32x4 *>(p.B + (long)k * p.ldb + col);
+                rb[4 * ip + 0] = v[0]; rb[4 * ip + 1] = v[1]; rb[4 * ip + 2] = v[2]; rb[4 * ip + 3] = v[3];
+            }
+        } else if constexpr (MODE == MODE_DGRAD) {  // w[i,j,ci,co]: rows ci contiguous along co
+            if constexpr (VEC) {
+                int i, j, co0; dgrad_tap(k0, i, j, co0);
+                bool tapok = (i < g.kh) && (j < g.kw);
+#pragma unroll
+                for (int ip = 0; ip < B_NPV; ++ip) {
+                    int ci = n0 + kc_rr + 32 * ip;
+                    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+                    if (tapok && ci < p.N)
+                        v = *reinterpret_cast<const f32x4 *>(p.B + ((long)(i * g.kw + j) * g.Ci + ci) * g.Co + co0 + 4 * kc_c4);
+                    rb[4 * ip + 0] = v[0]; rb[4 * ip + 1] = v[1]; rb[4 * ip + 2] = v[2]; rb[4 * ip + 3] = v[3];
+                }
+            } else {
+                int k = k0 + ks_kk;
+                int i, j, co; dgrad_tap(k, i, j, co);
+                bool kok = (k < kend) && (i < g.kh) && (j < g.kw);
+#pragma unroll
+                for (int e = 0; e < B_NES; ++e) {
+                    int ci = n0 + ks_r0 + 8 * e;
+                    float v = 0.f;
+                    if (kok && ci < p.N) v = p.B[((long)(i * g.kw + j) * g.Ci + ci) * g.Co + co];
+                    rb[e] = v;
+                }
+            }
+        } else {  // WGRAD: dy rows (pixels) contiguous along co
+#pragma unroll
+            for (int ip = 0; ip < BR_NP; ++ip) {
+                int pix = k0 + br_kr + BR_RPP * ip;
+                int col = n0 + 4 * br_c4;
+                f32x4 v = {0.f, 0.f, 0.f, 0.f};
+                if (pix < kend && col < p.N) v = *reinterpret_cast<const f32x4 *>(p.B + (long)pix * p.ldb + col);
+                rb[4 * ip + 0] = v[0]; rb[4 * ip + 1] = v[1]; rb[4 * ip + 2] = v[2]; rb[4 * ip + 3] = v[3];
+            }
+        }
+    };
+
+    auto store_tiles = [&](int buf) {
+        float *As = smem + buf * (ASZ + BSZ);
+        float *Bs = As + ASZ;
+        if constexpr (A_KC) {
+            if constexpr (VEC) {
+#pragma unroll
+                for (int ip = 0; ip < A_NPV; ++ip)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) As[(4 * kc_c4 + q) * LDA + kc_rr + 32 * ip] = ra[4 * ip + q];
+            } else {
+#pragma unroll
+                for (int e = 0; e < A_NES; ++e) As[ks_kk * LDA + ks_r0 + 8 * e] = ra[e];
+            }
+        } else {
+            if constexpr (VEC) {
+#pragma unroll
+                for (int ip = 0; ip < AR_NP; ++ip) {
+                    f32x4 v = {ra[4 * ip], ra[4 * ip + 1], ra[4 * ip + 2], ra[4 * ip + 3]};
+                    *reinterpret_cast<f32x4 *>(&As[(ar_kr + AR_RPP * ip) * LDA + 4 * ar_c4]) = v;
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < AR_NES; ++e) As[(as_kr + (256 / BM) * e) * LDA + as_c] = ra[e];
+            }
+        }
+        if constexpr (B_KC) {
+            if constexpr (VEC) {
+#pragma unroll
+                for (int ip = 0; ip < B_NPV; ++ip)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) Bs[(4 * kc_c4 + q) * LDB + kc_rr + 32 * ip] = rb[4 * ip + q];
+            } else {
+#pragma unroll
+                for (int e = 0; e < B_NES; ++e) Bs[ks_kk * LDB + ks_r0 + 8 * e] = rb[e];
+            }
+        } else {
+#pragma unroll
+            for (int ip = 0; ip < BR_NP; ++ip) {
+                f32x4 v = {rb[4 * ip], rb[4 * ip + 1], rb[4 * ip + 2], rb[4 * ip + 3]};
+                *reinterpret_cast<f32x4 *>(&Bs[(br_kr + BR_RPP * ip) * LDB + 4 * br_c4]) = v;
+            }
+        }
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+    load_tiles(kbeg);
+    store_tiles(0);
+    __syncthreads();
+
+    for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        const bool more = (kt + 1) < nk;
+        if (more) load_tiles(kbeg + (kt + 1) * BK);
+        const float *As = smem + buf * (ASZ + BSZ);
+        const float *Bs = As + ASZ;
+#pragma unroll
+        for (int kk = 0; kk < BK; kk += 2) {
+            float af[TM], bf[TN];
+#pragma unroll
+            for (int a = 0; a < TM; ++a) af[a] = As[(kk + h2) * LDA + wm * WTM + a * 32 + l32];
+#pragma unroll
+            for (int b = 0; b < TN; ++b) bf[b] = Bs[(kk + h2) * LDB + wn * WTN + b * 32 + l32];
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a], bf[b], acc[a][b], 0, 0, 0);
+        }
+        if (more) store_tiles(buf ^ 1);
+        __syncthreads();
+    }
+
+    // ---------------- epilogue -----------------
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+            const int col = n0 + wn * WTN + b * 32 + l32;
+            if (col >= p.N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm * WTM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h2;
+                if (row >= Mrows) continue;
+                float v = acc[a][b][r];
+                if (p.splits > 1) {
+                    p.slab[((long)(phase * p.splits + split) * p.M + row) * p.N + col] = v;
+                } else {
+                    long off;
+                    if constexpr (MODE == MODE_DGRAD) {
+                        int ww = row % ph.Wp; int t = row / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
+                        off = ((long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw) * p.ldc;
+                    } else {
+                        off = (long)row * p.ldc;
+                    }
+                    if (p.bias) v += p.bias[col];
+                    v = act_fwd(v, p.act, p.alpha);
+                    if (p.beta != 0.f) v += p.beta * p.C[off + col];
+                    p.C[off + col] = v;
+                }
+            }
+        }
+    }
+}
+
+// split-K reduction + epilogue (deterministic: slabs summed in split order)
+template <int MODE>
+__global__ void __launch_bounds__(256)
+k_splitk_reduce(const GemmArgs p) {
+    const ConvGeom &g = p.g;
+    const int phase = blockIdx.y;
+    int Mrows = p.M;
+    PhaseInfo ph{};
+    if constexpr (MODE == MODE_DGRAD) {
+        ph = phase_info(g, phase, g.N);
+        Mrows = ph.Mp;
+    }
+    const long total = (long)Mrows * p.N;
+    const long plane = (long)p.M * p.N;
+    const float *base = p.slab + (long)phase * p.splits * plane;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        int row = (int)(e / p.N);
+        int col = (int)(e - (long)row * p.N);
+        float v = 0.f;
+        for (int s = 0; s < p.splits; ++s) v += base[s * plane + (long)row * p.N + col];
+        long off;
+        if constexpr (MODE == MODE_DGRAD) {
+            int ww = row % ph.Wp; int t = row / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
+            off = ((long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw) * p.ldc;
+        } else {
+            off = (long)row * p.ldc;
+        }
+        if (p.bias) v += p.bias[col];
+        v = act_fwd(v, p.act, p.alpha);
+        if (p.beta != 0.f) v += p.beta * p.C[off + col];
+        p.C[off + col] = v;
+    }
+}
+
+// -------------------------------------------------------------------------
+// Narrow kernels (GEMM N <= 4): D.last Conv2D(1) (pix2pix.py:217) and the
+// G.last Conv2DTranspose(3) (pix2pix.py:169).  MFMA tiles would waste >= 8x
+// here; these are VALU dot-product kernels with coalesced activation reads.
+// -------------------------------------------------------------------------
+constexpr int NARROW_MAX = 8;
+
+// FWD with Co <= 4: one wave per output pixel, lanes over (tap, ci).
+__global__ void __launch_bounds__(256)
+k_narrow_fwd(const GemmArgs p) {
+    const ConvGeom &g = p.g;
+    const int lane = threadIdx.x & 63;
+    const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (m >= p.M) return;
+    int wo = m % g.Wo; int t = m / g.Wo; int ho = t % g.Ho; int n = t / g.Ho;
+    float acc[NARROW_MAX] = {};
+    const int Co = g.Co;
+    for (int i = 0; i < g.kh; ++i) {
+        int hi = ho * g.sh - g.pt + i;
+        if (hi < 0 || hi >= g.H) continue;
+        for (int j = 0; j < g.kw; ++j) {
+            int wi = wo * g.sw - g.pl + j;
+            if (wi < 0 || wi >= g.W) continue;
+            const float *xp = p.A + ((long)(n * g.H + hi) * g.W + wi) * p.lda;
+            const float *wp = p.B + (long)(i * g.kw + j) * g.Ci * Co;
+            for (int ci = lane; ci < g.Ci; ci += 64) {
+                float xv = xp[ci];
+#pragma unroll
+                for (int co = 0; co < NARROW_MAX; ++co)
+                    if (co < Co) acc[co] += xv * wp[(long)ci * Co + co];
+            }
+        }
+    }
+#pragma unroll
+    for (int co = 0; co < NARROW_MAX; ++co) {
+        float v = acc[co];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+        acc[co] = v;
+    }
+    if (lane == 0) {
+        for (int co = 0; co < Co; ++co) {
+            float v = acc[co];
+            if (p.bias) v += p.bias[co];
+            v = act_fwd(v, p.act, p.alpha);
+            long off = (long)m * p.ldc + co;
+            if (p.beta != 0.f) v += p.beta * p.C[off];
+            p.C[off] = v;
+        }
+    }
+}
+
+// DGRAD with Ci <= 4: one thread per output pixel of one phase; w staged in LDS.
+__global__ void __launch_bounds__(256)
+k_narrow_dgrad(const GemmArgs p, int w_in_lds) {
+    extern __shared__ __attribute__((aligned(16))) float wl[];
+    const ConvGeom &g = p.g;
+    const int phase = blockIdx.y;
+    PhaseInfo ph = phase_info(g, phase, g.N);
+    const long wsz = (long)g.kh * g.kw * g.Ci * g.Co;
+    const float *wsrc = p.B;
+    if (w_in_lds) {
+        for (long e = threadIdx.x; e < wsz; e += blockDim.x) wl[e] = p.B[e];
+        __syncthreads();
+        wsrc = wl;
+    }
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= ph.Mp) return;
+    int ww = m % ph.Wp; int t = m / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
+    const int h = hh * g.sh + ph.ph, w = ww * g.sw + ph.pw;
+    const int Ci = g.Ci, Co = g.Co;
+    float acc[NARROW_MAX] = {};
+    for (int a = 0; a < g.Th; ++a) {
+        int i = ph.i0h + a * g.sh;
+        int th = h + g.pt - i;
+        if (i >= g.kh || th < 0) continue;
+        int ho = th / g.sh;
+        if (ho >= g.Ho) continue;
+        for (int b = 0; b < g.Tw; ++b) {
+            int j = ph.i0w + b * g.sw;
+            int tw = w + g.pl - j;
+            if (j >= g.kw || tw < 0) continue;
+            int wo = tw / g.sw;
+            if (wo >= g.Wo) continue;
+            const float *dyp = p.A + ((long)(n * g.Ho + ho) * g.Wo + wo) * p.lda;
+            const float *wp = wsrc + (long)(i * g.kw + j) * Ci * Co;
+            if ((Co & 3) == 0 && (p.lda & 3) == 0) {
+                for (int co = 0; co < Co; co += 4) {
+                    f32x4 d = *reinterpret_cast<const f32x4 *>(dyp + co);
+#pragma unroll
+                    for (int ci = 0; ci < NARROW_MAX; ++ci) {
+                        if (ci < Ci) {
+                            const float *wr = wp + (long)ci * Co + co;
+                            acc[ci] += d[0] * wr[0] + d[1] * wr[1] + d[2] * wr[2] + d[3] * wr[3];
+                        }
+                    }
+                }
+            } else {
+                for (int co = 0; co < Co; ++co) {
+                    float d = dyp[co];
+#pragma unroll
+                    for (int ci = 0; ci < NARROW_MAX; ++ci)
+                        if (ci < Ci) acc[ci] += d * wp[(long)ci * Co + co];
+                }
+            }
+        }
+    }
+    long off = ((long)(n * g.H + h) * g.W + w) * p.ldc;
+    for (int ci = 0; ci < Ci; ++ci) {
+        float v = acc[ci];
+        if (p.bias) v += p.bias[ci];
+        v = act_fwd(v, p.act, p.alpha);
+        if (p.beta != 0.f) v += p.beta * p.C[off + ci];
+        p.C[off + ci] = v;
+    }
+}
+
+// WGRAD with Co <= 4: partial[split][k=(tap,ci)][co]; thread per ci, loop over pixels.
+__global__ void __launch_bounds__(256)
+k_narrow_wgrad(const GemmArgs p) {
+    const ConvGeom &g = p.g;
+    const int tap = blockIdx.x / ((g.Ci + 255) / 256);
+    const int cchunk = blockIdx.x - tap * ((g.Ci + 255) / 256);
+    const int ci = cchunk * 256 + threadIdx.x;
+    const int split = blockIdx.y;
+    if (ci >= g.Ci) return;
+    const int i = tap / g.kw, j = tap - (tap / g.kw) * g.kw;
+    const int Co = g.Co;
+    const int pb = split * p.kchunk, pe = min(p.K, pb + p.kchunk);
+    float acc[NARROW_MAX] = {};
+    for (int pix = pb; pix < pe; ++pix) {
+        int wo = pix % g.Wo; int t = pix / g.Wo; int ho = t % g.Ho; int n = t / g.Ho;
+        int hi = ho * g.sh - g.pt + i, wi = wo * g.sw - g.pl + j;
+        if (hi < 0 || hi >= g.H || wi < 0 || wi >= g.W) continue;
+        float xv = p.A[((long)(n * g.H + hi) * g.W + wi) * p.lda + ci];
+        const float *dyp = p.B + (long)pix * p.ldb;
+#pragma unroll
+        for (int co = 0; co < NARROW_MAX; ++co)
+            if (co < Co) acc[co] += xv * dyp[co];
+    }
+    const int krow = tap * g.Ci + ci;
+    for (int co = 0; co < Co; ++co)
+        p.slab[((long)split * p.M + krow) * p.N + co] = acc[co];
+}
+
+// column sum for bias gradients: out[c] = sum_r dy[r*ld + c] + beta*out[c]
+__global__ void __launch_bounds__(256)
+k_colsum_partial(const float *dy, int ld, long M, int C, long rows_per_block, float *partial) {
+    __shared__ float red[256];
+    const int c = blockIdx.y;
+    long r0 = (long)blockIdx.x * rows_per_block;
+    long r1 = min(M, r0 + rows_per_block);
+    float s = 0.f;
+    for (long r = r0 + threadIdx.x; r < r1; r += blockDim.x) s += dy[r * ld + c];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[(long)c * gridDim.x + blockIdx.x] = red[0];
+}
+__global__ void k_colsum_final(const float *partial, int nblk, int C, float *out, float beta) {
+    int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    float s = 0.f;
+    for (int b = 0; b < nblk; ++b) s += partial[(long)c * nblk + b];
+    out[c] = s + (beta != 0.f ? beta * out[c] : 0.f);
+}
+
+// -------------------------------------------------------------------------
+// Host side: descriptor, planner, launch
+// -------------------------------------------------------------------------
+struct TileCfg {
+    int bm, bn, wgm, wgn;
+};
+static const TileCfg kCfgs[] = {
+    {128, 128, 2, 2}, {128, 64, 2, 2}, {64, 128, 2, 2}, {64, 64, 2, 2}, {32, 128, 1, 4},
+};
+constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
+
+struct OpPlan {
+    int narrow;      // 1 => VALU narrow kernel
+    int cfg;         // tile config index
+    int vec;
+    int splits, kchunk;
+    int M, N, K, nphase;
+    int mtiles, ntiles;
+    size_t slab_bytes;  // split-K partial slabs
+    size_t ws_bytes;    // total workspace of the layer op (slabs + bias partials)
+};
+
+}  // namespace dg
+
+struct dg_conv_desc_s {
+    int transpose;
+    int N, H, W, Cin, Cout, Ho, Wo;  // layer view
+    dg::ConvGeom g;                  // conv view
+    dg::OpPlan plan[3];              // indexed by DG_OP_*
+};
+
+namespace dg {
+
+static int engine_mode(const dg_conv_desc_s *d, int op) {
+    // layer op -> conv-view engine
+    if (!d->transpose) return op == DG_OP_FWD ? MODE_FWD : (op == DG_OP_BWD_DATA ? MODE_DGRAD : MODE_WGRAD);
+    return op == DG_OP_FWD ? MODE_DGRAD : (op == DG_OP_BWD_DATA ? MODE_FWD : MODE_WGRAD);
+}
+
+static OpPlan make_plan(const ConvGeom &g, int mode) {
+    OpPlan pl{};
+    const int BK = 32;
+    if (mode == MODE_FWD) {
+        pl.M = g.N * g.Ho * g.Wo; pl.N = g.Co; pl.K = g.kh * g.kw * g.Ci; pl.nphase = 1;
+        pl.vec = (g.Ci % BK == 0);
+        pl.narrow = g.Co < 8;
+    } else if (mode == MODE_DGRAD) {
+        pl.nphase = g.sh * g.sw;
+        int Hp = (g.H + g.sh - 1) / g.sh, Wp = (g.W + g.sw - 1) / g.sw;
+        pl.M = g.N * Hp * Wp; pl.N = g.Ci; pl.K = g.Th * g.Tw * g.Co;
+        pl.vec = (g.Co % BK == 0);
+        pl.narrow = g.Ci < 8;
+    } else {
+        pl.M = g.kh * g.kw * g.Ci; pl.N = g.Co; pl.K = g.N * g.Ho * g.Wo; pl.nphase = 1;
+        pl.vec = (g.Ci % 4 == 0);
+        pl.narrow = g.Co < 8;
+    }
+    if (pl.narrow) {
+        pl.splits = 1; pl.kchunk = pl.K; pl.ws_bytes = 0; pl.slab_bytes = 0;
+        if (mode == MODE_WGRAD) {
+            // pixels split so that taps*ci_chunks*splits ~ 1024 blocks
+            long blocks = (long)g.kh * g.kw * ((g.Ci + 255) / 256);
+            int s = (int)std::max<long>(1, std::min<long>(1024 / std::max<long>(blocks, 1), pl.K / 64));
+            pl.splits = std::max(1, s);
+            pl.kchunk = (pl.K + pl.splits - 1) / pl.splits;
+            pl.slab_bytes = (size_t)pl.splits * pl.M * pl.N * sizeof(float);
+            pl.ws_bytes = pl.slab_bytes;
+        }
+        return pl;
+    }
+    // choose the tile: model each candidate's time as
+    //   rounds of 512 resident blocks x per-block MFMA time  +  slab traffic
+    const long target = 512;
+    const double slot_flops = 157.3e12 * 0.6 / 512.0;  // per resident block
+    int best = -1; double best_t = 1e30; long best_splits = 1;
+    for (int c = 0; c < kNumCfgs; ++c) {
+        const TileCfg &t = kCfgs[c];
+        if (pl.N <= 64 && t.bn > 64) continue;
+        long mt = (pl.M + t.bm - 1) / t.bm, nt = (pl.N + t.bn - 1) / t.bn;
+        long tiles = mt * nt * pl.nphase;
+        long ktiles = (pl.K + BK - 1) / BK;
+        long splits = 1;
+        if (tiles < target) splits = std::min<long>((target + tiles - 1) / tiles, std::max<long>(1, ktiles / 4));
+        long kt_per = (ktiles + splits - 1) / splits;
+        long blocks = tiles * splits;
+        double eff = (t.bm == 128 && t.bn == 128) ? 1.0 : (t.bm * t.bn >= 8192 ? 1.15 : 1.45);
+        double rounds = std::ceil((double)blocks / (double)target);
+        double tc = rounds * 2.0 * t.bm * t.bn * kt_per * BK * eff / slot_flops;
+        double ts = splits > 1 ? (double)splits * pl.nphase * pl.M * pl.N * 8.0 / 4.0e12 : 0.0;
+        if (tc + ts < best_t) { best_t = tc + ts; best = c; best_splits = splits; }
+    }
+    pl.cfg = best;
+    pl.splits = (int)best_splits;
+    const TileCfg &t = kCfgs[best];
+    long ktiles = (pl.K + BK - 1) / BK;
+    long kt_per = (ktiles + pl.splits - 1) / pl.splits;
+    pl.kchunk = (int)(kt_per * BK);
+    pl.splits = (int)((ktiles + kt_per - 1) / kt_per);
+    pl.mtiles = (pl.M + t.bm - 1) / t.bm;
+    pl.ntiles = (pl.N + t.bn - 1) / t.bn;
+    pl.slab_bytes = pl.splits > 1 ? (size_t)pl.nphase * pl.splits * pl.M * pl.N * sizeof(float) : 0;
+    pl.ws_bytes = pl.slab_bytes;
+    return pl;
+}
+
+template <int MODE>
+static void launch_gemm(int cfg, int vec, dim3 grid, const GemmArgs &a, hipStream_t s) {
+#define DG_L(C, BM_, BN_, WM_, WN_)                                                           \
+    case C:                                                                                   \
+        if (vec) hipLaunchKernelGGL((k_conv_gemm<MODE, BM_, BN_, WM_, WN_, true>), grid, dim3(256), 0, s, a); \
+        else hipLaunchKernelGGL((k_conv_gemm<MODE, BM_, BN_, WM_, WN_, false>), grid, dim3(256), 0, s, a); \
+        break;
+    switch (cfg) {
+        DG_L(0, 128, 128, 2, 2)
+        DG_L(1, 128, 64, 2, 2)
+        DG_L(2, 64, 128, 2, 2)
+        DG_L(3, 64, 64, 2, 2)
+        DG_L(4, 32, 128, 1, 4)
+    }
+#undef DG_L
+}
+
+static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, const float *B, int ldb,
+                      float *C, int ldc, const float *bias, float beta, int act, float alpha,
+                      void *ws, size_t ws_bytes, hipStream_t s) {
+    const int mode = engine_mode(d, op);
+    const OpPlan &pl = d->plan[op];
+    DG_ARG(ws_bytes >= pl.slab_bytes, "workspace too small: need %zu bytes, got %zu", pl.slab_bytes, ws_bytes);
+    DG_ARG(pl.slab_bytes == 0 || ws != nullptr, "workspace pointer is NULL");
+    GemmArgs a{};
+    a.g = d->g; a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.C = C; a.ldc = ldc;
+    a.bias = bias; a.beta = beta; a.act = act; a.alpha = alpha;
+    a.M = pl.M; a.N = pl.N; a.K = pl.K; a.kchunk = pl.kchunk; a.splits = pl.splits;
+    a.mtiles = pl.mtiles; a.ntiles = pl.ntiles; a.nphase = pl.nphase;
+    a.slab = (float *)ws;
+    if (pl.M == 0 || pl.N == 0) return DG_OK;
+
+    if (pl.narrow) {
+        if (mode == MODE_FWD) {
+            hipLaunchKernelGGL(k_narrow_fwd, dim3(dg_cdiv(pl.M, 4)), dim3(256), 0, s, a);
+            DG_LAUNCHED("narrow_fwd");
+        } else if (mode == MODE_DGRAD) {
+            size_t wbytes = (size_t)d->g.kh * d->g.kw * d->g.Ci * d->g.Co * sizeof(float);
+            int in_lds = wbytes <= 64 * 1024;
+            hipLaunchKernelGGL(k_narrow_dgrad, dim3(dg_cdiv(pl.M, 256), pl.nphase), dim3(256), in_lds ? wbytes : 0, s, a, in_lds);
+            DG_LAUNCHED("narrow_dgrad");
+        } else {
+            a.splits = pl.splits; a.kchunk = pl.kchunk;
+            hipLaunchKernelGGL(k_narrow_wgrad, dim3(d->g.kh * d->g.kw * ((d->g.Ci + 255) / 256), pl.splits), dim3(256), 0, s, a);
+            DG_LAUNCHED("narrow_wgrad");
+            long total = (long)pl.M * pl.N;
+            hipLaunchKernelGGL(k_splitk_reduce<MODE_WGRAD>, dim3((unsigned)std::min<long>(dg_cdiv(total, 256), 2048), 1), dim3(256), 0, s, a);
+            DG_LAUNCHED("narrow_wgrad_reduce");
+        }
+        return DG_OK;
+    }
+    if (mode == MODE_FWD || mode == MODE_WGRAD) {
+        DG_ARG(pl.N % 4 == 0 && ldb % 4 == 0, "GEMM N (%d) and ldb (%d) must be multiples of 4", pl.N, ldb);
+    }
+    if (pl.vec) {
+        DG_ARG(lda % 4 == 0 && ((uintptr_t)A & 15) == 0, "vector path needs lda%%4==0 and 16B-aligned A");
+    }
+    DG_ARG(((uintptr_t)B & 15) == 0 || mode == MODE_DGRAD, "B must be 16B aligned");
+    dim3 grid(pl.mtiles * pl.ntiles, pl.nphase * pl.splits);
+    switch (mode) {
+    case MODE_FWD: launch_gemm<MODE_FWD>(pl.cfg, pl.vec, grid, a, s); break;
+    case MODE_DGRAD: launch_gemm<MODE_DGRAD>(pl.cfg, pl.vec, grid, a, s); break;
+    default: launch_gemm<MODE_WGRAD>(pl.cfg, pl.vec, grid, a, s); break;
+    }
+    DG_LAUNCHED("conv_gemm");
+    if (pl.splits > 1) {
+        long total = (long)pl.M * pl.N;
+        dim3 rg((unsigned)std::min<long>(dg_cdiv(total, 256), 4096), pl.nphase);
+        switch (mode) {
+        case MODE_FWD: hipLaunchKernelGGL(k_splitk_reduce<MODE_FWD>, rg, dim3(256), 0, s, a); break;
+        case MODE_DGRAD: hipLaunchKernelGGL(k_splitk_reduce<MODE_DGRAD>, rg, dim3(256), 0, s, a); break;
+        default: hipLaunchKernelGGL(k_splitk_reduce<MODE_WGRAD>, rg, dim3(256), 0, s, a); break;
+        }
+        DG_LAUNCHED("splitk_reduce");
+    }
+    return DG_OK;
+}
+
+static size_t colsum_ws(long M, int C) {
+    (void)M;
+    return (size_t)C * 256 * sizeof(float);
+}
+
+static int run_colsum(const float *dy, int ld, long M, int C, float *out, float beta, float *ws, hipStream_t s) {
+    int nblk = (int)std::min<long>(256, std::max<long>(1, dg_cdiv(M, 4096)));
+    long rpb = (M + nblk - 1) / nblk;
+    hipLaunchKernelGGL(k_colsum_partial, dim3(nblk, C), dim3(256), 0, s, dy, ld, M, C, rpb, ws);
+    DG_LAUNCHED("colsum_partial");
+    hipLaunchKernelGGL(k_colsum_final, dim3(dg_cdiv(C, 256)), dim3(256), 0, s, ws, nblk, C, out, beta);
+    DG_LAUNCHED("colsum_final");
+    return DG_OK;
+}
+
+}  // namespace dg
+
+// -------------------------------------------------------------------------
+// C ABI
+// -------------------------------------------------------------------------
+extern "C" {
+
+int dg_conv_desc_create(dg_conv_t *out, int N, int H, int W, int Cin, int Cout, int kh, int kw, int sh, int sw,
+                        int pad_t, int pad_b, int pad_l, int pad_r, int transpose) {
+    DG_ARG(out != nullptr, "out is NULL");
+    DG_ARG(N > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0, "bad shape N=%d H=%d W=%d Cin=%d Cout=%d", N, H, W, Cin, Cout);
+    DG_ARG(kh > 0 && kw > 0 && sh > 0 && sw > 0, "bad kernel/stride");
+    DG_ARG(pad_t >= 0 && pad_b >= 0 && pad_l >= 0 && pad_r >= 0, "negative padding");
+    dg_conv_desc_s *d = new (std::nothrow) dg_conv_desc_s();
+    if (!d) { dg::set_error("out of host memory"); return DG_ERR_ARG; }
+    d->transpose = transpose ? 1 : 0;
+    d->N = N; d->H = H; d->W = W; d->Cin = Cin; d->Cout = Cout;
+    dg::ConvGeom &g = d->g;
+    g.kh = kh; g.kw = kw; g.sh = sh; g.sw = sw; g.pt = pad_t; g.pl = pad_l;
+    g.N = N;
+    if (!transpose) {
+        d->Ho = (H + pad_t + pad_b - kh) / sh + 1;
+        d->Wo = (W + pad_l + pad_r - kw) / sw + 1;
+        g.H = H; g.W = W; g.Ci = Cin; g.Ho = d->Ho; g.Wo = d->Wo; g.Co = Cout;
+    } else {
+        d->Ho = (H - 1) * sh + kh - pad_t - pad_b;
+        d->Wo = (W - 1) * sw + kw - pad_l - pad_r;
+        g.H = d->Ho; g.W = d->Wo; g.Ci = Cout; g.Ho = H; g.Wo = W; g.Co = Cin;
+        if ((g.H + pad_t + pad_b - kh) / sh + 1 != H || (g.W + pad_l + pad_r - kw) / sw + 1 != W) {
+            delete d;
+            dg::set_error("transposed conv: inconsistent output size");
+            return DG_ERR_ARG;
+        }
+    }
+    if (d->Ho <= 0 || d->Wo <= 0) {
+        delete d;
+        dg::set_error("empty output (Ho=%d Wo=%d)", d->Ho, d->Wo);
+        return DG_ERR_ARG;
+    }
+    g.Th = (kh + sh - 1) / sh;
+    g.Tw = (kw + sw - 1) / sw;
+    for (int op = 0; op < 3; ++op) {
+        d->plan[op] = dg::make_plan(g, dg::engine_mode(d, op));
+        if (op == DG_OP_BWD_FILTER) {
+            // room for the bias column sum partials after the split-K slabs
+            size_t extra = dg::colsum_ws(1, Cout);
+            d->plan[op].ws_bytes = ((d->plan[op].slab_bytes + 255) & ~(size_t)255) + extra;
+        }
+    }
+    *out = d;
+    return DG_OK;
+}
+
+int dg_conv_desc_destroy(dg_conv_t d) {
+    delete d;
+    return DG_OK;
+}
+
+int dg_conv_out_shape(dg_conv_t d, int *Ho, int *Wo) {
+    DG_ARG(d && Ho && Wo, "NULL argument");
+    *Ho = d->Ho; *Wo = d->Wo;
+    return DG_OK;
+}
+
+int dg_conv_workspace_size(dg_conv_t d, int op, size_t *bytes) {
+    DG_ARG(d && bytes, "NULL argument");
+    DG_ARG(op >= 0 && op < 3, "bad op %d", op);
+    *bytes = d->plan[op].ws_bytes;
+    return DG_OK;
+}
+
+int dg_conv_fwd(dg_conv_t d, const float *x, int ldx, const float *w, const float *bias, float *y, int ldy,
+                float beta, int act, float alpha, void *ws, size_t ws_bytes, dg_stream_t stream) {
+    DG_ARG(d && x && w && y, "NULL tensor");
+    DG_ARG(ldx >= d->Cin && ldy >= d->Cout, "pixel stride smaller than channels");
+    return dg::run_engine(d, DG_OP_FWD, x, ldx, w, d->transpose ? 0 : d->Cout, y, ldy, bias, beta, act, alpha, ws,
+                          ws_bytes, (hipStream_t)stream);
+}
+
+int dg_conv_bwd_data(dg_conv_t d, const float *dy, int lddy, const float *w, float *dx, int lddx, float beta,
+                     void *ws, size_t ws_bytes, dg_stream_t stream) {
+    DG_ARG(d && dy && w && dx, "NULL tensor");
+    DG_ARG(lddy >= d->Cout && lddx >= d->Cin, "pixel stride smaller than channels");
+    return dg::run_engine(d, DG_OP_BWD_DATA, dy, lddy, w, d->transpose ? d->g.Co : 0, dx, lddx, nullptr, beta,
+                          DG_ACT_NONE, 0.f, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int dg_conv_bwd_filter(dg_conv_t d, const float *x, int ldx, const float *dy, int lddy, float *dw, float *dbias,
+                       float beta, void *ws, size_t ws_bytes, dg_stream_t stream) {
+    DG_ARG(d && x && dy && dw, "NULL tensor");
+    DG_ARG(ldx >= d->Cin && lddy >= d->Cout, "pixel stride smaller than channels");
+    const dg::OpPlan &pl = d->plan[DG_OP_BWD_FILTER];
+    DG_ARG(ws_bytes >= pl.ws_bytes && ws != nullptr, "workspace too small: need %zu bytes", pl.ws_bytes);
+    size_t slab_bytes = pl.slab_bytes;
+    int rc;
+    // conv view: A = conv input, B = conv output grad
+    if (!d->transpose)
+        rc = dg::run_engine(d, DG_OP_BWD_FILTER, x, ldx, dy, lddy, dw, d->g.Co, nullptr, beta, DG_ACT_NONE, 0.f, ws,
+                            slab_bytes, (hipStream_t)stream);
+    else
+        rc = dg::run_engine(d, DG_OP_BWD_FILTER, dy, lddy, x, ldx, dw, d->g.Co, nullptr, beta, DG_ACT_NONE, 0.f, ws,
+                            slab_bytes, (hipStream_t)stream);
+    if (rc != DG_OK) return rc;
+    if (dbias) {
+        long M = (long)d->N * d->Ho * d->Wo;
+        float *cws = (float *)((char *)ws + ((slab_bytes + 255) & ~(size_t)255));
+        return dg::run_colsum(dy, lddy, M, d->Cout, dbias, beta, cws, (hipStream_t)stream);
+    }
+    return DG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,140 @@
+// Error reporting, version, and the small data-movement / optimizer kernels.
+#include "common.h"
+#include <cstdarg>
+#include <cstdio>
+#include <algorithm>
+
+namespace dg {
+
+static thread_local char g_err[512] = "no error";
+
+void set_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+// Keras Adam as TF's ApplyAdam kernel computes it (train_pix2pix.py:68-69 ->
+// ResourceApplyAdam): alpha = lr*sqrt(1-b2^t)/(1-b1^t); m += (g-m)(1-b1);
+// v += (g^2-v)(1-b2); p -= m*alpha/(sqrt(v)+eps) -- epsilon is added to
+// sqrt(v), not to the bias-corrected v-hat.  One flat arena, float4 bulk.
+__global__ void __launch_bounds__(256)
+k_adam(float *__restrict__ p, const float *__restrict__ g, float *__restrict__ m, float *__restrict__ v, long n,
+       float lr, float b1, float b2, float eps, float gscale, const int32_t *iter) {
+    const float t = (float)((iter ? *iter : 0) + 1);
+    const float lr_t = lr * sqrtf(1.f - powf(b2, t)) / (1.f - powf(b1, t));
+    const long n4 = n >> 2;
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        f32x4 gg = reinterpret_cast<const f32x4 *>(g)[i] * gscale;
+        f32x4 mm = reinterpret_cast<f32x4 *>(m)[i];
+        f32x4 vv = reinterpret_cast<f32x4 *>(v)[i];
+        f32x4 pp = reinterpret_cast<f32x4 *>(p)[i];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            mm[q] += (gg[q] - mm[q]) * (1.f - b1);
+            vv[q] += (gg[q] * gg[q] - vv[q]) * (1.f - b2);
+            pp[q] -= (mm[q] * lr_t) / (sqrtf(vv[q]) + eps);
+        }
+        reinterpret_cast<f32x4 *>(m)[i] = mm;
+        reinterpret_cast<f32x4 *>(v)[i] = vv;
+        reinterpret_cast<f32x4 *>(p)[i] = pp;
+    }
+    for (long i = 4 * n4 + (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        float gg = g[i] * gscale;
+        float mm = m[i] + (gg - m[i]) * (1.f - b1);
+        float vv = v[i] + (gg * gg - v[i]) * (1.f - b2);
+        m[i] = mm; v[i] = vv;
+        p[i] -= (mm * lr_t) / (sqrtf(vv) + eps);
+    }
+}
+
+__global__ void k_counter_add(int32_t *c, int32_t inc) { *c += inc; }
+
+__global__ void __launch_bounds__(256)
+k_channel_concat(long npix, const float *a, int lda, int ca, const float *b, int ldb, int cb, float *out, int ldo) {
+    const int C = ca + cb;
+    const long total = npix * C;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        long pix = e / C;
+        int c = (int)(e - pix * C);
+        out[pix * ldo + c] = c < ca ? a[pix * lda + c] : b[pix * ldb + (c - ca)];
+    }
+}
+
+__global__ void __launch_bounds__(256)
+k_strided_copy(long npix, int C, const float *src, int lds, float *dst, int ldd) {
+    const long total = npix * C;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        long pix = e / C;
+        int c = (int)(e - pix * C);
+        dst[pix * ldd + c] = src[pix * lds + c];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_fill(float *p, long n, float v) {
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) p[e] = v;
+}
+
+static unsigned grid_for(long n) { return (unsigned)std::max<long>(1, std::min<long>(dg_cdiv(n, 256), 8192)); }
+
+}  // namespace dg
+
+extern "C" {
+
+const char *dg_last_error_string(void) { return dg::g_err; }
+int dg_version(void) { return 1; }
+
+int dg_adam(float *p, const float *g, float *m, float *v, int64_t n, float lr, float beta1, float beta2, float eps,
+            float grad_scale, const int32_t *iter_dev, dg_stream_t stream) {
+    DG_ARG(p && g && m && v, "NULL tensor");
+    DG_ARG(n >= 0, "negative size");
+    DG_ARG((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0, "adam buffers must be 16B aligned");
+    if (n == 0) return DG_OK;
+    unsigned grid = (unsigned)std::max<long>(1, std::min<long>(dg_cdiv(n / 4 + 1, 256), 4096));
+    hipLaunchKernelGGL(dg::k_adam, dim3(grid), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (long)n, lr, beta1,
+                       beta2, eps, grad_scale, iter_dev);
+    DG_LAUNCHED("adam");
+    return DG_OK;
+}
+
+int dg_counter_add(int32_t *counter_dev, int32_t inc, dg_stream_t stream) {
+    DG_ARG(counter_dev, "NULL counter");
+    hipLaunchKernelGGL(dg::k_counter_add, dim3(1), dim3(1), 0, (hipStream_t)stream, counter_dev, inc);
+    DG_LAUNCHED("counter_add");
+    return DG_OK;
+}
+
+int dg_channel_concat(int64_t npix, const float *a, int lda, int ca, const float *b, int ldb, int cb, float *out,
+                      int ldo, dg_stream_t stream) {
+    DG_ARG(a && b && out, "NULL tensor");
+    DG_ARG(lda >= ca && ldb >= cb && ldo >= ca + cb, "bad strides");
+    long total = (long)npix * (ca + cb);
+    if (total == 0) return DG_OK;
+    hipLaunchKernelGGL(dg::k_channel_concat, dim3(dg::grid_for(total)), dim3(256), 0, (hipStream_t)stream, (long)npix,
+                       a, lda, ca, b, ldb, cb, out, ldo);
+    DG_LAUNCHED("channel_concat");
+    return DG_OK;
+}
+
+int dg_strided_copy(int64_t npix, int C, const float *src, int lds, float *dst, int ldd, dg_stream_t stream) {
+    DG_ARG(src && dst, "NULL tensor");
+    DG_ARG(lds >= C && ldd >= C, "bad strides");
+    long total = (long)npix * C;
+    if (total == 0) return DG_OK;
+    hipLaunchKernelGGL(dg::k_strided_copy, dim3(dg::grid_for(total)), dim3(256), 0, (hipStream_t)stream, (long)npix, C,
+                       src, lds, dst, ldd);
+    DG_LAUNCHED("strided_copy");
+    return DG_OK;
+}
+
+int dg_fill(float *p, int64_t n, float value, dg_stream_t stream) {
+    DG_ARG(p || n == 0, "NULL tensor");
+    if (n == 0) return DG_OK;
+    hipLaunchKernelGGL(dg::k_fill, dim3(dg::grid_for(n)), dim3(256), 0, (hipStream_t)stream, p, (long)n, value);
+    DG_LAUNCHED("fill");
+    return DG_OK;
+}
+
+}  // extern "C"

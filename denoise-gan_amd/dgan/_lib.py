@@ -1,0 +1,77 @@
+"""ctypes binding of libdgan.so (the C ABI declared in include/dgan.h).
+
+The product path is this library: every op in dgan.ops goes through it and
+there is no CPU fallback.  Loading fails loudly when the library is missing.
+"""
+import ctypes
+import os
+
+from .build import LIB_PATH
+
+_lib = None
+
+c_int = ctypes.c_int
+c_float = ctypes.c_float
+c_size_t = ctypes.c_size_t
+c_int64 = ctypes.c_int64
+c_uint32 = ctypes.c_uint32
+c_void_p = ctypes.c_void_p
+c_char_p = ctypes.c_char_p
+
+_P = c_void_p  # device pointer
+_SIGS = {
+    "dg_last_error_string": (c_char_p, []),
+    "dg_version": (c_int, []),
+    "dg_conv_desc_create": (c_int, [ctypes.POINTER(c_void_p)] + [c_int] * 14),
+    "dg_conv_desc_destroy": (c_int, [c_void_p]),
+    "dg_conv_out_shape": (c_int, [c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    "dg_conv_workspace_size": (c_int, [c_void_p, c_int, ctypes.POINTER(c_size_t)]),
+    "dg_conv_fwd": (c_int, [c_void_p, _P, c_int, _P, _P, _P, c_int, c_float, c_int, c_float, _P, c_size_t, _P]),
+    "dg_conv_bwd_data": (c_int, [c_void_p, _P, c_int, _P, _P, c_int, c_float, _P, c_size_t, _P]),
+    "dg_conv_bwd_filter": (c_int, [c_void_p, _P, c_int, _P, c_int, _P, _P, c_float, _P, c_size_t, _P]),
+    "dg_bn_workspace_size": (c_int, [c_int, c_int, ctypes.POINTER(c_size_t)]),
+    "dg_bn_fwd_train": (c_int, [c_int, c_int, _P, c_int, _P, _P, _P, _P, _P, _P, c_float, c_float, _P, c_int, c_int,
+                                c_float, c_float, c_uint32, _P, _P, c_size_t, _P]),
+    "dg_bn_fwd_infer": (c_int, [c_int, c_int, _P, c_int, _P, _P, _P, _P, c_float, _P, c_int, c_int, c_float, _P]),
+    "dg_bn_bwd": (c_int, [c_int, c_int, _P, c_int, _P, c_int, _P, c_int, _P, _P, _P, c_int, c_float, c_float, _P,
+                          c_int, _P, _P, c_float, _P, c_size_t, _P]),
+    "dg_act_bwd": (c_int, [c_int, c_int, _P, c_int, _P, c_int, c_int, c_float, _P, c_int, _P]),
+    "dg_p2p_loss_workspace_size": (c_int, [c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_size_t)]),
+    "dg_p2p_loss": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, _P, _P, c_int,
+                            ctypes.POINTER(c_float), _P, _P, _P, c_int, _P, c_int, _P, _P, _P, _P, c_size_t, _P]),
+    "dg_adam": (c_int, [_P, _P, _P, _P, c_int64, c_float, c_float, c_float, c_float, c_float, _P, _P]),
+    "dg_counter_add": (c_int, [_P, ctypes.c_int32, _P]),
+    "dg_channel_concat": (c_int, [c_int64, _P, c_int, c_int, _P, c_int, c_int, _P, c_int, _P]),
+    "dg_fill": (c_int, [_P, c_int64, c_float, _P]),
+    "dg_strided_copy": (c_int, [c_int64, c_int, _P, c_int, _P, c_int, _P]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+
+class DGError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise DGError(f"libdgan.so not found at {LIB_PATH}: run `python __graft_entry__.py` (build) first")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().dg_last_error_string().decode()
+        raise DGError(f"{what} failed (rc={rc}): {msg}")
+
+
+def call(name, *args):
+    check(getattr(lib(), name)(*args), name)

@@ -1,0 +1,284 @@
+"""Tensor-level wrappers over the libdgan C ABI.
+
+Tensors are torch CUDA (HIP) tensors used purely as device memory: NHWC,
+fp32, last dim contiguous; a channel slice of a wider buffer is passed with
+its pixel stride (zero-copy concat).  Every call enqueues on the current
+torch stream and never synchronises.
+"""
+import ctypes
+
+import torch
+
+from ._lib import call, lib, DGError
+
+ACT = {"none": 0, "linear": 0, None: 0, "lrelu": 1, "leaky_relu": 1, "relu": 2, "tanh": 3}
+OP_FWD, OP_BWD_DATA, OP_BWD_FILTER = 0, 1, 2
+
+
+def act_id(a):
+    if isinstance(a, int):
+        return a
+    if a not in ACT:
+        raise ValueError(f"unknown activation {a!r}")
+    return ACT[a]
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def pix_ld(t, C=None):
+    """Pixel stride (floats) of an NHWC (or [pixels, C]) view with contiguous channels."""
+    if t.dtype != torch.float32:
+        raise DGError(f"expected float32 tensor, got {t.dtype}")
+    if not t.is_cuda:
+        raise DGError("expected a device tensor (the HIP path has no CPU fallback)")
+    if t.dim() not in (2, 4):
+        raise DGError(f"expected NHWC or [pixels, C] tensor, got shape {tuple(t.shape)}")
+    Cc = t.shape[-1]
+    if Cc > 1 and t.stride(-1) != 1:
+        raise DGError("channel dim must be contiguous")
+    ld, expect = None, None
+    for d in range(t.dim() - 2, -1, -1):  # pixel dims, innermost first
+        size, st = t.shape[d], t.stride(d)
+        if size == 1:
+            continue
+        if ld is None:
+            ld = st
+        elif st != expect:
+            raise DGError(f"pixels of the view are not uniformly strided: shape {tuple(t.shape)} strides {t.stride()}")
+        expect = st * size
+    if ld is None:
+        ld = Cc
+    if C is not None and ld < C:
+        raise DGError("pixel stride smaller than channel count")
+    return ld
+
+
+def tf_same_pads(size, k, s):
+    """TF 'SAME' padding (before, after) for one spatial dim."""
+    out = -(-size // s)
+    total = max((out - 1) * s + k - size, 0)
+    return total // 2, total - total // 2
+
+
+class Workspace:
+    """Grow-only device scratch shared by ops issued on one stream."""
+
+    def __init__(self, device=None):
+        self.device = device
+        self.buf = None
+
+    def get(self, nbytes):
+        if nbytes == 0:
+            return None, 0
+        if self.buf is None or self.buf.numel() < nbytes:
+            self.buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=self.device or "cuda")
+        return self.buf, self.buf.numel()
+
+
+_default_ws = {}
+
+
+def default_workspace():
+    dev = torch.cuda.current_device()
+    if dev not in _default_ws:
+        _default_ws[dev] = Workspace(torch.device("cuda", dev))
+    return _default_ws[dev]
+
+
+class ConvDesc:
+    """A Conv2D / Conv2DTranspose layer geometry (immutable), libdgan descriptor.
+
+    padding: 'same' | 'valid' | (top, bottom, left, right).  For transposed
+    layers the pads are those of the equivalent forward conv, computed from
+    the output size the way TF's conv2d_transpose does.
+    """
+
+    def __init__(self, N, H, W, Cin, Cout, kernel, strides=1, padding="same", transpose=False):
+        kh, kw = (kernel, kernel) if isinstance(kernel, int) else kernel
+        sh, sw = (strides, strides) if isinstance(strides, int) else strides
+        if transpose:
+            if padding == "same":
+                Ho, Wo = H * sh, W * sw
+            elif padding == "valid":
+                Ho, Wo = H * sh + max(kh - sh, 0), W * sw + max(kw - sw, 0)
+            else:
+                pt, pb, pl, pr = padding
+                Ho, Wo = (H - 1) * sh + kh - pt - pb, (W - 1) * sw + kw - pl - pr
+            if padding in ("same", "valid"):
+                th = max((H - 1) * sh + kh - Ho, 0)
+                tw = max((W - 1) * sw + kw - Wo, 0)
+                pt, pb, pl, pr = th // 2, th - th // 2, tw // 2, tw - tw // 2
+        else:
+            if padding == "same":
+                pt, pb = tf_same_pads(H, kh, sh)
+                pl, pr = tf_same_pads(W, kw, sw)
+            elif padding == "valid":
+                pt = pb = pl = pr = 0
+            else:
+                pt, pb, pl, pr = padding
+        self.N, self.H, self.W, self.Cin, self.Cout = N, H, W, Cin, Cout
+        self.kh, self.kw, self.sh, self.sw = kh, kw, sh, sw
+        self.pads = (pt, pb, pl, pr)
+        self.transpose = bool(transpose)
+        h = ctypes.c_void_p()
+        call("dg_conv_desc_create", ctypes.byref(h), N, H, W, Cin, Cout, kh, kw, sh, sw, pt, pb, pl, pr,
+             int(self.transpose))
+        self._h = h
+        ho, wo = ctypes.c_int(), ctypes.c_int()
+        call("dg_conv_out_shape", h, ctypes.byref(ho), ctypes.byref(wo))
+        self.Ho, self.Wo = ho.value, wo.value
+        self.ws = []
+        for op in (OP_FWD, OP_BWD_DATA, OP_BWD_FILTER):
+            n = ctypes.c_size_t()
+            call("dg_conv_workspace_size", h, op, ctypes.byref(n))
+            self.ws.append(n.value)
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None) is not None:
+                lib().dg_conv_desc_destroy(self._h)
+        except Exception:
+            pass
+
+    @property
+    def out_shape(self):
+        return (self.N, self.Ho, self.Wo, self.Cout)
+
+    @property
+    def weight_shape(self):
+        return (self.kh, self.kw, self.Cout, self.Cin) if self.transpose else (self.kh, self.kw, self.Cin, self.Cout)
+
+    def max_ws(self):
+        return max(self.ws)
+
+    def _ws(self, op, ws):
+        ws = ws or default_workspace()
+        buf, n = ws.get(self.ws[op])
+        return (_p(buf), n)
+
+    def fwd(self, x, w, y, bias=None, act="none", alpha=0.3, beta=0.0, ws=None):
+        wp, wn = self._ws(OP_FWD, ws)
+        call("dg_conv_fwd", self._h, _p(x), pix_ld(x, self.Cin), _p(w), _p(bias), _p(y), pix_ld(y, self.Cout),
+             float(beta), act_id(act), float(alpha), wp, wn, _stream())
+        return y
+
+    def bwd_data(self, dy, w, dx, beta=0.0, ws=None):
+        wp, wn = self._ws(OP_BWD_DATA, ws)
+        call("dg_conv_bwd_data", self._h, _p(dy), pix_ld(dy, self.Cout), _p(w), _p(dx), pix_ld(dx, self.Cin),
+             float(beta), wp, wn, _stream())
+        return dx
+
+    def bwd_filter(self, x, dy, dw, dbias=None, beta=0.0, ws=None):
+        wp, wn = self._ws(OP_BWD_FILTER, ws)
+        call("dg_conv_bwd_filter", self._h, _p(x), pix_ld(x, self.Cin), _p(dy), pix_ld(dy, self.Cout), _p(dw),
+             _p(dbias), float(beta), wp, wn, _stream())
+        return dw
+
+
+def bn_workspace_bytes(M, C):
+    n = ctypes.c_size_t()
+    call("dg_bn_workspace_size", M, C, ctypes.byref(n))
+    return n.value
+
+
+def _rows(t):
+    return t.numel() // t.shape[-1] if t.dim() == 2 else t.shape[0] * t.shape[1] * t.shape[2]
+
+
+def bn_fwd_train(y, gamma, beta, save_mean, save_invstd, moving_mean, moving_var, z, act="none", alpha=0.3,
+                 momentum=0.99, eps=1e-3, drop_rate=0.0, drop_seed=0, step_dev=None, ws=None):
+    C = y.shape[-1]
+    M = _rows(y)
+    ws = ws or default_workspace()
+    buf, n = ws.get(bn_workspace_bytes(M, C))
+    call("dg_bn_fwd_train", M, C, _p(y), pix_ld(y, C), _p(gamma), _p(beta), _p(save_mean), _p(save_invstd),
+         _p(moving_mean), _p(moving_var), float(momentum), float(eps), _p(z), pix_ld(z, C), act_id(act),
+         float(alpha), float(drop_rate), ctypes.c_uint32(drop_seed & 0xFFFFFFFF), _p(step_dev), _p(buf), n,
+         _stream())
+    return z
+
+
+def bn_fwd_infer(y, gamma, beta, moving_mean, moving_var, z, act="none", alpha=0.3, eps=1e-3):
+    C = y.shape[-1]
+    call("dg_bn_fwd_infer", _rows(y), C, _p(y), pix_ld(y, C), _p(gamma), _p(beta), _p(moving_mean),
+         _p(moving_var), float(eps), _p(z), pix_ld(z, C), act_id(act), float(alpha), _stream())
+    return z
+
+
+def bn_bwd(dz, z, y, gamma, save_mean, save_invstd, dy, dgamma, dbeta, act="none", alpha=0.3, drop_rate=0.0,
+           beta=0.0, ws=None):
+    C = y.shape[-1]
+    M = _rows(y)
+    ws = ws or default_workspace()
+    buf, n = ws.get(bn_workspace_bytes(M, C))
+    call("dg_bn_bwd", M, C, _p(dz), pix_ld(dz, C), _p(z), pix_ld(z, C), _p(y), pix_ld(y, C), _p(gamma),
+         _p(save_mean), _p(save_invstd), act_id(act), float(alpha), float(drop_rate), _p(dy), pix_ld(dy, C),
+         _p(dgamma), _p(dbeta), float(beta), _p(buf), n, _stream())
+    return dy
+
+
+def act_bwd(dz, z, dy, act, alpha=0.3):
+    C = z.shape[-1]
+    call("dg_act_bwd", _rows(z), C, _p(dz), pix_ld(dz, C), _p(z), pix_ld(z, C), act_id(act), float(alpha),
+         _p(dy), pix_ld(dy, C), _stream())
+    return dy
+
+
+LOSS_WEIGHTS_REF = (1e-3, 1.0, 1.0, 1e-5, 1.0, 1.0)  # gan, l1, l2, tv, identity, content (pix2pix.py:75-92)
+
+
+def p2p_loss_workspace_bytes(B, H, W, C, n_logits):
+    n = ctypes.c_size_t()
+    call("dg_p2p_loss_workspace_size", B, H, W, C, n_logits, ctypes.byref(n))
+    return n.value
+
+
+def p2p_loss(gen, tgt, logit_real, logit_fake, out, ident=None, weights=LOSS_WEIGHTS_REF, content=None,
+             dgen=None, dident=None, dlogit_real_d=None, dlogit_fake_d=None, dlogit_fake_g=None, ws=None):
+    B, H, W, C = gen.shape
+    nlog = logit_fake.numel()
+    ws = ws or default_workspace()
+    buf, n = ws.get(p2p_loss_workspace_bytes(B, H, W, C, nlog))
+    warr = (ctypes.c_float * 6)(*[float(v) for v in weights])
+    call("dg_p2p_loss", B, H, W, C, _p(gen), pix_ld(gen, C), _p(tgt), pix_ld(tgt, C), _p(ident),
+         pix_ld(ident, C) if ident is not None else C, _p(logit_real), _p(logit_fake), nlog, warr, _p(content),
+         _p(out), _p(dgen), pix_ld(dgen, C) if dgen is not None else C, _p(dident),
+         pix_ld(dident, C) if dident is not None else C, _p(dlogit_real_d), _p(dlogit_fake_d), _p(dlogit_fake_g),
+         _p(buf), n, _stream())
+    return out
+
+
+def adam(p, g, m, v, lr, beta1, beta2, eps, iter_dev, grad_scale=1.0):
+    call("dg_adam", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), float(beta1), float(beta2), float(eps),
+         float(grad_scale), _p(iter_dev), _stream())
+
+
+def counter_add(c, inc=1):
+    call("dg_counter_add", _p(c), int(inc), _stream())
+
+
+def channel_concat(a, b, out):
+    ca, cb = a.shape[-1], b.shape[-1]
+    npix = _rows(a)
+    call("dg_channel_concat", npix, _p(a), pix_ld(a, ca), ca, _p(b), pix_ld(b, cb), cb, _p(out),
+         pix_ld(out, ca + cb), _stream())
+    return out
+
+
+def fill(t, value):
+    if not t.is_contiguous():
+        raise DGError("fill needs a contiguous tensor")
+    call("dg_fill", _p(t), t.numel(), float(value), _stream())
+    return t
+
+
+def strided_copy(src, dst):
+    C = src.shape[-1]
+    call("dg_strided_copy", _rows(src), C, _p(src), pix_ld(src, C), _p(dst), pix_ld(dst, C), _stream())
+    return dst

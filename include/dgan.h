@@ -1,0 +1,158 @@
+/*
+ * dgan.h — C ABI of libdgan.so, the MI355X (gfx950) hot path of the
+ * denoise-gan training step.
+ *
+ * The reference (pmcbride/denoise-gan) has no FFI: its hot path is the
+ * tf.keras graph traced by `train_step` (train_pix2pix.py:33-71) and every
+ * kernel below replaces a TensorFlow op that graph dispatches.  Each entry
+ * point names the reference call site it stands in for.  Conventions:
+ *
+ *   - every tensor is caller-owned device memory, fp32, NHWC; activations
+ *     carry an explicit pixel stride `ld*` (>= channels) so a layer can read
+ *     or write one channel slice of a concatenated buffer in place
+ *     (zero-copy skip concat, pix2pix.py:188 and :200);
+ *   - weights keep the Keras layout: Conv2D HWIO [kh,kw,Cin,Cout]
+ *     (pix2pix.py:115), Conv2DTranspose [kh,kw,Cout,Cin] (pix2pix.py:130);
+ *   - the library never allocates on the hot path: scratch is queried with
+ *     the *_workspace_size calls and handed in;
+ *   - all work is enqueued on the caller's HIP stream (`dg_stream_t` is a
+ *     hipStream_t); no call synchronises, so a whole step can be captured in
+ *     a hipGraph;
+ *   - every call returns DG_OK (0) or an error code; dg_last_error_string()
+ *     explains the last failure of the calling thread.  No C++ exception
+ *     crosses this boundary.
+ */
+#ifndef DGAN_H
+#define DGAN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void *dg_stream_t;                 /* hipStream_t (NULL = legacy stream) */
+typedef struct dg_conv_desc_s *dg_conv_t;  /* immutable once created */
+
+enum { DG_OK = 0, DG_ERR_ARG = 1, DG_ERR_HIP = 2, DG_ERR_WORKSPACE = 3, DG_ERR_UNSUPPORTED = 4 };
+
+/* fused activations (Keras defaults: LeakyReLU alpha=0.3, pix2pix.py:121) */
+enum { DG_ACT_NONE = 0, DG_ACT_LRELU = 1, DG_ACT_RELU = 2, DG_ACT_TANH = 3 };
+
+/* ops for dg_conv_workspace_size */
+enum { DG_OP_FWD = 0, DG_OP_BWD_DATA = 1, DG_OP_BWD_FILTER = 2 };
+
+const char *dg_last_error_string(void);
+int dg_version(void);
+
+/* ------------------------------------------------------------------------
+ * Convolution layers: Conv2D (pix2pix.py:115-116, :207-209, :217-218) and
+ * Conv2DTranspose (pix2pix.py:130-133, :169-173).  Replaces TF's Conv2D,
+ * Conv2DBackpropInput and Conv2DBackpropFilter kernels.
+ *
+ * Shapes are the LAYER's: input [N,H,W,Cin] -> output [N,Ho,Wo,Cout].
+ * Padding is explicit (top/bottom/left/right) so TF 'same' asymmetry is
+ * representable.  Conv2D:            Ho = (H + pt + pb - kh)/sh + 1.
+ * Conv2DTranspose (transpose = 1):  Ho = (H - 1)*sh + kh - pt - pb, and the
+ * pads are those of the equivalent forward conv (TF conv2d_backprop_input).
+ * ---------------------------------------------------------------------- */
+int dg_conv_desc_create(dg_conv_t *out, int N, int H, int W, int Cin, int Cout,
+                        int kh, int kw, int sh, int sw,
+                        int pad_t, int pad_b, int pad_l, int pad_r, int transpose);
+int dg_conv_desc_destroy(dg_conv_t d);
+int dg_conv_out_shape(dg_conv_t d, int *Ho, int *Wo);
+int dg_conv_workspace_size(dg_conv_t d, int op, size_t *bytes);
+
+/* y = act(conv(x, w) + bias) + beta * y            (bias may be NULL) */
+int dg_conv_fwd(dg_conv_t d, const float *x, int ldx, const float *w, const float *bias,
+                float *y, int ldy, float beta, int act, float alpha,
+                void *ws, size_t ws_bytes, dg_stream_t stream);
+/* dx = dL/dx + beta * dx */
+int dg_conv_bwd_data(dg_conv_t d, const float *dy, int lddy, const float *w,
+                     float *dx, int lddx, float beta,
+                     void *ws, size_t ws_bytes, dg_stream_t stream);
+/* dw = dL/dw + beta * dw ; dbias = sum(dy) + beta * dbias  (dbias may be NULL) */
+int dg_conv_bwd_filter(dg_conv_t d, const float *x, int ldx, const float *dy, int lddy,
+                       float *dw, float *dbias, float beta,
+                       void *ws, size_t ws_bytes, dg_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * BatchNormalization, training semantics of Keras' fused kernel
+ * (pix2pix.py:119, :135, :211): batch statistics over the M = N*H*W rows,
+ * biased variance for normalisation, moving stats updated with the
+ * unbiased variance, eps 1e-3, momentum 0.99.  The activation that follows
+ * in the reference block (LeakyReLU pix2pix.py:121/:213, Dropout+ReLU
+ * :137-140) is fused into the apply pass.  Dropout uses a counter-based
+ * hash keyed by (drop_seed, *step_dev, element) so results are reproducible
+ * and restatable on the CPU; drop_rate 0 disables it.
+ * ---------------------------------------------------------------------- */
+int dg_bn_workspace_size(int M, int C, size_t *bytes);
+int dg_bn_fwd_train(int M, int C, const float *y, int ldy, const float *gamma, const float *beta,
+                    float *save_mean, float *save_invstd,
+                    float *moving_mean, float *moving_var, float momentum, float eps,
+                    float *z, int ldz, int act, float alpha,
+                    float drop_rate, uint32_t drop_seed, const int32_t *step_dev,
+                    void *ws, size_t ws_bytes, dg_stream_t stream);
+int dg_bn_fwd_infer(int M, int C, const float *y, int ldy, const float *gamma, const float *beta,
+                    const float *moving_mean, const float *moving_var, float eps,
+                    float *z, int ldz, int act, float alpha, dg_stream_t stream);
+/* Backward of act(BN(y)) (+ dropout): reads dz (grad of the block output) and z (the
+ * block output, for the activation mask), writes dy; dgamma/dbeta = grad + beta*old. */
+int dg_bn_bwd(int M, int C, const float *dz, int lddz, const float *z, int ldz,
+              const float *y, int ldy, const float *gamma,
+              const float *save_mean, const float *save_invstd,
+              int act, float alpha, float drop_rate,
+              float *dy, int lddy, float *dgamma, float *dbeta, float beta,
+              void *ws, size_t ws_bytes, dg_stream_t stream);
+/* dy = dz * act'(z)  for blocks without BN (pix2pix.py:118-121 with apply_batchnorm=False) */
+int dg_act_bwd(int M, int C, const float *dz, int lddz, const float *z, int ldz,
+               int act, float alpha, float *dy, int lddy, dg_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * pix2pix losses, forward values and gradients in one call
+ * (Pix2Pix.generator_loss pix2pix.py:74-94, discriminator_loss :96-103).
+ * gen/tgt/ident are [B,H,W,C] with pixel strides; ident (= G(target)) may be
+ * NULL, then the identity term is 0.  weights[6] = {gan, l1, l2, tv, identity,
+ * content} scales (reference: 1e-3, 1, 1, 1e-5, 1, 1).  out[8] (device) =
+ * {gen_total, gan, l1, l2, content, disc, var, identity}: the tuple order of
+ * train_step (train_pix2pix.py:71).  Gradient outputs may be NULL.
+ * ---------------------------------------------------------------------- */
+int dg_p2p_loss_workspace_size(int B, int H, int W, int C, int n_logits, size_t *bytes);
+int dg_p2p_loss(int B, int H, int W, int C,
+                const float *gen, int ldgen, const float *tgt, int ldtgt,
+                const float *ident, int ldident,
+                const float *logit_real, const float *logit_fake, int n_logits,
+                const float *weights, const float *content_value, float *out,
+                float *dgen, int lddgen, float *dident, int lddident,
+                float *dlogit_real_d, float *dlogit_fake_d, float *dlogit_fake_g,
+                void *ws, size_t ws_bytes, dg_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Keras Adam (ResourceApplyAdam, train_pix2pix.py:68-69):
+ *   t = *iter_dev + 1; lr_t = lr*sqrt(1-b2^t)/(1-b1^t)
+ *   m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g^2 ; p -= lr_t m / (sqrt(v) + eps)
+ * with g = grad_scale * grad (grad_scale folds the data-parallel 1/world).
+ * Runs over one flat parameter arena.  dg_counter_add bumps the device
+ * iteration counter afterwards (optimizer.iterations).
+ * ---------------------------------------------------------------------- */
+int dg_adam(float *p, const float *g, float *m, float *v, int64_t n,
+            float lr, float beta1, float beta2, float eps, float grad_scale,
+            const int32_t *iter_dev, dg_stream_t stream);
+int dg_counter_add(int32_t *counter_dev, int32_t inc, dg_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Data movement helpers.
+ * dg_channel_concat: out[p, 0:ca] = a[p, 0:ca], out[p, ca:ca+cb] = b[p, 0:cb]
+ *   (tf.keras.layers.concatenate([inp, tar]) at pix2pix.py:200).
+ * dg_fill: p[0:n] = value.
+ * ---------------------------------------------------------------------- */
+int dg_channel_concat(int64_t npix, const float *a, int lda, int ca, const float *b, int ldb, int cb,
+                      float *out, int ldo, dg_stream_t stream);
+int dg_fill(float *p, int64_t n, float value, dg_stream_t stream);
+int dg_strided_copy(int64_t npix, int C, const float *src, int lds, float *dst, int ldd, dg_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DGAN_H */

@@ -1,0 +1,133 @@
+"""Numerics of the HIP conv engine (fwd / bwd_data / bwd_filter) against a
+plain PyTorch fp64 CPU reference of the same Keras layer, for every layer
+geometry of the pix2pix generator and discriminator (pix2pix.py:110-220)
+plus the SRGAN/FSRGAN shapes (k3 'same' with TF's asymmetric pads, k1).
+
+Tolerance (fp32 MFMA accumulation vs fp64): relative L2 error < 2e-6 and
+max-abs error < 1e-5 * max|ref| (scaled by sqrt(K/1024) for long K)."""
+import math
+
+import pytest
+import torch
+
+from torch_ref import conv2d_ref, conv2d_transpose_ref
+
+gpu = pytest.mark.gpu
+
+# (name, N, H, W, Cin, Cout, k, s, padding, transpose, bias)
+CASES = [
+    ("G.down1", 2, 64, 64, 3, 64, 4, 2, "same", False, False),
+    ("G.down2", 2, 32, 32, 64, 128, 4, 2, "same", False, False),
+    ("G.down4", 2, 16, 16, 256, 512, 4, 2, "same", False, False),
+    ("G.down8", 4, 2, 2, 512, 512, 4, 2, "same", False, False),
+    ("G.up1", 4, 1, 1, 512, 512, 4, 2, "same", True, False),
+    ("G.up2", 2, 2, 2, 1024, 512, 4, 2, "same", True, False),
+    ("G.up5", 2, 8, 8, 1024, 256, 4, 2, "same", True, False),
+    ("G.up7", 2, 16, 16, 256, 64, 4, 2, "same", True, False),
+    ("G.last", 2, 32, 32, 128, 3, 4, 2, "same", True, True),
+    ("D.down1", 2, 64, 64, 6, 64, 4, 2, "same", False, False),
+    ("D.conv", 2, 16, 16, 256, 512, 4, 1, (1, 1, 1, 1), False, False),
+    ("D.last", 2, 15, 15, 512, 1, 4, 1, (1, 1, 1, 1), False, True),
+    ("k3s1", 2, 12, 12, 64, 64, 3, 1, "same", False, True),
+    ("k3s2", 2, 12, 12, 32, 64, 3, 2, "same", False, True),
+    ("k1s1", 2, 6, 6, 64, 3, 1, 1, "same", False, True),
+    ("odd", 3, 9, 7, 8, 32, 4, 2, "same", False, False),
+]
+
+
+def _close(got, ref, K, what):
+    got = got.double().cpu()
+    err = (got - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-30
+    rel = ((got - ref).norm() / (ref.norm() + 1e-30)).item()
+    tol = 1e-5 * max(1.0, math.sqrt(K / 1024.0))
+    assert rel < 2e-6 * max(1.0, math.sqrt(K / 1024.0)), f"{what}: rel L2 {rel:.3e}"
+    assert err <= tol * scale, f"{what}: max abs {err:.3e} vs scale {scale:.3e}"
+
+
+@gpu
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_conv_layer(case):
+    from dgan.ops import ConvDesc
+    name, N, H, W, Cin, Cout, k, s, padding, transpose, has_bias = case
+    torch.manual_seed(hash(name) & 0xFFFF)
+    d = ConvDesc(N, H, W, Cin, Cout, k, s, padding, transpose)
+    x = torch.randn(N, H, W, Cin, dtype=torch.float64)
+    w = torch.randn(*d.weight_shape, dtype=torch.float64) * 0.05
+    b = torch.randn(Cout, dtype=torch.float64) if has_bias else None
+    dy = torch.randn(N, d.Ho, d.Wo, Cout, dtype=torch.float64)
+
+    xr, wr = x.clone().requires_grad_(), w.clone().requires_grad_()
+    br = b.clone().requires_grad_() if has_bias else None
+    if transpose:
+        yr = conv2d_transpose_ref(xr, wr, s, d.pads, (d.Ho, d.Wo), br)
+    else:
+        yr = conv2d_ref(xr, wr, s, d.pads, br)
+    assert tuple(yr.shape) == d.out_shape
+    yr.backward(dy)
+
+    dev = torch.device("cuda")
+    xg, wg, dyg = x.float().to(dev), w.float().to(dev), dy.float().to(dev)
+    bg = b.float().to(dev) if has_bias else None
+    y = torch.empty(d.out_shape, device=dev)
+    d.fwd(xg, wg, y, bias=bg)
+    dx = torch.empty_like(xg)
+    d.bwd_data(dyg, wg, dx)
+    dw = torch.empty_like(wg)
+    db = torch.empty(Cout, device=dev) if has_bias else None
+    d.bwd_filter(xg, dyg, dw, dbias=db)
+    torch.cuda.synchronize()
+    K = k * k * (Cin if not transpose else Cout)
+    _close(y, yr.detach(), K, f"{name} fwd")
+    _close(dx, xr.grad, k * k * Cout, f"{name} bwd_data")
+    _close(dw, wr.grad, N * d.Ho * d.Wo, f"{name} bwd_filter")
+    if has_bias:
+        _close(db, br.grad, N * d.Ho * d.Wo, f"{name} dbias")
+
+
+@gpu
+def test_conv_strided_views_and_accumulate():
+    """Zero-copy concat: read a channel slice, write into a slice with beta=1."""
+    from dgan.ops import ConvDesc
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    N, H, W, Cin, Cout = 2, 16, 16, 64, 128
+    d = ConvDesc(N, H, W, Cin, Cout, 4, 2, "same")
+    big_in = torch.randn(N, H, W, Cin + 64, device=dev)
+    x = big_in[..., 64:]
+    w = torch.randn(*d.weight_shape, device=dev) * 0.05
+    out = torch.randn(N, d.Ho, d.Wo, Cout + 128, device=dev)
+    y = out[..., :Cout]
+    y0 = y.clone()
+    d.fwd(x, w, y, beta=1.0)
+    ref = conv2d_ref(x.double().cpu(), w.double().cpu(), 2, d.pads) + y0.double().cpu()
+    torch.cuda.synchronize()
+    _close(y, ref, 16 * Cin, "strided fwd beta=1")
+    # untouched channels stay intact
+    assert torch.equal(out[..., Cout:].cpu(), out[..., Cout:].cpu())
+    # bwd_data into a slice, accumulate
+    dy = torch.randn(N, d.Ho, d.Wo, Cout, device=dev)
+    dxbuf = torch.randn(N, H, W, Cin + 32, device=dev)
+    dx = dxbuf[..., 32:]
+    dx0 = dx.clone()
+    d.bwd_data(dy, w, dx, beta=1.0)
+    xr = x.double().cpu().requires_grad_()
+    conv2d_ref(xr, w.double().cpu(), 2, d.pads).backward(dy.double().cpu())
+    torch.cuda.synchronize()
+    _close(dx, xr.grad + dx0.double().cpu(), 16 * Cout, "strided bwd_data beta=1")
+
+
+@gpu
+def test_conv_fused_lrelu_epilogue():
+    from dgan.ops import ConvDesc
+    torch.manual_seed(1)
+    dev = torch.device("cuda")
+    d = ConvDesc(2, 32, 32, 64, 128, 4, 2, "same")
+    x = torch.randn(2, 32, 32, 64, device=dev)
+    w = torch.randn(*d.weight_shape, device=dev) * 0.05
+    y = torch.empty(d.out_shape, device=dev)
+    d.fwd(x, w, y, act="lrelu", alpha=0.3)
+    ref = conv2d_ref(x.double().cpu(), w.double().cpu(), 2, d.pads)
+    ref = torch.where(ref > 0, ref, 0.3 * ref)
+    torch.cuda.synchronize()
+    _close(y, ref, 1024, "lrelu epilogue")
