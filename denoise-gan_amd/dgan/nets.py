@@ -1,0 +1,484 @@
+"""pix2pix generator / discriminator executors on libdgan.
+
+This replaces what tf.keras + GradientTape do for the reference's
+`train_step` (train_pix2pix.py:33-71): instead of a traced autodiff graph,
+each network has a static plan — layer descriptors, activation buffers,
+and an explicit backward schedule — built once per input shape.
+
+Memory layout (HBM, all fp32 NHWC):
+  * trainable variables of a network live in ONE flat arena (plus grad, m,
+    v arenas of identical layout), laid out in backward-completion order so
+    gradient buckets become final front-to-back (data-parallel all-reduce
+    and the single-launch Adam both run over contiguous ranges);
+  * the U-Net skip concat (pix2pix.py:188) is zero-copy: each down block
+    writes its activation straight into the channel tail of the up block's
+    concat buffer, and its gradient is accumulated there in place;
+  * the discriminator's input concat (pix2pix.py:200) is a 6-channel buffer
+    whose fake half is written directly by the generator's last layer.
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import ops
+from .ops import ConvDesc
+
+ALPHA = 0.3       # Keras LeakyReLU default (pix2pix.py:121, :213)
+BN_EPS = 1e-3     # Keras BatchNormalization defaults (pix2pix.py:119)
+BN_MOMENTUM = 0.99
+DROP_RATE = 0.5   # pix2pix.py:138
+
+
+# ---------------------------------------------------------------------------
+# layer specs (pix2pix.py:147-173, :200-218); `width` divides filter counts
+# (tiny variants for tests only; width=1 is the reference model)
+# ---------------------------------------------------------------------------
+def g_layer_specs(width=1, in_ch=3, out_ch=3):
+    f = lambda c: max(1, c // width)
+    downs = [("down1", in_ch, f(64), False), ("down2", f(64), f(128), True), ("down3", f(128), f(256), True),
+             ("down4", f(256), f(512), True), ("down5", f(512), f(512), True), ("down6", f(512), f(512), True),
+             ("down7", f(512), f(512), True), ("down8", f(512), f(512), True)]
+    ups = []
+    cin = f(512)
+    for u, c in enumerate([512, 512, 512, 512, 256, 128, 64]):
+        cout = f(c)
+        ups.append((f"up{u + 1}", cin, cout, u < 3))
+        cin = cout + downs[6 - u][2]
+    return downs, ups, ("last", cin, out_ch)
+
+
+def d_layer_specs(width=1, in_ch=6):
+    f = lambda c: max(1, c // width)
+    return [("down1", in_ch, f(64), False), ("down2", f(64), f(128), True), ("down3", f(128), f(256), True),
+            ("conv", f(256), f(512), True), ("last", f(512), 1, False)]
+
+
+def g_variables(width=1):
+    """(name, shape) in Keras trainable_variables order."""
+    downs, ups, last = g_layer_specs(width)
+    out = []
+    for name, ci, co, bn in downs:
+        out.append((f"{name}/kernel", (4, 4, ci, co)))
+        if bn:
+            out += [(f"{name}/gamma", (co,)), (f"{name}/beta", (co,))]
+    for name, ci, co, _ in ups:
+        out += [(f"{name}/kernel", (4, 4, co, ci)), (f"{name}/gamma", (co,)), (f"{name}/beta", (co,))]
+    out += [("last/kernel", (4, 4, last[2], last[1])), ("last/bias", (last[2],))]
+    return out
+
+
+def d_variables(width=1):
+    out = []
+    for name, ci, co, bn in d_layer_specs(width):
+        out.append((f"{name}/kernel", (4, 4, ci, co)))
+        if bn:
+            out += [(f"{name}/gamma", (co,)), (f"{name}/beta", (co,))]
+    out.append(("last/bias", (1,)))
+    return out
+
+
+def dropout_seed(base, layer_idx, pass_idx):
+    return (base * 1000003 + layer_idx * 7919 + pass_idx * 104729) & 0xFFFFFFFF
+
+
+def init_variables(var_list, seed):
+    """Keras-style init from a seeded numpy PCG64 stream: kernels N(0, 0.02)
+    (pix2pix.py:111, :126, :168, :195), BN gamma 1 / beta 0, biases 0."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = {}
+    for name, shape in var_list:
+        if name.endswith("/kernel"):
+            out[name] = (rng.standard_normal(shape) * 0.02).astype(np.float32)
+        elif name.endswith("/gamma"):
+            out[name] = np.ones(shape, np.float32)
+        else:
+            out[name] = np.zeros(shape, np.float32)
+    return out
+
+
+# ---------------------------------------------------------------------------
+# flat parameter arena
+# ---------------------------------------------------------------------------
+class Arena:
+    """Trainable variables (+grad, Adam m/v) of one network in flat device buffers."""
+    ALIGN = 64  # floats; keeps every variable 256-byte aligned for vector loads
+
+    def __init__(self, var_list, device, layout_order=None):
+        self.var_list = list(var_list)
+        self.shapes = dict(var_list)
+        order = layout_order or [n for n, _ in var_list]
+        assert sorted(order) == sorted(self.shapes)
+        self.offsets = {}
+        off = 0
+        for n in order:
+            self.offsets[n] = off
+            off += -(-int(np.prod(self.shapes[n])) // self.ALIGN) * self.ALIGN
+        self.layout = list(order)
+        self.numel = off
+        self.device = device
+        self.data = torch.zeros(off, dtype=torch.float32, device=device)
+        self.grad = torch.zeros(off, dtype=torch.float32, device=device)
+        self.m = torch.zeros(off, dtype=torch.float32, device=device)
+        self.v = torch.zeros(off, dtype=torch.float32, device=device)
+        self.iterations = torch.zeros(1, dtype=torch.int32, device=device)
+
+    def _v(self, buf, name):
+        o = self.offsets[name]
+        shape = self.shapes[name]
+        return buf[o:o + int(np.prod(shape))].view(shape)
+
+    def param(self, name):
+        return self._v(self.data, name)
+
+    def grad_of(self, name):
+        return self._v(self.grad, name)
+
+    def end_offset(self, name):
+        return self.offsets[name] + int(np.prod(self.shapes[name]))
+
+    def load(self, values):
+        for n, a in values.items():
+            self.param(n).copy_(torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float32))
+
+    def export(self, buf=None):
+        return {n: self._v(self.data if buf is None else buf, n).detach().cpu().numpy().copy()
+                for n, _ in self.var_list}
+
+    @property
+    def count(self):
+        return sum(int(np.prod(s)) for s in self.shapes.values())
+
+
+class BNState:
+    """Non-trainable moving statistics of every BN layer of a network."""
+
+    def __init__(self, channels, device):
+        self.mean = {k: torch.zeros(c, device=device) for k, c in channels.items()}
+        self.var = {k: torch.ones(c, device=device) for k, c in channels.items()}
+
+    def export(self):
+        out = {}
+        for k in self.mean:
+            out[f"{k}/moving_mean"] = self.mean[k].cpu().numpy()
+            out[f"{k}/moving_variance"] = self.var[k].cpu().numpy()
+        return out
+
+    def load(self, values):
+        for k in self.mean:
+            if f"{k}/moving_mean" in values:
+                self.mean[k].copy_(torch.as_tensor(values[f"{k}/moving_mean"]))
+                self.var[k].copy_(torch.as_tensor(values[f"{k}/moving_variance"]))
+
+
+def _bn_channels(var_list):
+    return {n.rsplit("/", 1)[0]: s[0] for n, s in var_list if n.endswith("/gamma")}
+
+
+def _empty(shape, device):
+    return torch.empty(shape, dtype=torch.float32, device=device)
+
+
+# ---------------------------------------------------------------------------
+# U-Net generator plan (pix2pix.py:144-192)
+# ---------------------------------------------------------------------------
+class GeneratorPlan:
+    """Static forward/backward schedule of the U-Net for one input shape.
+
+    slots: independent activation sets (slot 0 = G(x), slot 1 = G(target)
+    for the identity loss, pix2pix.py:90) so both backwards can run after
+    both forwards, as the two GradientTapes do."""
+
+    def __init__(self, N, H, W, width, arena, bn_state, device, slots=1, train=True):
+        self.N, self.H, self.W, self.width = N, H, W, width
+        self.arena, self.bn = arena, bn_state
+        self.device = device
+        self.downs, self.ups, self.last = g_layer_specs(width)
+        self.train = train
+        if H % 256 or W % 256:
+            # 8 stride-2 blocks need H, W divisible by 2^8 for the skip shapes to line up
+            if H % (1 << 8) or W % (1 << 8):
+                raise ValueError(f"pix2pix generator needs H, W divisible by 256, got {H}x{W}")
+        # descriptors
+        self.ddesc, self.udesc = [], []
+        h, w = H, W
+        self.down_hw = []
+        for name, ci, co, _ in self.downs:
+            d = ConvDesc(N, h, w, ci, co, 4, 2, "same")
+            self.ddesc.append(d)
+            h, w = d.Ho, d.Wo
+            self.down_hw.append((h, w))
+        for name, ci, co, _ in self.ups:
+            d = ConvDesc(N, h, w, ci, co, 4, 2, "same", transpose=True)
+            self.udesc.append(d)
+            h, w = d.Ho, d.Wo
+        self.ldesc = ConvDesc(N, h, w, self.last[1], self.last[2], 4, 2, "same", transpose=True)
+        self.out_shape = self.ldesc.out_shape
+        # activations per slot
+        self.slots = []
+        for _ in range(slots):
+            s = {}
+            s["cat"] = []
+            for u, (name, ci, co, _) in enumerate(self.ups):
+                d = self.udesc[u]
+                skip_c = self.downs[6 - u][2]
+                s["cat"].append(_empty((N, d.Ho, d.Wo, co + skip_c), device))
+            s["z8"] = _empty((N,) + self.down_hw[7] + (self.downs[7][2],), device)
+            s["yd"] = [(_empty((N,) + self.down_hw[i] + (self.downs[i][2],), device) if self.downs[i][3] else None)
+                       for i in range(8)]
+            s["yu"] = [_empty(self.udesc[u].out_shape, device) for u in range(7)]
+            s["mean"] = {}
+            s["inv"] = {}
+            for name, _, co, bn in self.downs + [(n, a, b, True) for n, a, b, _ in self.ups]:
+                if bn:
+                    s["mean"][name] = _empty((co,), device)
+                    s["inv"][name] = _empty((co,), device)
+            s["x"] = None
+            s["out"] = None
+            self.slots.append(s)
+        # gradient buffers (shared by slots: backwards run one after another)
+        if train:
+            self.dcat = [torch.empty_like(c) for c in self.slots[0]["cat"]]
+            self.dz8 = torch.empty_like(self.slots[0]["z8"])
+            maxdy = max([d.N * d.Ho * d.Wo * d.Cout for d in self.ddesc + self.udesc + [self.ldesc]])
+            self.dy = _empty((maxdy,), device)
+        sizes = [d.max_ws() for d in self.ddesc + self.udesc + [self.ldesc]]
+        for name, _, co, bn in self.downs:
+            pass
+        self.ws_bytes = max(sizes + [self._bn_ws_max()])
+
+    def _bn_ws_max(self):
+        m = 0
+        for i, (name, ci, co, bn) in enumerate(self.downs):
+            d = self.ddesc[i]
+            m = max(m, ops.bn_workspace_bytes(d.N * d.Ho * d.Wo, co))
+        for u, d in enumerate(self.udesc):
+            m = max(m, ops.bn_workspace_bytes(d.N * d.Ho * d.Wo, d.Cout))
+        return m
+
+    # views ---------------------------------------------------------------
+    def z_view(self, s, l):
+        """activation of down block l (post LeakyReLU) inside its concat buffer"""
+        if l == 7:
+            return s["z8"]
+        u = 6 - l
+        co = self.ups[u][2]
+        return s["cat"][u][..., co:]
+
+    def dz_view(self, l):
+        if l == 7:
+            return self.dz8
+        u = 6 - l
+        return self.dcat[u][..., self.ups[u][2]:]
+
+    def _dy(self, d, C):
+        return self.dy[: d.N * d.Ho * d.Wo * C].view(d.N, d.Ho, d.Wo, C)
+
+    # forward --------------------------------------------------------------
+    def forward(self, x, out, slot=0, training=True, ws=None, drop_rate=DROP_RATE, drop_seed=0, step_dev=None):
+        """x [N,H,W,3] view; writes tanh output into `out` (any NHWC view)."""
+        s = self.slots[slot]
+        s["x"], s["out"] = x, out
+        A = self.arena
+        h = x
+        for l, (name, ci, co, bn) in enumerate(self.downs):
+            d = self.ddesc[l]
+            z = self.z_view(s, l)
+            if not bn:
+                d.fwd(h, A.param(f"{name}/kernel"), z, act="lrelu", alpha=ALPHA, ws=ws)
+            else:
+                y = s["yd"][l]
+                d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws)
+                self._bn_fwd(s, name, y, z, "lrelu", training, ws)
+            h = z
+        for u, (name, ci, co, drop) in enumerate(self.ups):
+            d = self.udesc[u]
+            y = s["yu"][u]
+            d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws)
+            z = s["cat"][u][..., :co]
+            rate = drop_rate if (drop and training) else 0.0
+            self._bn_fwd(s, name, y, z, "relu", training, ws, rate, dropout_seed(drop_seed, u, slot), step_dev)
+            h = s["cat"][u]
+        self.ldesc.fwd(h, A.param("last/kernel"), out, bias=A.param("last/bias"), act="tanh", ws=ws)
+        return out
+
+    def _bn_fwd(self, s, name, y, z, act, training, ws, drop_rate=0.0, seed=0, step_dev=None):
+        A = self.arena
+        if training:
+            ops.bn_fwd_train(y, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), s["mean"][name], s["inv"][name],
+                             self.bn.mean[name], self.bn.var[name], z, act=act, alpha=ALPHA, momentum=BN_MOMENTUM,
+                             eps=BN_EPS, drop_rate=drop_rate, drop_seed=seed, step_dev=step_dev, ws=ws)
+        else:
+            ops.bn_fwd_infer(y, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.bn.mean[name],
+                             self.bn.var[name], z, act=act, alpha=ALPHA, eps=BN_EPS)
+
+    # backward ---------------------------------------------------------------
+    def backward(self, dout, slot=0, beta=0.0, ws=None, drop_rate=DROP_RATE, on_grads_ready=None):
+        """dout: grad of the tanh output (NHWC view).  Weight grads go to the
+        arena grad buffer: g = new + beta * g.  `on_grads_ready(name)` is
+        called after each layer's gradients are enqueued (bucketed all-reduce)."""
+        s = self.slots[slot]
+        A = self.arena
+        dl = self.ldesc
+        dpre = self._dy(dl, dl.Cout)
+        ops.act_bwd(dout, s["out"], dpre, "tanh")
+        dl.bwd_filter(s["cat"][6], dpre, A.grad_of("last/kernel"), dbias=A.grad_of("last/bias"), beta=beta, ws=ws)
+        dl.bwd_data(dpre, A.param("last/kernel"), self.dcat[6], ws=ws)
+        if on_grads_ready:
+            on_grads_ready("last")
+        for u in range(6, -1, -1):
+            name, ci, co, drop = self.ups[u]
+            d = self.udesc[u]
+            dy = self._dy(d, co)
+            ops.bn_bwd(self.dcat[u][..., :co], s["cat"][u][..., :co], s["yu"][u], A.param(f"{name}/gamma"),
+                       s["mean"][name], s["inv"][name], dy, A.grad_of(f"{name}/gamma"), A.grad_of(f"{name}/beta"),
+                       act="relu", alpha=ALPHA, drop_rate=drop_rate if drop else 0.0, beta=beta, ws=ws)
+            hin = s["z8"] if u == 0 else s["cat"][u - 1]
+            dhin = self.dz8 if u == 0 else self.dcat[u - 1]
+            d.bwd_filter(hin, dy, A.grad_of(f"{name}/kernel"), beta=beta, ws=ws)
+            d.bwd_data(dy, A.param(f"{name}/kernel"), dhin, ws=ws)
+            if on_grads_ready:
+                on_grads_ready(name)
+        for l in range(7, -1, -1):
+            name, ci, co, bn = self.downs[l]
+            d = self.ddesc[l]
+            dz = self.dz_view(l)
+            z = self.z_view(s, l)
+            dy = self._dy(d, co)
+            if bn:
+                ops.bn_bwd(dz, z, s["yd"][l], A.param(f"{name}/gamma"), s["mean"][name], s["inv"][name], dy,
+                           A.grad_of(f"{name}/gamma"), A.grad_of(f"{name}/beta"), act="lrelu", alpha=ALPHA,
+                           beta=beta, ws=ws)
+            else:
+                ops.act_bwd(dz, z, dy, "lrelu", ALPHA)
+            hin = s["x"] if l == 0 else self.z_view(s, l - 1)
+            d.bwd_filter(hin, dy, A.grad_of(f"{name}/kernel"), beta=beta, ws=ws)
+            if l > 0:
+                # accumulate into the skip-gradient already sitting in the concat grad buffer
+                d.bwd_data(dy, A.param(f"{name}/kernel"), self.dz_view(l - 1), beta=1.0, ws=ws)
+            if on_grads_ready:
+                on_grads_ready(name)
+
+
+def g_layout_order(width=1):
+    """Arena layout = backward completion order: last, up7..up1, down8..down1."""
+    downs, ups, last = g_layer_specs(width)
+    order = ["last/kernel", "last/bias"]
+    for name, ci, co, _ in reversed(ups):
+        order += [f"{name}/kernel", f"{name}/gamma", f"{name}/beta"]
+    for name, ci, co, bn in reversed(downs):
+        order.append(f"{name}/kernel")
+        if bn:
+            order += [f"{name}/gamma", f"{name}/beta"]
+    return order
+
+
+def d_layout_order(width=1):
+    order = ["last/kernel", "last/bias"]
+    for name, ci, co, bn in reversed(d_layer_specs(width)[:-1]):
+        order.append(f"{name}/kernel")
+        if bn:
+            order += [f"{name}/gamma", f"{name}/beta"]
+    return order
+
+
+# ---------------------------------------------------------------------------
+# PatchGAN discriminator plan (pix2pix.py:194-220)
+# ---------------------------------------------------------------------------
+class DiscriminatorPlan:
+    """slot 0 = D([x, y]) (real), slot 1 = D([x, G(x)]) (fake); every slot owns
+    its 6-channel input buffer `inp[slot]`."""
+
+    def __init__(self, N, H, W, width, arena, bn_state, device, slots=2, train=True):
+        self.N, self.H, self.W = N, H, W
+        self.arena, self.bn = arena, bn_state
+        self.specs = d_layer_specs(width)
+        self.desc = []
+        h, w = H, W
+        for name, ci, co, _ in self.specs:
+            if name.startswith("down"):
+                d = ConvDesc(N, h, w, ci, co, 4, 2, "same")
+            else:  # ZeroPadding2D() + Conv2D(k4, s1, 'valid') == explicit pad 1
+                d = ConvDesc(N, h, w, ci, co, 4, 1, (1, 1, 1, 1))
+            self.desc.append(d)
+            h, w = d.Ho, d.Wo
+        self.out_shape = self.desc[-1].out_shape
+        self.slots = []
+        for _ in range(slots):
+            s = {"inp": _empty((N, H, W, self.specs[0][1]), device)}
+            s["y"] = [(_empty(d.out_shape, device) if sp[3] else None) for d, sp in zip(self.desc, self.specs)]
+            s["z"] = [_empty(d.out_shape, device) for d in self.desc[:-1]]
+            s["logits"] = _empty(self.out_shape, device)
+            s["mean"] = {sp[0]: _empty((sp[2],), device) for sp in self.specs if sp[3]}
+            s["inv"] = {sp[0]: _empty((sp[2],), device) for sp in self.specs if sp[3]}
+            self.slots.append(s)
+        if train:
+            self.dz = [_empty(d.out_shape, device) for d in self.desc[:-1]]
+            maxdy = max(d.N * d.Ho * d.Wo * d.Cout for d in self.desc)
+            self.dy = _empty((maxdy,), device)
+            self.dinp = _empty((N, H, W, self.specs[0][1]), device)
+        self.ws_bytes = max([d.max_ws() for d in self.desc] +
+                            [ops.bn_workspace_bytes(d.N * d.Ho * d.Wo, d.Cout) for d in self.desc])
+
+    def _dy(self, d):
+        return self.dy[: d.N * d.Ho * d.Wo * d.Cout].view(d.N, d.Ho, d.Wo, d.Cout)
+
+    def forward(self, slot=0, training=True, ws=None):
+        s = self.slots[slot]
+        A = self.arena
+        h = s["inp"]
+        for i, (name, ci, co, bn) in enumerate(self.specs):
+            d = self.desc[i]
+            if name == "last":
+                d.fwd(h, A.param("last/kernel"), s["logits"], bias=A.param("last/bias"), ws=ws)
+                return s["logits"]
+            z = s["z"][i]
+            if not bn:
+                d.fwd(h, A.param(f"{name}/kernel"), z, act="lrelu", alpha=ALPHA, ws=ws)
+            else:
+                y = s["y"][i]
+                d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws)
+                if training:
+                    ops.bn_fwd_train(y, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), s["mean"][name],
+                                     s["inv"][name], self.bn.mean[name], self.bn.var[name], z, act="lrelu",
+                                     alpha=ALPHA, momentum=BN_MOMENTUM, eps=BN_EPS, ws=ws)
+                else:
+                    ops.bn_fwd_infer(y, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.bn.mean[name],
+                                     self.bn.var[name], z, act="lrelu", alpha=ALPHA, eps=BN_EPS)
+            h = z
+
+    def backward(self, dlogits, slot=0, param_grads=True, beta=0.0, input_grad=None, input_beta=0.0, ws=None,
+                 on_grads_ready=None):
+        """Backward through D for one slot.  param_grads: accumulate weight grads
+        (g = new + beta*g); input_grad: NHWC view receiving dL/d(input) (+input_beta*old)."""
+        s = self.slots[slot]
+        A = self.arena
+        dh = dlogits
+        n = len(self.specs)
+        for i in range(n - 1, -1, -1):
+            name, ci, co, bn = self.specs[i]
+            d = self.desc[i]
+            if name == "last":
+                dy = dh
+                if param_grads:
+                    d.bwd_filter(s["z"][i - 1], dy, A.grad_of("last/kernel"), dbias=A.grad_of("last/bias"),
+                                 beta=beta, ws=ws)
+            else:
+                dy = self._dy(d)
+                if bn:
+                    ops.bn_bwd(dh, s["z"][i], s["y"][i], A.param(f"{name}/gamma"), s["mean"][name], s["inv"][name],
+                               dy, A.grad_of(f"{name}/gamma") if param_grads else None,
+                               A.grad_of(f"{name}/beta") if param_grads else None, act="lrelu", alpha=ALPHA,
+                               beta=beta, ws=ws)
+                else:
+                    ops.act_bwd(dh, s["z"][i], dy, "lrelu", ALPHA)
+                if param_grads:
+                    hin = s["inp"] if i == 0 else s["z"][i - 1]
+                    d.bwd_filter(hin, dy, A.grad_of(f"{name}/kernel"), beta=beta, ws=ws)
+            if param_grads and on_grads_ready:
+                on_grads_ready(name)
+            if i > 0:
+                d.bwd_data(dy, A.param(f"{name}/kernel"), self.dz[i - 1], ws=ws)
+                dh = self.dz[i - 1]
+            elif input_grad is not None:
+                d.bwd_data(dy, A.param(f"{name}/kernel"), input_grad, beta=input_beta, ws=ws)

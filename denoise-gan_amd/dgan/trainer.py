@@ -1,0 +1,102 @@
+"""The fused pix2pix training step (train_pix2pix.py:33-71) on libdgan.
+
+One call = the reference's traced `train_step`:
+  G(x) [slot 0], G(y) [slot 1, identity loss pix2pix.py:90], D([x,y]),
+  D([x,G(x)]), the 8 loss values, the D-loss backward through both D
+  passes, the G-loss backward through D(fake) into G (both G passes), the
+  data-parallel gradient all-reduce, then Keras-Adam on G and on D.
+Both "tapes" see the same pre-update weights, as in the reference.
+
+Everything is enqueued on the current stream with pre-sized buffers and a
+pre-sized workspace, so a whole step can be captured in a HIP graph.
+"""
+import torch
+
+from . import ops
+from .nets import DiscriminatorPlan, GeneratorPlan, DROP_RATE
+
+LOSS_NAMES = ("gen_total_loss", "gen_gan_loss", "gen_l1_loss", "gen_l2_loss", "content_loss", "disc_loss",
+              "var_loss", "identity_loss")
+
+
+class AdamConfig:
+    def __init__(self, lr=2e-4, beta_1=0.5, beta_2=0.999, epsilon=1e-7):
+        self.lr, self.beta_1, self.beta_2, self.epsilon = lr, beta_1, beta_2, epsilon
+
+
+class Pix2PixTrainer:
+    def __init__(self, g_arena, g_bn, d_arena, d_bn, N, H, W, device, width=1, identity=True,
+                 loss_weights=ops.LOSS_WEIGHTS_REF, drop_rate=DROP_RATE, drop_seed=0, g_opt=None, d_opt=None,
+                 grad_sync=None):
+        self.gA, self.dA = g_arena, d_arena
+        self.N, self.H, self.W = N, H, W
+        self.identity = identity
+        self.weights = tuple(loss_weights)
+        self.drop_rate, self.drop_seed = drop_rate, drop_seed
+        self.g_opt = g_opt or AdamConfig()
+        self.d_opt = d_opt or AdamConfig()
+        self.grad_sync = grad_sync
+        self.G = GeneratorPlan(N, H, W, width, g_arena, g_bn, device, slots=2 if identity else 1, train=True)
+        self.D = DiscriminatorPlan(N, H, W, width, d_arena, d_bn, device, slots=2, train=True)
+        lshape = self.D.out_shape
+        e = lambda shape: torch.empty(shape, dtype=torch.float32, device=device)
+        self.ident = e((N, H, W, 3)) if identity else None
+        self.dident = e((N, H, W, 3)) if identity else None
+        self.dzr, self.dzf_d, self.dzf_g = e(lshape), e(lshape), e(lshape)
+        self.loss = torch.zeros(8, dtype=torch.float32, device=device)
+        ws_bytes = max(self.G.ws_bytes, self.D.ws_bytes,
+                       ops.p2p_loss_workspace_bytes(N, H, W, 3, lshape[0] * lshape[1] * lshape[2]))
+        self.ws = ops.Workspace(device)
+        self.ws.get(ws_bytes)
+
+    @property
+    def gen_output(self):
+        """G(x) of the last step: a view into the fake half of D's input."""
+        return self.D.slots[1]["inp"][..., 3:]
+
+    def step(self, x, y, apply=True):
+        """x, y: device NHWC [N,H,W,3] fp32 in [-1, 1].  Returns the 8 losses (device, no sync)."""
+        x = x if x.is_contiguous() else x.contiguous()
+        y = y if y.is_contiguous() else y.contiguous()
+        ws = self.ws
+        G, D = self.G, self.D
+        real_in, fake_in = D.slots[0]["inp"], D.slots[1]["inp"]
+        gen = fake_in[..., 3:]
+        step_dev = self.gA.iterations
+        # ---- forward (pix2pix.py:44-48 and the identity pass :90) -----------
+        ops.channel_concat(x, y, real_in)                 # concatenate([inp, tar]) (pix2pix.py:200)
+        ops.strided_copy(x, fake_in[..., :3])
+        G.forward(x, gen, slot=0, ws=ws, drop_rate=self.drop_rate, drop_seed=self.drop_seed, step_dev=step_dev)
+        if self.identity:
+            G.forward(y, self.ident, slot=1, ws=ws, drop_rate=self.drop_rate, drop_seed=self.drop_seed,
+                      step_dev=step_dev)
+        zr = D.forward(slot=0, ws=ws)
+        zf = D.forward(slot=1, ws=ws)
+        # ---- losses + their gradients (pix2pix.py:74-103) ----------------
+        dinp = D.dinp
+        ops.fill(dinp, 0.0)
+        ops.p2p_loss(gen, y, zr, zf, self.loss, ident=self.ident, weights=self.weights, dgen=dinp[..., 3:],
+                     dident=self.dident, dlogit_real_d=self.dzr, dlogit_fake_d=self.dzf_d, dlogit_fake_g=self.dzf_g,
+                     ws=ws)
+        sync = self.grad_sync
+        # ---- disc_tape.gradient (train_pix2pix.py:65) ---------------------
+        D.backward(self.dzr, slot=0, param_grads=True, beta=0.0, ws=ws)
+        D.backward(self.dzf_d, slot=1, param_grads=True, beta=1.0, ws=ws)
+        if sync:
+            sync.start("D")
+        # ---- gen_tape.gradient (train_pix2pix.py:64): through D(fake) into G
+        D.backward(self.dzf_g, slot=1, param_grads=False, input_grad=dinp, input_beta=1.0, ws=ws)
+        if self.identity:
+            G.backward(self.dident, slot=1, beta=0.0, ws=ws, drop_rate=self.drop_rate)
+        G.backward(dinp[..., 3:], slot=0, beta=1.0 if self.identity else 0.0, ws=ws, drop_rate=self.drop_rate,
+                   on_grads_ready=(sync.ready_G if sync else None))
+        if sync:
+            sync.finish()
+        # ---- apply_gradients (train_pix2pix.py:68-69) ----------------------
+        if apply:
+            scale = sync.grad_scale if sync else 1.0
+            for A, o in ((self.gA, self.g_opt), (self.dA, self.d_opt)):
+                ops.adam(A.data, A.grad, A.m, A.v, o.lr, o.beta_1, o.beta_2, o.epsilon, A.iterations,
+                         grad_scale=scale)
+                ops.counter_add(A.iterations, 1)
+        return self.loss

@@ -143,7 +143,7 @@ def synthetic_pair(batch, size, seed=0):
     zc = zr[:, :, i0, :] * (1 - fr)[None, None, :, None] + zr[:, :, i0 + 1, :] * fr[None, None, :, None]
     y = np.tanh(2.0 * zc)
     x = np.clip(y + 0.1 * rng.standard_normal(y.shape), -1.0, 1.0)
-    return x.astype(np.float32), y.astype(np.float32)
+    return np.ascontiguousarray(x, dtype=np.float32), np.ascontiguousarray(y, dtype=np.float32)
 
 
 # ---------------------------------------------------------------------------

@@ -1,0 +1,157 @@
+"""End-to-end parity of the fused pix2pix training step (train_pix2pix.py:33-71)
+on the HIP path against the float64 CPU oracle (oracle/p2p_oracle.py), on the
+same seeded weights and synthetic noisy/clean 256x256 pairs.
+
+Tolerances (BASELINE.json north_star): |dPSNR| < 0.01 dB on the generator
+output, max-abs gradient difference < 1e-4 for every G and D variable; loss
+values to 1e-5 relative; BN moving statistics to 1e-5.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import p2p_oracle as O
+
+gpu = pytest.mark.gpu
+
+
+class Args:
+    def __init__(self, **kw):
+        self.crop_size = 256
+        self.retrain = 0
+        self.__dict__.update(kw)
+
+
+def psnr(img, ref):
+    a = (np.asarray(img, np.float64) + 1) / 2
+    b = (np.asarray(ref, np.float64) + 1) / 2
+    mse = np.mean((a - b) ** 2)
+    return 10 * math.log10(1.0 / mse)
+
+
+def _compare_grads(arena, ref, label, tol=1e-4):
+    worst = (0.0, None, 0.0)
+    for name, g_ref in ref.items():
+        g = arena.grad_of(name).detach().double().cpu().numpy()
+        err = float(np.abs(g - g_ref).max())
+        rel = err / (float(np.abs(g_ref).max()) + 1e-30)
+        if err > worst[0]:
+            worst = (err, name, rel)
+        assert err < tol, f"{label} {name}: max-abs grad diff {err:.3e} (rel {rel:.3e})"
+    return worst
+
+
+def _run_parity(width, batch, drop_rate, seed=42, drop_seed=5, identity=True):
+    from pix2pix import Pix2Pix
+    st = O.P2PState(width=width, seed=seed, drop_rate=drop_rate, drop_seed=drop_seed, identity=identity)
+    x, y = O.synthetic_pair(batch, 256, seed=9)
+    ref = O.train_step(st, x, y, return_grads=True, apply=False)
+
+    m = Pix2Pix(Args(width=width, seed=seed, dropout_seed=drop_seed, dropout_rate=drop_rate,
+                     identity_loss=int(identity)))
+    tr = m.trainer(x.shape)
+    xd = torch.from_numpy(x).cuda()
+    yd = torch.from_numpy(y).cuda()
+    loss = tr.step(xd, yd, apply=False)
+    torch.cuda.synchronize()
+    got = loss.cpu().double().numpy()
+    want = np.array(ref["losses"], np.float64)
+    assert np.allclose(got, want, rtol=1e-5, atol=1e-7), (got, want)
+
+    gen = tr.gen_output.cpu().numpy()
+    dpsnr = abs(psnr(gen, y) - psnr(ref["gen"], y))
+    assert dpsnr < 0.01, f"PSNR delta {dpsnr:.5f} dB"
+    assert np.abs(gen - ref["gen"]).max() < 1e-4
+
+    wg = _compare_grads(m.generator.arena, ref["gG"], "G")
+    wd = _compare_grads(m.discriminator.arena, ref["gD"], "D")
+    # moving statistics after the step's BN calls (G(x), G(y), D real, D fake)
+    bn_g = m.generator.bn.export()
+    for k, v in st.Gs.items():
+        assert np.allclose(bn_g[k], v, rtol=1e-4, atol=1e-5), k
+    bn_d = m.discriminator.bn.export()
+    for k, v in st.Ds.items():
+        assert np.allclose(bn_d[k], v, rtol=1e-4, atol=1e-5), k
+    return dict(dpsnr=dpsnr, worst_g=wg, worst_d=wd)
+
+
+@gpu
+def test_step_parity_full_width_bs2_dropout():
+    r = _run_parity(width=1, batch=2, drop_rate=0.5)
+    print("full-width parity:", r)
+
+
+@gpu
+def test_step_parity_tiny_width_no_identity():
+    _run_parity(width=16, batch=2, drop_rate=0.0, identity=False)
+
+
+@gpu
+def test_step_parity_tiny_width_bs3():
+    _run_parity(width=8, batch=3, drop_rate=0.5)
+
+
+@gpu
+def test_adam_kernel_matches_keras_adam():
+    """dg_adam on identical (p, g, m, v, t) inputs vs the oracle's TF ApplyAdam restatement."""
+    from dgan import ops
+    rng = np.random.default_rng(0)
+    n = 100003  # odd size: exercises the float4 bulk and the scalar tail
+    p = rng.standard_normal(n).astype(np.float32)
+    g = (rng.standard_normal(n) * np.exp(rng.uniform(-20, 0, n))).astype(np.float32)
+    m = (rng.standard_normal(n) * 1e-3).astype(np.float32)
+    v = (rng.uniform(0, 1e-5, n)).astype(np.float32)
+    t = 7
+    dp, dg, dm, dv = (torch.from_numpy(a.copy()).cuda() for a in (p, g, m, v))
+    it = torch.tensor([t - 1], dtype=torch.int32, device="cuda")
+    ops.adam(dp, dg, dm, dv, 2e-4, 0.5, 0.999, 1e-7, it)
+    rp, rm, rv = O.adam_update(p, g.astype(np.float64), m, v, t)
+    torch.cuda.synchronize()
+    assert np.allclose(dm.cpu().numpy(), rm, rtol=1e-5, atol=1e-9)  # fp32 rounding of (g - m)
+    assert np.allclose(dv.cpu().numpy(), rv, rtol=1e-5, atol=1e-12)
+    assert np.abs(dp.cpu().numpy().astype(np.float64) - rp).max() < 2e-7
+
+
+@gpu
+def test_two_steps_with_adam_track_oracle():
+    """Two full steps incl. Keras-Adam.  Step-2 losses match to 1e-4; parameters
+    stay within Adam's per-step bound (|dp| <= lr per step) of the oracle, and
+    almost all of them far closer.  (fp32-vs-fp64 gradient differences of
+    ~1e-4 relative on near-cancelling first-layer sums are amplified by Adam's
+    sign-like normalisation, so parameters are not compared at 1e-6.)"""
+    from pix2pix import Pix2Pix
+    width, seed = 4, 17
+    st = O.P2PState(width=width, seed=seed, drop_rate=0.5, drop_seed=3)
+    m = Pix2Pix(Args(width=width, seed=seed, dropout_seed=3))
+    for k in range(2):
+        x, y = O.synthetic_pair(2, 256, seed=100 + k)
+        ref = O.train_step(st, x, y)
+        loss = m.trainer(x.shape).step(torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda())
+        torch.cuda.synchronize()
+        assert np.allclose(loss.cpu().numpy(), np.array(ref["losses"]), rtol=1e-4, atol=1e-6)
+    assert int(m.generator.arena.iterations.item()) == 2
+    for net, refp in ((m.generator, st.G), (m.discriminator, st.D)):
+        got = net.arena.export()
+        for k, v in refp.items():
+            d = np.abs(got[k].astype(np.float64) - v.astype(np.float64))
+            assert d.max() <= 2 * 2e-4 + 1e-6, (k, d.max())
+            assert np.median(d) < 2e-6, (k, np.median(d))
+
+
+@gpu
+def test_generator_inference_uses_moving_stats():
+    """G(x, training=False) (infer.py:55) vs the oracle run on the GPU's own
+    post-step weights and moving statistics."""
+    from pix2pix import Pix2Pix
+    width = 8
+    m = Pix2Pix(Args(width=width, seed=5))
+    x, y = O.synthetic_pair(2, 256, seed=1)
+    m.trainer(x.shape).step(torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda())
+    got = m.generator(x, training=False)
+    torch.cuda.synchronize()
+    params = m.generator.arena.export()
+    states = m.generator.bn.export()
+    ref, _ = O.generator_forward(params, x, width, training=False, states=states)
+    assert np.abs(got.cpu().numpy() - ref).max() < 1e-5
