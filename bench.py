@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Throughput of the pix2pix training step on MI355X (BASELINE.json metric:
+training images/sec, pix2pix 256x256 bs16 per GPU, 1/2/4/8 GPUs).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+One step = the reference's train_step (train_pix2pix.py:33-71) on 16 synthetic
+256x256 noisy/clean pairs per GPU already resident in HBM: G(x), the identity
+pass G(y), D real + fake, L1/L2/TV/GAN/identity losses, both gradients, the
+data-parallel gradient all-reduce (N>1) and Keras-Adam on G and D.  The VGG19
+content term is 0 (ImageNet weights unavailable offline).  fp32 throughout.
+
+Prints ONE JSON line (rank 0).  Extra fields:
+  roofline      conv engine (the dominant kernels): algorithmic conv FLOPs of
+                one step / summed conv launch time measured with HIP events on
+                the launching stream, vs the gfx950 fp32 MFMA peak 157.3 TF/s
+  cpu_baseline  the CPU restatement of the same graph (oracle/torch_p2p.py,
+                torch fp32 autograd) timed on this box's host cores, rank 0,
+                N=1 only, bounded sample
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "denoise-gan_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+FP32_MFMA_PEAK = 157.3e12  # gfx950 dense fp32 (MI355X_MICROARCH.md)
+
+
+class Args:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+def synthetic_batch(n, size, seed):
+    from dataloader import synthetic_pair
+    return synthetic_pair(n, size, seed)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=16, help="images per GPU")
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a captured HIP graph")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-identity", action="store_true")
+    ap.add_argument("--profile-only", action="store_true", help="skip roofline/cpu legs (for rocprofv3 runs)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    distributed = world > 1
+    if distributed:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    import dgan
+    dgan.build()  # no-op when the in-tree library is current
+    from pix2pix import Pix2Pix
+    from dgan import ops
+
+    model = Pix2Pix(Args(crop_size=args.size, retrain=0, width=1, seed=1234, dropout_seed=rank,
+                         identity_loss=0 if args.no_identity else 1))
+    if distributed:
+        from dgan.dist import setup_data_parallel
+        setup_data_parallel(model)
+    x_np, y_np = synthetic_batch(args.batch, args.size, seed=1000 + rank)
+    x = torch.from_numpy(x_np).to(dev)
+    y = torch.from_numpy(y_np).to(dev)
+    trainer = model.trainer(x.shape)
+
+    # ---- warmup (also plans/JIT-free: everything is prebuilt) ------------
+    for _ in range(max(1, args.warmup // 2)):
+        trainer.step(x, y)
+    torch.cuda.synchronize()
+
+    graph = None
+    use_graph = not args.no_graph and not distributed
+    if use_graph:
+        try:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                trainer.step(x, y)
+            torch.cuda.current_stream().wait_stream(s)
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                trainer.step(x, y)
+            torch.cuda.synchronize()
+        except Exception as e:  # report, fall back to eager launches
+            print(f"[bench] graph capture failed ({e}); eager launches", file=sys.stderr)
+            graph = None
+
+    def step():
+        if graph is not None:
+            graph.replay()
+        else:
+            trainer.step(x, y)
+
+    for _ in range(args.warmup - max(1, args.warmup // 2)):
+        step()
+    torch.cuda.synchronize()
+
+    # ---- timed region ------------------------------------------------------
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if distributed:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    losses = trainer.loss.cpu().numpy()
+    ms_per_step = elapsed / args.steps * 1e3
+    images = world * args.batch * args.steps
+    value = images / elapsed
+
+    # ---- roofline of the conv engine (HIP events, eager pass) ---------------
+    roofline = None
+    step_flops = None
+    if not args.profile_only:
+        with ops.ConvProfile() as prof:
+            trainer.step(x, y)
+        torch.cuda.synchronize()
+        recs = prof.summary()
+        conv_flops = sum(r["flops"] for r in recs)
+        conv_ms = sum(r["ms"] for r in recs)
+        step_flops = conv_flops
+        achieved = conv_flops / (conv_ms * 1e-3)
+        roofline = {"bound": "mfma", "achieved": round(achieved / 1e12, 2), "peak": FP32_MFMA_PEAK / 1e12,
+                    "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK, 4), "traffic": None,
+                    "kernel": "dg conv engine (k_conv_gemm + narrow + split-K reduce), all conv launches of one step",
+                    "conv_launch_ms_per_step": round(conv_ms, 3), "conv_gflop_per_step": round(conv_flops / 1e9, 1),
+                    "step_frac": round(conv_flops / (ms_per_step * 1e-3) / FP32_MFMA_PEAK, 4)}
+        if rank == 0 and os.environ.get("DG_BENCH_DETAIL"):
+            for r in sorted(recs, key=lambda r: -r["ms"])[:40]:
+                print(json.dumps({**r, "tflops": r["flops"] / (r["ms"] * 1e-3) / 1e12}), file=sys.stderr)
+
+    # ---- CPU baseline: torch fp32 restatement, rank 0, N=1 only -------------
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_only:
+        cpu = cpu_baseline(args.size, args.cpu_seconds, identity=not args.no_identity)
+
+    if rank == 0:
+        out = {
+            "metric": "training images/sec, pix2pix 256x256 bs16/GPU",
+            "value": round(value, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic (seeded noisy/clean 256x256 pairs resident in HBM; random-init weights)",
+            "config": {"workload": "pix2pix train_step (train_pix2pix.py:33-71): G(x)+G(y) identity pass, D real+fake, "
+                                   "GAN/L1/L2/TV/identity losses, D and G gradients, Keras Adam G and D; "
+                                   "VGG content term 0 (no ImageNet weights offline)",
+                       "model": "pix2pix U-Net G (54.4M) + PatchGAN D (2.77M)",
+                       "global_batch": world * args.batch, "batch_per_gpu": args.batch, "image_size": args.size,
+                       "parallelism": f"dp{world}", "hip_graph": graph is not None,
+                       "identity_pass": not args.no_identity,
+                       "conv_gflop_per_image": round(step_flops / args.batch / 1e9, 2) if step_flops else None},
+            "losses": [round(float(v), 6) for v in losses],
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if distributed:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(size, seconds, identity=True):
+    """The oracle's torch-fp32 restatement of the same step on the host cores."""
+    from oracle import torch_p2p as T
+    from oracle import p2p_oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    torch.set_num_threads(threads)
+    bs = 2
+    G = O.init_variables(O.g_variables(1), 1234)
+    D = O.init_variables(O.d_variables(1), 1235)
+    step = T.make_fp32_step(G, D)
+    x, y = O.synthetic_pair(bs, size, seed=7)
+    step(x, y)  # warm-up
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        step(x, y)
+        n += 1
+        if time.perf_counter() - t0 > seconds or n >= 20:
+            break
+    el = time.perf_counter() - t0
+    return {"value": round(n * bs / el, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} steps x {bs} images at {size}x{size}, torch fp32 CPU autograd restatement "
+                      f"(oracle/torch_p2p.py) incl. identity pass and Keras-Adam; {el:.1f}s"}
+
+
+if __name__ == "__main__":
+    main()

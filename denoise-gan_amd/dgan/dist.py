@@ -1,0 +1,71 @@
+"""Data-parallel gradient exchange for the pix2pix step (one process per GPU).
+
+The reference is single-GPU (train_pix2pix.py:15 pins CUDA_VISIBLE_DEVICES);
+BASELINE.json's north star adds batch data parallelism: each rank runs the
+full step on its own 16 images, then the fp32 gradient arenas are summed
+with RCCL (torch.distributed backend "nccl" on ROCm) over xGMI and Adam
+applies them scaled by 1/world (ops.adam grad_scale) on every rank, so the
+replicas stay bit-identical without any parameter broadcast.  BN statistics
+stay per replica (local batch), as tf.distribute would do.
+
+Overlap: D's gradients are final after the two D backwards and go out at
+once (they travel while G's backward runs); G's arena is laid out in
+backward-completion order (nets.g_layout_order), so a bucket is issued as
+soon as the last layer inside it has its gradient enqueued.  The
+collectives run on RCCL's own stream; `finish()` makes the compute stream
+wait for them before Adam.
+"""
+import torch
+import torch.distributed as dist
+
+
+class GradSync:
+    def __init__(self, g_arena, d_arena, bucket_bytes=64 << 20, group=None):
+        self.g, self.d = g_arena, d_arena
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.grad_scale = 1.0 / self.world
+        self.bucket = max(1, bucket_bytes // 4)
+        self.works = []
+        self.issued = 0
+        # arena end offset of every layer's last variable, in layout order
+        self.layer_end = {}
+        for name in g_arena.layout:
+            layer = name.split("/")[0]
+            self.layer_end[layer] = max(self.layer_end.get(layer, 0), g_arena.end_offset(name))
+
+    def _reduce(self, t):
+        self.works.append(dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+
+    def start(self, which):
+        if which == "D":
+            self._reduce(self.d.grad)
+
+    def ready_G(self, layer):
+        end = self.layer_end[layer]
+        if end - self.issued >= self.bucket:
+            self._reduce(self.g.grad[self.issued:end])
+            self.issued = end
+
+    def finish(self):
+        if self.issued < self.g.numel:
+            self._reduce(self.g.grad[self.issued:])
+        for w in self.works:
+            w.wait()
+        self.works.clear()
+        self.issued = 0
+
+
+def broadcast_parameters(model, src=0, group=None):
+    """Make every rank start from rank src's weights (seeded init already agrees;
+    this also covers restored checkpoints)."""
+    for net in (model.generator, model.discriminator):
+        dist.broadcast(net.arena.data, src, group=group)
+        for t in net.non_trainable_variables:
+            dist.broadcast(t, src, group=group)
+
+
+def setup_data_parallel(model, bucket_bytes=64 << 20):
+    model.grad_sync = GradSync(model.generator.arena, model.discriminator.arena, bucket_bytes)
+    broadcast_parameters(model)
+    return model.grad_sync

@@ -162,23 +162,83 @@ class ConvDesc:
         buf, n = ws.get(self.ws[op])
         return (_p(buf), n)
 
+    @property
+    def flops(self):
+        """Algorithmic FLOPs of one fwd / bwd_data / bwd_filter call (2 * MACs of the dense conv)."""
+        if self.transpose:
+            return 2 * self.N * self.H * self.W * self.Cin * self.kh * self.kw * self.Cout
+        return 2 * self.N * self.Ho * self.Wo * self.Cout * self.kh * self.kw * self.Cin
+
     def fwd(self, x, w, y, bias=None, act="none", alpha=0.3, beta=0.0, ws=None):
         wp, wn = self._ws(OP_FWD, ws)
+        ev = _prof_begin()
         call("dg_conv_fwd", self._h, _p(x), pix_ld(x, self.Cin), _p(w), _p(bias), _p(y), pix_ld(y, self.Cout),
              float(beta), act_id(act), float(alpha), wp, wn, _stream())
+        _prof_end(ev, self, "fwd")
         return y
 
     def bwd_data(self, dy, w, dx, beta=0.0, ws=None):
         wp, wn = self._ws(OP_BWD_DATA, ws)
+        ev = _prof_begin()
         call("dg_conv_bwd_data", self._h, _p(dy), pix_ld(dy, self.Cout), _p(w), _p(dx), pix_ld(dx, self.Cin),
              float(beta), wp, wn, _stream())
+        _prof_end(ev, self, "bwd_data")
         return dx
 
     def bwd_filter(self, x, dy, dw, dbias=None, beta=0.0, ws=None):
         wp, wn = self._ws(OP_BWD_FILTER, ws)
+        ev = _prof_begin()
         call("dg_conv_bwd_filter", self._h, _p(x), pix_ld(x, self.Cin), _p(dy), pix_ld(dy, self.Cout), _p(dw),
              _p(dbias), float(beta), wp, wn, _stream())
+        _prof_end(ev, self, "bwd_filter")
         return dw
+
+
+# ---------------------------------------------------------------------------
+# optional per-conv timing with HIP events on the launching stream (bench.py
+# roofline leg); off unless a ConvProfile is active
+# ---------------------------------------------------------------------------
+_PROF = None
+
+
+class ConvProfile:
+    """Records (HIP start event, end event, desc, op) around every conv call."""
+
+    def __init__(self):
+        self.records = []
+
+    def __enter__(self):
+        global _PROF
+        self._prev, _PROF = _PROF, self
+        return self
+
+    def __exit__(self, *a):
+        global _PROF
+        _PROF = self._prev
+
+    def summary(self):
+        """-> list of dicts (op, shape, flops, ms); call after synchronising."""
+        out = []
+        for e0, e1, d, op in self.records:
+            out.append(dict(op=op, transpose=d.transpose, shape=(d.N, d.H, d.W, d.Cin, d.Cout, d.kh, d.sh),
+                            flops=d.flops, ms=e0.elapsed_time(e1)))
+        return out
+
+
+def _prof_begin():
+    if _PROF is None:
+        return None
+    e = torch.cuda.Event(enable_timing=True)
+    e.record(torch.cuda.current_stream())
+    return e
+
+
+def _prof_end(e0, desc, op):
+    if e0 is None:
+        return
+    e1 = torch.cuda.Event(enable_timing=True)
+    e1.record(torch.cuda.current_stream())
+    _PROF.records.append((e0, e1, desc, op))
 
 
 def bn_workspace_bytes(M, C):

@@ -29,7 +29,7 @@ def _conv(x, w_hwio, s, pad):
     """NCHW activations, HWIO kernel; pad = 'same' or explicit (t,b,l,r)."""
     k = w_hwio.shape[0]
     xp = _pad_same(x, k, s) if pad == "same" else F.pad(x, (pad[2], pad[3], pad[0], pad[1]))
-    return F.conv2d(xp, w_hwio.permute(3, 2, 0, 1), stride=s)
+    return F.conv2d(xp, w_hwio.permute(3, 2, 0, 1).contiguous(), stride=s)
 
 
 def _convT(x, w_kkfc, s):
@@ -37,7 +37,7 @@ def _convT(x, w_kkfc, s):
     H, W = x.shape[2:]
     Ho, (pt, _) = O.convT_pads(H, w_kkfc.shape[0], s)
     Wo, (pl, _) = O.convT_pads(W, w_kkfc.shape[1], s)
-    y = F.conv_transpose2d(x, w_kkfc.permute(3, 2, 0, 1), stride=s)
+    y = F.conv_transpose2d(x, w_kkfc.permute(3, 2, 0, 1).contiguous(), stride=s)
     return y[:, :, pt:pt + Ho, pl:pl + Wo]
 
 
