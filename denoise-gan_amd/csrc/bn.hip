@@ -24,8 +24,10 @@ struct BnPlan {
 static BnPlan bn_plan(long M, int C) {
     BnPlan p;
     p.cg = (C + 63) / 64;
-    long r = std::max<long>(1, 1024 / p.cg);
-    r = std::min<long>(r, std::max<long>(1, (M + 15) / 16));
+    // ~512 blocks in the partial pass, >= 64 rows each; the finalize combines
+    // R partials per channel with 4 lanes, so R stays small
+    long r = std::max<long>(1, 512 / p.cg);
+    r = std::min<long>(r, std::max<long>(1, (M + 63) / 64));
     p.rows = (M + r - 1) / r;
     p.R = (int)((M + p.rows - 1) / p.rows);
     return p;
@@ -83,15 +85,40 @@ k_bn_stats_partial(const float *__restrict__ y, int ld, long M, int C, long rows
     }
 }
 
+// finalize: block = 64 channels x 4 lanes; two parallel passes over the R
+// chunk partials (Chan's combine written as sums: mean = sum n_i mean_i / n,
+// M2 = sum M2_i + n_i (mean_i - mean)^2), no serial merge chain
 __global__ void __launch_bounds__(256)
 k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, int C, const float *gamma,
                  const float *beta, float *save_mean, float *save_invstd, float *mm, float *mv, float momentum,
                  float eps, float *scale, float *shift) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    float n = 0.f, mu = 0.f, q = 0.f;
-    for (int r = 0; r < R; ++r) chan_merge(n, mu, q, pn[(long)r * C + c], pmean[(long)r * C + c], pm2[(long)r * C + c]);
-    const float var = n > 0.f ? q / n : 0.f;
+    __shared__ float s0[256], s1[256];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int l4 = threadIdx.x >> 6;
+    const int c64 = threadIdx.x & 63;
+    float sn = 0.f, sm = 0.f;
+    if (c < C)
+        for (int r = l4; r < R; r += 4) {
+            const float n = pn[(long)r * C + c];
+            sn += n;
+            sm += n * pmean[(long)r * C + c];
+        }
+    s0[threadIdx.x] = sn; s1[threadIdx.x] = sm;
+    __syncthreads();
+    const float n = s0[c64] + s0[c64 + 64] + s0[c64 + 128] + s0[c64 + 192];
+    const float mu = n > 0.f ? (s1[c64] + s1[c64 + 64] + s1[c64 + 128] + s1[c64 + 192]) / n : 0.f;
+    __syncthreads();
+    float q = 0.f;
+    if (c < C)
+        for (int r = l4; r < R; r += 4) {
+            const float d = pmean[(long)r * C + c] - mu;
+            q += pm2[(long)r * C + c] + pn[(long)r * C + c] * d * d;
+        }
+    s0[threadIdx.x] = q;
+    __syncthreads();
+    if (l4 != 0 || c >= C) return;
+    const float m2 = s0[c64] + s0[c64 + 64] + s0[c64 + 128] + s0[c64 + 192];
+    const float var = n > 0.f ? m2 / n : 0.f;
     const float inv = 1.f / sqrtf(var + eps);
     if (save_mean) save_mean[c] = mu;
     if (save_invstd) save_invstd[c] = inv;
@@ -101,7 +128,7 @@ k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, i
     shift[c] = b - mu * g * inv;
     if (mm) mm[c] -= (mm[c] - mu) * (1.f - momentum);
     if (mv) {
-        const float unb = n > 1.f ? q / (n - 1.f) : q;
+        const float unb = n > 1.f ? m2 / (n - 1.f) : m2;
         mv[c] -= (mv[c] - unb) * (1.f - momentum);
     }
 }
@@ -191,10 +218,18 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
 __global__ void __launch_bounds__(256)
 k_bn_bwd_final(const float *p1, const float *p2, int R, int C, long M, const float *gamma, const float *invstd,
                float *dgamma, float *dbeta, float beta, float *coef) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
+    __shared__ float s0[256], s1[256];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int l4 = threadIdx.x >> 6;
+    const int c64 = threadIdx.x & 63;
     float a1 = 0.f, a2 = 0.f;
-    for (int r = 0; r < R; ++r) { a1 += p1[(long)r * C + c]; a2 += p2[(long)r * C + c]; }
+    if (c < C)
+        for (int r = l4; r < R; r += 4) { a1 += p1[(long)r * C + c]; a2 += p2[(long)r * C + c]; }
+    s0[threadIdx.x] = a1; s1[threadIdx.x] = a2;
+    __syncthreads();
+    if (l4 != 0 || c >= C) return;
+    a1 = s0[c64] + s0[c64 + 64] + s0[c64 + 128] + s0[c64 + 192];
+    a2 = s1[c64] + s1[c64 + 64] + s1[c64 + 128] + s1[c64 + 192];
     if (dbeta) dbeta[c] = a1 + (beta != 0.f ? beta * dbeta[c] : 0.f);
     if (dgamma) dgamma[c] = a2 + (beta != 0.f ? beta * dgamma[c] : 0.f);
     const float g = gamma ? gamma[c] : 1.f;
@@ -257,7 +292,7 @@ int dg_bn_fwd_train(int M, int C, const float *y, int ldy, const float *gamma, c
     hipLaunchKernelGGL(dg::k_bn_stats_partial, dim3(bp.cg, bp.R), dim3(256), 0, s, y, ldy, (long)M, C, bp.rows, pn,
                        pmean, pm2);
     DG_LAUNCHED("bn_stats_partial");
-    hipLaunchKernelGGL(dg::k_bn_stats_final, dim3(dg_cdiv(C, 256)), dim3(256), 0, s, pn, pmean, pm2, bp.R, C, gamma,
+    hipLaunchKernelGGL(dg::k_bn_stats_final, dim3(bp.cg), dim3(256), 0, s, pn, pmean, pm2, bp.R, C, gamma,
                        beta, save_mean, save_invstd, moving_mean, moving_var, momentum, eps, scale, shift);
     DG_LAUNCHED("bn_stats_final");
     bool vec = (C % 4 == 0) && (ldy % 4 == 0) && (ldz % 4 == 0) && ((((uintptr_t)y) | ((uintptr_t)z)) & 15) == 0;
@@ -301,7 +336,7 @@ int dg_bn_bwd(int M, int C, const float *dz, int lddz, const float *z, int ldz, 
     hipLaunchKernelGGL(dg::k_bn_bwd_partial, dim3(bp.cg, bp.R), dim3(256), 0, s, dz, lddz, z, ldz, y, ldy, (long)M, C,
                        bp.rows, save_mean, save_invstd, act, alpha, dscale, p1, p2);
     DG_LAUNCHED("bn_bwd_partial");
-    hipLaunchKernelGGL(dg::k_bn_bwd_final, dim3(dg_cdiv(C, 256)), dim3(256), 0, s, p1, p2, bp.R, C, (long)M, gamma,
+    hipLaunchKernelGGL(dg::k_bn_bwd_final, dim3(bp.cg), dim3(256), 0, s, p1, p2, bp.R, C, (long)M, gamma,
                        save_invstd, dgamma, dbeta, beta, coef);
     DG_LAUNCHED("bn_bwd_final");
     hipLaunchKernelGGL(dg::k_bn_bwd_apply, dim3(dg::ew_grid((long)M * C)), dim3(256), 0, s, dz, lddz, z, ldz, y, ldy,

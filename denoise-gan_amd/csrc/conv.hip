@@ -645,6 +645,98 @@ __global__ void k_colsum_final(const float *partial, int nblk, int C, float *out
     out[c] = s + (beta != 0.f ? beta * out[c] : 0.f);
 }
 
+// ---- recast helpers (see Recast) -------------------------------------------
+__global__ void __launch_bounds__(256)
+k_transpose(const float *__restrict__ src, int R, int Cc, float *__restrict__ dst) {
+    // dst[c][r] = src[r][c]
+    const long total = (long)R * Cc;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        int c = (int)(e / R);
+        int r = (int)(e - (long)c * R);
+        dst[e] = src[(long)r * Cc + c];
+    }
+}
+
+// y[m] = sum over taps of V[input pixel of tap][tap] (+bias, act, beta)   (FWD, Co == 1)
+__global__ void __launch_bounds__(256)
+k_recast_fwd_gather(const GemmArgs p, const float *__restrict__ V, int nv) {
+    const ConvGeom &g = p.g;
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= g.N * g.Ho * g.Wo) return;
+    int wo = m % g.Wo; int t = m / g.Wo; int ho = t % g.Ho; int n = t / g.Ho;
+    float v = 0.f;
+    for (int i = 0; i < g.kh; ++i) {
+        int hi = ho * g.sh - g.pt + i;
+        if (hi < 0 || hi >= g.H) continue;
+        for (int j = 0; j < g.kw; ++j) {
+            int wi = wo * g.sw - g.pl + j;
+            if (wi < 0 || wi >= g.W) continue;
+            v += V[((long)(n * g.H + hi) * g.W + wi) * nv + i * g.kw + j];
+        }
+    }
+    if (p.bias) v += p.bias[0];
+    v = act_fwd(v, p.act, p.alpha);
+    long off = (long)m * p.ldc;
+    if (p.beta != 0.f) v += p.beta * p.C[off];
+    p.C[off] = v;
+}
+
+// dx[n,h,w,ci] = sum over taps hitting (h,w) of V[(n,ho,wo)][(i,j,ci)]   (DGRAD col2im)
+__global__ void __launch_bounds__(256)
+k_recast_col2im(const GemmArgs p, const float *__restrict__ V, int nv) {
+    const ConvGeom &g = p.g;
+    const long total = (long)g.N * g.H * g.W * g.Ci;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const int ci = (int)(e % g.Ci);
+        const long pix = e / g.Ci;
+        const int w = (int)(pix % g.W);
+        const int h = (int)((pix / g.W) % g.H);
+        const int n = (int)(pix / ((long)g.W * g.H));
+        float v = 0.f;
+        for (int i = 0; i < g.kh; ++i) {
+            int th = h + g.pt - i;
+            if (th < 0 || th % g.sh) continue;
+            int ho = th / g.sh;
+            if (ho >= g.Ho) continue;
+            for (int j = 0; j < g.kw; ++j) {
+                int tw = w + g.pl - j;
+                if (tw < 0 || tw % g.sw) continue;
+                int wo = tw / g.sw;
+                if (wo >= g.Wo) continue;
+                v += V[((long)(n * g.Ho + ho) * g.Wo + wo) * nv + (i * g.kw + j) * g.Ci + ci];
+            }
+        }
+        if (p.bias) v += p.bias[ci];
+        v = act_fwd(v, p.act, p.alpha);
+        long off = pix * p.ldc + ci;
+        if (p.beta != 0.f) v += p.beta * p.C[off];
+        p.C[off] = v;
+    }
+}
+
+// G[p_in][(i,j)] = dy[output pixel that reads p_in through tap (i,j)] or 0   (WGRAD, Co == 1)
+__global__ void __launch_bounds__(256)
+k_recast_wgrad_gather(const GemmArgs p, const float *__restrict__ dy, int lddy, float *__restrict__ G) {
+    const ConvGeom &g = p.g;
+    const int nt = g.kh * g.kw;
+    const long total = (long)g.N * g.H * g.W * nt;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const int tap = (int)(e % nt);
+        const long pix = e / nt;
+        const int w = (int)(pix % g.W);
+        const int h = (int)((pix / g.W) % g.H);
+        const int n = (int)(pix / ((long)g.W * g.H));
+        const int i = tap / g.kw, j = tap - (tap / g.kw) * g.kw;
+        float v = 0.f;
+        int th = h + g.pt - i, tw = w + g.pl - j;
+        if (th >= 0 && tw >= 0 && th % g.sh == 0 && tw % g.sw == 0) {
+            int ho = th / g.sh, wo = tw / g.sw;
+            if (ho < g.Ho && wo < g.Wo) v = dy[((long)(n * g.Ho + ho) * g.Wo + wo) * lddy];
+        }
+        G[e] = v;
+    }
+}
+
 // -------------------------------------------------------------------------
 // Host side: descriptor, planner, launch
 // -------------------------------------------------------------------------
@@ -665,6 +757,20 @@ struct OpPlan {
     int mtiles, ntiles;
     size_t slab_bytes;  // split-K partial slabs
     size_t ws_bytes;    // total workspace of the layer op (slabs + bias partials)
+    size_t colsum_off;  // bwd_filter: offset of the bias column-sum partials
+};
+
+// A narrow op (GEMM N <= 8) recast as a 1x1-geometry MFMA GEMM plus a gather:
+//   FWD,   Co == 1 : V[p_in][(i,j)]      = x[p_in][:] . w[(i,j)][:]   ; y = shift-and-add of V
+//   DGRAD, Ci <= 8 : V[p_out][(i,j,ci)]  = dy[p_out][:] . w[(i,j,ci)][:] ; dx = col2im(V)
+//   WGRAD, Co == 1 : dw[(i,j)][ci]       = sum_p G[p][(i,j)] x[p][ci], G = dy gathered per tap
+struct Recast {
+    int on;
+    int mode1;          // engine mode of the 1x1 GEMM
+    ConvGeom g1;        // its geometry (N=1, H=1, W=pixels)
+    OpPlan p1;          // its plan
+    int nv;             // columns of V / G
+    size_t wt_off, v_off, slab_off, bytes;
 };
 
 }  // namespace dg
@@ -674,6 +780,7 @@ struct dg_conv_desc_s {
     int N, H, W, Cin, Cout, Ho, Wo;  // layer view
     dg::ConvGeom g;                  // conv view
     dg::OpPlan plan[3];              // indexed by DG_OP_*
+    dg::Recast rc[3];
 };
 
 namespace dg {
@@ -750,6 +857,57 @@ static OpPlan make_plan(const ConvGeom &g, int mode) {
     return pl;
 }
 
+static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static ConvGeom geom_1x1(long pixels, int ci, int co) {
+    ConvGeom q{};
+    q.N = 1; q.H = 1; q.W = (int)pixels; q.Ci = ci; q.Ho = 1; q.Wo = (int)pixels; q.Co = co;
+    q.kh = q.kw = q.sh = q.sw = 1; q.pt = q.pl = 0; q.Th = q.Tw = 1;
+    return q;
+}
+
+// decide whether a narrow op runs as a recast 1x1 MFMA GEMM (+ gather), and size its workspace
+static void plan_recast(dg_conv_desc_s *d, int op) {
+    Recast &rc = d->rc[op];
+    rc = Recast{};
+    if (!d->plan[op].narrow) return;
+    const ConvGeom &g = d->g;
+    const int mode = engine_mode(d, op);
+    const int ntap = g.kh * g.kw;
+    if (mode == MODE_FWD) {
+        if (g.Co != 1 || g.Ci % 32 || ntap % 4 || ntap < 8) return;
+        long P = (long)g.N * g.H * g.W;
+        rc.nv = ntap; rc.mode1 = MODE_FWD;
+        rc.g1 = geom_1x1(P, g.Ci, ntap);
+        rc.p1 = make_plan(rc.g1, MODE_FWD);
+        rc.wt_off = 0;
+        rc.v_off = al256((size_t)g.Ci * ntap * 4);
+        rc.slab_off = al256(rc.v_off + (size_t)P * ntap * 4);
+    } else if (mode == MODE_DGRAD) {
+        const int nv = ntap * g.Ci;
+        if (g.Co % 32 || nv % 4 || nv < 8) return;
+        long P = (long)g.N * g.Ho * g.Wo;
+        rc.nv = nv; rc.mode1 = MODE_FWD;
+        rc.g1 = geom_1x1(P, g.Co, nv);
+        rc.p1 = make_plan(rc.g1, MODE_FWD);
+        rc.wt_off = 0;
+        rc.v_off = al256((size_t)g.Co * nv * 4);
+        rc.slab_off = al256(rc.v_off + (size_t)P * nv * 4);
+    } else {
+        if (g.Co != 1 || g.Ci % 4 || g.Ci < 8 || ntap % 4) return;
+        long P = (long)g.N * g.H * g.W;
+        rc.nv = ntap; rc.mode1 = MODE_WGRAD;
+        rc.g1 = geom_1x1(P, ntap, g.Ci);
+        rc.p1 = make_plan(rc.g1, MODE_WGRAD);
+        rc.wt_off = 0;
+        rc.v_off = 0;
+        rc.slab_off = al256((size_t)P * ntap * 4);
+    }
+    if (rc.p1.narrow) return;
+    rc.bytes = rc.slab_off + rc.p1.slab_bytes;
+    rc.on = 1;
+}
+
 template <int MODE>
 static void launch_gemm(int cfg, int vec, dim3 grid, const GemmArgs &a, hipStream_t s) {
 #define DG_L(C, BM_, BN_, WM_, WN_)                                                           \
@@ -767,21 +925,75 @@ static void launch_gemm(int cfg, int vec, dim3 grid, const GemmArgs &a, hipStrea
 #undef DG_L
 }
 
+static GemmArgs make_args(const ConvGeom &g, const OpPlan &pl, const float *A, int lda, const float *B, int ldb,
+                          float *C, int ldc, const float *bias, float beta, int act, float alpha, void *slab) {
+    GemmArgs a{};
+    a.g = g; a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.C = C; a.ldc = ldc;
+    a.bias = bias; a.beta = beta; a.act = act; a.alpha = alpha;
+    a.M = pl.M; a.N = pl.N; a.K = pl.K; a.kchunk = pl.kchunk; a.splits = pl.splits;
+    a.mtiles = pl.mtiles; a.ntiles = pl.ntiles; a.nphase = pl.nphase;
+    a.slab = (float *)slab;
+    return a;
+}
+
+static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a, hipStream_t s);
+
+// narrow op through its recast (1x1 MFMA GEMM + gather)
+static int run_recast(const dg_conv_desc_s *d, int op, const GemmArgs &a0, char *ws, hipStream_t s) {
+    const Recast &rc = d->rc[op];
+    const ConvGeom &g = d->g;
+    float *wt = (float *)(ws + rc.wt_off);
+    float *V = (float *)(ws + rc.v_off);
+    void *slab = ws + rc.slab_off;
+    if (rc.mode1 == MODE_FWD && engine_mode(d, op) == MODE_FWD) {
+        // Co == 1: V = x . wt, wt[ci][(i,j)] = w[(i,j)][ci]
+        hipLaunchKernelGGL(k_transpose, dim3(std::min<unsigned>(dg_cdiv((long)rc.nv * g.Ci, 256), 1024)), dim3(256), 0, s,
+                           a0.B, rc.nv, g.Ci, wt);
+        DG_LAUNCHED("recast_transpose");
+        GemmArgs a = make_args(rc.g1, rc.p1, a0.A, a0.lda, wt, rc.nv, V, rc.nv, nullptr, 0.f, DG_ACT_NONE, 0.f, slab);
+        int r = run_gemm(MODE_FWD, rc.p1, a, s);
+        if (r != DG_OK) return r;
+        hipLaunchKernelGGL(k_recast_fwd_gather, dim3(dg_cdiv((long)g.N * g.Ho * g.Wo, 256)), dim3(256), 0, s, a0, V, rc.nv);
+        DG_LAUNCHED("recast_fwd_gather");
+        return DG_OK;
+    }
+    if (rc.mode1 == MODE_FWD) {
+        // DGRAD, Ci <= 8: V = dy . wt, wt[co][(i,j,ci)] = w[(i,j,ci)][co]; dx = col2im(V)
+        hipLaunchKernelGGL(k_transpose, dim3(std::min<unsigned>(dg_cdiv((long)rc.nv * g.Co, 256), 1024)), dim3(256), 0, s,
+                           a0.B, rc.nv, g.Co, wt);
+        DG_LAUNCHED("recast_transpose");
+        GemmArgs a = make_args(rc.g1, rc.p1, a0.A, a0.lda, wt, rc.nv, V, rc.nv, nullptr, 0.f, DG_ACT_NONE, 0.f, slab);
+        int r = run_gemm(MODE_FWD, rc.p1, a, s);
+        if (r != DG_OK) return r;
+        long total = (long)g.N * g.H * g.W * g.Ci;
+        hipLaunchKernelGGL(k_recast_col2im, dim3((unsigned)std::min<long>(dg_cdiv(total, 256), 8192)), dim3(256), 0, s,
+                           a0, V, rc.nv);
+        DG_LAUNCHED("recast_col2im");
+        return DG_OK;
+    }
+    // WGRAD, Co == 1: G gathered from dy, dw[(i,j)][ci] = G^T . x (a WGRAD GEMM of 1x1 geometry)
+    long total = (long)g.N * g.H * g.W * rc.nv;
+    hipLaunchKernelGGL(k_recast_wgrad_gather, dim3((unsigned)std::min<long>(dg_cdiv(total, 256), 8192)), dim3(256), 0, s,
+                       a0, a0.B, a0.ldb, V);
+    DG_LAUNCHED("recast_wgrad_gather");
+    GemmArgs a = make_args(rc.g1, rc.p1, V, rc.nv, a0.A, a0.lda, a0.C, g.Ci, nullptr, a0.beta, DG_ACT_NONE, 0.f, slab);
+    return run_gemm(MODE_WGRAD, rc.p1, a, s);
+}
+
 static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, const float *B, int ldb,
                       float *C, int ldc, const float *bias, float beta, int act, float alpha,
                       void *ws, size_t ws_bytes, hipStream_t s) {
     const int mode = engine_mode(d, op);
     const OpPlan &pl = d->plan[op];
-    DG_ARG(ws_bytes >= pl.slab_bytes, "workspace too small: need %zu bytes, got %zu", pl.slab_bytes, ws_bytes);
-    DG_ARG(pl.slab_bytes == 0 || ws != nullptr, "workspace pointer is NULL");
-    GemmArgs a{};
-    a.g = d->g; a.A = A; a.lda = lda; a.B = B; a.ldb = ldb; a.C = C; a.ldc = ldc;
-    a.bias = bias; a.beta = beta; a.act = act; a.alpha = alpha;
-    a.M = pl.M; a.N = pl.N; a.K = pl.K; a.kchunk = pl.kchunk; a.splits = pl.splits;
-    a.mtiles = pl.mtiles; a.ntiles = pl.ntiles; a.nphase = pl.nphase;
-    a.slab = (float *)ws;
+    const size_t need = d->rc[op].on ? d->rc[op].bytes : pl.slab_bytes;
+    DG_ARG(ws_bytes >= need, "workspace too small: need %zu bytes, got %zu", need, ws_bytes);
+    DG_ARG(need == 0 || ws != nullptr, "workspace pointer is NULL");
+    GemmArgs a = make_args(d->g, pl, A, lda, B, ldb, C, ldc, bias, beta, act, alpha, ws);
     if (pl.M == 0 || pl.N == 0) return DG_OK;
-
+    if (d->rc[op].on) {
+        DG_ARG(lda % 4 == 0 && ((uintptr_t)A & 15) == 0, "recast path needs lda%%4==0 and 16B-aligned A");
+        return run_recast(d, op, a, (char *)ws, s);
+    }
     if (pl.narrow) {
         if (mode == MODE_FWD) {
             hipLaunchKernelGGL(k_narrow_fwd, dim3(dg_cdiv(pl.M, 4)), dim3(256), 0, s, a);
@@ -801,6 +1013,12 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
         }
         return DG_OK;
     }
+    return run_gemm(mode, pl, a, s);
+}
+
+static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a, hipStream_t s) {
+    const float *A = a.A, *B = a.B;
+    const int lda = a.lda, ldb = a.ldb;
     if (mode == MODE_FWD || mode == MODE_WGRAD) {
         DG_ARG(pl.N % 4 == 0 && ldb % 4 == 0, "GEMM N (%d) and ldb (%d) must be multiples of 4", pl.N, ldb);
     }
@@ -886,10 +1104,14 @@ int dg_conv_desc_create(dg_conv_t *out, int N, int H, int W, int Cin, int Cout, 
     g.Tw = (kw + sw - 1) / sw;
     for (int op = 0; op < 3; ++op) {
         d->plan[op] = dg::make_plan(g, dg::engine_mode(d, op));
+        dg::plan_recast(d, op);
+        if (d->rc[op].on) d->plan[op].ws_bytes = d->rc[op].bytes;
         if (op == DG_OP_BWD_FILTER) {
             // room for the bias column sum partials after the split-K slabs
             size_t extra = dg::colsum_ws(1, Cout);
-            d->plan[op].ws_bytes = ((d->plan[op].slab_bytes + 255) & ~(size_t)255) + extra;
+            size_t base = d->rc[op].on ? d->rc[op].bytes : d->plan[op].slab_bytes;
+            d->plan[op].colsum_off = (base + 255) & ~(size_t)255;
+            d->plan[op].ws_bytes = d->plan[op].colsum_off + extra;
         }
     }
     *out = d;
@@ -936,7 +1158,7 @@ int dg_conv_bwd_filter(dg_conv_t d, const float *x, int ldx, const float *dy, in
     DG_ARG(ldx >= d->Cin && lddy >= d->Cout, "pixel stride smaller than channels");
     const dg::OpPlan &pl = d->plan[DG_OP_BWD_FILTER];
     DG_ARG(ws_bytes >= pl.ws_bytes && ws != nullptr, "workspace too small: need %zu bytes", pl.ws_bytes);
-    size_t slab_bytes = pl.slab_bytes;
+    size_t slab_bytes = pl.colsum_off;
     int rc;
     // conv view: A = conv input, B = conv output grad
     if (!d->transpose)
@@ -948,7 +1170,7 @@ int dg_conv_bwd_filter(dg_conv_t d, const float *x, int ldx, const float *dy, in
     if (rc != DG_OK) return rc;
     if (dbias) {
         long M = (long)d->N * d->Ho * d->Wo;
-        float *cws = (float *)((char *)ws + ((slab_bytes + 255) & ~(size_t)255));
+        float *cws = (float *)((char *)ws + pl.colsum_off);
         return dg::run_colsum(dy, lddy, M, d->Cout, dbias, beta, cws, (hipStream_t)stream);
     }
     return DG_OK;

@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -m pytest tests -q -m gpu -x > gpurun_out/test.log 2>&1 && \
+DG_BENCH_DETAIL=1 timeout -k 10 600 python bench.py --steps 20 --warmup 6 --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err
+echo rc=$?

@@ -6,6 +6,7 @@ plus the SRGAN/FSRGAN shapes (k3 'same' with TF's asymmetric pads, k1).
 Tolerance (fp32 MFMA accumulation vs fp64): relative L2 error < 2e-6 and
 max-abs error < 1e-5 * max|ref| (scaled by sqrt(K/1024) for long K)."""
 import math
+import zlib
 
 import pytest
 import torch
@@ -50,7 +51,7 @@ def _close(got, ref, K, what):
 def test_conv_layer(case):
     from dgan.ops import ConvDesc
     name, N, H, W, Cin, Cout, k, s, padding, transpose, has_bias = case
-    torch.manual_seed(hash(name) & 0xFFFF)
+    torch.manual_seed(zlib.crc32(name.encode()))
     d = ConvDesc(N, H, W, Cin, Cout, k, s, padding, transpose)
     x = torch.randn(N, H, W, Cin, dtype=torch.float64)
     w = torch.randn(*d.weight_shape, dtype=torch.float64) * 0.05
@@ -82,7 +83,9 @@ def test_conv_layer(case):
     _close(dx, xr.grad, k * k * Cout, f"{name} bwd_data")
     _close(dw, wr.grad, N * d.Ho * d.Wo, f"{name} bwd_filter")
     if has_bias:
-        _close(db, br.grad, N * d.Ho * d.Wo, f"{name} dbias")
+        # a column sum of random-sign terms can cancel: scale by sum |dy| instead of |sum|
+        err = (db.double().cpu() - br.grad).abs().max().item()
+        assert err <= 1e-6 * dy.abs().sum(dim=(0, 1, 2)).max().item(), f"{name} dbias: {err:.3e}"
 
 
 @gpu
