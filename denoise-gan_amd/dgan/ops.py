@@ -170,25 +170,28 @@ class ConvDesc:
         return 2 * self.N * self.Ho * self.Wo * self.Cout * self.kh * self.kw * self.Cin
 
     def fwd(self, x, w, y, bias=None, act="none", alpha=0.3, beta=0.0, ws=None):
+        ldx, ldy = pix_ld(x, self.Cin), pix_ld(y, self.Cout)
         wp, wn = self._ws(OP_FWD, ws)
         ev = _prof_begin()
-        call("dg_conv_fwd", self._h, _p(x), pix_ld(x, self.Cin), _p(w), _p(bias), _p(y), pix_ld(y, self.Cout),
+        call("dg_conv_fwd", self._h, _p(x), ldx, _p(w), _p(bias), _p(y), ldy,
              float(beta), act_id(act), float(alpha), wp, wn, _stream())
         _prof_end(ev, self, "fwd")
         return y
 
     def bwd_data(self, dy, w, dx, beta=0.0, ws=None):
+        lddy, lddx = pix_ld(dy, self.Cout), pix_ld(dx, self.Cin)
         wp, wn = self._ws(OP_BWD_DATA, ws)
         ev = _prof_begin()
-        call("dg_conv_bwd_data", self._h, _p(dy), pix_ld(dy, self.Cout), _p(w), _p(dx), pix_ld(dx, self.Cin),
+        call("dg_conv_bwd_data", self._h, _p(dy), lddy, _p(w), _p(dx), lddx,
              float(beta), wp, wn, _stream())
         _prof_end(ev, self, "bwd_data")
         return dx
 
     def bwd_filter(self, x, dy, dw, dbias=None, beta=0.0, ws=None):
+        ldx, lddy = pix_ld(x, self.Cin), pix_ld(dy, self.Cout)
         wp, wn = self._ws(OP_BWD_FILTER, ws)
         ev = _prof_begin()
-        call("dg_conv_bwd_filter", self._h, _p(x), pix_ld(x, self.Cin), _p(dy), pix_ld(dy, self.Cout), _p(dw),
+        call("dg_conv_bwd_filter", self._h, _p(x), ldx, _p(dy), lddy, _p(dw),
              _p(dbias), float(beta), wp, wn, _stream())
         _prof_end(ev, self, "bwd_filter")
         return dw
