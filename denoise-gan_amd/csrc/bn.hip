@@ -7,117 +7,151 @@
 // Bessel-corrected one into the moving average.
 //
 // All reductions are per channel over the M = N*H*W rows of an NHWC tensor
-// and deterministic: fixed row chunks -> (n, mean, M2) partials (Chan
-// merge, shifted sums inside a chunk) -> ordered finalize.  A block is
-// 64 channels x 4 row lanes, so each wave reads 256 contiguous bytes of a row.
+// and deterministic: fixed row chunks -> per-chunk partials -> an ordered,
+// parallel finalize.  Streaming passes move float4 per lane whenever the
+// channel count and strides allow it (V = 4), else one float (V = 1).
+// Statistics inside a chunk use sums shifted by the chunk's first row (no
+// catastrophic cancellation); chunks are combined with Chan's formula.
 #include "common.h"
 #include <algorithm>
 
 namespace dg {
 
 struct BnPlan {
-    int cg;      // channel groups of 64
     int R;       // row chunks
     long rows;   // rows per chunk
 };
 
 static BnPlan bn_plan(long M, int C) {
+    (void)C;
     BnPlan p;
-    p.cg = (C + 63) / 64;
-    // ~512 blocks in the partial pass, >= 64 rows each; the finalize combines
-    // R partials per channel with 4 lanes, so R stays small
-    long r = std::max<long>(1, 512 / p.cg);
-    r = std::min<long>(r, std::max<long>(1, (M + 63) / 64));
+    long r = std::min<long>(256, std::max<long>(1, (M + 63) / 64));
     p.rows = (M + r - 1) / r;
     p.R = (int)((M + p.rows - 1) / p.rows);
     return p;
 }
 
-// ws layout (floats): [3*R*C partials] [2*C scale/shift or 3*C bwd coefs]
+// ws layout (floats): [3*R*C partials] [4*C scale/shift or bwd coefs]
 static size_t bn_ws_floats(long M, int C) {
     BnPlan p = bn_plan(M, C);
     return (size_t)3 * p.R * C + (size_t)4 * C + 64;
 }
 
-__device__ __forceinline__ void chan_merge(float &n, float &mean, float &m2, float nb, float meanb, float m2b) {
-    if (nb == 0.f) return;
-    if (n == 0.f) { n = nb; mean = meanb; m2 = m2b; return; }
-    float nn = n + nb;
-    float d = meanb - mean;
-    mean += d * (nb / nn);
-    m2 += m2b + d * d * (n * nb / nn);
-    n = nn;
+// block geometry of the partial passes: CPB channel slots (V channels each) x RL row lanes
+struct PartGeom {
+    int V, cpb, rl, cg;
+};
+static PartGeom part_geom(int C, int V) {
+    PartGeom g;
+    g.V = V;
+    int slots = (C + V - 1) / V;
+    int cpb = 1;
+    while (cpb < slots && cpb < 64) cpb <<= 1;
+    g.cpb = cpb;
+    g.rl = 256 / cpb;
+    g.cg = (slots + cpb - 1) / cpb;
+    return g;
 }
 
+template <int V>
+__device__ __forceinline__ void loadv(const float *p, float (&v)[V]) {
+    if constexpr (V == 4) {
+        f32x4 t = *reinterpret_cast<const f32x4 *>(p);
+        v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+    } else {
+        v[0] = p[0];
+    }
+}
+
+template <int V>
+__device__ __forceinline__ void storev(float *p, const float (&v)[V]) {
+    if constexpr (V == 4) {
+        f32x4 t = {v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<f32x4 *>(p) = t;
+    } else {
+        p[0] = v[0];
+    }
+}
+
+// per (chunk, channel): n, mean, M2
+template <int V>
 __global__ void __launch_bounds__(256)
-k_bn_stats_partial(const float *__restrict__ y, int ld, long M, int C, long rows, float *__restrict__ pn,
+k_bn_stats_partial(const float *__restrict__ y, int ld, long M, int C, long rows, int cpb, float *__restrict__ pn,
                    float *__restrict__ pmean, float *__restrict__ pm2) {
-    __shared__ float sn[256], smean[256], sm2[256];
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int rl = threadIdx.x >> 6;
+    __shared__ float s1s[256 * V], s2s[256 * V];
+    const int slot = threadIdx.x % cpb, rl = threadIdx.x / cpb, RL = 256 / cpb;
+    const int c0 = (blockIdx.x * cpb + slot) * V;
     const long r0 = (long)blockIdx.y * rows;
     const long r1 = min(M, r0 + rows);
-    float cnt = 0.f, mean = 0.f, m2 = 0.f;
-    if (c < C && r0 < r1) {
-        const float K = y[r0 * ld + c];
-        float s1 = 0.f, s2 = 0.f;
-        for (long r = r0 + rl; r < r1; r += 4) {
-            float d = y[r * ld + c] - K;
-            s1 += d;
-            s2 += d * d;
-            cnt += 1.f;
-        }
-        if (cnt > 0.f) {
-            mean = K + s1 / cnt;
-            m2 = fmaxf(s2 - s1 * s1 / cnt, 0.f);
+    float s1[V], s2[V], K[V];
+#pragma unroll
+    for (int q = 0; q < V; ++q) s1[q] = s2[q] = 0.f;
+    const bool cok = c0 < C;
+    if (cok) {
+        loadv<V>(y + r0 * ld + c0, K);
+        for (long r = r0 + rl; r < r1; r += RL) {
+            float v[V];
+            loadv<V>(y + r * ld + c0, v);
+#pragma unroll
+            for (int q = 0; q < V; ++q) {
+                float d = v[q] - K[q];
+                s1[q] += d;
+                s2[q] += d * d;
+            }
         }
     }
-    sn[threadIdx.x] = cnt; smean[threadIdx.x] = mean; sm2[threadIdx.x] = m2;
+#pragma unroll
+    for (int q = 0; q < V; ++q) { s1s[threadIdx.x * V + q] = s1[q]; s2s[threadIdx.x * V + q] = s2[q]; }
     __syncthreads();
-    if (rl == 0 && c < C) {
-        float n = sn[threadIdx.x], mu = smean[threadIdx.x], q = sm2[threadIdx.x];
-        for (int k = 1; k < 4; ++k) {
-            int t = threadIdx.x + 64 * k;
-            chan_merge(n, mu, q, sn[t], smean[t], sm2[t]);
-        }
-        const long o = (long)blockIdx.y * C + c;
-        pn[o] = n; pmean[o] = mu; pm2[o] = q;
+    if (rl != 0 || !cok) return;
+    for (int l = 1; l < RL; ++l) {
+        const int t = threadIdx.x + l * cpb;
+#pragma unroll
+        for (int q = 0; q < V; ++q) { s1[q] += s1s[t * V + q]; s2[q] += s2s[t * V + q]; }
+    }
+    const float n = (float)(r1 - r0);
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+        const long o = (long)blockIdx.y * C + c0 + q;
+        pn[o] = n;
+        pmean[o] = K[q] + s1[q] / n;
+        pm2[o] = fmaxf(s2[q] - s1[q] * s1[q] / n, 0.f);
     }
 }
 
-// finalize: block = 64 channels x 4 lanes; two parallel passes over the R
-// chunk partials (Chan's combine written as sums: mean = sum n_i mean_i / n,
-// M2 = sum M2_i + n_i (mean_i - mean)^2), no serial merge chain
+// finalize: block = 16 channels x 16 lanes; two parallel passes over the R chunk
+// partials (Chan's combine as sums: mean = sum n_i mean_i / n, M2 = sum M2_i + n_i (mean_i - mean)^2)
 __global__ void __launch_bounds__(256)
 k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, int C, const float *gamma,
                  const float *beta, float *save_mean, float *save_invstd, float *mm, float *mv, float momentum,
                  float eps, float *scale, float *shift) {
     __shared__ float s0[256], s1[256];
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int l4 = threadIdx.x >> 6;
-    const int c64 = threadIdx.x & 63;
+    const int cl = threadIdx.x & 15, ln = threadIdx.x >> 4;
+    const int c = blockIdx.x * 16 + cl;
     float sn = 0.f, sm = 0.f;
     if (c < C)
-        for (int r = l4; r < R; r += 4) {
+        for (int r = ln; r < R; r += 16) {
             const float n = pn[(long)r * C + c];
             sn += n;
             sm += n * pmean[(long)r * C + c];
         }
     s0[threadIdx.x] = sn; s1[threadIdx.x] = sm;
     __syncthreads();
-    const float n = s0[c64] + s0[c64 + 64] + s0[c64 + 128] + s0[c64 + 192];
-    const float mu = n > 0.f ? (s1[c64] + s1[c64 + 64] + s1[c64 + 128] + s1[c64 + 192]) / n : 0.f;
+    float n = 0.f, msum = 0.f;
+    for (int l = 0; l < 16; ++l) { n += s0[cl + 16 * l]; msum += s1[cl + 16 * l]; }
+    const float mu = n > 0.f ? msum / n : 0.f;
     __syncthreads();
     float q = 0.f;
     if (c < C)
-        for (int r = l4; r < R; r += 4) {
+        for (int r = ln; r < R; r += 16) {
             const float d = pmean[(long)r * C + c] - mu;
             q += pm2[(long)r * C + c] + pn[(long)r * C + c] * d * d;
         }
     s0[threadIdx.x] = q;
     __syncthreads();
-    if (l4 != 0 || c >= C) return;
-    const float m2 = s0[c64] + s0[c64 + 64] + s0[c64 + 128] + s0[c64 + 192];
+    if (ln != 0 || c >= C) return;
+    float m2 = 0.f;
+    for (int l = 0; l < 16; ++l) m2 += s0[cl + 16 * l];
     const float var = n > 0.f ? m2 / n : 0.f;
     const float inv = 1.f / sqrtf(var + eps);
     if (save_mean) save_mean[c] = mu;
@@ -133,39 +167,30 @@ k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, i
     }
 }
 
-template <bool VEC4>
+template <int V>
 __global__ void __launch_bounds__(256)
 k_bn_apply(const float *__restrict__ y, int ld, long M, int C, const float *__restrict__ scale,
            const float *__restrict__ shift, float *__restrict__ z, int ldz, int act, float alpha, float drop_rate,
            uint32_t seed, const int32_t *step_dev) {
     const uint32_t step = step_dev ? (uint32_t)*step_dev : 0u;
     const float keep_scale = drop_rate > 0.f ? 1.f / (1.f - drop_rate) : 1.f;
-    const long stride = (long)gridDim.x * blockDim.x;
-    if constexpr (VEC4) {
-        const int C4 = C >> 2;
-        const long total = M * C4;
-        for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
-            long r = e / C4;
-            int c = (int)(e - r * C4) * 4;
-            f32x4 v = *reinterpret_cast<const f32x4 *>(y + r * ld + c);
-            f32x4 o;
+    const int CV = C / V;
+    const long total = M * CV;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long r = e / CV;
+        const int c = (int)(e - r * CV) * V;
+        float v[V], o[V], sc[V], sh[V];
+        loadv<V>(y + r * ld + c, v);
+        loadv<V>(scale + c, sc);
+        loadv<V>(shift + c, sh);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                float t = v[q] * scale[c + q] + shift[c + q];
-                if (drop_rate > 0.f) t = dropout_keep(seed, step, (uint32_t)(r * C + c + q), drop_rate) ? t * keep_scale : 0.f;
-                o[q] = act_fwd(t, act, alpha);
-            }
-            *reinterpret_cast<f32x4 *>(z + r * ldz + c) = o;
+        for (int q = 0; q < V; ++q) {
+            float t = v[q] * sc[q] + sh[q];
+            if (drop_rate > 0.f)
+                t = dropout_keep(seed, step, (uint32_t)(r * C + c + q), drop_rate) ? t * keep_scale : 0.f;
+            o[q] = act_fwd(t, act, alpha);
         }
-    } else {
-        const long total = M * C;
-        for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
-            long r = e / C;
-            int c = (int)(e - r * C);
-            float t = y[r * ld + c] * scale[c] + shift[c];
-            if (drop_rate > 0.f) t = dropout_keep(seed, step, (uint32_t)e, drop_rate) ? t * keep_scale : 0.f;
-            z[r * ldz + c] = act_fwd(t, act, alpha);
-        }
+        storev<V>(z + r * ldz + c, o);
     }
 }
 
@@ -185,86 +210,133 @@ k_bn_apply_infer(const float *__restrict__ y, int ld, long M, int C, const float
 }
 
 // backward: partial sums of dbn and dbn*xhat per (chunk, channel)
+template <int V>
 __global__ void __launch_bounds__(256)
 k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict__ z, int ldz,
-                 const float *__restrict__ y, int ldy, long M, int C, long rows, const float *__restrict__ mean,
-                 const float *__restrict__ invstd, int act, float alpha, float dscale, float *__restrict__ p1,
-                 float *__restrict__ p2) {
-    __shared__ float s1[256], s2[256];
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int rl = threadIdx.x >> 6;
+                 const float *__restrict__ y, int ldy, long M, int C, long rows, int cpb,
+                 const float *__restrict__ mean, const float *__restrict__ invstd, int act, float alpha, float dscale,
+                 float *__restrict__ p1, float *__restrict__ p2) {
+    __shared__ float a1s[256 * V], a2s[256 * V];
+    const int slot = threadIdx.x % cpb, rl = threadIdx.x / cpb, RL = 256 / cpb;
+    const int c0 = (blockIdx.x * cpb + slot) * V;
     const long r0 = (long)blockIdx.y * rows;
     const long r1 = min(M, r0 + rows);
-    float a1 = 0.f, a2 = 0.f;
-    if (c < C) {
-        const float mu = mean[c], inv = invstd[c];
-        for (long r = r0 + rl; r < r1; r += 4) {
-            float dbn = dz[r * lddz + c] * act_grad_from_out(z[r * ldz + c], act, alpha) * dscale;
-            float xh = (y[r * ldy + c] - mu) * inv;
-            a1 += dbn;
-            a2 += dbn * xh;
+    float a1[V], a2[V], mu[V], inv[V];
+#pragma unroll
+    for (int q = 0; q < V; ++q) a1[q] = a2[q] = 0.f;
+    const bool cok = c0 < C;
+    if (cok) {
+        loadv<V>(mean + c0, mu);
+        loadv<V>(invstd + c0, inv);
+        for (long r = r0 + rl; r < r1; r += RL) {
+            float dv[V], zv[V], yv[V];
+            loadv<V>(dz + r * lddz + c0, dv);
+            loadv<V>(z + r * ldz + c0, zv);
+            loadv<V>(y + r * ldy + c0, yv);
+#pragma unroll
+            for (int q = 0; q < V; ++q) {
+                float dbn = dv[q] * act_grad_from_out(zv[q], act, alpha) * dscale;
+                a1[q] += dbn;
+                a2[q] += dbn * (yv[q] - mu[q]) * inv[q];
+            }
         }
     }
-    s1[threadIdx.x] = a1; s2[threadIdx.x] = a2;
+#pragma unroll
+    for (int q = 0; q < V; ++q) { a1s[threadIdx.x * V + q] = a1[q]; a2s[threadIdx.x * V + q] = a2[q]; }
     __syncthreads();
-    if (rl == 0 && c < C) {
-        float b1 = s1[threadIdx.x] + s1[threadIdx.x + 64] + s1[threadIdx.x + 128] + s1[threadIdx.x + 192];
-        float b2 = s2[threadIdx.x] + s2[threadIdx.x + 64] + s2[threadIdx.x + 128] + s2[threadIdx.x + 192];
-        const long o = (long)blockIdx.y * C + c;
-        p1[o] = b1; p2[o] = b2;
+    if (rl != 0 || !cok) return;
+    for (int l = 1; l < RL; ++l) {
+        const int t = threadIdx.x + l * cpb;
+#pragma unroll
+        for (int q = 0; q < V; ++q) { a1[q] += a1s[t * V + q]; a2[q] += a2s[t * V + q]; }
+    }
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+        const long o = (long)blockIdx.y * C + c0 + q;
+        p1[o] = a1[q];
+        p2[o] = a2[q];
     }
 }
 
 __global__ void __launch_bounds__(256)
-k_bn_bwd_final(const float *p1, const float *p2, int R, int C, long M, const float *gamma, const float *invstd,
-               float *dgamma, float *dbeta, float beta, float *coef) {
+k_bn_bwd_final(const float *p1, const float *p2, int R, int C, long M, const float *gamma, const float *mean,
+               const float *invstd, float *dgamma, float *dbeta, float beta, float *coef) {
     __shared__ float s0[256], s1[256];
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int l4 = threadIdx.x >> 6;
-    const int c64 = threadIdx.x & 63;
+    const int cl = threadIdx.x & 15, ln = threadIdx.x >> 4;
+    const int c = blockIdx.x * 16 + cl;
     float a1 = 0.f, a2 = 0.f;
     if (c < C)
-        for (int r = l4; r < R; r += 4) { a1 += p1[(long)r * C + c]; a2 += p2[(long)r * C + c]; }
+        for (int r = ln; r < R; r += 16) { a1 += p1[(long)r * C + c]; a2 += p2[(long)r * C + c]; }
     s0[threadIdx.x] = a1; s1[threadIdx.x] = a2;
     __syncthreads();
-    if (l4 != 0 || c >= C) return;
-    a1 = s0[c64] + s0[c64 + 64] + s0[c64 + 128] + s0[c64 + 192];
-    a2 = s1[c64] + s1[c64 + 64] + s1[c64 + 128] + s1[c64 + 192];
+    if (ln != 0 || c >= C) return;
+    a1 = 0.f; a2 = 0.f;
+    for (int l = 0; l < 16; ++l) { a1 += s0[cl + 16 * l]; a2 += s1[cl + 16 * l]; }
     if (dbeta) dbeta[c] = a1 + (beta != 0.f ? beta * dbeta[c] : 0.f);
     if (dgamma) dgamma[c] = a2 + (beta != 0.f ? beta * dgamma[c] : 0.f);
+    // dy = k1 (dbn - m1 - xhat m2), xhat = (y - mean) invstd  ==>  dy = A dbn + B (y - mean) + D
     const float g = gamma ? gamma[c] : 1.f;
-    coef[c] = g * invstd[c];
-    coef[C + c] = a1 / (float)M;
-    coef[2 * C + c] = a2 / (float)M;
+    const float k1 = g * invstd[c];
+    const float m1 = a1 / (float)M, m2 = a2 / (float)M;
+    coef[c] = k1;
+    coef[C + c] = -k1 * m2 * invstd[c];
+    coef[2 * C + c] = -k1 * m1;
+    coef[3 * C + c] = mean[c];
 }
 
+template <int V>
 __global__ void __launch_bounds__(256)
 k_bn_bwd_apply(const float *__restrict__ dz, int lddz, const float *__restrict__ z, int ldz,
-               const float *__restrict__ y, int ldy, long M, int C, const float *__restrict__ mean,
-               const float *__restrict__ invstd, int act, float alpha, float dscale, const float *__restrict__ coef,
-               float *__restrict__ dy, int lddy) {
-    const long total = M * C;
+               const float *__restrict__ y, int ldy, long M, int C, int act, float alpha, float dscale,
+               const float *__restrict__ coef, float *__restrict__ dy, int lddy) {
+    // coef = [A | B | D | mean] per channel:  dy = A * dbn + B * (y - mean) + D
+    const int CV = C / V;
+    const long total = M * CV;
     for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-        long r = e / C;
-        int c = (int)(e - r * C);
-        float dbn = dz[r * lddz + c] * act_grad_from_out(z[r * ldz + c], act, alpha) * dscale;
-        float xh = (y[r * ldy + c] - mean[c]) * invstd[c];
-        dy[r * lddy + c] = coef[c] * (dbn - coef[C + c] - xh * coef[2 * C + c]);
+        const long r = e / CV;
+        const int c = (int)(e - r * CV) * V;
+        float dv[V], zv[V], yv[V], A[V], B[V], D[V], Mu[V], o[V];
+        loadv<V>(dz + r * lddz + c, dv);
+        loadv<V>(z + r * ldz + c, zv);
+        loadv<V>(y + r * ldy + c, yv);
+        loadv<V>(coef + c, A);
+        loadv<V>(coef + C + c, B);
+        loadv<V>(coef + 2 * C + c, D);
+        loadv<V>(coef + 3 * C + c, Mu);
+#pragma unroll
+        for (int q = 0; q < V; ++q)
+            o[q] = A[q] * (dv[q] * act_grad_from_out(zv[q], act, alpha) * dscale) + B[q] * (yv[q] - Mu[q]) + D[q];
+        storev<V>(dy + r * lddy + c, o);
     }
 }
 
+template <int V>
 __global__ void __launch_bounds__(256)
 k_act_bwd(const float *__restrict__ dz, int lddz, const float *__restrict__ z, int ldz, long M, int C, int act,
           float alpha, float *__restrict__ dy, int lddy) {
-    const long total = M * C;
+    const int CV = C / V;
+    const long total = M * CV;
     for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-        long r = e / C;
-        int c = (int)(e - r * C);
-        dy[r * lddy + c] = dz[r * lddz + c] * act_grad_from_out(z[r * ldz + c], act, alpha);
+        const long r = e / CV;
+        const int c = (int)(e - r * CV) * V;
+        float dv[V], zv[V], o[V];
+        loadv<V>(dz + r * lddz + c, dv);
+        loadv<V>(z + r * ldz + c, zv);
+#pragma unroll
+        for (int q = 0; q < V; ++q) o[q] = dv[q] * act_grad_from_out(zv[q], act, alpha);
+        storev<V>(dy + r * lddy + c, o);
     }
 }
 
 static unsigned ew_grid(long n) { return (unsigned)std::max<long>(1, std::min<long>(dg_cdiv(n, 256), 8192)); }
+
+// float4 path usable: channels and every stride multiple of 4, 16-byte aligned bases
+static bool vec4_ok(int C, std::initializer_list<std::pair<const void *, int>> ts) {
+    if (C % 4) return false;
+    for (auto &t : ts)
+        if (t.first && ((((uintptr_t)t.first) & 15) || (t.second % 4))) return false;
+    return true;
+}
 
 }  // namespace dg
 
@@ -289,18 +361,25 @@ int dg_bn_fwd_train(int M, int C, const float *y, int ldy, const float *gamma, c
     float *w = (float *)ws;
     float *pn = w, *pmean = w + (size_t)bp.R * C, *pm2 = w + (size_t)2 * bp.R * C;
     float *scale = w + (size_t)3 * bp.R * C, *shift = scale + C;
-    hipLaunchKernelGGL(dg::k_bn_stats_partial, dim3(bp.cg, bp.R), dim3(256), 0, s, y, ldy, (long)M, C, bp.rows, pn,
-                       pmean, pm2);
+    const bool v4y = dg::vec4_ok(C, {{y, ldy}});
+    if (v4y) {
+        dg::PartGeom pg = dg::part_geom(C, 4);
+        hipLaunchKernelGGL(dg::k_bn_stats_partial<4>, dim3(pg.cg, bp.R), dim3(256), 0, s, y, ldy, (long)M, C, bp.rows,
+                           pg.cpb, pn, pmean, pm2);
+    } else {
+        dg::PartGeom pg = dg::part_geom(C, 1);
+        hipLaunchKernelGGL(dg::k_bn_stats_partial<1>, dim3(pg.cg, bp.R), dim3(256), 0, s, y, ldy, (long)M, C, bp.rows,
+                           pg.cpb, pn, pmean, pm2);
+    }
     DG_LAUNCHED("bn_stats_partial");
-    hipLaunchKernelGGL(dg::k_bn_stats_final, dim3(bp.cg), dim3(256), 0, s, pn, pmean, pm2, bp.R, C, gamma,
+    hipLaunchKernelGGL(dg::k_bn_stats_final, dim3(dg_cdiv(C, 16)), dim3(256), 0, s, pn, pmean, pm2, bp.R, C, gamma,
                        beta, save_mean, save_invstd, moving_mean, moving_var, momentum, eps, scale, shift);
     DG_LAUNCHED("bn_stats_final");
-    bool vec = (C % 4 == 0) && (ldy % 4 == 0) && (ldz % 4 == 0) && ((((uintptr_t)y) | ((uintptr_t)z)) & 15) == 0;
-    if (vec)
-        hipLaunchKernelGGL(dg::k_bn_apply<true>, dim3(dg::ew_grid((long)M * C / 4)), dim3(256), 0, s, y, ldy, (long)M,
-                           C, scale, shift, z, ldz, act, alpha, drop_rate, drop_seed, step_dev);
+    if (dg::vec4_ok(C, {{y, ldy}, {z, ldz}}))
+        hipLaunchKernelGGL(dg::k_bn_apply<4>, dim3(dg::ew_grid((long)M * C / 4)), dim3(256), 0, s, y, ldy, (long)M, C,
+                           scale, shift, z, ldz, act, alpha, drop_rate, drop_seed, step_dev);
     else
-        hipLaunchKernelGGL(dg::k_bn_apply<false>, dim3(dg::ew_grid((long)M * C)), dim3(256), 0, s, y, ldy, (long)M, C,
+        hipLaunchKernelGGL(dg::k_bn_apply<1>, dim3(dg::ew_grid((long)M * C)), dim3(256), 0, s, y, ldy, (long)M, C,
                            scale, shift, z, ldz, act, alpha, drop_rate, drop_seed, step_dev);
     DG_LAUNCHED("bn_apply");
     return DG_OK;
@@ -333,14 +412,26 @@ int dg_bn_bwd(int M, int C, const float *dz, int lddz, const float *z, int ldz, 
     dg::BnPlan bp = dg::bn_plan(M, C);
     float *w = (float *)ws;
     float *p1 = w, *p2 = w + (size_t)bp.R * C, *coef = w + (size_t)3 * bp.R * C;
-    hipLaunchKernelGGL(dg::k_bn_bwd_partial, dim3(bp.cg, bp.R), dim3(256), 0, s, dz, lddz, z, ldz, y, ldy, (long)M, C,
-                       bp.rows, save_mean, save_invstd, act, alpha, dscale, p1, p2);
+    const bool v4 = dg::vec4_ok(C, {{dz, lddz}, {z, ldz}, {y, ldy}, {save_mean, 4}, {save_invstd, 4}});
+    if (v4) {
+        dg::PartGeom pg = dg::part_geom(C, 4);
+        hipLaunchKernelGGL(dg::k_bn_bwd_partial<4>, dim3(pg.cg, bp.R), dim3(256), 0, s, dz, lddz, z, ldz, y, ldy,
+                           (long)M, C, bp.rows, pg.cpb, save_mean, save_invstd, act, alpha, dscale, p1, p2);
+    } else {
+        dg::PartGeom pg = dg::part_geom(C, 1);
+        hipLaunchKernelGGL(dg::k_bn_bwd_partial<1>, dim3(pg.cg, bp.R), dim3(256), 0, s, dz, lddz, z, ldz, y, ldy,
+                           (long)M, C, bp.rows, pg.cpb, save_mean, save_invstd, act, alpha, dscale, p1, p2);
+    }
     DG_LAUNCHED("bn_bwd_partial");
-    hipLaunchKernelGGL(dg::k_bn_bwd_final, dim3(bp.cg), dim3(256), 0, s, p1, p2, bp.R, C, (long)M, gamma,
-                       save_invstd, dgamma, dbeta, beta, coef);
+    hipLaunchKernelGGL(dg::k_bn_bwd_final, dim3(dg_cdiv(C, 16)), dim3(256), 0, s, p1, p2, bp.R, C, (long)M, gamma,
+                       save_mean, save_invstd, dgamma, dbeta, beta, coef);
     DG_LAUNCHED("bn_bwd_final");
-    hipLaunchKernelGGL(dg::k_bn_bwd_apply, dim3(dg::ew_grid((long)M * C)), dim3(256), 0, s, dz, lddz, z, ldz, y, ldy,
-                       (long)M, C, save_mean, save_invstd, act, alpha, dscale, coef, dy, lddy);
+    if (dg::vec4_ok(C, {{dz, lddz}, {z, ldz}, {y, ldy}, {dy, lddy}}))
+        hipLaunchKernelGGL(dg::k_bn_bwd_apply<4>, dim3(dg::ew_grid((long)M * C / 4)), dim3(256), 0, s, dz, lddz, z,
+                           ldz, y, ldy, (long)M, C, act, alpha, dscale, coef, dy, lddy);
+    else
+        hipLaunchKernelGGL(dg::k_bn_bwd_apply<1>, dim3(dg::ew_grid((long)M * C)), dim3(256), 0, s, dz, lddz, z, ldz,
+                           y, ldy, (long)M, C, act, alpha, dscale, coef, dy, lddy);
     DG_LAUNCHED("bn_bwd_apply");
     return DG_OK;
 }
@@ -350,8 +441,12 @@ int dg_act_bwd(int M, int C, const float *dz, int lddz, const float *z, int ldz,
     DG_ARG(dz && z && dy, "NULL tensor");
     DG_ARG(M >= 0 && C > 0 && lddz >= C && ldz >= C && lddy >= C, "bad shape");
     if (M == 0) return DG_OK;
-    hipLaunchKernelGGL(dg::k_act_bwd, dim3(dg::ew_grid((long)M * C)), dim3(256), 0, (hipStream_t)stream, dz, lddz, z,
-                       ldz, (long)M, C, act, alpha, dy, lddy);
+    if (dg::vec4_ok(C, {{dz, lddz}, {z, ldz}, {dy, lddy}}))
+        hipLaunchKernelGGL(dg::k_act_bwd<4>, dim3(dg::ew_grid((long)M * C / 4)), dim3(256), 0, (hipStream_t)stream, dz,
+                           lddz, z, ldz, (long)M, C, act, alpha, dy, lddy);
+    else
+        hipLaunchKernelGGL(dg::k_act_bwd<1>, dim3(dg::ew_grid((long)M * C)), dim3(256), 0, (hipStream_t)stream, dz,
+                           lddz, z, ldz, (long)M, C, act, alpha, dy, lddy);
     DG_LAUNCHED("act_bwd");
     return DG_OK;
 }

@@ -49,7 +49,23 @@ struct GemmArgs {
     int mtiles, ntiles;
     int nphase;
     float *slab;       // split-K partials [nphase*splits][M][N]
+    unsigned a_bytes, b_bytes;  // extents of A and B for the buffer-resource range check
 };
+
+// Branch-free operand loads: raw buffer loads through a resource whose range
+// check returns 0 for an out-of-range offset, so padding taps and ragged tile
+// edges need no exec-masked branches (an invalid element is given DG_OOB).
+constexpr unsigned DG_OOB = 0x80000000u;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const float *base, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4 bload4(rsrc_t r, unsigned byte_off) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+__device__ __forceinline__ float bload1(rsrc_t r, unsigned byte_off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
 
 struct PhaseInfo {
     int ph, pw, Hp, Wp, Mp, i0h, i0w;
@@ -184,6 +200,12 @@ k_conv_gemm(const GemmArgs p) {
         i = ph.i0h + a * g.sh; j = ph.i0w + b * g.sw;
     };
 
+    const rsrc_t rA = make_rsrc(p.A, p.a_bytes);
+    const rsrc_t rB = make_rsrc(p.B, p.b_bytes);
+    auto put4 = [](float *r, int ip, f32x4 v) {
+        r[4 * ip + 0] = v[0]; r[4 * ip + 1] = v[1]; r[4 * ip + 2] = v[2]; r[4 * ip + 3] = v[3];
+    };
+
     auto load_tiles = [&](int k0) {
         // ----- A -----
         if constexpr (MODE == MODE_FWD) {
@@ -193,12 +215,9 @@ k_conv_gemm(const GemmArgs p) {
 #pragma unroll
                 for (int ip = 0; ip < A_NPV; ++ip) {
                     int hi = arow_h[ip] + i, wi = arow_w[ip] + j;
-                    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-                    if (arow_n[ip] >= 0 && hi >= 0 && hi < g.H && wi >= 0 && wi < g.W) {
-                        const float *ptr = p.A + ((long)(arow_n[ip] * g.H + hi) * g.W + wi) * p.lda + ci0 + 4 * kc_c4;
-                        v = *reinterpret_cast<const f32x4 *>(ptr);
-                    }
-                    ra[4 * ip + 0] = v[0]; ra[4 * ip + 1] = v[1]; ra[4 * ip + 2] = v[2]; ra[4 * ip + 3] = v[3];
+                    bool ok = arow_n[ip] >= 0 && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+                    unsigned off = ((unsigned)((arow_n[ip] * g.H + hi) * g.W + wi) * p.lda + ci0 + 4 * kc_c4) * 4u;
+                    put4(ra, ip, bload4(rA, ok ? off : DG_OOB));
                 }
             } else {
                 int k = k0 + ks_kk;
@@ -208,14 +227,11 @@ k_conv_gemm(const GemmArgs p) {
 #pragma unroll
                 for (int e = 0; e < A_NES; ++e) {
                     int m = m0 + ks_r0 + 8 * e;
-                    float v = 0.f;
-                    if (kok && m < Mrows) {
-                        int wo = m % g.Wo; int t = m / g.Wo; int ho = t % g.Ho; int n = t / g.Ho;
-                        int hi = ho * g.sh - g.pt + i, wi = wo * g.sw - g.pl + j;
-                        if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
-                            v = p.A[((long)(n * g.H + hi) * g.W + wi) * p.lda + ci];
-                    }
-                    ra[e] = v;
+                    int wo = m % g.Wo; int t = m / g.Wo; int ho = t % g.Ho; int n = t / g.Ho;
+                    int hi = ho * g.sh - g.pt + i, wi = wo * g.sw - g.pl + j;
+                    bool ok = kok && m < Mrows && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+                    unsigned off = ((unsigned)((n * g.H + hi) * g.W + wi) * p.lda + ci) * 4u;
+                    ra[e] = bload1(rA, ok ? off : DG_OOB);
                 }
             }
         } else if constexpr (MODE == MODE_DGRAD) {
@@ -224,16 +240,11 @@ k_conv_gemm(const GemmArgs p) {
                 bool tapok = (i < g.kh) && (j < g.kw);
 #pragma unroll
                 for (int ip = 0; ip < A_NPV; ++ip) {
-                    f32x4 v = {0.f, 0.f, 0.f, 0.f};
                     int th = arow_h[ip] + g.pt - i, tw = arow_w[ip] + g.pl - j;
-                    if (tapok && arow_n[ip] >= 0 && th >= 0 && tw >= 0) {
-                        int ho = th / g.sh, wo = tw / g.sw;
-                        if (ho < g.Ho && wo < g.Wo) {
-                            const float *ptr = p.A + ((long)(arow_n[ip] * g.Ho + ho) * g.Wo + wo) * p.lda + co0 + 4 * kc_c4;
-                            v = *reinterpret_cast<const f32x4 *>(ptr);
-                        }
-                    }
-                    ra[4 * ip + 0] = v[0]; ra[4 * ip + 1] = v[1]; ra[4 * ip + 2] = v[2]; ra[4 * ip + 3] = v[3];
+                    int ho = th / g.sh, wo = tw / g.sw;  // exact when th, tw >= 0 (phase-aligned taps)
+                    bool ok = tapok && arow_n[ip] >= 0 && th >= 0 && tw >= 0 && ho < g.Ho && wo < g.Wo;
+                    unsigned off = ((unsigned)((arow_n[ip] * g.Ho + ho) * g.Wo + wo) * p.lda + co0 + 4 * kc_c4) * 4u;
+                    put4(ra, ip, bload4(rA, ok ? off : DG_OOB));
                 }
             } else {
                 int k = k0 + ks_kk;
@@ -242,17 +253,12 @@ k_conv_gemm(const GemmArgs p) {
 #pragma unroll
                 for (int e = 0; e < A_NES; ++e) {
                     int m = m0 + ks_r0 + 8 * e;
-                    float v = 0.f;
-                    if (kok && m < Mrows) {
-                        int ww = m % ph.Wp; int t = m / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
-                        int th = hh * g.sh + ph.ph + g.pt - i, tw = ww * g.sw + ph.pw + g.pl - j;
-                        if (th >= 0 && tw >= 0) {
-                            int ho = th / g.sh, wo = tw / g.sw;
-                            if (ho < g.Ho && wo < g.Wo)
-                                v = p.A[((long)(n * g.Ho + ho) * g.Wo + wo) * p.lda + co];
-                        }
-                    }
-                    ra[e] = v;
+                    int ww = m % ph.Wp; int t = m / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
+                    int th = hh * g.sh + ph.ph + g.pt - i, tw = ww * g.sw + ph.pw + g.pl - j;
+                    int ho = th / g.sh, wo = tw / g.sw;
+                    bool ok = kok && m < Mrows && th >= 0 && tw >= 0 && ho < g.Ho && wo < g.Wo;
+                    unsigned off = ((unsigned)((n * g.Ho + ho) * g.Wo + wo) * p.lda + co) * 4u;
+                    ra[e] = bload1(rA, ok ? off : DG_OOB);
                 }
             }
         } else {  // WGRAD: A k-rows are pixels, columns are (tap, ci)
@@ -260,27 +266,21 @@ k_conv_gemm(const GemmArgs p) {
 #pragma unroll
                 for (int ip = 0; ip < AR_NP; ++ip) {
                     int pix = k0 + ar_kr + AR_RPP * ip;
-                    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-                    if (wg_colok && pix < kend) {
-                        int wo = pix % g.Wo; int t = pix / g.Wo; int ho = t % g.Ho; int n = t / g.Ho;
-                        int hi = ho * g.sh - g.pt + wg_i, wi = wo * g.sw - g.pl + wg_j;
-                        if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
-                            v = *reinterpret_cast<const f32x4 *>(p.A + ((long)(n * g.H + hi) * g.W + wi) * p.lda + wg_ci);
-                    }
-                    ra[4 * ip + 0] = v[0]; ra[4 * ip + 1] = v[1]; ra[4 * ip + 2] = v[2]; ra[4 * ip + 3] = v[3];
+                    int wo = pix % g.Wo; int t = pix / g.Wo; int ho = t % g.Ho; int n = t / g.Ho;
+                    int hi = ho * g.sh - g.pt + wg_i, wi = wo * g.sw - g.pl + wg_j;
+                    bool ok = wg_colok && pix < kend && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+                    unsigned off = ((unsigned)((n * g.H + hi) * g.W + wi) * p.lda + wg_ci) * 4u;
+                    put4(ra, ip, bload4(rA, ok ? off : DG_OOB));
                 }
             } else {
 #pragma unroll
                 for (int e = 0; e < AR_NES; ++e) {
                     int pix = k0 + as_kr + (256 / BM) * e;
-                    float v = 0.f;
-                    if (wg_colok && pix < kend) {
-                        int wo = pix % g.Wo; int t = pix / g.Wo; int ho = t % g.Ho; int n = t / g.Ho;
-                        int hi = ho * g.sh - g.pt + wg_i, wi = wo * g.sw - g.pl + wg_j;
-                        if (hi >= 0 && hi < g.H && wi >= 0 && wi < g.W)
-                            v = p.A[((long)(n * g.H + hi) * g.W + wi) * p.lda + wg_ci];
-                    }
-                    ra[e] = v;
+                    int wo = pix % g.Wo; int t = pix / g.Wo; int ho = t % g.Ho; int n = t / g.Ho;
+                    int hi = ho * g.sh - g.pt + wg_i, wi = wo * g.sw - g.pl + wg_j;
+                    bool ok = wg_colok && pix < kend && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+                    unsigned off = ((unsigned)((n * g.H + hi) * g.W + wi) * p.lda + wg_ci) * 4u;
+                    ra[e] = bload1(rA, ok ? off : DG_OOB);
                 }
             }
         }
@@ -290,9 +290,8 @@ k_conv_gemm(const GemmArgs p) {
             for (int ip = 0; ip < BR_NP; ++ip) {
                 int k = k0 + br_kr + BR_RPP * ip;
                 int col = n0 + 4 * br_c4;
-                f32x4 v = {0.f, 0.f, 0.f, 0.f};
-                if (k < kend && col < p.N) v = *reinterpret_cast<const f32x4 *>(p.B + (long)k * p.ldb + col);
-                rb[4 * ip + 0] = v[0]; rb[4 * ip + 1] = v[1]; rb[4 * ip + 2] = v[2]; rb[4 * ip + 3] = v[3];
+                bool ok = k < kend && col < p.N;
+                put4(rb, ip, bload4(rB, ok ? ((unsigned)k * p.ldb + col) * 4u : DG_OOB));
             }
         } else if constexpr (MODE == MODE_DGRAD) {  // w[i,j,ci,co]: rows ci contiguous along co
             if constexpr (VEC) {
@@ -301,10 +300,9 @@ k_conv_gemm(const GemmArgs p) {
 #pragma unroll
                 for (int ip = 0; ip < B_NPV; ++ip) {
                     int ci = n0 + kc_rr + 32 * ip;
-                    f32x4 v = {0.f, 0.f, 0.f, 0.f};
-                    if (tapok && ci < p.N)
-                        v = *reinterpret_cast<const f32x4 *>(p.B + ((long)(i * g.kw + j) * g.Ci + ci) * g.Co + co0 + 4 * kc_c4);
-                    rb[4 * ip + 0] = v[0]; rb[4 * ip + 1] = v[1]; rb[4 * ip + 2] = v[2]; rb[4 * ip + 3] = v[3];
+                    bool ok = tapok && ci < p.N;
+                    unsigned off = ((unsigned)((i * g.kw + j) * g.Ci + ci) * g.Co + co0 + 4 * kc_c4) * 4u;
+                    put4(rb, ip, bload4(rB, ok ? off : DG_OOB));
                 }
             } else {
                 int k = k0 + ks_kk;
@@ -313,9 +311,9 @@ k_conv_gemm(const GemmArgs p) {
 #pragma unroll
                 for (int e = 0; e < B_NES; ++e) {
                     int ci = n0 + ks_r0 + 8 * e;
-                    float v = 0.f;
-                    if (kok && ci < p.N) v = p.B[((long)(i * g.kw + j) * g.Ci + ci) * g.Co + co];
-                    rb[e] = v;
+                    bool ok = kok && ci < p.N;
+                    unsigned off = ((unsigned)((i * g.kw + j) * g.Ci + ci) * g.Co + co) * 4u;
+                    rb[e] = bload1(rB, ok ? off : DG_OOB);
                 }
             }
         } else {  // WGRAD: dy rows (pixels) contiguous along co
@@ -323,9 +321,8 @@ k_conv_gemm(const GemmArgs p) {
             for (int ip = 0; ip < BR_NP; ++ip) {
                 int pix = k0 + br_kr + BR_RPP * ip;
                 int col = n0 + 4 * br_c4;
-                f32x4 v = {0.f, 0.f, 0.f, 0.f};
-                if (pix < kend && col < p.N) v = *reinterpret_cast<const f32x4 *>(p.B + (long)pix * p.ldb + col);
-                rb[4 * ip + 0] = v[0]; rb[4 * ip + 1] = v[1]; rb[4 * ip + 2] = v[2]; rb[4 * ip + 3] = v[3];
+                bool ok = pix < kend && col < p.N;
+                put4(rb, ip, bload4(rB, ok ? ((unsigned)pix * p.ldb + col) * 4u : DG_OOB));
             }
         }
     };
@@ -382,30 +379,51 @@ k_conv_gemm(const GemmArgs p) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
+    // Pipeline (one barrier per K-tile): at the top of iteration kt, LDS buffer
+    // kt%2 holds tile kt and the staging registers hold tile kt+1 (loads in
+    // flight).  The MFMA chain of tile kt is split in two; between the halves
+    // the wave writes tile kt+1 into the other buffer (free: every wave passed
+    // the barrier after its last read of it) and issues the loads of tile kt+2,
+    // so the matrix pipe keeps running across the staging work.
     load_tiles(kbeg);
     store_tiles(0);
+    if (nk > 1) load_tiles(kbeg + BK);
     __syncthreads();
 
     for (int kt = 0; kt < nk; ++kt) {
         const int buf = kt & 1;
-        const bool more = (kt + 1) < nk;
-        if (more) load_tiles(kbeg + (kt + 1) * BK);
-        const float *As = smem + buf * (ASZ + BSZ);
-        const float *Bs = As + ASZ;
+        const float *As = smem + buf * (ASZ + BSZ) + h2 * LDA + wm * WTM + l32;
+        const float *Bs = smem + buf * (ASZ + BSZ) + ASZ + h2 * LDB + wn * WTN + l32;
+        // all fragments of the K-tile first (one LDS round trip), then the MFMA chain
+        float af[BK / 2][TM], bf[BK / 2][TN];
 #pragma unroll
-        for (int kk = 0; kk < BK; kk += 2) {
-            float af[TM], bf[TN];
+        for (int s2 = 0; s2 < BK / 2; ++s2) {
 #pragma unroll
-            for (int a = 0; a < TM; ++a) af[a] = As[(kk + h2) * LDA + wm * WTM + a * 32 + l32];
+            for (int a = 0; a < TM; ++a) af[s2][a] = As[2 * s2 * LDA + a * 32];
 #pragma unroll
-            for (int b = 0; b < TN; ++b) bf[b] = Bs[(kk + h2) * LDB + wn * WTN + b * 32 + l32];
+            for (int b = 0; b < TN; ++b) bf[s2][b] = Bs[2 * s2 * LDB + b * 32];
+        }
+        // keep the whole read block ahead of the MFMA chain (the scheduler would
+        // otherwise sink each read next to its MFMA and expose LDS latency per k-step)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s2 = 0; s2 < BK / 4; ++s2)
 #pragma unroll
             for (int a = 0; a < TM; ++a)
 #pragma unroll
                 for (int b = 0; b < TN; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a], bf[b], acc[a][b], 0, 0, 0);
-        }
-        if (more) store_tiles(buf ^ 1);
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s2][a], bf[s2][b], acc[a][b], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + 1 < nk) store_tiles(buf ^ 1);
+        if (kt + 2 < nk) load_tiles(kbeg + (kt + 2) * BK);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s2 = BK / 4; s2 < BK / 2; ++s2)
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s2][a], bf[s2][b], acc[a][b], 0, 0, 0);
         __syncthreads();
     }
 
@@ -444,7 +462,7 @@ k_conv_gemm(const GemmArgs p) {
 // split-K reduction + epilogue (deterministic: slabs summed in split order)
 template <int MODE>
 __global__ void __launch_bounds__(256)
-k_splitk_reduce(const GemmArgs p) {
+k_splitk_reduce(const GemmArgs p, int V4) {
     const ConvGeom &g = p.g;
     const int phase = blockIdx.y;
     int Mrows = p.M;
@@ -453,9 +471,46 @@ k_splitk_reduce(const GemmArgs p) {
         ph = phase_info(g, phase, g.N);
         Mrows = ph.Mp;
     }
-    const long total = (long)Mrows * p.N;
     const long plane = (long)p.M * p.N;
     const float *base = p.slab + (long)phase * p.splits * plane;
+    if (V4) {  // N % 4 == 0, ldc % 4 == 0, 16-byte aligned C: float4 outputs, V4 lanes per output
+        const int tpo = V4;  // power of two <= 16: lane j sums slabs j, j+tpo, ...; fixed butterfly after
+        const int lane = threadIdx.x & (tpo - 1);
+        const int N4 = p.N >> 2;
+        const long total = (long)Mrows * N4;
+        const long stride = ((long)gridDim.x * blockDim.x) / tpo;
+        for (long e = ((long)blockIdx.x * blockDim.x + threadIdx.x) / tpo; e < total; e += stride) {
+            const int row = (int)(e / N4);
+            const int col = (int)(e - (long)row * N4) * 4;
+            const float *src = base + (long)row * p.N + col;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            for (int s = lane; s < p.splits; s += tpo) v += *reinterpret_cast<const f32x4 *>(src + s * plane);
+            for (int o = tpo >> 1; o >= 1; o >>= 1) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] += __shfl_xor(v[q], o);
+            }
+            if (lane != 0) continue;
+            long off;
+            if constexpr (MODE == MODE_DGRAD) {
+                int ww = row % ph.Wp; int t = row / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
+                off = ((long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw) * p.ldc;
+            } else {
+                off = (long)row * p.ldc;
+            }
+            f32x4 o;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float x = v[q];
+                if (p.bias) x += p.bias[col + q];
+                o[q] = act_fwd(x, p.act, p.alpha);
+            }
+            f32x4 *dst = reinterpret_cast<f32x4 *>(p.C + off + col);
+            if (p.beta != 0.f) o += p.beta * (*dst);
+            *dst = o;
+        }
+        return;
+    }
+    const long total = (long)Mrows * p.N;
     for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
         int row = (int)(e / p.N);
         int col = (int)(e - (long)row * p.N);
@@ -1008,7 +1063,7 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
             hipLaunchKernelGGL(k_narrow_wgrad, dim3(d->g.kh * d->g.kw * ((d->g.Ci + 255) / 256), pl.splits), dim3(256), 0, s, a);
             DG_LAUNCHED("narrow_wgrad");
             long total = (long)pl.M * pl.N;
-            hipLaunchKernelGGL(k_splitk_reduce<MODE_WGRAD>, dim3((unsigned)std::min<long>(dg_cdiv(total, 256), 2048), 1), dim3(256), 0, s, a);
+            hipLaunchKernelGGL(k_splitk_reduce<MODE_WGRAD>, dim3((unsigned)std::min<long>(dg_cdiv(total, 256), 2048), 1), dim3(256), 0, s, a, 0);
             DG_LAUNCHED("narrow_wgrad_reduce");
         }
         return DG_OK;
@@ -1016,9 +1071,28 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
     return run_gemm(mode, pl, a, s);
 }
 
-static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a, hipStream_t s) {
+static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_t s) {
+    GemmArgs a = a_in;
     const float *A = a.A, *B = a.B;
     const int lda = a.lda, ldb = a.ldb;
+    {   // operand extents for the buffer-resource range checks
+        const ConvGeom &g = a.g;
+        const long xin = (long)g.N * g.H * g.W, xout = (long)g.N * g.Ho * g.Wo;
+        long ab, bb;
+        if (mode == MODE_FWD) {
+            ab = ((xin - 1) * lda + g.Ci) * 4;
+            bb = ((long)(pl.K - 1) * ldb + pl.N) * 4;
+        } else if (mode == MODE_DGRAD) {
+            ab = ((xout - 1) * lda + g.Co) * 4;
+            bb = (long)g.kh * g.kw * g.Ci * g.Co * 4;
+        } else {
+            ab = ((xin - 1) * lda + g.Ci) * 4;
+            bb = ((xout - 1) * ldb + g.Co) * 4;
+        }
+        DG_ARG(ab < (1L << 31) && bb < (1L << 31), "operand larger than 2 GiB (buffer-resource offsets are 32-bit)");
+        a.a_bytes = (unsigned)ab;
+        a.b_bytes = (unsigned)bb;
+    }
     if (mode == MODE_FWD || mode == MODE_WGRAD) {
         DG_ARG(pl.N % 4 == 0 && ldb % 4 == 0, "GEMM N (%d) and ldb (%d) must be multiples of 4", pl.N, ldb);
     }
@@ -1034,12 +1108,19 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a, hipStream_t s
     }
     DG_LAUNCHED("conv_gemm");
     if (pl.splits > 1) {
-        long total = (long)pl.M * pl.N;
+        // float4 outputs with tpo lanes per output (tpo = 0 -> scalar path)
+        int tpo = 0;
+        if ((pl.N % 4 == 0) && (a.ldc % 4 == 0) && ((((uintptr_t)a.C) | ((uintptr_t)a.slab)) & 15) == 0) {
+            tpo = 1;
+            while (tpo < 16 && tpo * 4 <= pl.splits) tpo <<= 1;
+        }
+        const int v4 = tpo;
+        long total = tpo ? (long)pl.M * pl.N / 4 * tpo : (long)pl.M * pl.N;
         dim3 rg((unsigned)std::min<long>(dg_cdiv(total, 256), 4096), pl.nphase);
         switch (mode) {
-        case MODE_FWD: hipLaunchKernelGGL(k_splitk_reduce<MODE_FWD>, rg, dim3(256), 0, s, a); break;
-        case MODE_DGRAD: hipLaunchKernelGGL(k_splitk_reduce<MODE_DGRAD>, rg, dim3(256), 0, s, a); break;
-        default: hipLaunchKernelGGL(k_splitk_reduce<MODE_WGRAD>, rg, dim3(256), 0, s, a); break;
+        case MODE_FWD: hipLaunchKernelGGL(k_splitk_reduce<MODE_FWD>, rg, dim3(256), 0, s, a, v4); break;
+        case MODE_DGRAD: hipLaunchKernelGGL(k_splitk_reduce<MODE_DGRAD>, rg, dim3(256), 0, s, a, v4); break;
+        default: hipLaunchKernelGGL(k_splitk_reduce<MODE_WGRAD>, rg, dim3(256), 0, s, a, v4); break;
         }
         DG_LAUNCHED("splitk_reduce");
     }
