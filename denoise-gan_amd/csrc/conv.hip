@@ -21,77 +21,20 @@
 // staged global -> registers -> LDS (double buffered, one barrier per
 // K-tile), stored k-major ([k][m], [k][n]) so every MFMA operand fetch is a
 // conflict-free ds_read_b32 of 32 consecutive floats per half-wave.
-#include "common.h"
+#include "conv_impl.h"
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <new>
 
 namespace dg {
 
-enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
-
-struct ConvGeom {
-    int N, H, W, Ci;  // conv-view input
-    int Ho, Wo, Co;   // conv-view output
-    int kh, kw, sh, sw, pt, pl;
-    int Th, Tw;       // DGRAD taps per phase
-};
-
-struct GemmArgs {
-    ConvGeom g;
-    const float *A; int lda;
-    const float *B; int ldb;
-    float *C; int ldc;
-    const float *bias;
-    float beta; int act; float alpha;
-    int M, N, K;       // GEMM dims; DGRAD: M = max rows over phases
-    int kchunk;        // K per split (multiple of BK)
-    int splits;
-    int mtiles, ntiles;
-    int nphase;
-    float *slab;       // split-K partials [nphase*splits][M][N]
-    unsigned a_bytes, b_bytes;  // extents of A and B for the buffer-resource range check
-};
-
-// Branch-free operand loads: raw buffer loads through a resource whose range
-// check returns 0 for an out-of-range offset, so padding taps and ragged tile
-// edges need no exec-masked branches (an invalid element is given DG_OOB).
-constexpr unsigned DG_OOB = 0x80000000u;
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-__device__ __forceinline__ rsrc_t make_rsrc(const float *base, unsigned bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ f32x4 bload4(rsrc_t r, unsigned byte_off) {
-    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
-}
-__device__ __forceinline__ float bload1(rsrc_t r, unsigned byte_off) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
-}
-
-struct PhaseInfo {
-    int ph, pw, Hp, Wp, Mp, i0h, i0w;
-};
-
-__device__ __forceinline__ PhaseInfo phase_info(const ConvGeom &g, int phase, int N) {
-    PhaseInfo q;
-    q.ph = phase / g.sw;
-    q.pw = phase - q.ph * g.sw;
-    q.Hp = (g.H - q.ph + g.sh - 1) / g.sh;
-    q.Wp = (g.W - q.pw + g.sw - 1) / g.sw;
-    if (q.Hp < 0) q.Hp = 0;
-    if (q.Wp < 0) q.Wp = 0;
-    q.Mp = N * q.Hp * q.Wp;
-    q.i0h = ((q.ph + g.pt) % g.sh + g.sh) % g.sh;
-    q.i0w = ((q.pw + g.pl) % g.sw + g.sw) % g.sw;
-    return q;
-}
-
 // -------------------------------------------------------------------------
 // The MFMA implicit-GEMM kernel
 // -------------------------------------------------------------------------
-template <int MODE, int BM, int BN, int WGM, int WGN, bool VEC>
-__global__ void __launch_bounds__(256)
+template <int MODE, int BM, int BN, int WGM, int WGN, bool VEC, int BK, int MINW>
+__global__ void __launch_bounds__(256, MINW)
 k_conv_gemm(const GemmArgs p) {
-    constexpr int BK = 32;
     constexpr bool A_KC = (MODE != MODE_WGRAD);  // A rows contiguous along k
     constexpr bool B_KC = (MODE == MODE_DGRAD);  // B rows (n) contiguous along k
     constexpr int LDA = A_KC ? BM + 1 : BM + 4;
@@ -102,6 +45,8 @@ k_conv_gemm(const GemmArgs p) {
     constexpr int TM = WTM / 32, TN = WTN / 32;
     static_assert(WGM * WGN == 4, "4 waves");
     static_assert(TM >= 1 && TN >= 1, "wave tile >= 32x32");
+    static_assert(BK % 4 == 0 && BM >= 256 / (BK / 4) && BN >= 256 / (BK / 4), "KC loader geometry");
+    static_assert(1024 / BM <= BK && 1024 / BN <= BK, "RC loader geometry");
 
     __shared__ __attribute__((aligned(16))) float smem[2 * (ASZ + BSZ)];
 
@@ -134,14 +79,16 @@ k_conv_gemm(const GemmArgs p) {
 
     // ---------------- A operand -----------------
     // KC (FWD / DGRAD): tile BM rows x BK, row r contiguous along k.
-    constexpr int A_NPV = BM / 32;          // vec rows per thread (8 threads per row)
+    constexpr int KC_TPR = BK / 4, KC_RPP = 256 / KC_TPR;  // KC vec: threads per row, rows per pass
+    constexpr int KS_RPP = 256 / BK;                        // KC scalar: rows per pass
+    constexpr int A_NPV = BM / KC_RPP;      // vec rows per thread
     constexpr int A_NES = BM * BK / 256;    // scalar elements per thread
     // RC (WGRAD): tile BK k-rows x BM, contiguous along m.
     constexpr int AR_TPR = BM / 4, AR_RPP = 256 / AR_TPR, AR_NP = BK / AR_RPP;
     constexpr int AR_NES = BM * BK / 256;
 
     // ---------------- B operand -----------------
-    constexpr int B_NPV = BN / 32;          // KC vec rows per thread (DGRAD)
+    constexpr int B_NPV = BN / KC_RPP;      // KC vec rows per thread (DGRAD)
     constexpr int B_NES = BN * BK / 256;    // KC scalar elements per thread (DGRAD)
     constexpr int BR_TPR = BN / 4, BR_RPP = 256 / BR_TPR, BR_NP = BK / BR_RPP;  // RC vec
 
@@ -153,16 +100,16 @@ k_conv_gemm(const GemmArgs p) {
 
     // ---- per-thread precomputation ----
     // KC vec: thread -> (row rr + 32*ip, k-chunk c4)
-    const int kc_c4 = tid & 7, kc_rr = tid >> 3;
+    const int kc_c4 = tid % KC_TPR, kc_rr = tid / KC_TPR;
     // KC scalar: thread -> (kk = tid % 32, rows r0 + 8*e)
-    const int ks_kk = tid & 31, ks_r0 = tid >> 5;
+    const int ks_kk = tid % BK, ks_r0 = tid / BK;
 
     // row geometry for the A operand (FWD/DGRAD vec path), up to 4 rows
     int arow_n[A_NPV > 0 ? A_NPV : 1], arow_h[A_NPV > 0 ? A_NPV : 1], arow_w[A_NPV > 0 ? A_NPV : 1];
     if constexpr (A_KC && VEC) {
 #pragma unroll
         for (int ip = 0; ip < A_NPV; ++ip) {
-            int m = m0 + kc_rr + 32 * ip;
+            int m = m0 + kc_rr + KC_RPP * ip;
             if (m < Mrows) {
                 if constexpr (MODE == MODE_FWD) {
                     int wo = m % g.Wo; int t = m / g.Wo; int ho = t % g.Ho; int n = t / g.Ho;
@@ -206,11 +153,28 @@ k_conv_gemm(const GemmArgs p) {
         r[4 * ip + 0] = v[0]; r[4 * ip + 1] = v[1]; r[4 * ip + 2] = v[2]; r[4 * ip + 3] = v[3];
     };
 
+    // VEC FWD/DGRAD walk the K-tiles channel-chunk-major (all taps of one
+    // BK-channel chunk, then the next chunk): a block's input window for one
+    // chunk (~30 KB) is re-read by the next kh*kw tiles while it is still in
+    // L1/L2, instead of once per tap after the whole channel range streamed by.
+    // k0 is the position in that walk; kr0 the real (tap, channel) K index.
+    auto k_real = [&](int k0) -> int {
+        if constexpr (VEC && MODE != MODE_WGRAD) {
+            const int C = MODE == MODE_FWD ? g.Ci : g.Co;
+            const int ntap = MODE == MODE_FWD ? g.kh * g.kw : g.Th * g.Tw;
+            int kk = k0 / BK; int chunk = kk / ntap; int tap = kk - chunk * ntap;
+            return tap * C + chunk * BK;
+        } else {
+            return k0;
+        }
+    };
+
     auto load_tiles = [&](int k0) {
+        const int kr0 = k_real(k0);
         // ----- A -----
         if constexpr (MODE == MODE_FWD) {
             if constexpr (VEC) {
-                int tap = k0 / g.Ci; int ci0 = k0 - tap * g.Ci;
+                int tap = kr0 / g.Ci; int ci0 = kr0 - tap * g.Ci;
                 int i = tap / g.kw; int j = tap - i * g.kw;
 #pragma unroll
                 for (int ip = 0; ip < A_NPV; ++ip) {
@@ -226,7 +190,7 @@ k_conv_gemm(const GemmArgs p) {
                 bool kok = k < kend;
 #pragma unroll
                 for (int e = 0; e < A_NES; ++e) {
-                    int m = m0 + ks_r0 + 8 * e;
+                    int m = m0 + ks_r0 + KS_RPP * e;
                     int wo = m % g.Wo; int t = m / g.Wo; int ho = t % g.Ho; int n = t / g.Ho;
                     int hi = ho * g.sh - g.pt + i, wi = wo * g.sw - g.pl + j;
                     bool ok = kok && m < Mrows && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
@@ -236,7 +200,7 @@ k_conv_gemm(const GemmArgs p) {
             }
         } else if constexpr (MODE == MODE_DGRAD) {
             if constexpr (VEC) {
-                int i, j, co0; dgrad_tap(k0, i, j, co0);
+                int i, j, co0; dgrad_tap(kr0, i, j, co0);
                 bool tapok = (i < g.kh) && (j < g.kw);
 #pragma unroll
                 for (int ip = 0; ip < A_NPV; ++ip) {
@@ -252,7 +216,7 @@ k_conv_gemm(const GemmArgs p) {
                 bool kok = (k < kend) && (i < g.kh) && (j < g.kw);
 #pragma unroll
                 for (int e = 0; e < A_NES; ++e) {
-                    int m = m0 + ks_r0 + 8 * e;
+                    int m = m0 + ks_r0 + KS_RPP * e;
                     int ww = m % ph.Wp; int t = m / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
                     int th = hh * g.sh + ph.ph + g.pt - i, tw = ww * g.sw + ph.pw + g.pl - j;
                     int ho = th / g.sh, wo = tw / g.sw;
@@ -288,18 +252,18 @@ k_conv_gemm(const GemmArgs p) {
         if constexpr (MODE == MODE_FWD) {  // w rows k contiguous along co
 #pragma unroll
             for (int ip = 0; ip < BR_NP; ++ip) {
-                int k = k0 + br_kr + BR_RPP * ip;
+                int k = kr0 + br_kr + BR_RPP * ip;
                 int col = n0 + 4 * br_c4;
-                bool ok = k < kend && col < p.N;
+                bool ok = (VEC || k < kend) && col < p.N;
                 put4(rb, ip, bload4(rB, ok ? ((unsigned)k * p.ldb + col) * 4u : DG_OOB));
             }
         } else if constexpr (MODE == MODE_DGRAD) {  // w[i,j,ci,co]: rows ci contiguous along co
             if constexpr (VEC) {
-                int i, j, co0; dgrad_tap(k0, i, j, co0);
+                int i, j, co0; dgrad_tap(kr0, i, j, co0);
                 bool tapok = (i < g.kh) && (j < g.kw);
 #pragma unroll
                 for (int ip = 0; ip < B_NPV; ++ip) {
-                    int ci = n0 + kc_rr + 32 * ip;
+                    int ci = n0 + kc_rr + KC_RPP * ip;
                     bool ok = tapok && ci < p.N;
                     unsigned off = ((unsigned)((i * g.kw + j) * g.Ci + ci) * g.Co + co0 + 4 * kc_c4) * 4u;
                     put4(rb, ip, bload4(rB, ok ? off : DG_OOB));
@@ -310,7 +274,7 @@ k_conv_gemm(const GemmArgs p) {
                 bool kok = (k < kend) && (i < g.kh) && (j < g.kw);
 #pragma unroll
                 for (int e = 0; e < B_NES; ++e) {
-                    int ci = n0 + ks_r0 + 8 * e;
+                    int ci = n0 + ks_r0 + KS_RPP * e;
                     bool ok = kok && ci < p.N;
                     unsigned off = ((unsigned)((i * g.kw + j) * g.Ci + ci) * g.Co + co) * 4u;
                     rb[e] = bload1(rB, ok ? off : DG_OOB);
@@ -335,10 +299,10 @@ k_conv_gemm(const GemmArgs p) {
 #pragma unroll
                 for (int ip = 0; ip < A_NPV; ++ip)
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) As[(4 * kc_c4 + q) * LDA + kc_rr + 32 * ip] = ra[4 * ip + q];
+                    for (int q = 0; q < 4; ++q) As[(4 * kc_c4 + q) * LDA + kc_rr + KC_RPP * ip] = ra[4 * ip + q];
             } else {
 #pragma unroll
-                for (int e = 0; e < A_NES; ++e) As[ks_kk * LDA + ks_r0 + 8 * e] = ra[e];
+                for (int e = 0; e < A_NES; ++e) As[ks_kk * LDA + ks_r0 + KS_RPP * e] = ra[e];
             }
         } else {
             if constexpr (VEC) {
@@ -357,10 +321,10 @@ k_conv_gemm(const GemmArgs p) {
 #pragma unroll
                 for (int ip = 0; ip < B_NPV; ++ip)
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) Bs[(4 * kc_c4 + q) * LDB + kc_rr + 32 * ip] = rb[4 * ip + q];
+                    for (int q = 0; q < 4; ++q) Bs[(4 * kc_c4 + q) * LDB + kc_rr + KC_RPP * ip] = rb[4 * ip + q];
             } else {
 #pragma unroll
-                for (int e = 0; e < B_NES; ++e) Bs[ks_kk * LDB + ks_r0 + 8 * e] = rb[e];
+                for (int e = 0; e < B_NES; ++e) Bs[ks_kk * LDB + ks_r0 + KS_RPP * e] = rb[e];
             }
         } else {
 #pragma unroll
@@ -427,36 +391,7 @@ k_conv_gemm(const GemmArgs p) {
         __syncthreads();
     }
 
-    // ---------------- epilogue -----------------
-#pragma unroll
-    for (int a = 0; a < TM; ++a) {
-#pragma unroll
-        for (int b = 0; b < TN; ++b) {
-            const int col = n0 + wn * WTN + b * 32 + l32;
-            if (col >= p.N) continue;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = m0 + wm * WTM + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h2;
-                if (row >= Mrows) continue;
-                float v = acc[a][b][r];
-                if (p.splits > 1) {
-                    p.slab[((long)(phase * p.splits + split) * p.M + row) * p.N + col] = v;
-                } else {
-                    long off;
-                    if constexpr (MODE == MODE_DGRAD) {
-                        int ww = row % ph.Wp; int t = row / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
-                        off = ((long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw) * p.ldc;
-                    } else {
-                        off = (long)row * p.ldc;
-                    }
-                    if (p.bias) v += p.bias[col];
-                    v = act_fwd(v, p.act, p.alpha);
-                    if (p.beta != 0.f) v += p.beta * p.C[off + col];
-                    p.C[off + col] = v;
-                }
-            }
-        }
-    }
+    conv_epilogue<MODE, TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, Mrows, ph, phase, split, l32, h2);
 }
 
 // split-K reduction + epilogue (deterministic: slabs summed in split order)
@@ -795,16 +730,29 @@ k_recast_wgrad_gather(const GemmArgs p, const float *__restrict__ dy, int lddy, 
 // -------------------------------------------------------------------------
 // Host side: descriptor, planner, launch
 // -------------------------------------------------------------------------
+// tile configs: block tile, wave grid, K-tile depth, min waves/SIMD (register budget),
+// resident blocks per CU (LDS / registers), relative cost per FLOP (measured on MI355X)
 struct TileCfg {
-    int bm, bn, wgm, wgn;
+    int bm, bn, wgm, wgn, bk, minw, bpc;
+    double eff;
 };
 static const TileCfg kCfgs[] = {
-    {128, 128, 2, 2}, {128, 64, 2, 2}, {64, 128, 2, 2}, {64, 64, 2, 2}, {32, 128, 1, 4},
+    {128, 128, 2, 2, 32, 2, 2, 1.00}, {128, 64, 2, 2, 32, 2, 2, 1.12}, {64, 128, 2, 2, 32, 2, 2, 1.12},
+    {64, 64, 2, 2, 32, 2, 3, 1.35},   {32, 128, 1, 4, 32, 2, 3, 1.50}, {128, 128, 2, 2, 16, 3, 3, 1.00},
+    {128, 64, 2, 2, 16, 3, 3, 1.12},
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
+// bf16x6 kernel configs (conv_x6.hip launch_gemm_x6), K-tile 16
+static const TileCfg kX6Cfgs[] = {
+    {128, 128, 2, 2, 16, 2, 2, 1.00}, {128, 64, 2, 2, 16, 2, 3, 1.15}, {64, 128, 2, 2, 16, 2, 3, 1.15},
+    {64, 64, 2, 2, 16, 3, 4, 1.40},   {128, 128, 2, 2, 16, 3, 3, 1.00}, {256, 128, 4, 2, 16, 2, 1, 1.00},
+    {128, 256, 2, 4, 16, 2, 1, 1.00},
+};
+constexpr int kNumX6Cfgs = sizeof(kX6Cfgs) / sizeof(kX6Cfgs[0]);
 
 struct OpPlan {
     int narrow;      // 1 => VALU narrow kernel
+    int x6;          // 1 => bf16x6 split-precision kernel (kX6Cfgs), else fp32 MFMA (kCfgs)
     int cfg;         // tile config index
     int vec;
     int splits, kchunk;
@@ -832,6 +780,7 @@ struct Recast {
 
 struct dg_conv_desc_s {
     int transpose;
+    int math;                        // DG_MATH_*
     int N, H, W, Cin, Cout, Ho, Wo;  // layer view
     dg::ConvGeom g;                  // conv view
     dg::OpPlan plan[3];              // indexed by DG_OP_*
@@ -846,24 +795,27 @@ static int engine_mode(const dg_conv_desc_s *d, int op) {
     return op == DG_OP_FWD ? MODE_DGRAD : (op == DG_OP_BWD_DATA ? MODE_FWD : MODE_WGRAD);
 }
 
-static OpPlan make_plan(const ConvGeom &g, int mode) {
+static bool cfg_vec(const ConvGeom &g, int mode, int bk) {
+    if (mode == MODE_FWD) return g.Ci % bk == 0;
+    if (mode == MODE_DGRAD) return g.Co % bk == 0;
+    return g.Ci % 4 == 0;
+}
+
+static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     OpPlan pl{};
-    const int BK = 32;
     if (mode == MODE_FWD) {
         pl.M = g.N * g.Ho * g.Wo; pl.N = g.Co; pl.K = g.kh * g.kw * g.Ci; pl.nphase = 1;
-        pl.vec = (g.Ci % BK == 0);
         pl.narrow = g.Co < 8;
     } else if (mode == MODE_DGRAD) {
         pl.nphase = g.sh * g.sw;
         int Hp = (g.H + g.sh - 1) / g.sh, Wp = (g.W + g.sw - 1) / g.sw;
         pl.M = g.N * Hp * Wp; pl.N = g.Ci; pl.K = g.Th * g.Tw * g.Co;
-        pl.vec = (g.Co % BK == 0);
         pl.narrow = g.Ci < 8;
     } else {
         pl.M = g.kh * g.kw * g.Ci; pl.N = g.Co; pl.K = g.N * g.Ho * g.Wo; pl.nphase = 1;
-        pl.vec = (g.Ci % 4 == 0);
         pl.narrow = g.Co < 8;
     }
+    pl.vec = cfg_vec(g, mode, 32);
     if (pl.narrow) {
         pl.splits = 1; pl.kchunk = pl.K; pl.ws_bytes = 0; pl.slab_bytes = 0;
         if (mode == MODE_WGRAD) {
@@ -877,33 +829,46 @@ static OpPlan make_plan(const ConvGeom &g, int mode) {
         }
         return pl;
     }
-    // choose the tile: model each candidate's time as
-    //   rounds of 512 resident blocks x per-block MFMA time  +  slab traffic
-    const long target = 512;
-    const double slot_flops = 157.3e12 * 0.6 / 512.0;  // per resident block
+    // Tile + split-K choice.  Modelled time of a candidate:
+    //   rounds x (blocks per CU x per-block MFMA work) / (CU peak x occupancy efficiency)
+    // + split-K slab traffic, where blocks per CU = min(resident limit, blocks / 256).
+    // bf16x6 needs whole 16-wide K-tiles inside one tap (FWD / DGRAD) and
+    // 4-aligned column quads (WGRAD)
+    pl.x6 = math == DG_MATH_BF16X6 &&
+            (mode == MODE_FWD ? g.Ci % 16 == 0 : mode == MODE_DGRAD ? g.Co % 16 == 0 : (g.Ci % 4 == 0 && g.Co % 4 == 0));
+    const TileCfg *cfgs = pl.x6 ? kX6Cfgs : kCfgs;
+    const int ncfg = pl.x6 ? kNumX6Cfgs : kNumCfgs;
+    // fp32 MFMA peak per CU; bf16x6 = six bf16 products per fp32 product
+    const double cu_flops = (pl.x6 ? 2516.6e12 / 6.0 : 157.3e12) / 256.0;
+    static const double occ_eff[] = {0.0, 0.62, 0.80, 0.88, 0.92};
+    int forced = -1;
+    if (const char *f = getenv(pl.x6 ? "DG_FORCE_X6CFG" : "DG_FORCE_CFG")) forced = atoi(f);
     int best = -1; double best_t = 1e30; long best_splits = 1;
-    for (int c = 0; c < kNumCfgs; ++c) {
-        const TileCfg &t = kCfgs[c];
-        if (pl.N <= 64 && t.bn > 64) continue;
+    for (int c = 0; c < ncfg; ++c) {
+        const TileCfg &t = cfgs[c];
+        if (forced >= 0 && c != forced) continue;
+        if (forced < 0 && pl.N <= 64 && t.bn > 64) continue;
         long mt = (pl.M + t.bm - 1) / t.bm, nt = (pl.N + t.bn - 1) / t.bn;
         long tiles = mt * nt * pl.nphase;
-        long ktiles = (pl.K + BK - 1) / BK;
-        long splits = 1;
-        if (tiles < target) splits = std::min<long>((target + tiles - 1) / tiles, std::max<long>(1, ktiles / 4));
-        long kt_per = (ktiles + splits - 1) / splits;
-        long blocks = tiles * splits;
-        double eff = (t.bm == 128 && t.bn == 128) ? 1.0 : (t.bm * t.bn >= 8192 ? 1.15 : 1.45);
-        double rounds = std::ceil((double)blocks / (double)target);
-        double tc = rounds * 2.0 * t.bm * t.bn * kt_per * BK * eff / slot_flops;
-        double ts = splits > 1 ? (double)splits * pl.nphase * pl.M * pl.N * 8.0 / 4.0e12 : 0.0;
-        if (tc + ts < best_t) { best_t = tc + ts; best = c; best_splits = splits; }
+        long ktiles = (pl.K + t.bk - 1) / t.bk;
+        for (long splits = 1; splits <= std::max<long>(1, ktiles / 4); splits *= 2) {
+            long kt_per = (ktiles + splits - 1) / splits;
+            long blocks = tiles * splits;
+            long bpc = std::min<long>(t.bpc, (blocks + 255) / 256);
+            double rounds = std::ceil((double)blocks / (256.0 * bpc));
+            double tc = rounds * bpc * 2.0 * t.bm * t.bn * kt_per * t.bk * t.eff / (cu_flops * occ_eff[bpc]);
+            double ts = splits > 1 ? (double)splits * pl.nphase * pl.M * pl.N * 8.0 / 5.0e12 + 2e-6 : 0.0;
+            if (tc + ts < best_t) { best_t = tc + ts; best = c; best_splits = splits; }
+            if (blocks >= 1024) break;
+        }
     }
+    if (best < 0) best = 0;
     pl.cfg = best;
-    pl.splits = (int)best_splits;
-    const TileCfg &t = kCfgs[best];
-    long ktiles = (pl.K + BK - 1) / BK;
-    long kt_per = (ktiles + pl.splits - 1) / pl.splits;
-    pl.kchunk = (int)(kt_per * BK);
+    const TileCfg &t = cfgs[best];
+    pl.vec = pl.x6 ? 1 : cfg_vec(g, mode, t.bk);
+    long ktiles = (pl.K + t.bk - 1) / t.bk;
+    long kt_per = (ktiles + best_splits - 1) / best_splits;
+    pl.kchunk = (int)(kt_per * t.bk);
     pl.splits = (int)((ktiles + kt_per - 1) / kt_per);
     pl.mtiles = (pl.M + t.bm - 1) / t.bm;
     pl.ntiles = (pl.N + t.bn - 1) / t.bn;
@@ -934,7 +899,7 @@ static void plan_recast(dg_conv_desc_s *d, int op) {
         long P = (long)g.N * g.H * g.W;
         rc.nv = ntap; rc.mode1 = MODE_FWD;
         rc.g1 = geom_1x1(P, g.Ci, ntap);
-        rc.p1 = make_plan(rc.g1, MODE_FWD);
+        rc.p1 = make_plan(rc.g1, MODE_FWD, d->math);
         rc.wt_off = 0;
         rc.v_off = al256((size_t)g.Ci * ntap * 4);
         rc.slab_off = al256(rc.v_off + (size_t)P * ntap * 4);
@@ -944,7 +909,7 @@ static void plan_recast(dg_conv_desc_s *d, int op) {
         long P = (long)g.N * g.Ho * g.Wo;
         rc.nv = nv; rc.mode1 = MODE_FWD;
         rc.g1 = geom_1x1(P, g.Co, nv);
-        rc.p1 = make_plan(rc.g1, MODE_FWD);
+        rc.p1 = make_plan(rc.g1, MODE_FWD, d->math);
         rc.wt_off = 0;
         rc.v_off = al256((size_t)g.Co * nv * 4);
         rc.slab_off = al256(rc.v_off + (size_t)P * nv * 4);
@@ -953,7 +918,7 @@ static void plan_recast(dg_conv_desc_s *d, int op) {
         long P = (long)g.N * g.H * g.W;
         rc.nv = ntap; rc.mode1 = MODE_WGRAD;
         rc.g1 = geom_1x1(P, ntap, g.Ci);
-        rc.p1 = make_plan(rc.g1, MODE_WGRAD);
+        rc.p1 = make_plan(rc.g1, MODE_WGRAD, d->math);
         rc.wt_off = 0;
         rc.v_off = 0;
         rc.slab_off = al256((size_t)P * ntap * 4);
@@ -963,19 +928,47 @@ static void plan_recast(dg_conv_desc_s *d, int op) {
     rc.on = 1;
 }
 
+static size_t colsum_ws(long M, int C);
+
+// (re)plan the three ops of a descriptor for its math mode
+static void plan_all(dg_conv_desc_s *d) {
+    for (int op = 0; op < 3; ++op) {
+        d->plan[op] = make_plan(d->g, engine_mode(d, op), d->math);
+        plan_recast(d, op);
+        if (d->rc[op].on) d->plan[op].ws_bytes = d->rc[op].bytes;
+        if (op == DG_OP_BWD_FILTER) {
+            // room for the bias column sum partials after the split-K slabs
+            size_t extra = colsum_ws(1, d->Cout);
+            size_t base = d->rc[op].on ? d->rc[op].bytes : d->plan[op].slab_bytes;
+            d->plan[op].colsum_off = (base + 255) & ~(size_t)255;
+            d->plan[op].ws_bytes = d->plan[op].colsum_off + extra;
+        }
+    }
+}
+
+static int default_math() {
+    const char *m = getenv("DG_CONV_MATH");
+    if (m && (!strcmp(m, "fp32") || !strcmp(m, "0"))) return DG_MATH_FP32;
+    if (m && (!strcmp(m, "bf16x6") || !strcmp(m, "1"))) return DG_MATH_BF16X6;
+    return DG_MATH_FP32;
+}
+
+
 template <int MODE>
 static void launch_gemm(int cfg, int vec, dim3 grid, const GemmArgs &a, hipStream_t s) {
-#define DG_L(C, BM_, BN_, WM_, WN_)                                                           \
-    case C:                                                                                   \
-        if (vec) hipLaunchKernelGGL((k_conv_gemm<MODE, BM_, BN_, WM_, WN_, true>), grid, dim3(256), 0, s, a); \
-        else hipLaunchKernelGGL((k_conv_gemm<MODE, BM_, BN_, WM_, WN_, false>), grid, dim3(256), 0, s, a); \
+#define DG_L(C, BM_, BN_, WM_, WN_, BK_, MW_)                                                           \
+    case C:                                                                                             \
+        if (vec) hipLaunchKernelGGL((k_conv_gemm<MODE, BM_, BN_, WM_, WN_, true, BK_, MW_>), grid, dim3(256), 0, s, a); \
+        else hipLaunchKernelGGL((k_conv_gemm<MODE, BM_, BN_, WM_, WN_, false, BK_, MW_>), grid, dim3(256), 0, s, a); \
         break;
     switch (cfg) {
-        DG_L(0, 128, 128, 2, 2)
-        DG_L(1, 128, 64, 2, 2)
-        DG_L(2, 64, 128, 2, 2)
-        DG_L(3, 64, 64, 2, 2)
-        DG_L(4, 32, 128, 1, 4)
+        DG_L(0, 128, 128, 2, 2, 32, 2)
+        DG_L(1, 128, 64, 2, 2, 32, 2)
+        DG_L(2, 64, 128, 2, 2, 32, 2)
+        DG_L(3, 64, 64, 2, 2, 32, 2)
+        DG_L(4, 32, 128, 1, 4, 32, 2)
+        DG_L(5, 128, 128, 2, 2, 16, 3)
+        DG_L(6, 128, 64, 2, 2, 16, 3)
     }
 #undef DG_L
 }
@@ -1101,7 +1094,8 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
     }
     DG_ARG(((uintptr_t)B & 15) == 0 || mode == MODE_DGRAD, "B must be 16B aligned");
     dim3 grid(pl.mtiles * pl.ntiles, pl.nphase * pl.splits);
-    switch (mode) {
+    if (pl.x6) launch_gemm_x6(mode, pl.cfg, grid, a, s);
+    else switch (mode) {
     case MODE_FWD: launch_gemm<MODE_FWD>(pl.cfg, pl.vec, grid, a, s); break;
     case MODE_DGRAD: launch_gemm<MODE_DGRAD>(pl.cfg, pl.vec, grid, a, s); break;
     default: launch_gemm<MODE_WGRAD>(pl.cfg, pl.vec, grid, a, s); break;
@@ -1183,19 +1177,23 @@ int dg_conv_desc_create(dg_conv_t *out, int N, int H, int W, int Cin, int Cout, 
     }
     g.Th = (kh + sh - 1) / sh;
     g.Tw = (kw + sw - 1) / sw;
-    for (int op = 0; op < 3; ++op) {
-        d->plan[op] = dg::make_plan(g, dg::engine_mode(d, op));
-        dg::plan_recast(d, op);
-        if (d->rc[op].on) d->plan[op].ws_bytes = d->rc[op].bytes;
-        if (op == DG_OP_BWD_FILTER) {
-            // room for the bias column sum partials after the split-K slabs
-            size_t extra = dg::colsum_ws(1, Cout);
-            size_t base = d->rc[op].on ? d->rc[op].bytes : d->plan[op].slab_bytes;
-            d->plan[op].colsum_off = (base + 255) & ~(size_t)255;
-            d->plan[op].ws_bytes = d->plan[op].colsum_off + extra;
-        }
-    }
+    d->math = dg::default_math();
+    dg::plan_all(d);
     *out = d;
+    return DG_OK;
+}
+
+int dg_conv_set_math(dg_conv_t d, int math) {
+    DG_ARG(d != nullptr, "descriptor is NULL");
+    DG_ARG(math == DG_MATH_FP32 || math == DG_MATH_BF16X6, "unknown conv math mode %d", math);
+    d->math = math;
+    dg::plan_all(d);
+    return DG_OK;
+}
+
+int dg_conv_get_math(dg_conv_t d, int *math) {
+    DG_ARG(d != nullptr && math != nullptr, "NULL argument");
+    *math = d->math;
     return DG_OK;
 }
 

@@ -1,0 +1,108 @@
+// Shared device-side definitions of the conv engine (conv.hip: fp32 MFMA
+// kernels, planner and C ABI; conv_x6.hip: the bf16x6 split-precision kernel).
+#pragma once
+#include "common.h"
+
+namespace dg {
+
+enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+
+struct ConvGeom {
+    int N, H, W, Ci;  // conv-view input
+    int Ho, Wo, Co;   // conv-view output
+    int kh, kw, sh, sw, pt, pl;
+    int Th, Tw;       // DGRAD taps per phase
+};
+
+struct GemmArgs {
+    ConvGeom g;
+    const float *A; int lda;
+    const float *B; int ldb;
+    float *C; int ldc;
+    const float *bias;
+    float beta; int act; float alpha;
+    int M, N, K;       // GEMM dims; DGRAD: M = max rows over phases
+    int kchunk;        // K per split (multiple of BK)
+    int splits;
+    int mtiles, ntiles;
+    int nphase;
+    float *slab;       // split-K partials [nphase*splits][M][N]
+    unsigned a_bytes, b_bytes;  // extents of A and B for the buffer-resource range check
+};
+
+// Branch-free operand loads: raw buffer loads through a resource whose range
+// check returns 0 for an out-of-range offset, so padding taps and ragged tile
+// edges need no exec-masked branches (an invalid element is given DG_OOB).
+constexpr unsigned DG_OOB = 0x80000000u;
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t make_rsrc(const float *base, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4 bload4(rsrc_t r, unsigned byte_off) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+__device__ __forceinline__ float bload1(rsrc_t r, unsigned byte_off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
+
+struct PhaseInfo {
+    int ph, pw, Hp, Wp, Mp, i0h, i0w;
+};
+
+__device__ __forceinline__ PhaseInfo phase_info(const ConvGeom &g, int phase, int N) {
+    PhaseInfo q;
+    q.ph = phase / g.sw;
+    q.pw = phase - q.ph * g.sw;
+    q.Hp = (g.H - q.ph + g.sh - 1) / g.sh;
+    q.Wp = (g.W - q.pw + g.sw - 1) / g.sw;
+    if (q.Hp < 0) q.Hp = 0;
+    if (q.Wp < 0) q.Wp = 0;
+    q.Mp = N * q.Hp * q.Wp;
+    q.i0h = ((q.ph + g.pt) % g.sh + g.sh) % g.sh;
+    q.i0w = ((q.pw + g.pl) % g.sw + g.sw) % g.sw;
+    return q;
+}
+
+// Shared epilogue of the GEMM kernels: a wave's TM x TN 32x32 accumulator
+// tiles (MFMA C layout: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5))
+// written either to its split-K slab or through bias + activation + beta
+// accumulation into C (DGRAD rows scattered back to their phase pixels).
+template <int MODE, int TM, int TN>
+__device__ __forceinline__ void conv_epilogue(const GemmArgs &p, f32x16 (&acc)[TM][TN], int rbase, int cbase,
+                                              int Mrows, const PhaseInfo &ph, int phase, int split, int l32, int h2) {
+    const ConvGeom &g = p.g;
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+            const int col = cbase + b * 32 + l32;
+            if (col >= p.N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = rbase + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h2;
+                if (row >= Mrows) continue;
+                float v = acc[a][b][r];
+                if (p.splits > 1) {
+                    p.slab[((long)(phase * p.splits + split) * p.M + row) * p.N + col] = v;
+                } else {
+                    long off;
+                    if constexpr (MODE == MODE_DGRAD) {
+                        int ww = row % ph.Wp; int t = row / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
+                        off = ((long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw) * p.ldc;
+                    } else {
+                        off = (long)row * p.ldc;
+                    }
+                    if (p.bias) v += p.bias[col];
+                    v = act_fwd(v, p.act, p.alpha);
+                    if (p.beta != 0.f) v += p.beta * p.C[off + col];
+                    p.C[off + col] = v;
+                }
+            }
+        }
+    }
+}
+
+// launcher of the bf16x6 kernels (conv_x6.hip); cfg indexes kX6Cfgs
+void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s);
+
+}  // namespace dg

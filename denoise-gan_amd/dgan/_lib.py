@@ -26,6 +26,8 @@ _SIGS = {
     "dg_conv_desc_destroy": (c_int, [c_void_p]),
     "dg_conv_out_shape": (c_int, [c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     "dg_conv_workspace_size": (c_int, [c_void_p, c_int, ctypes.POINTER(c_size_t)]),
+    "dg_conv_set_math": (c_int, [c_void_p, c_int]),
+    "dg_conv_get_math": (c_int, [c_void_p, ctypes.POINTER(c_int)]),
     "dg_conv_fwd": (c_int, [c_void_p, _P, c_int, _P, _P, _P, c_int, c_float, c_int, c_float, _P, c_size_t, _P]),
     "dg_conv_bwd_data": (c_int, [c_void_p, _P, c_int, _P, _P, c_int, c_float, _P, c_size_t, _P]),
     "dg_conv_bwd_filter": (c_int, [c_void_p, _P, c_int, _P, c_int, _P, _P, c_float, _P, c_size_t, _P]),

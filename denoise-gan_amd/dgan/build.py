@@ -36,7 +36,7 @@ def _newer(src_paths, dst):
 
 def build(verbose=False, jobs=None):
     os.makedirs(OBJDIR, exist_ok=True)
-    deps = [os.path.join(CSRC, "common.h"), os.path.join(INCLUDE, "dgan.h")]
+    deps = [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")] + [os.path.join(INCLUDE, "dgan.h")]
     todo = []
     objs = []
     for f in _sources():

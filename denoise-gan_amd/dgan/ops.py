@@ -91,6 +91,11 @@ def default_workspace():
     return _default_ws[dev]
 
 
+# conv GEMM arithmetic (include/dgan.h DG_MATH_*)
+MATH_FP32, MATH_BF16X6 = 0, 1
+MATH_MODES = {"fp32": MATH_FP32, "bf16x6": MATH_BF16X6}
+
+
 class ConvDesc:
     """A Conv2D / Conv2DTranspose layer geometry (immutable), libdgan descriptor.
 
@@ -99,7 +104,7 @@ class ConvDesc:
     the output size the way TF's conv2d_transpose does.
     """
 
-    def __init__(self, N, H, W, Cin, Cout, kernel, strides=1, padding="same", transpose=False):
+    def __init__(self, N, H, W, Cin, Cout, kernel, strides=1, padding="same", transpose=False, math=None):
         kh, kw = (kernel, kernel) if isinstance(kernel, int) else kernel
         sh, sw = (strides, strides) if isinstance(strides, int) else strides
         if transpose:
@@ -133,6 +138,11 @@ class ConvDesc:
         ho, wo = ctypes.c_int(), ctypes.c_int()
         call("dg_conv_out_shape", h, ctypes.byref(ho), ctypes.byref(wo))
         self.Ho, self.Wo = ho.value, wo.value
+        if math is not None:
+            call("dg_conv_set_math", h, MATH_MODES[math] if isinstance(math, str) else int(math))
+        m = ctypes.c_int()
+        call("dg_conv_get_math", h, ctypes.byref(m))
+        self.math = m.value
         self.ws = []
         for op in (OP_FWD, OP_BWD_DATA, OP_BWD_FILTER):
             n = ctypes.c_size_t()

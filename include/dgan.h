@@ -33,7 +33,7 @@ extern "C" {
 #endif
 
 typedef void *dg_stream_t;                 /* hipStream_t (NULL = legacy stream) */
-typedef struct dg_conv_desc_s *dg_conv_t;  /* immutable once created */
+typedef struct dg_conv_desc_s *dg_conv_t;  /* shapes immutable once created */
 
 enum { DG_OK = 0, DG_ERR_ARG = 1, DG_ERR_HIP = 2, DG_ERR_WORKSPACE = 3, DG_ERR_UNSUPPORTED = 4 };
 
@@ -63,6 +63,18 @@ int dg_conv_desc_create(dg_conv_t *out, int N, int H, int W, int Cin, int Cout,
 int dg_conv_desc_destroy(dg_conv_t d);
 int dg_conv_out_shape(dg_conv_t d, int *Ho, int *Wo);
 int dg_conv_workspace_size(dg_conv_t d, int op, size_t *bytes);
+
+/* Arithmetic of the conv GEMMs (TF runs them in fp32).
+ *   DG_MATH_FP32   : v_mfma_f32_32x32x2_f32, exact fp32 FMA chains.
+ *   DG_MATH_BF16X6 : each fp32 operand split exactly into bf16 hi+mid+lo, the
+ *                    six piece products >= 2^-18 |ab| summed in the fp32 MFMA
+ *                    accumulator (dropped terms < 2^-26 |ab|, below fp32
+ *                    rounding) on the bf16 matrix cores, 2.7x the f32 MFMA rate.
+ * New descriptors take $DG_CONV_MATH ("fp32" | "bf16x6"; default fp32).
+ * Changing the mode re-plans the descriptor: query workspace sizes after it. */
+enum { DG_MATH_FP32 = 0, DG_MATH_BF16X6 = 1 };
+int dg_conv_set_math(dg_conv_t d, int math);
+int dg_conv_get_math(dg_conv_t d, int *math);
 
 /* y = act(conv(x, w) + bias) + beta * y            (bias may be NULL) */
 int dg_conv_fwd(dg_conv_t d, const float *x, int ldx, const float *w, const float *bias,

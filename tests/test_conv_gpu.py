@@ -3,8 +3,11 @@ plain PyTorch fp64 CPU reference of the same Keras layer, for every layer
 geometry of the pix2pix generator and discriminator (pix2pix.py:110-220)
 plus the SRGAN/FSRGAN shapes (k3 'same' with TF's asymmetric pads, k1).
 
-Tolerance (fp32 MFMA accumulation vs fp64): relative L2 error < 2e-6 and
-max-abs error < 1e-5 * max|ref| (scaled by sqrt(K/1024) for long K)."""
+Both conv arithmetics (include/dgan.h DG_MATH_*) are held to the same
+fp32-level tolerance: exact fp32 MFMA, and bf16x6 (fp32 operands split into
+three bf16 pieces, six piece products on the bf16 matrix cores).
+Tolerance vs fp64: relative L2 error < 2e-6 and max-abs error
+< 1e-5 * max|ref| (scaled by sqrt(K/1024) for long K)."""
 import math
 import zlib
 
@@ -46,13 +49,17 @@ def _close(got, ref, K, what):
     assert err <= tol * scale, f"{what}: max abs {err:.3e} vs scale {scale:.3e}"
 
 
+MATHS = ["fp32", "bf16x6"]
+
+
 @gpu
+@pytest.mark.parametrize("math_mode", MATHS)
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-def test_conv_layer(case):
+def test_conv_layer(case, math_mode):
     from dgan.ops import ConvDesc
     name, N, H, W, Cin, Cout, k, s, padding, transpose, has_bias = case
     torch.manual_seed(zlib.crc32(name.encode()))
-    d = ConvDesc(N, H, W, Cin, Cout, k, s, padding, transpose)
+    d = ConvDesc(N, H, W, Cin, Cout, k, s, padding, transpose, math=math_mode)
     x = torch.randn(N, H, W, Cin, dtype=torch.float64)
     w = torch.randn(*d.weight_shape, dtype=torch.float64) * 0.05
     b = torch.randn(Cout, dtype=torch.float64) if has_bias else None
@@ -89,13 +96,14 @@ def test_conv_layer(case):
 
 
 @gpu
-def test_conv_strided_views_and_accumulate():
+@pytest.mark.parametrize("math_mode", MATHS)
+def test_conv_strided_views_and_accumulate(math_mode):
     """Zero-copy concat: read a channel slice, write into a slice with beta=1."""
     from dgan.ops import ConvDesc
     torch.manual_seed(0)
     dev = torch.device("cuda")
     N, H, W, Cin, Cout = 2, 16, 16, 64, 128
-    d = ConvDesc(N, H, W, Cin, Cout, 4, 2, "same")
+    d = ConvDesc(N, H, W, Cin, Cout, 4, 2, "same", math=math_mode)
     big_in = torch.randn(N, H, W, Cin + 64, device=dev)
     x = big_in[..., 64:]
     w = torch.randn(*d.weight_shape, device=dev) * 0.05
@@ -134,3 +142,24 @@ def test_conv_fused_lrelu_epilogue():
     ref = torch.where(ref > 0, ref, 0.3 * ref)
     torch.cuda.synchronize()
     _close(y, ref, 1024, "lrelu epilogue")
+
+
+@gpu
+def test_bf16x6_error_matches_fp32():
+    """The split arithmetic's error vs fp64 stays at the fp32 path's level
+    (exact-fp32 inputs, so only the GEMM arithmetic differs)."""
+    from dgan.ops import ConvDesc
+    torch.manual_seed(7)
+    dev = torch.device("cuda")
+    N, H, W, Cin, Cout = 4, 16, 16, 256, 256
+    x = torch.randn(N, H, W, Cin).float()
+    errs = {}
+    for m in MATHS:
+        d = ConvDesc(N, H, W, Cin, Cout, 4, 1, (1, 1, 1, 1), math=m)
+        w = (torch.randn(*d.weight_shape, generator=torch.Generator().manual_seed(3)) * 0.05).float()
+        ref = conv2d_ref(x.double(), w.double(), 1, d.pads)
+        y = torch.empty(d.out_shape, device=dev)
+        d.fwd(x.to(dev), w.to(dev), y)
+        torch.cuda.synchronize()
+        errs[m] = ((y.double().cpu() - ref).norm() / ref.norm()).item()
+    assert errs["bf16x6"] < 2.0 * errs["fp32"] + 1e-9, errs
