@@ -57,10 +57,10 @@ k_conv_gemm(const GemmArgs p) {
     const int wm = wid / WGN, wn = wid % WGN;
     const int l32 = lane & 31, h2 = lane >> 5;
 
-    const int zz = blockIdx.y;
+    int zz, tile;
+    xcd_remap(zz, tile);
     const int phase = zz / p.splits;
     const int split = zz - phase * p.splits;
-    const int tile = blockIdx.x;
     const int mt = tile / p.ntiles;
     const int nt = tile - mt * p.ntiles;
     const int m0 = mt * BM, n0 = nt * BN;
@@ -759,8 +759,13 @@ struct OpPlan {
     int M, N, K, nphase;
     int mtiles, ntiles;
     size_t slab_bytes;  // split-K partial slabs
-    size_t ws_bytes;    // total workspace of the layer op (slabs + bias partials)
+    size_t gemm_bytes;  // workspace of the GEMM (split-K slabs + bf16x6 planes)
+    size_t ws_bytes;    // total workspace of the layer op (GEMM + bias partials)
     size_t colsum_off;  // bwd_filter: offset of the bias column-sum partials
+    // bf16x6: operand plane dims (rows x C for A and B) and workspace offsets
+    long x6_ra, x6_rb;
+    int x6_ca, x6_cb;
+    size_t x6_a_off, x6_b_off;
 };
 
 // A narrow op (GEMM N <= 8) recast as a 1x1-geometry MFMA GEMM plus a gather:
@@ -801,6 +806,46 @@ static bool cfg_vec(const ConvGeom &g, int mode, int bk) {
     return g.Ci % 4 == 0;
 }
 
+// Tile config + split-K count for plan pl (M, N, K, nphase set) from a config
+// table; returns the modelled time.  Modelled time of a candidate:
+//   rounds x (blocks per CU x per-block MFMA work) / (CU peak x occupancy efficiency)
+// + split-K slab traffic, where blocks per CU = min(resident limit, blocks / 256).
+static double choose_tiles(OpPlan &pl, const TileCfg *cfgs, int ncfg, double peak, const char *force_env, void *) {
+    const double cu_flops = peak / 256.0;
+    static const double occ_eff[] = {0.0, 0.62, 0.80, 0.88, 0.92};
+    int forced = -1;
+    if (const char *f = getenv(force_env)) forced = atoi(f);
+    int best = -1; double best_t = 1e30; long best_splits = 1;
+    for (int c = 0; c < ncfg; ++c) {
+        const TileCfg &t = cfgs[c];
+        if (forced >= 0 && c != forced) continue;
+        if (forced < 0 && pl.N <= 64 && t.bn > 64) continue;
+        long mt = (pl.M + t.bm - 1) / t.bm, nt = (pl.N + t.bn - 1) / t.bn;
+        long tiles = mt * nt * pl.nphase;
+        long ktiles = (pl.K + t.bk - 1) / t.bk;
+        for (long splits = 1; splits <= std::max<long>(1, ktiles / 4); splits *= 2) {
+            long kt_per = (ktiles + splits - 1) / splits;
+            long blocks = tiles * splits;
+            long bpc = std::min<long>(t.bpc, (blocks + 255) / 256);
+            double rounds = std::ceil((double)blocks / (256.0 * bpc));
+            double tc = rounds * bpc * 2.0 * t.bm * t.bn * kt_per * t.bk * t.eff / (cu_flops * occ_eff[bpc]);
+            double ts = splits > 1 ? (double)splits * pl.nphase * pl.M * pl.N * 8.0 / 5.0e12 + 2e-6 : 0.0;
+            if (tc + ts < best_t) { best_t = tc + ts; best = c; best_splits = splits; }
+            if (blocks >= 1024) break;
+        }
+    }
+    if (best < 0) best = 0;
+    pl.cfg = best;
+    const TileCfg &t = cfgs[best];
+    long ktiles = (pl.K + t.bk - 1) / t.bk;
+    long kt_per = (ktiles + best_splits - 1) / best_splits;
+    pl.kchunk = (int)(kt_per * t.bk);
+    pl.splits = (int)((ktiles + kt_per - 1) / kt_per);
+    pl.mtiles = (pl.M + t.bm - 1) / t.bm;
+    pl.ntiles = (pl.N + t.bn - 1) / t.bn;
+    return best_t;
+}
+
 static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     OpPlan pl{};
     if (mode == MODE_FWD) {
@@ -827,53 +872,46 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
             pl.slab_bytes = (size_t)pl.splits * pl.M * pl.N * sizeof(float);
             pl.ws_bytes = pl.slab_bytes;
         }
+        pl.gemm_bytes = pl.ws_bytes;
         return pl;
     }
-    // Tile + split-K choice.  Modelled time of a candidate:
-    //   rounds x (blocks per CU x per-block MFMA work) / (CU peak x occupancy efficiency)
-    // + split-K slab traffic, where blocks per CU = min(resident limit, blocks / 256).
-    // bf16x6 needs whole 16-wide K-tiles inside one tap (FWD / DGRAD) and
-    // 4-aligned column quads (WGRAD)
-    pl.x6 = math == DG_MATH_BF16X6 &&
-            (mode == MODE_FWD ? g.Ci % 16 == 0 : mode == MODE_DGRAD ? g.Co % 16 == 0 : (g.Ci % 4 == 0 && g.Co % 4 == 0));
-    const TileCfg *cfgs = pl.x6 ? kX6Cfgs : kCfgs;
-    const int ncfg = pl.x6 ? kNumX6Cfgs : kNumCfgs;
-    // fp32 MFMA peak per CU; bf16x6 = six bf16 products per fp32 product
-    const double cu_flops = (pl.x6 ? 2516.6e12 / 6.0 : 157.3e12) / 256.0;
-    static const double occ_eff[] = {0.0, 0.62, 0.80, 0.88, 0.92};
-    int forced = -1;
-    if (const char *f = getenv(pl.x6 ? "DG_FORCE_X6CFG" : "DG_FORCE_CFG")) forced = atoi(f);
-    int best = -1; double best_t = 1e30; long best_splits = 1;
-    for (int c = 0; c < ncfg; ++c) {
-        const TileCfg &t = cfgs[c];
-        if (forced >= 0 && c != forced) continue;
-        if (forced < 0 && pl.N <= 64 && t.bn > 64) continue;
-        long mt = (pl.M + t.bm - 1) / t.bm, nt = (pl.N + t.bn - 1) / t.bn;
-        long tiles = mt * nt * pl.nphase;
-        long ktiles = (pl.K + t.bk - 1) / t.bk;
-        for (long splits = 1; splits <= std::max<long>(1, ktiles / 4); splits *= 2) {
-            long kt_per = (ktiles + splits - 1) / splits;
-            long blocks = tiles * splits;
-            long bpc = std::min<long>(t.bpc, (blocks + 255) / 256);
-            double rounds = std::ceil((double)blocks / (256.0 * bpc));
-            double tc = rounds * bpc * 2.0 * t.bm * t.bn * kt_per * t.bk * t.eff / (cu_flops * occ_eff[bpc]);
-            double ts = splits > 1 ? (double)splits * pl.nphase * pl.M * pl.N * 8.0 / 5.0e12 + 2e-6 : 0.0;
-            if (tc + ts < best_t) { best_t = tc + ts; best = c; best_splits = splits; }
-            if (blocks >= 1024) break;
+    // Tile + split-K choice: the cheaper of the fp32 kernel and (math mode
+    // BF16X6, eligible shapes) the bf16x6 kernel plus its two split passes.
+    double t32 = choose_tiles(pl, kCfgs, kNumCfgs, 157.3e12, "DG_FORCE_CFG", nullptr);
+    int x6_ok = 0;
+    long ra = 0, ca = 0, rb = 0, cb = 0;
+    if (mode == MODE_FWD) {
+        x6_ok = g.Ci % 16 == 0 && g.Co % 16 == 0;
+        ra = (long)g.N * g.H * g.W; ca = g.Ci; rb = (long)g.kh * g.kw * g.Ci; cb = g.Co;
+    } else if (mode == MODE_DGRAD) {
+        x6_ok = g.Co % 16 == 0;
+        ra = (long)g.N * g.Ho * g.Wo; ca = g.Co; rb = (long)g.kh * g.kw * g.Ci; cb = g.Co;
+    } else {
+        x6_ok = g.Ci % 16 == 0 && g.Co % 16 == 0;
+        ra = (long)g.N * g.H * g.W; ca = g.Ci; rb = (long)g.N * g.Ho * g.Wo; cb = g.Co;
+    }
+    x6_ok = x6_ok && math == DG_MATH_BF16X6 && 6.0 * ra * ca < 2.0e9 && 6.0 * rb * cb < 2.0e9;
+    if (x6_ok) {
+        OpPlan p6 = pl;
+        double t6 = choose_tiles(p6, kX6Cfgs, kNumX6Cfgs, 2516.6e12 / 6.0, "DG_FORCE_X6CFG", nullptr);
+        t6 += (double)(ra * ca + rb * cb) * 10.0 / 4.0e12 + 4e-6;  // split passes: read 4 B, write 6 B
+        if (t6 < t32 || getenv("DG_FORCE_X6CFG")) {
+            pl = p6;
+            pl.x6 = 1;
+            pl.x6_ra = ra; pl.x6_ca = (int)ca; pl.x6_rb = rb; pl.x6_cb = (int)cb;
         }
     }
-    if (best < 0) best = 0;
-    pl.cfg = best;
-    const TileCfg &t = cfgs[best];
-    pl.vec = pl.x6 ? 1 : cfg_vec(g, mode, t.bk);
-    long ktiles = (pl.K + t.bk - 1) / t.bk;
-    long kt_per = (ktiles + best_splits - 1) / best_splits;
-    pl.kchunk = (int)(kt_per * t.bk);
-    pl.splits = (int)((ktiles + kt_per - 1) / kt_per);
-    pl.mtiles = (pl.M + t.bm - 1) / t.bm;
-    pl.ntiles = (pl.N + t.bn - 1) / t.bn;
+    if (!pl.x6) choose_tiles(pl, kCfgs, kNumCfgs, 157.3e12, "DG_FORCE_CFG", nullptr);
+    pl.vec = pl.x6 ? 1 : cfg_vec(g, mode, kCfgs[pl.cfg].bk);
     pl.slab_bytes = pl.splits > 1 ? (size_t)pl.nphase * pl.splits * pl.M * pl.N * sizeof(float) : 0;
     pl.ws_bytes = pl.slab_bytes;
+    if (pl.x6) {
+        // workspace: [split-K slabs][A planes][B planes]
+        pl.x6_a_off = (pl.ws_bytes + 255) & ~(size_t)255;
+        pl.x6_b_off = (pl.x6_a_off + (size_t)6 * ra * ca + 255) & ~(size_t)255;
+        pl.ws_bytes = pl.x6_b_off + (size_t)6 * rb * cb;
+    }
+    pl.gemm_bytes = pl.ws_bytes;
     return pl;
 }
 
@@ -924,7 +962,7 @@ static void plan_recast(dg_conv_desc_s *d, int op) {
         rc.slab_off = al256((size_t)P * ntap * 4);
     }
     if (rc.p1.narrow) return;
-    rc.bytes = rc.slab_off + rc.p1.slab_bytes;
+    rc.bytes = rc.slab_off + rc.p1.gemm_bytes;
     rc.on = 1;
 }
 
@@ -939,7 +977,7 @@ static void plan_all(dg_conv_desc_s *d) {
         if (op == DG_OP_BWD_FILTER) {
             // room for the bias column sum partials after the split-K slabs
             size_t extra = colsum_ws(1, d->Cout);
-            size_t base = d->rc[op].on ? d->rc[op].bytes : d->plan[op].slab_bytes;
+            size_t base = d->rc[op].on ? d->rc[op].bytes : d->plan[op].gemm_bytes;
             d->plan[op].colsum_off = (base + 255) & ~(size_t)255;
             d->plan[op].ws_bytes = d->plan[op].colsum_off + extra;
         }
@@ -985,6 +1023,7 @@ static GemmArgs make_args(const ConvGeom &g, const OpPlan &pl, const float *A, i
 }
 
 static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a, hipStream_t s);
+static int finish_splitk(int mode, const OpPlan &pl, const GemmArgs &a, hipStream_t s);
 
 // narrow op through its recast (1x1 MFMA GEMM + gather)
 static int run_recast(const dg_conv_desc_s *d, int op, const GemmArgs &a0, char *ws, hipStream_t s) {
@@ -1033,7 +1072,7 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
                       void *ws, size_t ws_bytes, hipStream_t s) {
     const int mode = engine_mode(d, op);
     const OpPlan &pl = d->plan[op];
-    const size_t need = d->rc[op].on ? d->rc[op].bytes : pl.slab_bytes;
+    const size_t need = d->rc[op].on ? d->rc[op].bytes : pl.gemm_bytes;
     DG_ARG(ws_bytes >= need, "workspace too small: need %zu bytes, got %zu", need, ws_bytes);
     DG_ARG(need == 0 || ws != nullptr, "workspace pointer is NULL");
     GemmArgs a = make_args(d->g, pl, A, lda, B, ldb, C, ldc, bias, beta, act, alpha, ws);
@@ -1086,6 +1125,28 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
         a.a_bytes = (unsigned)ab;
         a.b_bytes = (unsigned)bb;
     }
+    if (pl.x6) {
+        // split both operands into bf16 hi/mid/lo planes in the workspace, then
+        // point the GEMM at plane 0 of each (dense rows of x6_ca / x6_cb)
+        char *ws = (char *)a.slab;
+        DG_ARG(ws != nullptr, "workspace pointer is NULL");
+        unsigned short *pa = (unsigned short *)(ws + pl.x6_a_off);
+        unsigned short *pb = (unsigned short *)(ws + pl.x6_b_off);
+        const long pas = pl.x6_ra * pl.x6_ca, pbs = pl.x6_rb * pl.x6_cb;
+        const int ldbw = (mode == MODE_DGRAD) ? a.g.Co : ldb;  // DGRAD B is the dense weight tensor
+        launch_split3(A, lda, pl.x6_ra, pl.x6_ca, pa, s);
+        DG_LAUNCHED("split3_a");
+        launch_split3(B, ldbw, pl.x6_rb, pl.x6_cb, pb, s);
+        DG_LAUNCHED("split3_b");
+        a.A = (const float *)pa; a.lda = pl.x6_ca; a.a_bytes = (unsigned)(3 * pas * 2);
+        fastdiv_magic((unsigned)a.g.Wo, a.mg_wo, a.sh_wo);
+        fastdiv_magic((unsigned)a.g.Ho, a.mg_ho, a.sh_ho);
+        a.B = (const float *)pb; a.ldb = pl.x6_cb; a.b_bytes = (unsigned)(3 * pbs * 2);
+        dim3 grid(pl.mtiles * pl.ntiles, pl.nphase * pl.splits);
+        launch_gemm_x6(mode, pl.cfg, grid, a, s);
+        DG_LAUNCHED("conv_gemm_x6");
+        return finish_splitk(mode, pl, a, s);
+    }
     if (mode == MODE_FWD || mode == MODE_WGRAD) {
         DG_ARG(pl.N % 4 == 0 && ldb % 4 == 0, "GEMM N (%d) and ldb (%d) must be multiples of 4", pl.N, ldb);
     }
@@ -1094,13 +1155,17 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
     }
     DG_ARG(((uintptr_t)B & 15) == 0 || mode == MODE_DGRAD, "B must be 16B aligned");
     dim3 grid(pl.mtiles * pl.ntiles, pl.nphase * pl.splits);
-    if (pl.x6) launch_gemm_x6(mode, pl.cfg, grid, a, s);
-    else switch (mode) {
+    switch (mode) {
     case MODE_FWD: launch_gemm<MODE_FWD>(pl.cfg, pl.vec, grid, a, s); break;
     case MODE_DGRAD: launch_gemm<MODE_DGRAD>(pl.cfg, pl.vec, grid, a, s); break;
     default: launch_gemm<MODE_WGRAD>(pl.cfg, pl.vec, grid, a, s); break;
     }
     DG_LAUNCHED("conv_gemm");
+    return finish_splitk(mode, pl, a, s);
+}
+
+// split-K reduction + epilogue of a GEMM whose kernel wrote partial slabs
+static int finish_splitk(int mode, const OpPlan &pl, const GemmArgs &a, hipStream_t s) {
     if (pl.splits > 1) {
         // float4 outputs with tpo lanes per output (tpo = 0 -> scalar path)
         int tpo = 0;

@@ -28,6 +28,8 @@ struct GemmArgs {
     int nphase;
     float *slab;       // split-K partials [nphase*splits][M][N]
     unsigned a_bytes, b_bytes;  // extents of A and B for the buffer-resource range check
+    unsigned mg_wo, mg_ho;      // multiply-shift division by g.Wo / g.Ho (bf16x6 WGRAD)
+    int sh_wo, sh_ho;
 };
 
 // Branch-free operand loads: raw buffer loads through a resource whose range
@@ -43,6 +45,30 @@ __device__ __forceinline__ f32x4 bload4(rsrc_t r, unsigned byte_off) {
 }
 __device__ __forceinline__ float bload1(rsrc_t r, unsigned byte_off) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
+
+// XCD-aware tile order.  Workgroups are dispatched round-robin over the 8
+// XCDs (linear id % 8), each with its own 4 MiB L2.  Renumber the linear id
+// so that each XCD receives a contiguous range of (split, tile) ids: with the
+// n-tile fastest in the tile id, the n-tiles of one m-tile (which read the
+// same A rows) and neighbouring m-tiles (which share halo rows) then run on
+// one XCD and hit its L2 instead of each XCD fetching them.
+__device__ __forceinline__ void xcd_remap(int &y, int &x) {
+    const int nx = gridDim.x;
+    const int total = nx * gridDim.y;
+    const int lin = blockIdx.y * nx + blockIdx.x;
+    const int q = total >> 3, r = total & 7, xcd = lin & 7, idx = lin >> 3;
+    const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+    y = id / nx;
+    x = id - y * nx;
+}
+
+// n / d = (umulhi(n, mul) + n) >> shr for 0 <= n < 2^31 (round-up magic number)
+inline void fastdiv_magic(unsigned d, unsigned &mul, int &shr) {
+    int s = 0;
+    while ((1ull << s) < d) ++s;
+    mul = (unsigned)(((1ull << 32) * ((1ull << s) - d)) / d + 1);
+    shr = s;
 }
 
 struct PhaseInfo {
@@ -104,5 +130,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs &p, f32x16 (&acc)[T
 
 // launcher of the bf16x6 kernels (conv_x6.hip); cfg indexes kX6Cfgs
 void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s);
+// fp32 [rows][ld] (first C columns, C % 8 == 0) -> bf16 hi/mid/lo planes [rows][C]
+void launch_split3(const float *src, int ld, long rows, int C, unsigned short *dst, hipStream_t s);
 
 }  // namespace dg

@@ -30,6 +30,14 @@
 // Double-buffered LDS, one barrier per K-tile, the MFMA chain split around
 // the staging of the next tiles, as in k_conv_gemm.
 #include "conv_impl.h"
+#include <algorithm>
+
+#ifndef DG_X6_SCHED
+#define DG_X6_SCHED 1
+#endif
+#ifndef DG_X6_VPM
+#define DG_X6_VPM 3
+#endif
 
 namespace dg {
 
@@ -85,21 +93,56 @@ __device__ __forceinline__ bf16x8 x6_rc_frag(const char *plane, int c0, int lane
     return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
+// Split pass: fp32 [rows][ld] (first C columns, C % 16 == 0) -> the packed
+// bf16 plane layout of the bf16x6 GEMM: row r holds, per 16-column group j,
+// hi[16] mid[16] lo[16] -- element (r, c) of plane p at r*3C + (c/16)*48 +
+// 16p + c%16 -- so the three planes of one K-tile row are 96 contiguous bytes.
+__global__ void __launch_bounds__(256)
+k_split3(const float *__restrict__ src, int ld, long rows, int C, unsigned short *__restrict__ dst) {
+    const int C8 = C >> 3;
+    const long total = rows * C8;
+    const bool vec = ((ld & 3) == 0) && ((((uintptr_t)src) & 15) == 0);
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long r = e / C8;
+        const int c = (int)(e - r * C8) * 8;
+        const float *sp = src + r * ld + c;
+        f32x4 v0, v1;
+        if (vec) {
+            v0 = *reinterpret_cast<const f32x4 *>(sp);
+            v1 = *reinterpret_cast<const f32x4 *>(sp + 4);
+        } else {
+            v0 = f32x4{sp[0], sp[1], sp[2], sp[3]};
+            v1 = f32x4{sp[4], sp[5], sp[6], sp[7]};
+        }
+        unsigned h0, m0, l0, h1, m1, l1, h2, m2, l2, h3, m3, l3;
+        split3(v0[0], v0[1], h0, m0, l0);
+        split3(v0[2], v0[3], h1, m1, l1);
+        split3(v1[0], v1[1], h2, m2, l2);
+        split3(v1[2], v1[3], h3, m3, l3);
+        unsigned short *d = dst + r * 3 * C + (c >> 4) * 48 + (c & 8);
+        *reinterpret_cast<u32x4 *>(d) = u32x4{h0, h1, h2, h3};
+        *reinterpret_cast<u32x4 *>(d + 16) = u32x4{m0, m1, m2, m3};
+        *reinterpret_cast<u32x4 *>(d + 32) = u32x4{l0, l1, l2, l3};
+    }
+}
+
+// The GEMM.  A and B of GemmArgs point at the operands' packed bf16 planes
+// (k_split3 output); lda / ldb are their column counts C (rows are 3C
+// elements), a_bytes / b_bytes their extents.
 template <int MODE, int BM, int BN, int WGM, int WGN, int MINW>
 __global__ void __launch_bounds__(64 * WGM * WGN, MINW)
 k_conv_gemm_x6(const GemmArgs p) {
     constexpr int BK = 16;
     constexpr bool A_KC = (MODE != MODE_WGRAD);
     constexpr bool B_KC = (MODE == MODE_DGRAD);
+    constexpr int NT = 64 * WGM * WGN;  // threads
     constexpr int WTM = BM / WGM, WTN = BN / WGN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
-    constexpr int APL = BM * 32, BPL = BN * 32;     // bytes per plane
+    constexpr int APL = BM * 32, BPL = BN * 32;     // bytes per plane tile
     constexpr int BUF = 3 * (APL + BPL);            // bytes per buffer
-    constexpr int NT = 64 * WGM * WGN;  // threads
     static_assert(WGM * WGN == 4 || WGM * WGN == 8, "4 or 8 waves");
     static_assert(TM >= 1 && TN >= 1, "wave tile >= 32x32");
-    static_assert(BM % (NT / 4) == 0 && BN % (NT / 4) == 0 && (4 * BM) % NT == 0 && (4 * BN) % NT == 0 &&
-                  BM <= 256 && BN <= 256, "loader geometry");
+    static_assert(BM % 32 == 0 && BN % 32 == 0 && BM <= 256 && BN <= 256, "tile");
 
     __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
 
@@ -110,10 +153,10 @@ k_conv_gemm_x6(const GemmArgs p) {
     const int wm = wid / WGN, wn = wid % WGN;
     const int l32 = lane & 31, h2 = lane >> 5;
 
-    const int zz = blockIdx.y;
+    int zz, tile;
+    xcd_remap(zz, tile);
     const int phase = zz / p.splits;
     const int split = zz - phase * p.splits;
-    const int tile = blockIdx.x;
     const int mt = tile / p.ntiles;
     const int nt = tile - mt * p.ntiles;
     const int m0 = mt * BM, n0 = nt * BN;
@@ -130,161 +173,172 @@ k_conv_gemm_x6(const GemmArgs p) {
     if (kbeg >= kend) return;
     const int nk = (kend - kbeg + BK - 1) / BK;
 
-    // ---- loader geometry ----
-    // KC: rows x 16 k, one float4 (4 k) per (row, c4); NT/4 rows per pass
-    const int kc_c4 = tid & 3, kc_r = tid >> 2;
-    constexpr int KRP = NT / 4;
-    constexpr int A_KCP = BM / KRP, B_KCP = BN / KRP;
-    // RC: 16 k-rows x COLS, one float4 (4 columns) per (k-row, column quad)
-    constexpr int A_RCQ = BM / 4, B_RCQ = BN / 4;    // column quads per k-row
-    constexpr int A_RCP = 4 * BM / NT, B_RCP = 4 * BN / NT;  // passes (k-rows per thread)
-    const int ar_cq = tid % A_RCQ, ar_r = tid / A_RCQ;
-    const int br_cq = tid % B_RCQ, br_r = tid / B_RCQ;
+    // ---- loader geometry: 16-byte chunks (8 bf16 of one plane) ----
+    // A row of a K-tile (KC) or 16 columns of a k-row (RC) is 6 chunks = 96
+    // contiguous bytes: s = 2*plane + half.  KC tile: ROWS x 6 chunks; RC tile:
+    // 16 k-rows x COLS/16 groups u x 6.  Either way 6*ROWS chunks, q = tid + NT*i.
+    constexpr int A_CH = 6 * BM, B_CH = 6 * BN;
+    constexpr int A_NI = (A_CH + NT - 1) / NT, B_NI = (B_CH + NT - 1) / NT;
+    struct Chunk { int r, u, s; bool live; };
+    auto kc_chunk = [](int q, int) { Chunk h; h.r = q / 6; h.u = 0; h.s = q - h.r * 6; return h; };
+    auto rc_chunk = [](int q, int COLS) {
+        Chunk h; const int per = 6 * (COLS / 16);
+        h.r = q / per; int w = q - h.r * per; h.u = w / 6; h.s = w - h.u * 6; return h;
+    };
 
-    // KC A rows (FWD / DGRAD)
-    int arow_n[A_KCP], arow_h[A_KCP], arow_w[A_KCP];
-    if constexpr (A_KC) {
+    Chunk ach[A_NI], bch[B_NI];
 #pragma unroll
-        for (int ip = 0; ip < A_KCP; ++ip) {
-            int m = m0 + kc_r + KRP * ip;
-            if (m < Mrows) {
+    for (int i = 0; i < A_NI; ++i) {
+        const int q = tid + NT * i;
+        ach[i] = A_KC ? kc_chunk(q, BM) : rc_chunk(q, BM);
+        ach[i].live = (A_CH % NT == 0) || q < A_CH;
+    }
+#pragma unroll
+    for (int i = 0; i < B_NI; ++i) {
+        const int q = tid + NT * i;
+        bch[i] = B_KC ? kc_chunk(q, BN) : rc_chunk(q, BN);
+        bch[i].live = (B_CH % NT == 0) || q < B_CH;
+    }
+
+    // KC A rows (FWD / DGRAD): output-pixel geometry of each chunk's row
+    int arow_n[A_NI], arow_h[A_NI], arow_w[A_NI];
+    // WGRAD A: (tap, ci) of each chunk's 8 columns
+    int wg_i[A_NI], wg_j[A_NI], wg_ci[A_NI];
+#pragma unroll
+    for (int i = 0; i < A_NI; ++i) {
+        arow_n[i] = -1; arow_h[i] = 0; arow_w[i] = 0; wg_i[i] = 0; wg_j[i] = 0; wg_ci[i] = 0;
+        if constexpr (A_KC) {
+            int m = m0 + ach[i].r;
+            if (ach[i].live && m < Mrows) {
                 if constexpr (MODE == MODE_FWD) {
                     int wo = m % g.Wo; int t = m / g.Wo; int ho = t % g.Ho; int n = t / g.Ho;
-                    arow_n[ip] = n; arow_h[ip] = ho * g.sh - g.pt; arow_w[ip] = wo * g.sw - g.pl;
+                    arow_n[i] = n; arow_h[i] = ho * g.sh - g.pt; arow_w[i] = wo * g.sw - g.pl;
                 } else {
+                    // tap (a, b) of this phase reads dy[hh + ch - a][ww + cw - b]
+                    // (exact: i = i0h + a*sh and ph + pt - i0h is a multiple of sh)
                     int ww = m % ph.Wp; int t = m / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
-                    arow_n[ip] = n; arow_h[ip] = hh * g.sh + ph.ph; arow_w[ip] = ww * g.sw + ph.pw;
+                    arow_n[i] = n;
+                    arow_h[i] = hh + (ph.ph + g.pt - ph.i0h) / g.sh;
+                    arow_w[i] = ww + (ph.pw + g.pl - ph.i0w) / g.sw;
                 }
-            } else {
-                arow_n[ip] = -1; arow_h[ip] = 0; arow_w[ip] = 0;
+            }
+        } else {
+            int mc = m0 + 16 * ach[i].u + 8 * (ach[i].s & 1);
+            if (ach[i].live && mc < p.M) {
+                arow_n[i] = 0;  // column valid
+                int tap = mc / g.Ci; int ci = mc - tap * g.Ci; wg_i[i] = tap / g.kw; wg_j[i] = tap - wg_i[i] * g.kw;
+                wg_ci[i] = (ci >> 4) * 48 + 16 * (ach[i].s >> 1) + (ci & 8);  // packed column offset
             }
         }
     }
-    // WGRAD A: the thread's column quad is 4 consecutive ci of one tap
-    int wg_i = 0, wg_j = 0, wg_ci = 0; bool wg_ok = false;
-    if constexpr (MODE == MODE_WGRAD) {
-        int mc = m0 + 4 * ar_cq;
-        wg_ok = mc < p.M;
-        int tap = mc / g.Ci; wg_ci = mc - tap * g.Ci; wg_i = tap / g.kw; wg_j = tap - wg_i * g.kw;
+
+    // K walk of FWD / DGRAD, channel-chunk-major: all taps (a, b) of one
+    // 16-channel chunk, then the next chunk (see k_conv_gemm).  Kept as
+    // wave-uniform counters advanced once per loaded K-tile.
+    const int TA = MODE == MODE_FWD ? g.kh : g.Th, TB = MODE == MODE_FWD ? g.kw : g.Tw;
+    int wk_a = 0, wk_b = 0, wk_chunk = 0;
+    if constexpr (MODE != MODE_WGRAD) {
+        int kk = kbeg / BK; wk_chunk = kk / (TA * TB); int t = kk - wk_chunk * TA * TB;
+        wk_a = t / TB; wk_b = t - wk_a * TB;
     }
-
-    auto dgrad_tap = [&](int k, int &i, int &j, int &co) {
-        int tap = k / g.Co; co = k - tap * g.Co;
-        int a = tap / g.Tw; int b = tap - a * g.Tw;
-        i = ph.i0h + a * g.sh; j = ph.i0w + b * g.sw;
-    };
-    // channel-chunk-major K walk for FWD / DGRAD (see k_conv_gemm)
-    auto k_real = [&](int k0) -> int {
-        if constexpr (MODE != MODE_WGRAD) {
-            const int C = MODE == MODE_FWD ? g.Ci : g.Co;
-            const int ntap = MODE == MODE_FWD ? g.kh * g.kw : g.Th * g.Tw;
-            int kk = k0 / BK; int chunk = kk / ntap; int tap = kk - chunk * ntap;
-            return tap * C + chunk * BK;
-        } else {
-            return k0;
-        }
+    auto walk_next = [&]() {
+        if (++wk_b == TB) { wk_b = 0; if (++wk_a == TA) { wk_a = 0; ++wk_chunk; } }
     };
 
-    const rsrc_t rA = make_rsrc(p.A, p.a_bytes);
-    const rsrc_t rB = make_rsrc(p.B, p.b_bytes);
+    const rsrc_t rA = make_rsrc((const float *)p.A, p.a_bytes);
+    const rsrc_t rB = make_rsrc((const float *)p.B, p.b_bytes);
+    auto bload16 = [](rsrc_t r, unsigned off) {
+        return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+    };
 
-    // staging registers
-    constexpr int A_REGS = A_KC ? A_KCP : A_RCP;
-    constexpr int B_REGS = B_KC ? B_KCP : B_RCP;
-    f32x4 ra[A_REGS], rb[B_REGS];
+    u32x4 ra[A_NI], rb[B_NI];
+
+    // WGRAD: output pixel -> (n, ho, wo) by multiply-shift division
+    auto fdiv = [](unsigned n, unsigned mul, int shr) { return (__umulhi(n, mul) + n) >> shr; };
 
     auto load_tiles = [&](int k0) {
-        const int kr0 = k_real(k0);
         // ----- A -----
         if constexpr (MODE == MODE_FWD) {
-            int tap = kr0 / g.Ci; int ci0 = kr0 - tap * g.Ci;
-            int i = tap / g.kw; int j = tap - i * g.kw;
+            const int i = wk_a, j = wk_b, ci0 = wk_chunk * BK;
 #pragma unroll
-            for (int ip = 0; ip < A_KCP; ++ip) {
-                int hi = arow_h[ip] + i, wi = arow_w[ip] + j;
-                bool ok = arow_n[ip] >= 0 && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
-                unsigned off = ((unsigned)((arow_n[ip] * g.H + hi) * g.W + wi) * p.lda + ci0 + 4 * kc_c4) * 4u;
-                ra[ip] = bload4(rA, ok ? off : DG_OOB);
+            for (int q = 0; q < A_NI; ++q) {
+                int hi = arow_h[q] + i, wi = arow_w[q] + j;
+                bool ok = arow_n[q] >= 0 && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+                unsigned off = ((unsigned)((arow_n[q] * g.H + hi) * g.W + wi) * (3 * p.lda) + (ci0 >> 4) * 48 + 8 * ach[q].s) * 2u;
+                ra[q] = bload16(rA, ok ? off : DG_OOB);
             }
         } else if constexpr (MODE == MODE_DGRAD) {
-            int i, j, co0; dgrad_tap(kr0, i, j, co0);
-            bool tapok = (i < g.kh) && (j < g.kw);
+            const int i = ph.i0h + wk_a * g.sh, j = ph.i0w + wk_b * g.sw, co0 = wk_chunk * BK;
+            const bool tapok = (i < g.kh) && (j < g.kw);
 #pragma unroll
-            for (int ip = 0; ip < A_KCP; ++ip) {
-                int th = arow_h[ip] + g.pt - i, tw = arow_w[ip] + g.pl - j;
-                int ho = th / g.sh, wo = tw / g.sw;
-                bool ok = tapok && arow_n[ip] >= 0 && th >= 0 && tw >= 0 && ho < g.Ho && wo < g.Wo;
-                unsigned off = ((unsigned)((arow_n[ip] * g.Ho + ho) * g.Wo + wo) * p.lda + co0 + 4 * kc_c4) * 4u;
-                ra[ip] = bload4(rA, ok ? off : DG_OOB);
+            for (int q = 0; q < A_NI; ++q) {
+                int ho = arow_h[q] - wk_a, wo = arow_w[q] - wk_b;
+                bool ok = tapok && arow_n[q] >= 0 && (unsigned)ho < (unsigned)g.Ho && (unsigned)wo < (unsigned)g.Wo;
+                unsigned off = ((unsigned)((arow_n[q] * g.Ho + ho) * g.Wo + wo) * (3 * p.lda) + (co0 >> 4) * 48 + 8 * ach[q].s) * 2u;
+                ra[q] = bload16(rA, ok ? off : DG_OOB);
             }
-        } else {  // WGRAD: x gathered at the thread's tap, k-rows are output pixels
+        } else {  // WGRAD: x gathered at each chunk's tap, k-rows are output pixels
 #pragma unroll
-            for (int ip = 0; ip < A_RCP; ++ip) {
-                int pix = k0 + ar_r + (NT / A_RCQ) * ip;
-                int wo = pix % g.Wo; int t = pix / g.Wo; int ho = t % g.Ho; int n = t / g.Ho;
-                int hi = ho * g.sh - g.pt + wg_i, wi = wo * g.sw - g.pl + wg_j;
-                bool ok = wg_ok && pix < kend && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
-                unsigned off = ((unsigned)((n * g.H + hi) * g.W + wi) * p.lda + wg_ci) * 4u;
-                ra[ip] = bload4(rA, ok ? off : DG_OOB);
+            for (int q = 0; q < A_NI; ++q) {
+                unsigned pix = (unsigned)(k0 + ach[q].r);
+                unsigned t = fdiv(pix, p.mg_wo, p.sh_wo); int wo = (int)(pix - t * g.Wo);
+                unsigned n = fdiv(t, p.mg_ho, p.sh_ho); int ho = (int)(t - n * g.Ho);
+                int hi = ho * g.sh - g.pt + wg_i[q], wi = wo * g.sw - g.pl + wg_j[q];
+                bool ok = arow_n[q] >= 0 && (int)pix < kend && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+                unsigned off = ((unsigned)(((int)n * g.H + hi) * g.W + wi) * (3 * p.lda) + wg_ci[q]) * 2u;
+                ra[q] = bload16(rA, ok ? off : DG_OOB);
             }
         }
         // ----- B -----
-        if constexpr (MODE == MODE_FWD) {  // w[k][co]
-            const int col = n0 + 4 * br_cq;
+        if constexpr (MODE == MODE_FWD) {  // w[k][co], k = (tap, ci)
+            const int kr0 = (wk_a * g.kw + wk_b) * g.Ci + wk_chunk * BK;
 #pragma unroll
-            for (int ip = 0; ip < B_RCP; ++ip) {
-                unsigned k = (unsigned)(kr0 + br_r + (NT / B_RCQ) * ip);
-                rb[ip] = bload4(rB, col < p.N ? (k * p.ldb + col) * 4u : DG_OOB);
+            for (int q = 0; q < B_NI; ++q) {
+                const int col = n0 + 16 * bch[q].u;
+                const unsigned k = (unsigned)(kr0 + bch[q].r);
+                const bool ok = bch[q].live && col < p.N;
+                const unsigned off = (k * (3 * p.ldb) + (col >> 4) * 48 + 8 * bch[q].s) * 2u;
+                rb[q] = bload16(rB, ok ? off : DG_OOB);
             }
         } else if constexpr (MODE == MODE_DGRAD) {  // w[i,j,ci,co]: rows ci contiguous along co
-            int i, j, co0; dgrad_tap(kr0, i, j, co0);
-            bool tapok = (i < g.kh) && (j < g.kw);
+            const int i = ph.i0h + wk_a * g.sh, j = ph.i0w + wk_b * g.sw, co0 = wk_chunk * BK;
+            const bool tapok = (i < g.kh) && (j < g.kw);
 #pragma unroll
-            for (int ip = 0; ip < B_KCP; ++ip) {
-                int ci = n0 + kc_r + KRP * ip;
-                bool ok = tapok && ci < p.N;
-                unsigned off = ((unsigned)((i * g.kw + j) * g.Ci + ci) * g.Co + co0 + 4 * kc_c4) * 4u;
-                rb[ip] = bload4(rB, ok ? off : DG_OOB);
+            for (int q = 0; q < B_NI; ++q) {
+                int ci = n0 + bch[q].r;
+                bool ok = bch[q].live && tapok && ci < p.N;
+                unsigned off = ((unsigned)((i * g.kw + j) * g.Ci + ci) * (3 * p.ldb) + (co0 >> 4) * 48 + 8 * bch[q].s) * 2u;
+                rb[q] = bload16(rB, ok ? off : DG_OOB);
             }
         } else {  // WGRAD: dy rows (pixels) contiguous along co
-            const int col = n0 + 4 * br_cq;
 #pragma unroll
-            for (int ip = 0; ip < B_RCP; ++ip) {
-                int pix = k0 + br_r + (NT / B_RCQ) * ip;
-                bool ok = col < p.N && pix < kend;
-                rb[ip] = bload4(rB, ok ? ((unsigned)pix * p.ldb + col) * 4u : DG_OOB);
+            for (int q = 0; q < B_NI; ++q) {
+                const int col = n0 + 16 * bch[q].u;
+                const int pix = k0 + bch[q].r;
+                const bool ok = bch[q].live && col < p.N && pix < kend;
+                const unsigned off = ((unsigned)pix * (3 * p.ldb) + (col >> 4) * 48 + 8 * bch[q].s) * 2u;
+                rb[q] = bload16(rB, ok ? off : DG_OOB);
             }
         }
-    };
-
-    // one float4 -> three 8-byte plane writes at byte offset o
-    auto store4 = [&](char *base, int plane_bytes, int o, const f32x4 &v) {
-        unsigned h0, m0_, l0, h1, m1, l1;
-        split3(v[0], v[1], h0, m0_, l0);
-        split3(v[2], v[3], h1, m1, l1);
-        *reinterpret_cast<u32x2 *>(base + o) = u32x2{h0, h1};
-        *reinterpret_cast<u32x2 *>(base + plane_bytes + o) = u32x2{m0_, m1};
-        *reinterpret_cast<u32x2 *>(base + 2 * plane_bytes + o) = u32x2{l0, l1};
+        if constexpr (MODE != MODE_WGRAD) walk_next();
     };
 
     auto store_tiles = [&](int buf) {
         char *As = smem + buf * BUF;
         char *Bs = As + 3 * APL;
-        if constexpr (A_KC) {
 #pragma unroll
-            for (int ip = 0; ip < A_KCP; ++ip) store4(As, APL, x6_off(kc_r + KRP * ip, 4 * kc_c4), ra[ip]);
-        } else {
-#pragma unroll
-            for (int ip = 0; ip < A_RCP; ++ip)
-                store4(As, APL, x6_rc_off<BM>(ar_r + (NT / A_RCQ) * ip, 4 * ar_cq), ra[ip]);
+        for (int q = 0; q < A_NI; ++q) {
+            if (!ach[q].live) continue;
+            const int h = ach[q].s & 1;
+            const int o = A_KC ? x6_off(ach[q].r, 8 * h) : x6_rc_off<BM>(ach[q].r, 16 * ach[q].u + 8 * h);
+            *reinterpret_cast<u32x4 *>(As + (ach[q].s >> 1) * APL + o) = ra[q];
         }
-        if constexpr (B_KC) {
 #pragma unroll
-            for (int ip = 0; ip < B_KCP; ++ip) store4(Bs, BPL, x6_off(kc_r + KRP * ip, 4 * kc_c4), rb[ip]);
-        } else {
-#pragma unroll
-            for (int ip = 0; ip < B_RCP; ++ip)
-                store4(Bs, BPL, x6_rc_off<BN>(br_r + (NT / B_RCQ) * ip, 4 * br_cq), rb[ip]);
+        for (int q = 0; q < B_NI; ++q) {
+            if (!bch[q].live) continue;
+            const int h = bch[q].s & 1;
+            const int o = B_KC ? x6_off(bch[q].r, 8 * h) : x6_rc_off<BN>(bch[q].r, 16 * bch[q].u + 8 * h);
+            *reinterpret_cast<u32x4 *>(Bs + (bch[q].s >> 1) * BPL + o) = rb[q];
         }
     };
 
@@ -327,6 +381,7 @@ k_conv_gemm_x6(const GemmArgs p) {
                 for (int s = 0; s < 3; ++s) bf[s][b] = x6_rc_frag<BN>(Bs + s * BPL, wn * WTN + b * 32, lane);
             }
         }
+#if DG_X6_SCHED == 0
         __builtin_amdgcn_sched_barrier(0);
         // small products first, then the large ones
 #pragma unroll
@@ -349,10 +404,44 @@ k_conv_gemm_x6(const GemmArgs p) {
                 acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[1][b], acc[a][b], 0, 0, 0);
                 acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
             }
+#else
+        // One basic block: the staging of tiles kt+1 / kt+2 (buffer loads never
+        // fault and the extra tiles past nk land in the idle LDS buffer, so it
+        // runs unconditionally) is interleaved with the MFMA chain, a few
+        // staging instructions in the shadow of each MFMA.
+        store_tiles((kt & 1) ^ 1);
+        load_tiles(kbeg + (kt + 2) * BK);
+#pragma unroll
+        for (int s = 0; s < 6; ++s) {
+            const int pa = s < 3 ? (s == 0 ? 2 : s == 1 ? 0 : 1) : (s == 3 ? 1 : 0);
+            const int pb = s < 3 ? (s == 0 ? 0 : s == 1 ? 2 : 1) : (s == 4 ? 1 : 0);
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[pa][a], bf[pb][b], acc[a][b], 0, 0, 0);
+        }
+        constexpr int NMF = 6 * TM * TN;
+#pragma unroll
+        for (int i = 0; i < NMF; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, DG_X6_VPM, 0);  // VALU
+            __builtin_amdgcn_sched_group_barrier(0x004, 4, 0);  // SALU
+            if (i % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+            if (i % 2 == 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
+        }
+#endif
         __syncthreads();
     }
 
     conv_epilogue<MODE, TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, Mrows, ph, phase, split, l32, h2);
+}
+
+void launch_split3(const float *src, int ld, long rows, int C, unsigned short *dst, hipStream_t s) {
+    const long total = rows * (C / 8);
+    if (total == 0) return;
+    const unsigned blocks = (unsigned)std::min<long>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_split3, dim3(blocks), dim3(256), 0, s, src, ld, rows, C, dst);
 }
 
 // tile configs of the bf16x6 kernel (index = kX6Cfgs in conv.hip)
