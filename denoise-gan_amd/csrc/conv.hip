@@ -746,7 +746,7 @@ constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 static const TileCfg kX6Cfgs[] = {
     {128, 128, 2, 2, 16, 2, 2, 1.00}, {128, 64, 2, 2, 16, 2, 3, 1.15}, {64, 128, 2, 2, 16, 2, 3, 1.15},
     {64, 64, 2, 2, 16, 3, 4, 1.40},   {128, 128, 2, 2, 16, 3, 3, 1.00}, {256, 128, 4, 2, 16, 2, 1, 1.00},
-    {128, 256, 2, 4, 16, 2, 1, 1.00},
+    {128, 256, 2, 4, 16, 2, 1, 1.00}, {256, 128, 2, 2, 16, 2, 2, 0.95}, {128, 256, 2, 2, 16, 2, 2, 0.95},
 };
 constexpr int kNumX6Cfgs = sizeof(kX6Cfgs) / sizeof(kX6Cfgs[0]);
 
@@ -987,8 +987,8 @@ static void plan_all(dg_conv_desc_s *d) {
 static int default_math() {
     const char *m = getenv("DG_CONV_MATH");
     if (m && (!strcmp(m, "fp32") || !strcmp(m, "0"))) return DG_MATH_FP32;
-    if (m && (!strcmp(m, "bf16x6") || !strcmp(m, "1"))) return DG_MATH_BF16X6;
-    return DG_MATH_FP32;
+    (void)m;
+    return DG_MATH_BF16X6;
 }
 
 

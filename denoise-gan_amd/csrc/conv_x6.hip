@@ -138,7 +138,10 @@ k_conv_gemm_x6(const GemmArgs p) {
     constexpr int NT = 64 * WGM * WGN;  // threads
     constexpr int WTM = BM / WGM, WTN = BN / WGN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
-    constexpr int APL = BM * 32, BPL = BN * 32;     // bytes per plane tile
+    // bytes per plane tile; the 96-byte pad shifts plane p by 6p 16-byte bank
+    // groups, so the 8 lanes of a ds_write_b128 group (chunks of 2 rows x 3
+    // planes) land on distinct banks
+    constexpr int APL = BM * 32 + 96, BPL = BN * 32 + 96;
     constexpr int BUF = 3 * (APL + BPL);            // bytes per buffer
     static_assert(WGM * WGN == 4 || WGM * WGN == 8, "4 or 8 waves");
     static_assert(TM >= 1 && TN >= 1, "wave tile >= 32x32");
@@ -359,26 +362,23 @@ k_conv_gemm_x6(const GemmArgs p) {
         const char *As = smem + (kt & 1) * BUF;
         const char *Bs = As + 3 * APL;
         bf16x8 af[3][TM], bf[3][TN];
+        // plane-major read order (hi, mid, lo), matching the MFMA order below,
+        // so the first products wait only for the hi fragments
 #pragma unroll
-        for (int a = 0; a < TM; ++a) {
-            if constexpr (A_KC) {
-                const int o = x6_off(wm * WTM + a * 32 + l32, 8 * h2);
+        for (int s = 0; s < 3; ++s) {
 #pragma unroll
-                for (int s = 0; s < 3; ++s) af[s][a] = *reinterpret_cast<const bf16x8 *>(As + s * APL + o);
-            } else {
-#pragma unroll
-                for (int s = 0; s < 3; ++s) af[s][a] = x6_rc_frag<BM>(As + s * APL, wm * WTM + a * 32, lane);
+            for (int a = 0; a < TM; ++a) {
+                if constexpr (A_KC)
+                    af[s][a] = *reinterpret_cast<const bf16x8 *>(As + s * APL + x6_off(wm * WTM + a * 32 + l32, 8 * h2));
+                else
+                    af[s][a] = x6_rc_frag<BM>(As + s * APL, wm * WTM + a * 32, lane);
             }
-        }
 #pragma unroll
-        for (int b = 0; b < TN; ++b) {
-            if constexpr (B_KC) {
-                const int o = x6_off(wn * WTN + b * 32 + l32, 8 * h2);
-#pragma unroll
-                for (int s = 0; s < 3; ++s) bf[s][b] = *reinterpret_cast<const bf16x8 *>(Bs + s * BPL + o);
-            } else {
-#pragma unroll
-                for (int s = 0; s < 3; ++s) bf[s][b] = x6_rc_frag<BN>(Bs + s * BPL, wn * WTN + b * 32, lane);
+            for (int b = 0; b < TN; ++b) {
+                if constexpr (B_KC)
+                    bf[s][b] = *reinterpret_cast<const bf16x8 *>(Bs + s * BPL + x6_off(wn * WTN + b * 32 + l32, 8 * h2));
+                else
+                    bf[s][b] = x6_rc_frag<BN>(Bs + s * BPL, wn * WTN + b * 32, lane);
             }
         }
 #if DG_X6_SCHED == 0
@@ -413,8 +413,9 @@ k_conv_gemm_x6(const GemmArgs p) {
         load_tiles(kbeg + (kt + 2) * BK);
 #pragma unroll
         for (int s = 0; s < 6; ++s) {
-            const int pa = s < 3 ? (s == 0 ? 2 : s == 1 ? 0 : 1) : (s == 3 ? 1 : 0);
-            const int pb = s < 3 ? (s == 0 ? 0 : s == 1 ? 2 : 1) : (s == 4 ? 1 : 0);
+            // hi.hi, mid.hi, hi.mid, mid.mid, lo.hi, hi.lo
+            const int pa = s == 1 || s == 3 ? 1 : s == 4 ? 2 : 0;
+            const int pb = s == 2 || s == 3 ? 1 : s == 5 ? 2 : 0;
 #pragma unroll
             for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -462,6 +463,8 @@ void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t
         DG_X6(4, 128, 128, 2, 2, 3)
         DG_X6(5, 256, 128, 4, 2, 2)
         DG_X6(6, 128, 256, 2, 4, 2)
+        DG_X6(7, 256, 128, 2, 2, 2)
+        DG_X6(8, 128, 256, 2, 2, 2)
     }
 #undef DG_X6
 }

@@ -70,7 +70,7 @@ int dg_conv_workspace_size(dg_conv_t d, int op, size_t *bytes);
  *                    six piece products >= 2^-18 |ab| summed in the fp32 MFMA
  *                    accumulator (dropped terms < 2^-26 |ab|, below fp32
  *                    rounding) on the bf16 matrix cores, 2.7x the f32 MFMA rate.
- * New descriptors take $DG_CONV_MATH ("fp32" | "bf16x6"; default fp32).
+ * New descriptors take $DG_CONV_MATH ("fp32" | "bf16x6"; default bf16x6).
  * Changing the mode re-plans the descriptor: query workspace sizes after it. */
 enum { DG_MATH_FP32 = 0, DG_MATH_BF16X6 = 1 };
 int dg_conv_set_math(dg_conv_t d, int math);
