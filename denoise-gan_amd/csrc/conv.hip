@@ -744,9 +744,8 @@ static const TileCfg kCfgs[] = {
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 // bf16x6 kernel configs (conv_x6.hip launch_gemm_x6), K-tile 16
 static const TileCfg kX6Cfgs[] = {
-    {128, 128, 2, 2, 16, 2, 2, 1.00}, {128, 64, 2, 2, 16, 2, 3, 1.15}, {64, 128, 2, 2, 16, 2, 3, 1.15},
-    {64, 64, 2, 2, 16, 3, 4, 1.40},   {128, 128, 2, 2, 16, 3, 3, 1.00}, {256, 128, 4, 2, 16, 2, 1, 1.00},
-    {128, 256, 2, 4, 16, 2, 1, 1.00}, {256, 128, 2, 2, 16, 2, 2, 0.95}, {128, 256, 2, 2, 16, 2, 2, 0.95},
+    {128, 128, 2, 2, 16, 2, 2, 1.00}, {128, 64, 2, 2, 16, 2, 2, 1.15}, {64, 128, 2, 2, 16, 2, 2, 1.15},
+    {64, 64, 2, 2, 16, 3, 4, 1.40},   {256, 128, 4, 2, 16, 2, 1, 1.00}, {128, 256, 2, 4, 16, 2, 1, 1.00},
 };
 constexpr int kNumX6Cfgs = sizeof(kX6Cfgs) / sizeof(kX6Cfgs[0]);
 

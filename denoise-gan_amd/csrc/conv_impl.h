@@ -128,6 +128,43 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs &p, f32x16 (&acc)[T
     }
 }
 
+// The same for 16x16 accumulator tiles (v_mfma_f32_16x16x32_bf16 C layout:
+// col = lane&15, row = 4(lane>>4) + r).
+template <int MODE, int TM, int TN>
+__device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[TM][TN], int rbase, int cbase,
+                                                int Mrows, const PhaseInfo &ph, int phase, int split, int lane) {
+    const ConvGeom &g = p.g;
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+            const int col = cbase + b * 16 + (lane & 15);
+            if (col >= p.N) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = rbase + a * 16 + 4 * (lane >> 4) + r;
+                if (row >= Mrows) continue;
+                float v = acc[a][b][r];
+                if (p.splits > 1) {
+                    p.slab[((long)(phase * p.splits + split) * p.M + row) * p.N + col] = v;
+                } else {
+                    long off;
+                    if constexpr (MODE == MODE_DGRAD) {
+                        int ww = row % ph.Wp; int t = row / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
+                        off = ((long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw) * p.ldc;
+                    } else {
+                        off = (long)row * p.ldc;
+                    }
+                    if (p.bias) v += p.bias[col];
+                    v = act_fwd(v, p.act, p.alpha);
+                    if (p.beta != 0.f) v += p.beta * p.C[off + col];
+                    p.C[off + col] = v;
+                }
+            }
+        }
+    }
+}
+
 // launcher of the bf16x6 kernels (conv_x6.hip); cfg indexes kX6Cfgs
 void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s);
 // fp32 [rows][ld] (first C columns, C % 8 == 0) -> bf16 hi/mid/lo planes [rows][C]

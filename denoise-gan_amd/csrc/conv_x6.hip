@@ -63,34 +63,47 @@ __device__ __forceinline__ void split3(float x0, float x1, unsigned &h, unsigned
     l = cvt_pk_bf16(s0, s1);
 }
 
-// byte offset of bf16 element (row, kk) in a [rows][16] plane image
-__device__ __forceinline__ int x6_off(int row, int kk) {
-    return row * 32 + ((((kk >> 3) ^ (row >> 3)) & 1) << 4) + ((kk & 7) << 1);
-}
+// LDS plane images (bf16), read by v_mfma_f32_16x16x32_bf16 fragments whose
+// 32-wide K is two 16-wide plane pieces side by side (see the kernel):
+//   KC image [rows][16 k], 32-byte rows: lane l of a read takes row l&15 and
+//   the 8-k half (l>>4)&1 of plane (l>>5 ? P1 : P0) -- conflict-free as is.
+//   RC image [16 k][COLS], read transposed (ds_read_b64_tr_b16): the 8-dword
+//   blocks of k-row k are XOR-swizzled by f(k) so the eight k-rows one 32-lane
+//   half touches (k and k+8 for 4 consecutive k) land on distinct banks.
+// (Both verified exhaustively against the gfx950 bank model for 64/128/256.)
+__device__ __forceinline__ int x6_off(int row, int half) { return row * 32 + 16 * half; }
 
+template <int COLS>
+__device__ __forceinline__ int x6_rc_swz(int k) {  // in dwords
+    return COLS >= 128 ? 8 * ((k & 3) | (((k >> 3) & 1) << 2)) : 8 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
+}
 // byte offset of bf16 element (k, col) in a [16][COLS] plane image (col even)
 template <int COLS>
 __device__ __forceinline__ int x6_rc_off(int k, int col) {
-    constexpr int RW = COLS / 2;  // dwords per k-row
-    const int swz = COLS >= 128 ? ((k & 3) << 4) : (((k >> 1) & 1) << 4);
-    return 4 * (k * RW + ((col >> 1) ^ swz));
+    return 4 * (k * (COLS / 2) + ((col >> 1) ^ x6_rc_swz<COLS>(k)));
 }
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-// 32x32x16 operand fragment (lane: column c0 + lane&31, k = 8(lane>>5) + 0..7)
-// of an RC image, by two transposed reads
+// 16x16x32 operand fragment of an RC image pair: lane l gets column
+// c0 + (l&15) at k = 8(l>>4) + 0..7 of the concatenated K, i.e. k-rows
+// 8((l>>4)&1) + 0..7 of plane P0 (l < 32) or P1 (l >= 32); two transposed reads
 template <int COLS>
-__device__ __forceinline__ bf16x8 x6_rc_frag(const char *plane, int c0, int lane) {
+__device__ __forceinline__ bf16x8 x6_rc_frag(const char *p0, const char *p1, int c0, int lane) {
     const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
-    const int col = c0 + 16 * (g & 1) + 4 * pp;
-    const int k = 8 * (g >> 1) + q;
-    lds_s16x4 *p0 = (lds_s16x4 *)(plane + x6_rc_off<COLS>(k, col));
-    lds_s16x4 *p1 = (lds_s16x4 *)(plane + x6_rc_off<COLS>(k + 4, col));
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(p0);
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(p1);
+    const char *pl = g < 2 ? p0 : p1;
+    const int col = c0 + 4 * pp, k = 8 * (g & 1) + q;
+    lds_s16x4 *a0 = (lds_s16x4 *)(pl + x6_rc_off<COLS>(k, col));
+    lds_s16x4 *a1 = (lds_s16x4 *)(pl + x6_rc_off<COLS>(k + 4, col));
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(a0);
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(a1);
     return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+// the same from a KC image pair: one 16-byte read per lane
+__device__ __forceinline__ bf16x8 x6_kc_frag(const char *p0, const char *p1, int r0, int lane) {
+    const int g = lane >> 4;
+    return *reinterpret_cast<const bf16x8 *>((g < 2 ? p0 : p1) + x6_off(r0 + (lane & 15), g & 1));
 }
 
 // Split pass: fp32 [rows][ld] (first C columns, C % 16 == 0) -> the packed
@@ -137,22 +150,28 @@ k_conv_gemm_x6(const GemmArgs p) {
     constexpr bool B_KC = (MODE == MODE_DGRAD);
     constexpr int NT = 64 * WGM * WGN;  // threads
     constexpr int WTM = BM / WGM, WTN = BN / WGN;
-    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int TM = WTM / 16, TN = WTN / 16;  // 16x16 accumulator tiles per wave
     // bytes per plane tile; the 96-byte pad shifts plane p by 6p 16-byte bank
     // groups, so the 8 lanes of a ds_write_b128 group (chunks of 2 rows x 3
     // planes) land on distinct banks
     constexpr int APL = BM * 32 + 96, BPL = BN * 32 + 96;
     constexpr int BUF = 3 * (APL + BPL);            // bytes per buffer
     static_assert(WGM * WGN == 4 || WGM * WGN == 8, "4 or 8 waves");
-    static_assert(TM >= 1 && TN >= 1, "wave tile >= 32x32");
+    static_assert(TM >= 1 && TN >= 1 && WTM % 16 == 0 && WTN % 16 == 0, "wave tile of 16x16 tiles");
     static_assert(BM % 32 == 0 && BN % 32 == 0 && BM <= 256 && BN <= 256, "tile");
 
-    __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+    // three LDS buffers as separate objects: with the main loop unrolled by
+    // three every DMA and every fragment read names its buffer statically, so
+    // the compiler's LDS-DMA alias tracking does not drain the in-flight DMAs
+    // of the other buffers before each read
+    __shared__ __attribute__((aligned(16))) char smem0[BUF];
+    __shared__ __attribute__((aligned(16))) char smem1[BUF];
+    __shared__ __attribute__((aligned(16))) char smem2[BUF];
 
     const ConvGeom &g = p.g;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wid = tid >> 6;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid / WGN, wn = wid % WGN;
     const int l32 = lane & 31, h2 = lane >> 5;
 
@@ -176,68 +195,87 @@ k_conv_gemm_x6(const GemmArgs p) {
     if (kbeg >= kend) return;
     const int nk = (kend - kbeg + BK - 1) / BK;
 
-    // ---- loader geometry: 16-byte chunks (8 bf16 of one plane) ----
-    // A row of a K-tile (KC) or 16 columns of a k-row (RC) is 6 chunks = 96
-    // contiguous bytes: s = 2*plane + half.  KC tile: ROWS x 6 chunks; RC tile:
-    // 16 k-rows x COLS/16 groups u x 6.  Either way 6*ROWS chunks, q = tid + NT*i.
-    constexpr int A_CH = 6 * BM, B_CH = 6 * BN;
-    constexpr int A_NI = (A_CH + NT - 1) / NT, B_NI = (B_CH + NT - 1) / NT;
-    struct Chunk { int r, u, s; bool live; };
-    auto kc_chunk = [](int q, int) { Chunk h; h.r = q / 6; h.u = 0; h.s = q - h.r * 6; return h; };
-    auto rc_chunk = [](int q, int COLS) {
-        Chunk h; const int per = 6 * (COLS / 16);
-        h.r = q / per; int w = q - h.r * per; h.u = w / 6; h.s = w - h.u * 6; return h;
+    // ---- LDS-DMA staging (buffer_load ... lds, 16 B per lane) ----
+    // Each DMA instruction writes 1 KB of one plane image, lane L at byte 16L
+    // (the destination is lane-linear); the swizzles of the images are
+    // applied on the SOURCE side: lane L fetches the global 16-byte chunk that
+    // belongs at its position.  Operand with X rows (KC) / X columns (RC) has
+    // 3*X/32 such 1-KB slots per K-tile, dealt round-robin over the waves.
+    constexpr int NW = WGM * WGN;
+    constexpr int A_SL = 3 * BM / 32, B_SL = 3 * BN / 32;          // slots per tile
+    constexpr int A_NJ = (A_SL + NW - 1) / NW, B_NJ = (B_SL + NW - 1) / NW;
+    struct Slot { int plane, r, c; bool live; };  // KC: row r, half c; RC: k-row r, column c
+    auto slot_of = [&](int d, bool kc, int X) {
+        Slot sl; const int per = X / 32;  // 1-KB blocks per plane image
+        sl.plane = d / per;
+        const int pos = (d - sl.plane * per) * 1024 + 16 * lane;
+        if (kc) {
+            sl.r = pos >> 5;
+            sl.c = (pos >> 4) & 1;
+        } else {
+            sl.r = pos / (2 * X);
+            const int pdw = (pos - sl.r * 2 * X) >> 2;
+            const int swz = X >= 128 ? 8 * ((sl.r & 3) | (((sl.r >> 3) & 1) << 2))
+                                     : 8 * (((sl.r >> 1) & 1) | (((sl.r >> 3) & 1) << 1));
+            sl.c = 2 * (pdw ^ swz);
+        }
+        return sl;
     };
-
-    Chunk ach[A_NI], bch[B_NI];
+    Slot asl[A_NJ], bsl[B_NJ];
 #pragma unroll
-    for (int i = 0; i < A_NI; ++i) {
-        const int q = tid + NT * i;
-        ach[i] = A_KC ? kc_chunk(q, BM) : rc_chunk(q, BM);
-        ach[i].live = (A_CH % NT == 0) || q < A_CH;
+    for (int j = 0; j < A_NJ; ++j) {
+        const int d = wid + NW * j;
+        asl[j] = slot_of(d < A_SL ? d : 0, A_KC, BM);
+        asl[j].live = d < A_SL;
     }
 #pragma unroll
-    for (int i = 0; i < B_NI; ++i) {
-        const int q = tid + NT * i;
-        bch[i] = B_KC ? kc_chunk(q, BN) : rc_chunk(q, BN);
-        bch[i].live = (B_CH % NT == 0) || q < B_CH;
+    for (int j = 0; j < B_NJ; ++j) {
+        const int d = wid + NW * j;
+        bsl[j] = slot_of(d < B_SL ? d : 0, B_KC, BN);
+        bsl[j].live = d < B_SL;
     }
-
-    // KC A rows (FWD / DGRAD): output-pixel geometry of each chunk's row
-    int arow_n[A_NI], arow_h[A_NI], arow_w[A_NI];
-    // WGRAD A: (tap, ci) of each chunk's 8 columns
-    int wg_i[A_NI], wg_j[A_NI], wg_ci[A_NI];
+    // DMA instructions this wave issues per K-tile (wave-uniform)
+    int nmine = 0;
 #pragma unroll
-    for (int i = 0; i < A_NI; ++i) {
-        arow_n[i] = -1; arow_h[i] = 0; arow_w[i] = 0; wg_i[i] = 0; wg_j[i] = 0; wg_ci[i] = 0;
+    for (int j = 0; j < A_NJ; ++j) nmine += asl[j].live;
+#pragma unroll
+    for (int j = 0; j < B_NJ; ++j) nmine += bsl[j].live;
+
+    // A geometry per slot.  KC (FWD / DGRAD): the output pixel of row r.
+    // WGRAD (RC): the (tap, ci) of columns c..c+7 and their packed offset.
+    int arow_n[A_NJ], arow_h[A_NJ], arow_w[A_NJ];
+    int wg_i[A_NJ], wg_j[A_NJ], wg_ci[A_NJ];
+#pragma unroll
+    for (int j = 0; j < A_NJ; ++j) {
+        arow_n[j] = -1; arow_h[j] = 0; arow_w[j] = 0; wg_i[j] = 0; wg_j[j] = 0; wg_ci[j] = 0;
         if constexpr (A_KC) {
-            int m = m0 + ach[i].r;
-            if (ach[i].live && m < Mrows) {
+            int m = m0 + asl[j].r;
+            if (m < Mrows) {
                 if constexpr (MODE == MODE_FWD) {
                     int wo = m % g.Wo; int t = m / g.Wo; int ho = t % g.Ho; int n = t / g.Ho;
-                    arow_n[i] = n; arow_h[i] = ho * g.sh - g.pt; arow_w[i] = wo * g.sw - g.pl;
+                    arow_n[j] = n; arow_h[j] = ho * g.sh - g.pt; arow_w[j] = wo * g.sw - g.pl;
                 } else {
                     // tap (a, b) of this phase reads dy[hh + ch - a][ww + cw - b]
                     // (exact: i = i0h + a*sh and ph + pt - i0h is a multiple of sh)
                     int ww = m % ph.Wp; int t = m / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
-                    arow_n[i] = n;
-                    arow_h[i] = hh + (ph.ph + g.pt - ph.i0h) / g.sh;
-                    arow_w[i] = ww + (ph.pw + g.pl - ph.i0w) / g.sw;
+                    arow_n[j] = n;
+                    arow_h[j] = hh + (ph.ph + g.pt - ph.i0h) / g.sh;
+                    arow_w[j] = ww + (ph.pw + g.pl - ph.i0w) / g.sw;
                 }
             }
         } else {
-            int mc = m0 + 16 * ach[i].u + 8 * (ach[i].s & 1);
-            if (ach[i].live && mc < p.M) {
-                arow_n[i] = 0;  // column valid
-                int tap = mc / g.Ci; int ci = mc - tap * g.Ci; wg_i[i] = tap / g.kw; wg_j[i] = tap - wg_i[i] * g.kw;
-                wg_ci[i] = (ci >> 4) * 48 + 16 * (ach[i].s >> 1) + (ci & 8);  // packed column offset
+            int mc = m0 + asl[j].c;
+            if (mc < p.M) {
+                arow_n[j] = 0;  // column valid
+                int tap = mc / g.Ci; int ci = mc - tap * g.Ci; wg_i[j] = tap / g.kw; wg_j[j] = tap - wg_i[j] * g.kw;
+                wg_ci[j] = (ci >> 4) * 48 + 16 * asl[j].plane + (ci & 8);  // packed column offset
             }
         }
     }
 
     // K walk of FWD / DGRAD, channel-chunk-major: all taps (a, b) of one
     // 16-channel chunk, then the next chunk (see k_conv_gemm).  Kept as
-    // wave-uniform counters advanced once per loaded K-tile.
+    // wave-uniform counters advanced once per issued K-tile.
     const int TA = MODE == MODE_FWD ? g.kh : g.Th, TB = MODE == MODE_FWD ? g.kw : g.Tw;
     int wk_a = 0, wk_b = 0, wk_chunk = 0;
     if constexpr (MODE != MODE_WGRAD) {
@@ -250,192 +288,183 @@ k_conv_gemm_x6(const GemmArgs p) {
 
     const rsrc_t rA = make_rsrc((const float *)p.A, p.a_bytes);
     const rsrc_t rB = make_rsrc((const float *)p.B, p.b_bytes);
-    auto bload16 = [](rsrc_t r, unsigned off) {
-        return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+    typedef __attribute__((address_space(3))) void lds_void;
+    auto dma = [](rsrc_t r, char *lds_base, unsigned off) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void *)lds_base, 16, off, 0, 0, 0);
     };
-
-    u32x4 ra[A_NI], rb[B_NI];
-
     // WGRAD: output pixel -> (n, ho, wo) by multiply-shift division
     auto fdiv = [](unsigned n, unsigned mul, int shr) { return (__umulhi(n, mul) + n) >> shr; };
 
-    auto load_tiles = [&](int k0) {
-        // ----- A -----
-        if constexpr (MODE == MODE_FWD) {
-            const int i = wk_a, j = wk_b, ci0 = wk_chunk * BK;
+    // issue the DMA of the K-tile at k0 (the walker's tile) into LDS buffer sm
+    auto issue_tile = [&](int k0, char *sm) {
+        char *As = sm;
+        char *Bs = As + 3 * APL;
 #pragma unroll
-            for (int q = 0; q < A_NI; ++q) {
-                int hi = arow_h[q] + i, wi = arow_w[q] + j;
-                bool ok = arow_n[q] >= 0 && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
-                unsigned off = ((unsigned)((arow_n[q] * g.H + hi) * g.W + wi) * (3 * p.lda) + (ci0 >> 4) * 48 + 8 * ach[q].s) * 2u;
-                ra[q] = bload16(rA, ok ? off : DG_OOB);
+        for (int j = 0; j < A_NJ; ++j) {
+            if (!asl[j].live) continue;
+            const int d = wid + NW * j, per = BM / 32;
+            char *dst = As + asl[j].plane * APL + (d - asl[j].plane * per) * 1024;
+            unsigned off;
+            bool ok;
+            if constexpr (MODE == MODE_FWD) {
+                const int hi = arow_h[j] + wk_a, wi = arow_w[j] + wk_b;
+                ok = arow_n[j] >= 0 && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+                off = ((unsigned)((arow_n[j] * g.H + hi) * g.W + wi) * (3 * p.lda) + wk_chunk * 48 +
+                       16 * asl[j].plane + 8 * asl[j].c) * 2u;
+            } else if constexpr (MODE == MODE_DGRAD) {
+                const int i = ph.i0h + wk_a * g.sh, jj = ph.i0w + wk_b * g.sw;
+                const int ho = arow_h[j] - wk_a, wo = arow_w[j] - wk_b;
+                ok = i < g.kh && jj < g.kw && arow_n[j] >= 0 && (unsigned)ho < (unsigned)g.Ho && (unsigned)wo < (unsigned)g.Wo;
+                off = ((unsigned)((arow_n[j] * g.Ho + ho) * g.Wo + wo) * (3 * p.lda) + wk_chunk * 48 +
+                       16 * asl[j].plane + 8 * asl[j].c) * 2u;
+            } else {
+                const unsigned pix = (unsigned)(k0 + asl[j].r);
+                const unsigned t = fdiv(pix, p.mg_wo, p.sh_wo); const int wo = (int)(pix - t * g.Wo);
+                const unsigned n = fdiv(t, p.mg_ho, p.sh_ho); const int ho = (int)(t - n * g.Ho);
+                const int hi = ho * g.sh - g.pt + wg_i[j], wi = wo * g.sw - g.pl + wg_j[j];
+                ok = arow_n[j] >= 0 && (int)pix < kend && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
+                off = ((unsigned)(((int)n * g.H + hi) * g.W + wi) * (3 * p.lda) + wg_ci[j]) * 2u;
             }
-        } else if constexpr (MODE == MODE_DGRAD) {
-            const int i = ph.i0h + wk_a * g.sh, j = ph.i0w + wk_b * g.sw, co0 = wk_chunk * BK;
-            const bool tapok = (i < g.kh) && (j < g.kw);
-#pragma unroll
-            for (int q = 0; q < A_NI; ++q) {
-                int ho = arow_h[q] - wk_a, wo = arow_w[q] - wk_b;
-                bool ok = tapok && arow_n[q] >= 0 && (unsigned)ho < (unsigned)g.Ho && (unsigned)wo < (unsigned)g.Wo;
-                unsigned off = ((unsigned)((arow_n[q] * g.Ho + ho) * g.Wo + wo) * (3 * p.lda) + (co0 >> 4) * 48 + 8 * ach[q].s) * 2u;
-                ra[q] = bload16(rA, ok ? off : DG_OOB);
-            }
-        } else {  // WGRAD: x gathered at each chunk's tap, k-rows are output pixels
-#pragma unroll
-            for (int q = 0; q < A_NI; ++q) {
-                unsigned pix = (unsigned)(k0 + ach[q].r);
-                unsigned t = fdiv(pix, p.mg_wo, p.sh_wo); int wo = (int)(pix - t * g.Wo);
-                unsigned n = fdiv(t, p.mg_ho, p.sh_ho); int ho = (int)(t - n * g.Ho);
-                int hi = ho * g.sh - g.pt + wg_i[q], wi = wo * g.sw - g.pl + wg_j[q];
-                bool ok = arow_n[q] >= 0 && (int)pix < kend && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
-                unsigned off = ((unsigned)(((int)n * g.H + hi) * g.W + wi) * (3 * p.lda) + wg_ci[q]) * 2u;
-                ra[q] = bload16(rA, ok ? off : DG_OOB);
-            }
+            dma(rA, dst, ok ? off : DG_OOB);
         }
-        // ----- B -----
-        if constexpr (MODE == MODE_FWD) {  // w[k][co], k = (tap, ci)
-            const int kr0 = (wk_a * g.kw + wk_b) * g.Ci + wk_chunk * BK;
 #pragma unroll
-            for (int q = 0; q < B_NI; ++q) {
-                const int col = n0 + 16 * bch[q].u;
-                const unsigned k = (unsigned)(kr0 + bch[q].r);
-                const bool ok = bch[q].live && col < p.N;
-                const unsigned off = (k * (3 * p.ldb) + (col >> 4) * 48 + 8 * bch[q].s) * 2u;
-                rb[q] = bload16(rB, ok ? off : DG_OOB);
+        for (int j = 0; j < B_NJ; ++j) {
+            if (!bsl[j].live) continue;
+            const int d = wid + NW * j, per = BN / 32;
+            char *dst = Bs + bsl[j].plane * BPL + (d - bsl[j].plane * per) * 1024;
+            unsigned off;
+            bool ok;
+            if constexpr (MODE == MODE_FWD) {  // w[k][co], k = (tap, ci); RC: k-row r, columns c..c+7
+                const int col = n0 + bsl[j].c;
+                const unsigned k = (unsigned)((wk_a * g.kw + wk_b) * g.Ci + wk_chunk * BK + bsl[j].r);
+                ok = col < p.N;
+                off = (k * (3 * p.ldb) + (col >> 4) * 48 + 16 * bsl[j].plane + (col & 8)) * 2u;
+            } else if constexpr (MODE == MODE_DGRAD) {  // w[i,j,ci,co]: KC rows ci
+                const int i = ph.i0h + wk_a * g.sh, jj = ph.i0w + wk_b * g.sw;
+                const int ci = n0 + bsl[j].r;
+                ok = i < g.kh && jj < g.kw && ci < p.N;
+                off = ((unsigned)((i * g.kw + jj) * g.Ci + ci) * (3 * p.ldb) + wk_chunk * 48 + 16 * bsl[j].plane +
+                       8 * bsl[j].c) * 2u;
+            } else {  // WGRAD: dy rows (pixels) contiguous along co
+                const int col = n0 + bsl[j].c;
+                const int pix = k0 + bsl[j].r;
+                ok = col < p.N && pix < kend;
+                off = ((unsigned)pix * (3 * p.ldb) + (col >> 4) * 48 + 16 * bsl[j].plane + (col & 8)) * 2u;
             }
-        } else if constexpr (MODE == MODE_DGRAD) {  // w[i,j,ci,co]: rows ci contiguous along co
-            const int i = ph.i0h + wk_a * g.sh, j = ph.i0w + wk_b * g.sw, co0 = wk_chunk * BK;
-            const bool tapok = (i < g.kh) && (j < g.kw);
-#pragma unroll
-            for (int q = 0; q < B_NI; ++q) {
-                int ci = n0 + bch[q].r;
-                bool ok = bch[q].live && tapok && ci < p.N;
-                unsigned off = ((unsigned)((i * g.kw + j) * g.Ci + ci) * (3 * p.ldb) + (co0 >> 4) * 48 + 8 * bch[q].s) * 2u;
-                rb[q] = bload16(rB, ok ? off : DG_OOB);
-            }
-        } else {  // WGRAD: dy rows (pixels) contiguous along co
-#pragma unroll
-            for (int q = 0; q < B_NI; ++q) {
-                const int col = n0 + 16 * bch[q].u;
-                const int pix = k0 + bch[q].r;
-                const bool ok = bch[q].live && col < p.N && pix < kend;
-                const unsigned off = ((unsigned)pix * (3 * p.ldb) + (col >> 4) * 48 + 8 * bch[q].s) * 2u;
-                rb[q] = bload16(rB, ok ? off : DG_OOB);
-            }
+            dma(rB, dst, ok ? off : DG_OOB);
         }
         if constexpr (MODE != MODE_WGRAD) walk_next();
     };
-
-    auto store_tiles = [&](int buf) {
-        char *As = smem + buf * BUF;
-        char *Bs = As + 3 * APL;
-#pragma unroll
-        for (int q = 0; q < A_NI; ++q) {
-            if (!ach[q].live) continue;
-            const int h = ach[q].s & 1;
-            const int o = A_KC ? x6_off(ach[q].r, 8 * h) : x6_rc_off<BM>(ach[q].r, 16 * ach[q].u + 8 * h);
-            *reinterpret_cast<u32x4 *>(As + (ach[q].s >> 1) * APL + o) = ra[q];
-        }
-#pragma unroll
-        for (int q = 0; q < B_NI; ++q) {
-            if (!bch[q].live) continue;
-            const int h = bch[q].s & 1;
-            const int o = B_KC ? x6_off(bch[q].r, 8 * h) : x6_rc_off<BN>(bch[q].r, 16 * bch[q].u + 8 * h);
-            *reinterpret_cast<u32x4 *>(Bs + (bch[q].s >> 1) * BPL + o) = rb[q];
+    // wait until at most n of this wave's DMAs are in flight (n wave-uniform)
+    auto wait_dma = [](int n) {
+        switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+        case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
         }
     };
+    // barrier without the vmcnt(0) drain of __syncthreads (DMAs stay in flight)
+    auto barrier = []() {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
 
-    f32x16 acc[TM][TN];
+    f32x4 acc[TM][TN];
 #pragma unroll
     for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int b = 0; b < TN; ++b)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+        for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    load_tiles(kbeg);
-    store_tiles(0);
-    if (nk > 1) load_tiles(kbeg + BK);
-    __syncthreads();
-
-    for (int kt = 0; kt < nk; ++kt) {
-        const char *As = smem + (kt & 1) * BUF;
-        const char *Bs = As + 3 * APL;
-        bf16x8 af[3][TM], bf[3][TN];
-        // plane-major read order (hi, mid, lo), matching the MFMA order below,
-        // so the first products wait only for the hi fragments
+    // Fragments of one K-tile for v_mfma_f32_16x16x32_bf16 with the 32-wide K
+    // = two 16-wide plane pieces:  A [hi|mid], [hi|lo];  B [hi;mid], [mid;hi],
+    // [lo;hi].  Per 16x16 tile three MFMAs then sum all six piece products:
+    //   [hi|mid].[hi;mid] = hi.hi + mid.mid,  [hi|mid].[mid;hi] = hi.mid + mid.hi,
+    //   [hi|lo].[lo;hi]   = hi.lo + lo.hi.
+    auto read_frags = [&](const char *sm, bf16x8 (&ahm)[TM], bf16x8 (&ahl)[TM], bf16x8 (&b1)[TN],
+                          bf16x8 (&b2)[TN], bf16x8 (&b3)[TN]) {
+        const char *A0 = sm, *A1 = sm + APL, *A2 = sm + 2 * APL;
+        const char *B0 = sm + 3 * APL, *B1 = B0 + BPL, *B2 = B0 + 2 * BPL;
 #pragma unroll
-        for (int s = 0; s < 3; ++s) {
-#pragma unroll
-            for (int a = 0; a < TM; ++a) {
-                if constexpr (A_KC)
-                    af[s][a] = *reinterpret_cast<const bf16x8 *>(As + s * APL + x6_off(wm * WTM + a * 32 + l32, 8 * h2));
-                else
-                    af[s][a] = x6_rc_frag<BM>(As + s * APL, wm * WTM + a * 32, lane);
-            }
-#pragma unroll
-            for (int b = 0; b < TN; ++b) {
-                if constexpr (B_KC)
-                    bf[s][b] = *reinterpret_cast<const bf16x8 *>(Bs + s * BPL + x6_off(wn * WTN + b * 32 + l32, 8 * h2));
-                else
-                    bf[s][b] = x6_rc_frag<BN>(Bs + s * BPL, wn * WTN + b * 32, lane);
+        for (int a = 0; a < TM; ++a) {
+            const int r0 = wm * WTM + a * 16;
+            if constexpr (A_KC) {
+                ahm[a] = x6_kc_frag(A0, A1, r0, lane);
+                ahl[a] = x6_kc_frag(A0, A2, r0, lane);
+            } else {
+                ahm[a] = x6_rc_frag<BM>(A0, A1, r0, lane);
+                ahl[a] = x6_rc_frag<BM>(A0, A2, r0, lane);
             }
         }
-#if DG_X6_SCHED == 0
-        __builtin_amdgcn_sched_barrier(0);
-        // small products first, then the large ones
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+            const int c0 = wn * WTN + b * 16;
+            if constexpr (B_KC) {
+                b1[b] = x6_kc_frag(B0, B1, c0, lane);
+                b2[b] = x6_kc_frag(B1, B0, c0, lane);
+                b3[b] = x6_kc_frag(B2, B0, c0, lane);
+            } else {
+                b1[b] = x6_rc_frag<BN>(B0, B1, c0, lane);
+                b2[b] = x6_rc_frag<BN>(B1, B0, c0, lane);
+                b3[b] = x6_rc_frag<BN>(B2, B0, c0, lane);
+            }
+        }
+    };
+
+    // Three LDS buffers, two K-tiles in flight: iteration kt reads the
+    // fragments of tile kt, issues the DMA of tile kt+2 into the buffer tile
+    // kt-1 used (every wave passed the barrier after reading it), runs the
+    // MFMAs of tile kt, then waits until only tile kt+2's DMAs are outstanding
+    // and crosses the barrier.  DMAs past nk fetch harmless data into the
+    // idle buffer.
+    auto ktile = [&](int kt, const char *cur, char *nxt2) {
+        bf16x8 ahm[TM], ahl[TM], b1[TN], b2[TN], b3[TN];
+        read_frags(cur, ahm, ahl, b1, b2, b3);
+        issue_tile(kbeg + (kt + 2) * BK, nxt2);
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
-            for (int b = 0; b < TN; ++b) {
-                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2][a], bf[0][b], acc[a][b], 0, 0, 0);
-                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[2][b], acc[a][b], 0, 0, 0);
-                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][a], bf[1][b], acc[a][b], 0, 0, 0);
-            }
-        __builtin_amdgcn_sched_barrier(0);
-        if (kt + 1 < nk) store_tiles((kt & 1) ^ 1);
-        if (kt + 2 < nk) load_tiles(kbeg + (kt + 2) * BK);
-        __builtin_amdgcn_sched_barrier(0);
+            for (int b = 0; b < TN; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahm[a], b1[b], acc[a][b], 0, 0, 0);
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
-            for (int b = 0; b < TN; ++b) {
-                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][a], bf[0][b], acc[a][b], 0, 0, 0);
-                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[1][b], acc[a][b], 0, 0, 0);
-                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][a], bf[0][b], acc[a][b], 0, 0, 0);
-            }
-#else
-        // One basic block: the staging of tiles kt+1 / kt+2 (buffer loads never
-        // fault and the extra tiles past nk land in the idle LDS buffer, so it
-        // runs unconditionally) is interleaved with the MFMA chain, a few
-        // staging instructions in the shadow of each MFMA.
-        store_tiles((kt & 1) ^ 1);
-        load_tiles(kbeg + (kt + 2) * BK);
+            for (int b = 0; b < TN; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahm[a], b2[b], acc[a][b], 0, 0, 0);
 #pragma unroll
-        for (int s = 0; s < 6; ++s) {
-            // hi.hi, mid.hi, hi.mid, mid.mid, lo.hi, hi.lo
-            const int pa = s == 1 || s == 3 ? 1 : s == 4 ? 2 : 0;
-            const int pb = s == 2 || s == 3 ? 1 : s == 5 ? 2 : 0;
+        for (int a = 0; a < TM; ++a)
 #pragma unroll
-            for (int a = 0; a < TM; ++a)
-#pragma unroll
-                for (int b = 0; b < TN; ++b)
-                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[pa][a], bf[pb][b], acc[a][b], 0, 0, 0);
-        }
-        constexpr int NMF = 6 * TM * TN;
-#pragma unroll
-        for (int i = 0; i < NMF; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, DG_X6_VPM, 0);  // VALU
-            __builtin_amdgcn_sched_group_barrier(0x004, 4, 0);  // SALU
-            if (i % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
-            if (i % 2 == 1) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // DS write
-        }
-#endif
-        __syncthreads();
+            for (int b = 0; b < TN; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahl[a], b3[b], acc[a][b], 0, 0, 0);
+        wait_dma(nmine);
+        barrier();
+    };
+    issue_tile(kbeg, smem0);
+    issue_tile(kbeg + BK, smem1);
+    wait_dma(nmine);
+    barrier();
+    int kt = 0;
+    for (; kt + 2 < nk; kt += 3) {
+        ktile(kt, smem0, smem2);
+        ktile(kt + 1, smem1, smem0);
+        ktile(kt + 2, smem2, smem1);
     }
+    if (kt < nk) ktile(kt, smem0, smem2);
+    if (kt + 1 < nk) ktile(kt + 1, smem1, smem0);
+    wait_dma(0);
 
-    conv_epilogue<MODE, TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, Mrows, ph, phase, split, l32, h2);
+    conv_epilogue16<MODE, TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, Mrows, ph, phase, split, lane);
 }
 
 void launch_split3(const float *src, int ld, long rows, int C, unsigned short *dst, hipStream_t s) {
@@ -460,11 +489,8 @@ void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t
         DG_X6(1, 128, 64, 2, 2, 2)
         DG_X6(2, 64, 128, 2, 2, 2)
         DG_X6(3, 64, 64, 2, 2, 3)
-        DG_X6(4, 128, 128, 2, 2, 3)
-        DG_X6(5, 256, 128, 4, 2, 2)
-        DG_X6(6, 128, 256, 2, 4, 2)
-        DG_X6(7, 256, 128, 2, 2, 2)
-        DG_X6(8, 128, 256, 2, 2, 2)
+        DG_X6(4, 256, 128, 4, 2, 2)
+        DG_X6(5, 128, 256, 2, 4, 2)
     }
 #undef DG_X6
 }
