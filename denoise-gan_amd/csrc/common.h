@@ -17,18 +17,20 @@ __device__ __forceinline__ float act_fwd(float v, int act, float alpha) {
     case DG_ACT_LRELU: return v > 0.f ? v : v * alpha;
     case DG_ACT_RELU: return v > 0.f ? v : 0.f;
     case DG_ACT_TANH: return tanhf(v);
+    case DG_ACT_SIGMOID: return 1.f / (1.f + expf(-v));
     default: return v;
     }
 }
 
 // derivative of the activation expressed through its OUTPUT z
 // (LeakyReLU/ReLU: TF uses `features > 0 ? g : alpha*g`, sign(z) == sign(features);
-//  tanh: 1 - z^2).
+//  tanh: 1 - z^2; sigmoid: z (1 - z)).
 __device__ __forceinline__ float act_grad_from_out(float z, int act, float alpha) {
     switch (act) {
     case DG_ACT_LRELU: return z > 0.f ? 1.f : alpha;
     case DG_ACT_RELU: return z > 0.f ? 1.f : 0.f;
     case DG_ACT_TANH: return 1.f - z * z;
+    case DG_ACT_SIGMOID: return z * (1.f - z);
     default: return 1.f;
     }
 }

@@ -1,0 +1,794 @@
+// Layer kernels of the SRGAN / FastSRGAN / Autoencoder generators and
+// discriminators and of the frozen VGG19 feature extractor (content loss):
+//
+//   PReLU(shared_axes=[1,2]) with an optional tf.nn.depth_to_space(., 2)
+//       in front of it                      srgan.py:137-139, :152, fsrgan.py:197-199, :207
+//   residual Add                             srgan.py:165, :170; fsrgan.py:187, :212
+//   DepthwiseConv2D(3, s1, 'same', bias)     fsrgan.py:162-167
+//   MaxPool2D(2, 2)                          autoencoder.py:111-115 (and VGG19's block pools)
+//   UpSampling2D(2, 'nearest') + ReLU        autoencoder.py:117-131
+//   vgg19.preprocess_input((x+1)*255/2)      srgan.py:71-73, fsrgan.py:74-76, pix2pix.py:45-51
+//   content MSE on VGG features / 12.75      srgan.py:74-76
+//   the SR-GAN loss set (adv / mae / mse / tv / disc) with gradients
+//                                            train_srgan.py:84-96, train_fsrgan.py:86-96,
+//                                            train_autoencoder.py:84-100
+//
+// Every activation is NHWC fp32 with an explicit pixel stride.  All
+// per-channel reductions are deterministic: fixed row chunks -> per-chunk
+// partials -> an ordered final sum.  Input-gradient outputs take `beta`
+// (dx = new + beta * dx) so a tensor with several consumers accumulates its
+// gradient in place.
+#include "common.h"
+#include <algorithm>
+
+namespace dg {
+
+static unsigned lgrid(long n) { return (unsigned)std::max<long>(1, std::min<long>(dg_cdiv(n, 256), 16384)); }
+
+// row chunking of the per-channel partial reductions: 64 channels x 4 row lanes per block
+struct RedPlan {
+    int R;      // row chunks (grid.y)
+    long rows;  // rows per chunk
+};
+static RedPlan red_plan(long M) {
+    RedPlan p;
+    long r = std::min<long>(512, std::max<long>(1, (M + 255) / 256));
+    p.rows = (M + r - 1) / r;
+    p.R = (int)((M + p.rows - 1) / p.rows);
+    return p;
+}
+
+// out[c] = sum_r part[r * rstride + c] (+ beta * out[c]), fixed order
+__global__ void __launch_bounds__(256) k_rows_final(const float *part, int R, long rstride, int C, float *out,
+                                                   float beta) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    float s = 0.f;
+    for (int r = 0; r < R; ++r) s += part[(long)r * rstride + c];
+    out[c] = beta != 0.f ? s + beta * out[c] : s;
+}
+
+// --------------------------------------------------------------------------
+// PReLU with optional depth_to_space (block B).  Input y [N,H,W,C*B*B],
+// output z [N,H*B,W*B,C]; TF depth_to_space (NHWC, DCR):
+//   z[n, h*B+i, w*B+j, c] = y[n, h, w, (i*B + j)*C + c]
+// PReLU = relu(x) - alpha*relu(-x)  (Keras): x>0 ? x : alpha[c]*x; its
+// gradient is 1 / alpha / 0 for x >0 / <0 / ==0, d alpha = -relu(-x).
+// --------------------------------------------------------------------------
+struct ShufGeom {
+    int H, W, C, B;
+};
+__device__ __forceinline__ long shuf_out_pix(long pix, int ch, const ShufGeom &g, int &c) {
+    const int q = ch / g.C;
+    c = ch - q * g.C;
+    const int i = q / g.B, j = q - i * g.B;
+    const long hw = (long)g.H * g.W;
+    const long n = pix / hw;
+    const int r = (int)(pix - n * hw);
+    const int h = r / g.W, w = r - h * g.W;
+    return (n * g.H * g.B + (long)h * g.B + i) * ((long)g.W * g.B) + (long)w * g.B + j;
+}
+
+__global__ void __launch_bounds__(256) k_prelu_fwd(long npix, ShufGeom g, const float *__restrict__ y, int ldy,
+                                                  const float *__restrict__ alpha, float *__restrict__ z, int ldz) {
+    const int CB = g.C * g.B * g.B;
+    const long total = npix * CB;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long pix = e / CB;
+        const int ch = (int)(e - pix * CB);
+        int c;
+        const long op = shuf_out_pix(pix, ch, g, c);
+        const float v = y[pix * ldy + ch];
+        z[op * ldz + c] = v > 0.f ? v : alpha[c] * v;
+    }
+}
+
+// dy = dz * prelu'(y) (+beta*dy); partial d alpha sums over row chunks
+__global__ void __launch_bounds__(256) k_prelu_bwd(long npix, ShufGeom g, const float *__restrict__ y, int ldy,
+                                                  const float *__restrict__ alpha, const float *__restrict__ dz,
+                                                  int lddz, float *__restrict__ dy, int lddy, float beta, long rows,
+                                                  float *__restrict__ part) {
+    const int CB = g.C * g.B * g.B;
+    const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+    const int ch = blockIdx.x * 64 + cl;
+    const long r0 = (long)blockIdx.y * rows;
+    const long r1 = std::min<long>(npix, r0 + rows);
+    float acc = 0.f;
+    int c = 0;
+    if (ch < CB) {
+        for (long pix = r0 + rl; pix < r1; pix += 4) {
+            const long op = shuf_out_pix(pix, ch, g, c);
+            const float v = y[pix * ldy + ch];
+            const float gz = dz[op * lddz + c];
+            const float d = v > 0.f ? gz : (v < 0.f ? alpha[c] * gz : 0.f);
+            float *o = dy + pix * lddy + ch;
+            *o = beta != 0.f ? d + beta * *o : d;
+            acc += gz * fminf(v, 0.f);
+        }
+    }
+    __shared__ float red[4][64];
+    red[rl][cl] = acc;
+    __syncthreads();
+    if (rl == 0 && ch < CB) {
+        float s = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+        part[(long)blockIdx.y * CB + ch] = s;  // per input channel; folded over the B*B sub-positions below
+    }
+}
+
+// d alpha[c] = sum_q sum_r part[r][q*C + c]  (+ beta * dalpha)
+__global__ void __launch_bounds__(256) k_prelu_alpha_final(const float *part, int R, int C, int BB, float *dalpha,
+                                                          float beta) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    float s = 0.f;
+    for (int r = 0; r < R; ++r)
+        for (int q = 0; q < BB; ++q) s += part[(long)r * C * BB + q * C + c];
+    dalpha[c] = beta != 0.f ? s + beta * dalpha[c] : s;
+}
+
+// --------------------------------------------------------------------------
+// elementwise helpers
+// --------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_add(long npix, int C, const float *a, int lda, const float *b, int ldb,
+                                            float *out, int ldo) {
+    const long total = npix * C;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long p = e / C;
+        const int c = (int)(e - p * C);
+        out[p * ldo + c] = a[p * lda + c] + b[p * ldb + c];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_accumulate(long npix, int C, const float *src, int lds, float *dst, int ldd,
+                                                   float beta) {
+    const long total = npix * C;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long p = e / C;
+        const int c = (int)(e - p * C);
+        float *o = dst + p * ldd + c;
+        const float v = src[p * lds + c];
+        *o = beta != 0.f ? v + beta * *o : v;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_act_fwd(long npix, int C, const float *x, int ldx, int act, float alpha,
+                                                float *z, int ldz) {
+    const long total = npix * C;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long p = e / C;
+        const int c = (int)(e - p * C);
+        z[p * ldz + c] = act_fwd(x[p * ldx + c], act, alpha);
+    }
+}
+
+// --------------------------------------------------------------------------
+// MaxPool2D(2, strides 2, 'valid' == 'same' for even sizes).  Ho = H/2.
+// The gradient goes to the first maximum of each window in row-major order
+// (TF's MaxPoolGrad routes to the forward argmax).  Rows/cols beyond 2*Ho
+// (odd sizes, 'valid') get zero gradient.
+// --------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_maxpool_fwd(int N, int H, int W, int C, const float *x, int ldx, float *y,
+                                                    int ldy) {
+    const int Ho = H / 2, Wo = W / 2;
+    const long total = (long)N * Ho * Wo * C;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long op = e / C;
+        const int c = (int)(e - op * C);
+        const int wo = (int)(op % Wo);
+        const long t = op / Wo;
+        const int ho = (int)(t % Ho);
+        const long n = t / Ho;
+        const long ip = (n * H + 2 * ho) * W + 2 * wo;
+        const float a = x[ip * ldx + c], b = x[(ip + 1) * ldx + c];
+        const float d = x[(ip + W) * ldx + c], f = x[(ip + W + 1) * ldx + c];
+        y[op * ldy + c] = fmaxf(fmaxf(a, b), fmaxf(d, f));
+    }
+}
+
+__global__ void __launch_bounds__(256) k_maxpool_bwd(int N, int H, int W, int C, const float *x, int ldx,
+                                                    const float *dy, int lddy, float *dx, int lddx, float beta) {
+    const int Ho = H / 2, Wo = W / 2;
+    const long total = (long)N * H * W * C;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long ip = e / C;
+        const int c = (int)(e - ip * C);
+        const int w = (int)(ip % W);
+        const long t = ip / W;
+        const int h = (int)(t % H);
+        const long n = t / H;
+        float g = 0.f;
+        const int ho = h >> 1, wo = w >> 1;
+        if (ho < Ho && wo < Wo) {
+            const long p0 = (n * H + 2 * ho) * W + 2 * wo;
+            const float v[4] = {x[p0 * ldx + c], x[(p0 + 1) * ldx + c], x[(p0 + W) * ldx + c],
+                                x[(p0 + W + 1) * ldx + c]};
+            int am = 0;
+#pragma unroll
+            for (int q = 1; q < 4; ++q)
+                if (v[q] > v[am]) am = q;
+            const int mine = (h & 1) * 2 + (w & 1);
+            if (am == mine) g = dy[((n * Ho + ho) * Wo + wo) * lddy + c];
+        }
+        float *o = dx + ip * lddx + c;
+        *o = beta != 0.f ? g + beta * *o : g;
+    }
+}
+
+// --------------------------------------------------------------------------
+// UpSampling2D(2, nearest) followed by ReLU (autoencoder.py:117-131: the
+// unpool's relu commutes with the replication).  x [N,H,W,C] -> z [N,2H,2W,C].
+// --------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_upsample_relu_fwd(int N, int H, int W, int C, const float *x, int ldx,
+                                                          float *z, int ldz) {
+    const int Ho = 2 * H, Wo = 2 * W;
+    const long total = (long)N * Ho * Wo * C;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long op = e / C;
+        const int c = (int)(e - op * C);
+        const int wo = (int)(op % Wo);
+        const long t = op / Wo;
+        const int ho = (int)(t % Ho);
+        const long n = t / Ho;
+        const float v = x[((n * H + (ho >> 1)) * W + (wo >> 1)) * ldx + c];
+        z[op * ldz + c] = v > 0.f ? v : 0.f;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_upsample_relu_bwd(int N, int H, int W, int C, const float *x, int ldx,
+                                                          const float *dz, int lddz, float *dx, int lddx, float beta) {
+    const int Wo = 2 * W;
+    const long total = (long)N * H * W * C;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long ip = e / C;
+        const int c = (int)(e - ip * C);
+        const int w = (int)(ip % W);
+        const long t = ip / W;
+        const int h = (int)(t % H);
+        const long n = t / H;
+        float g = 0.f;
+        if (x[ip * ldx + c] > 0.f) {
+            const long o0 = (n * 2 * H + 2 * h) * (long)Wo + 2 * w;
+            g = (dz[o0 * lddz + c] + dz[(o0 + 1) * lddz + c]) + (dz[(o0 + Wo) * lddz + c] + dz[(o0 + Wo + 1) * lddz + c]);
+        }
+        float *o = dx + ip * lddx + c;
+        *o = beta != 0.f ? g + beta * *o : g;
+    }
+}
+
+// --------------------------------------------------------------------------
+// DepthwiseConv2D(3x3, stride 1, 'same' (pad 1/1), depth_multiplier 1, bias)
+// kernel k[i][j][c] (Keras [3,3,C,1]).
+//   y[n,h,w,c] = b[c] + sum_ij x[n,h+i-1,w+j-1,c] k[i,j,c]
+// --------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_dw_fwd(int N, int H, int W, int C, const float *__restrict__ x, int ldx,
+                                               const float *__restrict__ k, const float *__restrict__ b,
+                                               float *__restrict__ y, int ldy) {
+    const long total = (long)N * H * W * C;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long p = e / C;
+        const int c = (int)(e - p * C);
+        const int w = (int)(p % W);
+        const long t = p / W;
+        const int h = (int)(t % H);
+        const long n = t / H;
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int hh = h + i - 1;
+            if (hh < 0 || hh >= H) continue;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const int ww = w + j - 1;
+                if (ww < 0 || ww >= W) continue;
+                s = fmaf(x[((n * H + hh) * W + ww) * ldx + c], k[(i * 3 + j) * C + c], s);
+            }
+        }
+        y[p * ldy + c] = s + (b ? b[c] : 0.f);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_dw_bwd_data(int N, int H, int W, int C, const float *__restrict__ dy,
+                                                    int lddy, const float *__restrict__ k, float *__restrict__ dx,
+                                                    int lddx, float beta) {
+    const long total = (long)N * H * W * C;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long p = e / C;
+        const int c = (int)(e - p * C);
+        const int w = (int)(p % W);
+        const long t = p / W;
+        const int h = (int)(t % H);
+        const long n = t / H;
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int hh = h - i + 1;  // output row that reads x[h] through tap i
+            if (hh < 0 || hh >= H) continue;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const int ww = w - j + 1;
+                if (ww < 0 || ww >= W) continue;
+                s = fmaf(dy[((n * H + hh) * W + ww) * lddy + c], k[(i * 3 + j) * C + c], s);
+            }
+        }
+        float *o = dx + p * lddx + c;
+        *o = beta != 0.f ? s + beta * *o : s;
+    }
+}
+
+// partial sums of dk[i][j][c] (9 taps) and db[c] over a row chunk: part[r][10][C]
+__global__ void __launch_bounds__(256) k_dw_bwd_filter(int N, int H, int W, int C, const float *__restrict__ x,
+                                                      int ldx, const float *__restrict__ dy, int lddy, long rows,
+                                                      float *__restrict__ part) {
+    const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + cl;
+    const long M = (long)N * H * W;
+    const long r0 = (long)blockIdx.y * rows;
+    const long r1 = std::min<long>(M, r0 + rows);
+    float acc[10];
+#pragma unroll
+    for (int q = 0; q < 10; ++q) acc[q] = 0.f;
+    if (c < C) {
+        for (long p = r0 + rl; p < r1; p += 4) {
+            const int w = (int)(p % W);
+            const long t = p / W;
+            const int h = (int)(t % H);
+            const long n = t / H;
+            const float g = dy[p * lddy + c];
+            acc[9] += g;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const int hh = h + i - 1;
+                if (hh < 0 || hh >= H) continue;
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const int ww = w + j - 1;
+                    if (ww < 0 || ww >= W) continue;
+                    acc[i * 3 + j] = fmaf(x[((n * H + hh) * W + ww) * ldx + c], g, acc[i * 3 + j]);
+                }
+            }
+        }
+    }
+    __shared__ float red[4][10][64];
+#pragma unroll
+    for (int q = 0; q < 10; ++q) red[rl][q][cl] = acc[q];
+    __syncthreads();
+    if (c < C) {
+        for (int q = rl; q < 10; q += 4) {
+            const float s = red[0][q][cl] + red[1][q][cl] + red[2][q][cl] + red[3][q][cl];
+            part[((long)blockIdx.y * 10 + q) * C + c] = s;
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
+// vgg19.preprocess_input (caffe mode) of (x + 1) * 255 / 2:
+//   z[p, c'] = 127.5 * (x[p, 2 - c'] + 1) - mean[c'],  mean = (103.939, 116.779, 123.68) (BGR)
+// ((x+1)*255)/2 and (x+1)*127.5 round identically in fp32: halving is exact.
+// --------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_vgg_pre_fwd(long npix, const float *x, int ldx, float *z, int ldz) {
+    const long total = npix * 3;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long p = e / 3;
+        const int c = (int)(e - p * 3);
+        const float mean = c == 0 ? 103.939f : (c == 1 ? 116.779f : 123.68f);
+        z[p * ldz + c] = (x[p * ldx + (2 - c)] + 1.f) * 255.f / 2.f - mean;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_vgg_pre_bwd(long npix, const float *dz, int lddz, float *dx, int lddx,
+                                                    float beta) {
+    const long total = npix * 3;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long p = e / 3;
+        const int c = (int)(e - p * 3);
+        const float g = 127.5f * dz[p * lddz + (2 - c)];
+        float *o = dx + p * lddx + c;
+        *o = beta != 0.f ? g + beta * *o : g;
+    }
+}
+
+// --------------------------------------------------------------------------
+// scaled MSE: value = mean((s*a - s*b)^2) (Keras MeanSquaredError of
+// features / 12.75); da = w * 2 s (s*a - s*b) / n.   Two-stage sum.
+// --------------------------------------------------------------------------
+constexpr int MSE_BLOCKS = 512;
+
+__device__ __forceinline__ float block_sum256(float v, float *red) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) red[w] = v;
+    __syncthreads();
+    return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void __launch_bounds__(256) k_mse_partial(long npix, int C, const float *a, int lda, const float *b,
+                                                    int ldb, float s, float wgrad, float inv_n, float *da, int ldda,
+                                                    float *part) {
+    __shared__ float red[4];
+    const long total = npix * C;
+    float acc = 0.f;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long p = e / C;
+        const int c = (int)(e - p * C);
+        const float d = a[p * lda + c] * s - b[p * ldb + c] * s;
+        acc += d * d;
+        if (da) da[p * ldda + c] = wgrad * 2.f * s * d * inv_n;
+    }
+    const float r = block_sum256(acc, red);
+    if (threadIdx.x == 0) part[blockIdx.x] = r;
+}
+
+__global__ void k_mse_final(const float *part, int nb, float inv_n, float *out) {
+    if (threadIdx.x != 0) return;
+    float s = 0.f;
+    for (int i = 0; i < nb; ++i) s += part[i];
+    out[0] = s * inv_n;
+}
+
+// --------------------------------------------------------------------------
+// SR-GAN loss set (train_srgan.py:84-96, train_fsrgan.py:86-96,
+// train_autoencoder.py:84-100):
+//   adv  = w_adv * BCE_logits(1, D(G(x)))         content = *content_value
+//   mae  = mean|y - g|          mse = mean (y - g)^2
+//   var  = w_var * mean_b total_variation(y - g)
+//   disc = disc_scale * (BCE_logits(1, D(y)) + BCE_logits(0, D(G(x))))
+//   gen_total = adv + t_mae*mae + t_mse*mse + t_content*content + t_var*var
+// out[7] = {gen_total, adv, mae, mse, content, disc, var}; gradients of
+// gen_total w.r.t. g (excluding the adv and content paths, which flow back
+// through D and VGG) and of the two BCE sums w.r.t. the logits.
+// --------------------------------------------------------------------------
+struct GanLossArgs {
+    int B, H, W, C;
+    const float *gen; int ldgen;
+    const float *tgt; int ldtgt;
+    const float *zr; const float *zf; int nlog;
+    float w_adv, w_var, disc_scale, t_mae, t_mse, t_content, t_var;
+    const float *content;
+    float *out;
+    float *dgen; int lddgen;
+    float *dzr_d, *dzf_d, *dzf_g;
+    float *part_img;  // [LOSS_BLOCKS][3]
+    float *part_log;  // [LOG_BLOCKS][3]
+};
+constexpr int GL_IMG_BLOCKS = 1024;
+constexpr int GL_LOG_BLOCKS = 64;
+
+__device__ __forceinline__ float sgnf(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
+__device__ __forceinline__ float bce_logit(float z, float y) { return fmaxf(z, 0.f) - z * y + log1pf(expf(-fabsf(z))); }
+__device__ __forceinline__ float sigm(float z) { return 1.f / (1.f + expf(-z)); }
+
+__global__ void __launch_bounds__(256) k_ganloss_img(const GanLossArgs a) {
+    __shared__ float red[4];
+    const long npix = (long)a.B * a.H * a.W;
+    const long total = npix * a.C;
+    const float inv_n = 1.f / (float)total;
+    const float tvs = a.t_var * a.w_var / (float)a.B;
+    float s1 = 0.f, s2 = 0.f, stv = 0.f;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long pix = e / a.C;
+        const int c = (int)(e - pix * a.C);
+        const int w = (int)(pix % a.W);
+        const int h = (int)((pix / a.W) % a.H);
+        auto dv = [&](long px) { return a.tgt[px * a.ldtgt + c] - a.gen[px * a.ldgen + c]; };
+        const float d = dv(pix);
+        s1 += fabsf(d);
+        s2 += d * d;
+        float gtv = 0.f;
+        if (h + 1 < a.H) { const float dd = dv(pix + a.W) - d; stv += fabsf(dd); gtv -= sgnf(dd); }
+        if (w + 1 < a.W) { const float dd = dv(pix + 1) - d; stv += fabsf(dd); gtv -= sgnf(dd); }
+        if (a.dgen) {
+            if (h > 0) gtv += sgnf(d - dv(pix - a.W));
+            if (w > 0) gtv += sgnf(d - dv(pix - 1));
+            const float gd = a.t_mae * sgnf(d) * inv_n + a.t_mse * 2.f * d * inv_n + tvs * gtv;
+            a.dgen[pix * a.lddgen + c] = -gd;  // d = y - g
+        }
+    }
+    float r;
+    r = block_sum256(s1, red); if (threadIdx.x == 0) a.part_img[blockIdx.x * 3 + 0] = r;
+    r = block_sum256(s2, red); if (threadIdx.x == 0) a.part_img[blockIdx.x * 3 + 1] = r;
+    r = block_sum256(stv, red); if (threadIdx.x == 0) a.part_img[blockIdx.x * 3 + 2] = r;
+}
+
+__global__ void __launch_bounds__(256) k_ganloss_logits(const GanLossArgs a) {
+    __shared__ float red[4];
+    const float inv_n = 1.f / (float)a.nlog;
+    float r1 = 0.f, f0 = 0.f, f1 = 0.f;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < a.nlog; e += gridDim.x * blockDim.x) {
+        const float zr = a.zr[e], zf = a.zf[e];
+        r1 += bce_logit(zr, 1.f);
+        f0 += bce_logit(zf, 0.f);
+        f1 += bce_logit(zf, 1.f);
+        if (a.dzr_d) a.dzr_d[e] = a.disc_scale * (sigm(zr) - 1.f) * inv_n;
+        if (a.dzf_d) a.dzf_d[e] = a.disc_scale * sigm(zf) * inv_n;
+        if (a.dzf_g) a.dzf_g[e] = a.w_adv * (sigm(zf) - 1.f) * inv_n;
+    }
+    float r;
+    r = block_sum256(r1, red); if (threadIdx.x == 0) a.part_log[blockIdx.x * 3 + 0] = r;
+    r = block_sum256(f0, red); if (threadIdx.x == 0) a.part_log[blockIdx.x * 3 + 1] = r;
+    r = block_sum256(f1, red); if (threadIdx.x == 0) a.part_log[blockIdx.x * 3 + 2] = r;
+}
+
+__global__ void k_ganloss_final(const GanLossArgs a) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    float l1 = 0.f, l2 = 0.f, tv = 0.f, r1 = 0.f, f0 = 0.f, f1 = 0.f;
+    for (int b = 0; b < GL_IMG_BLOCKS; ++b) {
+        l1 += a.part_img[b * 3 + 0]; l2 += a.part_img[b * 3 + 1]; tv += a.part_img[b * 3 + 2];
+    }
+    for (int b = 0; b < GL_LOG_BLOCKS; ++b) {
+        r1 += a.part_log[b * 3 + 0]; f0 += a.part_log[b * 3 + 1]; f1 += a.part_log[b * 3 + 2];
+    }
+    const float n = (float)((long)a.B * a.H * a.W * a.C);
+    const float nl = (float)a.nlog;
+    const float adv = a.w_adv * (f1 / nl);
+    const float mae = l1 / n, mse = l2 / n;
+    const float var = a.w_var * (tv / (float)a.B);
+    const float cont = a.content ? a.content[0] : 0.f;
+    a.out[0] = adv + a.t_mae * mae + a.t_mse * mse + a.t_content * cont + a.t_var * var;
+    a.out[1] = adv;
+    a.out[2] = mae;
+    a.out[3] = mse;
+    a.out[4] = cont;
+    a.out[5] = a.disc_scale * (r1 / nl + f0 / nl);
+    a.out[6] = var;
+}
+
+}  // namespace dg
+
+extern "C" {
+
+int dg_prelu_workspace_size(int N, int H, int W, int C, int block, size_t *bytes) {
+    DG_ARG(bytes, "NULL argument");
+    DG_ARG(N > 0 && H > 0 && W > 0 && C > 0 && (block == 1 || block == 2), "bad shape");
+    dg::RedPlan rp = dg::red_plan((long)N * H * W);
+    *bytes = (size_t)rp.R * C * block * block * sizeof(float) + 256;
+    return DG_OK;
+}
+
+int dg_prelu_fwd(int N, int H, int W, int C, int block, const float *y, int ldy, const float *alpha, float *z,
+                 int ldz, dg_stream_t stream) {
+    DG_ARG(y && alpha && z, "NULL tensor");
+    DG_ARG(N > 0 && H > 0 && W > 0 && C > 0 && (block == 1 || block == 2), "bad shape");
+    DG_ARG(ldy >= C * block * block && ldz >= C, "bad strides");
+    const long npix = (long)N * H * W;
+    dg::ShufGeom g{H, W, C, block};
+    hipLaunchKernelGGL(dg::k_prelu_fwd, dim3(dg::lgrid(npix * C * block * block)), dim3(256), 0, (hipStream_t)stream,
+                       npix, g, y, ldy, alpha, z, ldz);
+    DG_LAUNCHED("prelu_fwd");
+    return DG_OK;
+}
+
+int dg_prelu_bwd(int N, int H, int W, int C, int block, const float *y, int ldy, const float *alpha, const float *dz,
+                 int lddz, float *dy, int lddy, float beta, float *dalpha, float alpha_beta, void *ws,
+                 size_t ws_bytes, dg_stream_t stream) {
+    DG_ARG(y && alpha && dz && dy && ws, "NULL tensor");
+    DG_ARG(N > 0 && H > 0 && W > 0 && C > 0 && (block == 1 || block == 2), "bad shape");
+    DG_ARG(ldy >= C * block * block && lddy >= C * block * block && lddz >= C, "bad strides");
+    size_t need;
+    dg_prelu_workspace_size(N, H, W, C, block, &need);
+    DG_ARG(ws_bytes >= need, "workspace too small");
+    const long npix = (long)N * H * W;
+    const int CB = C * block * block;
+    dg::RedPlan rp = dg::red_plan(npix);
+    dg::ShufGeom g{H, W, C, block};
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(dg::k_prelu_bwd, dim3(dg_cdiv(CB, 64), rp.R), dim3(256), 0, s, npix, g, y, ldy, alpha, dz, lddz,
+                       dy, lddy, beta, rp.rows, (float *)ws);
+    DG_LAUNCHED("prelu_bwd");
+    if (dalpha) {
+        hipLaunchKernelGGL(dg::k_prelu_alpha_final, dim3(dg_cdiv(C, 256)), dim3(256), 0, s, (const float *)ws, rp.R, C,
+                           block * block, dalpha, alpha_beta);
+        DG_LAUNCHED("prelu_alpha_final");
+    }
+    return DG_OK;
+}
+
+int dg_add(int64_t npix, int C, const float *a, int lda, const float *b, int ldb, float *out, int ldo,
+           dg_stream_t stream) {
+    DG_ARG(a && b && out, "NULL tensor");
+    DG_ARG(C > 0 && lda >= C && ldb >= C && ldo >= C, "bad strides");
+    if (npix == 0) return DG_OK;
+    hipLaunchKernelGGL(dg::k_add, dim3(dg::lgrid(npix * C)), dim3(256), 0, (hipStream_t)stream, (long)npix, C, a, lda,
+                       b, ldb, out, ldo);
+    DG_LAUNCHED("add");
+    return DG_OK;
+}
+
+int dg_accumulate(int64_t npix, int C, const float *src, int lds, float *dst, int ldd, float beta,
+                  dg_stream_t stream) {
+    DG_ARG(src && dst, "NULL tensor");
+    DG_ARG(C > 0 && lds >= C && ldd >= C, "bad strides");
+    if (npix == 0) return DG_OK;
+    hipLaunchKernelGGL(dg::k_accumulate, dim3(dg::lgrid(npix * C)), dim3(256), 0, (hipStream_t)stream, (long)npix, C,
+                       src, lds, dst, ldd, beta);
+    DG_LAUNCHED("accumulate");
+    return DG_OK;
+}
+
+int dg_act_fwd(int64_t npix, int C, const float *x, int ldx, int act, float alpha, float *z, int ldz,
+               dg_stream_t stream) {
+    DG_ARG(x && z, "NULL tensor");
+    DG_ARG(C > 0 && ldx >= C && ldz >= C, "bad strides");
+    if (npix == 0) return DG_OK;
+    hipLaunchKernelGGL(dg::k_act_fwd, dim3(dg::lgrid(npix * C)), dim3(256), 0, (hipStream_t)stream, (long)npix, C, x,
+                       ldx, act, alpha, z, ldz);
+    DG_LAUNCHED("act_fwd");
+    return DG_OK;
+}
+
+int dg_maxpool2_fwd(int N, int H, int W, int C, const float *x, int ldx, float *y, int ldy, dg_stream_t stream) {
+    DG_ARG(x && y, "NULL tensor");
+    DG_ARG(N > 0 && H >= 2 && W >= 2 && C > 0 && ldx >= C && ldy >= C, "bad shape");
+    const long total = (long)N * (H / 2) * (W / 2) * C;
+    hipLaunchKernelGGL(dg::k_maxpool_fwd, dim3(dg::lgrid(total)), dim3(256), 0, (hipStream_t)stream, N, H, W, C, x, ldx,
+                       y, ldy);
+    DG_LAUNCHED("maxpool_fwd");
+    return DG_OK;
+}
+
+int dg_maxpool2_bwd(int N, int H, int W, int C, const float *x, int ldx, const float *dy, int lddy, float *dx,
+                    int lddx, float beta, dg_stream_t stream) {
+    DG_ARG(x && dy && dx, "NULL tensor");
+    DG_ARG(N > 0 && H >= 2 && W >= 2 && C > 0 && ldx >= C && lddy >= C && lddx >= C, "bad shape");
+    const long total = (long)N * H * W * C;
+    hipLaunchKernelGGL(dg::k_maxpool_bwd, dim3(dg::lgrid(total)), dim3(256), 0, (hipStream_t)stream, N, H, W, C, x, ldx,
+                       dy, lddy, dx, lddx, beta);
+    DG_LAUNCHED("maxpool_bwd");
+    return DG_OK;
+}
+
+int dg_upsample2_relu_fwd(int N, int H, int W, int C, const float *x, int ldx, float *z, int ldz,
+                          dg_stream_t stream) {
+    DG_ARG(x && z, "NULL tensor");
+    DG_ARG(N > 0 && H > 0 && W > 0 && C > 0 && ldx >= C && ldz >= C, "bad shape");
+    const long total = (long)N * 4 * H * W * C;
+    hipLaunchKernelGGL(dg::k_upsample_relu_fwd, dim3(dg::lgrid(total)), dim3(256), 0, (hipStream_t)stream, N, H, W, C,
+                       x, ldx, z, ldz);
+    DG_LAUNCHED("upsample_relu_fwd");
+    return DG_OK;
+}
+
+int dg_upsample2_relu_bwd(int N, int H, int W, int C, const float *x, int ldx, const float *dz, int lddz, float *dx,
+                          int lddx, float beta, dg_stream_t stream) {
+    DG_ARG(x && dz && dx, "NULL tensor");
+    DG_ARG(N > 0 && H > 0 && W > 0 && C > 0 && ldx >= C && lddz >= C && lddx >= C, "bad shape");
+    const long total = (long)N * H * W * C;
+    hipLaunchKernelGGL(dg::k_upsample_relu_bwd, dim3(dg::lgrid(total)), dim3(256), 0, (hipStream_t)stream, N, H, W, C,
+                       x, ldx, dz, lddz, dx, lddx, beta);
+    DG_LAUNCHED("upsample_relu_bwd");
+    return DG_OK;
+}
+
+int dg_dwconv3_workspace_size(int N, int H, int W, int C, size_t *bytes) {
+    DG_ARG(bytes, "NULL argument");
+    DG_ARG(N > 0 && H > 0 && W > 0 && C > 0, "bad shape");
+    dg::RedPlan rp = dg::red_plan((long)N * H * W);
+    *bytes = (size_t)rp.R * 10 * C * sizeof(float) + 256;
+    return DG_OK;
+}
+
+int dg_dwconv3_fwd(int N, int H, int W, int C, const float *x, int ldx, const float *k, const float *bias, float *y,
+                   int ldy, dg_stream_t stream) {
+    DG_ARG(x && k && y, "NULL tensor");
+    DG_ARG(N > 0 && H > 0 && W > 0 && C > 0 && ldx >= C && ldy >= C, "bad shape");
+    hipLaunchKernelGGL(dg::k_dw_fwd, dim3(dg::lgrid((long)N * H * W * C)), dim3(256), 0, (hipStream_t)stream, N, H, W,
+                       C, x, ldx, k, bias, y, ldy);
+    DG_LAUNCHED("dwconv_fwd");
+    return DG_OK;
+}
+
+int dg_dwconv3_bwd_data(int N, int H, int W, int C, const float *dy, int lddy, const float *k, float *dx, int lddx,
+                        float beta, dg_stream_t stream) {
+    DG_ARG(dy && k && dx, "NULL tensor");
+    DG_ARG(N > 0 && H > 0 && W > 0 && C > 0 && lddy >= C && lddx >= C, "bad shape");
+    hipLaunchKernelGGL(dg::k_dw_bwd_data, dim3(dg::lgrid((long)N * H * W * C)), dim3(256), 0, (hipStream_t)stream, N, H,
+                       W, C, dy, lddy, k, dx, lddx, beta);
+    DG_LAUNCHED("dwconv_bwd_data");
+    return DG_OK;
+}
+
+int dg_dwconv3_bwd_filter(int N, int H, int W, int C, const float *x, int ldx, const float *dy, int lddy, float *dk,
+                          float *dbias, float beta, void *ws, size_t ws_bytes, dg_stream_t stream) {
+    DG_ARG(x && dy && dk && ws, "NULL tensor");
+    DG_ARG(N > 0 && H > 0 && W > 0 && C > 0 && ldx >= C && lddy >= C, "bad shape");
+    size_t need;
+    dg_dwconv3_workspace_size(N, H, W, C, &need);
+    DG_ARG(ws_bytes >= need, "workspace too small");
+    dg::RedPlan rp = dg::red_plan((long)N * H * W);
+    hipStream_t s = (hipStream_t)stream;
+    float *part = (float *)ws;
+    hipLaunchKernelGGL(dg::k_dw_bwd_filter, dim3(dg_cdiv(C, 64), rp.R), dim3(256), 0, s, N, H, W, C, x, ldx, dy, lddy,
+                       rp.rows, part);
+    DG_LAUNCHED("dwconv_bwd_filter");
+    // dk[q][c] (q = tap i*3+j) and dbias[c] (q = 9): ordered sums over the row chunks
+    for (int q = 0; q < 10; ++q) {
+        float *o = q < 9 ? dk + (size_t)q * C : dbias;
+        if (!o) continue;
+        hipLaunchKernelGGL(dg::k_rows_final, dim3(dg_cdiv(C, 256)), dim3(256), 0, s,
+                           (const float *)(part + (size_t)q * C), rp.R, (long)10 * C, C, o, beta);
+        DG_LAUNCHED("dwconv_filter_final");
+    }
+    return DG_OK;
+}
+
+int dg_vgg_preprocess_fwd(int64_t npix, const float *x, int ldx, float *z, int ldz, dg_stream_t stream) {
+    DG_ARG(x && z, "NULL tensor");
+    DG_ARG(ldx >= 3 && ldz >= 3, "bad strides");
+    if (npix == 0) return DG_OK;
+    hipLaunchKernelGGL(dg::k_vgg_pre_fwd, dim3(dg::lgrid(npix * 3)), dim3(256), 0, (hipStream_t)stream, (long)npix, x,
+                       ldx, z, ldz);
+    DG_LAUNCHED("vgg_preprocess_fwd");
+    return DG_OK;
+}
+
+int dg_vgg_preprocess_bwd(int64_t npix, const float *dz, int lddz, float *dx, int lddx, float beta,
+                          dg_stream_t stream) {
+    DG_ARG(dz && dx, "NULL tensor");
+    DG_ARG(lddz >= 3 && lddx >= 3, "bad strides");
+    if (npix == 0) return DG_OK;
+    hipLaunchKernelGGL(dg::k_vgg_pre_bwd, dim3(dg::lgrid(npix * 3)), dim3(256), 0, (hipStream_t)stream, (long)npix,
+                       dz, lddz, dx, lddx, beta);
+    DG_LAUNCHED("vgg_preprocess_bwd");
+    return DG_OK;
+}
+
+int dg_mse_workspace_size(size_t *bytes) {
+    DG_ARG(bytes, "NULL argument");
+    *bytes = (size_t)dg::MSE_BLOCKS * sizeof(float) + 256;
+    return DG_OK;
+}
+
+int dg_mse(int64_t npix, int C, const float *a, int lda, const float *b, int ldb, float scale, float *out,
+           float *da, int ldda, float grad_weight, void *ws, size_t ws_bytes, dg_stream_t stream) {
+    DG_ARG(a && b && out && ws, "NULL tensor");
+    DG_ARG(npix > 0 && C > 0 && lda >= C && ldb >= C && (!da || ldda >= C), "bad shape");
+    DG_ARG(ws_bytes >= (size_t)dg::MSE_BLOCKS * sizeof(float), "workspace too small");
+    const float inv_n = 1.f / (float)(npix * C);
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(dg::k_mse_partial, dim3(dg::MSE_BLOCKS), dim3(256), 0, s, (long)npix, C, a, lda, b, ldb, scale,
+                       grad_weight, inv_n, da, ldda, (float *)ws);
+    DG_LAUNCHED("mse_partial");
+    hipLaunchKernelGGL(dg::k_mse_final, dim3(1), dim3(64), 0, s, (const float *)ws, dg::MSE_BLOCKS, inv_n, out);
+    DG_LAUNCHED("mse_final");
+    return DG_OK;
+}
+
+int dg_gan_loss_workspace_size(size_t *bytes) {
+    DG_ARG(bytes, "NULL argument");
+    *bytes = (size_t)(dg::GL_IMG_BLOCKS * 3 + dg::GL_LOG_BLOCKS * 3 + 64) * sizeof(float);
+    return DG_OK;
+}
+
+int dg_gan_loss(int B, int H, int W, int C, const float *gen, int ldgen, const float *tgt, int ldtgt,
+                const float *logit_real, const float *logit_fake, int n_logits, const float *coef,
+                const float *content_value, float *out, float *dgen, int lddgen, float *dlogit_real_d,
+                float *dlogit_fake_d, float *dlogit_fake_g, void *ws, size_t ws_bytes, dg_stream_t stream) {
+    DG_ARG(gen && tgt && logit_real && logit_fake && coef && out && ws, "NULL tensor");
+    DG_ARG(B > 0 && H > 0 && W > 0 && C > 0 && n_logits > 0, "bad shape");
+    DG_ARG(ldgen >= C && ldtgt >= C && (!dgen || lddgen >= C), "bad strides");
+    size_t need;
+    dg_gan_loss_workspace_size(&need);
+    DG_ARG(ws_bytes >= need, "workspace too small");
+    dg::GanLossArgs a{};
+    a.B = B; a.H = H; a.W = W; a.C = C;
+    a.gen = gen; a.ldgen = ldgen; a.tgt = tgt; a.ldtgt = ldtgt;
+    a.zr = logit_real; a.zf = logit_fake; a.nlog = n_logits;
+    a.w_adv = coef[0]; a.w_var = coef[1]; a.disc_scale = coef[2];
+    a.t_mae = coef[3]; a.t_mse = coef[4]; a.t_content = coef[5]; a.t_var = coef[6];
+    a.content = content_value; a.out = out;
+    a.dgen = dgen; a.lddgen = lddgen;
+    a.dzr_d = dlogit_real_d; a.dzf_d = dlogit_fake_d; a.dzf_g = dlogit_fake_g;
+    a.part_img = (float *)ws;
+    a.part_log = a.part_img + dg::GL_IMG_BLOCKS * 3;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(dg::k_ganloss_img, dim3(dg::GL_IMG_BLOCKS), dim3(256), 0, s, a);
+    DG_LAUNCHED("gan_loss_img");
+    hipLaunchKernelGGL(dg::k_ganloss_logits, dim3(dg::GL_LOG_BLOCKS), dim3(256), 0, s, a);
+    DG_LAUNCHED("gan_loss_logits");
+    hipLaunchKernelGGL(dg::k_ganloss_final, dim3(1), dim3(64), 0, s, a);
+    DG_LAUNCHED("gan_loss_final");
+    return DG_OK;
+}
+
+}  // extern "C"

@@ -21,8 +21,15 @@ void set_error(const char *fmt, ...) {
 // sqrt(v), not to the bias-corrected v-hat.  One flat arena, float4 bulk.
 __global__ void __launch_bounds__(256)
 k_adam(float *__restrict__ p, const float *__restrict__ g, float *__restrict__ m, float *__restrict__ v, long n,
-       float lr, float b1, float b2, float eps, float gscale, const int32_t *iter) {
-    const float t = (float)((iter ? *iter : 0) + 1);
+       float lr, float b1, float b2, float eps, float gscale, const int32_t *iter, long decay_steps,
+       float decay_rate, int staircase) {
+    const int it = iter ? *iter : 0;
+    if (decay_steps > 0) {  // ExponentialDecay evaluated at optimizer.iterations (before the increment)
+        float e = (float)it / (float)decay_steps;
+        if (staircase) e = floorf(e);
+        lr = lr * powf(decay_rate, e);
+    }
+    const float t = (float)(it + 1);
     const float lr_t = lr * sqrtf(1.f - powf(b2, t)) / (1.f - powf(b1, t));
     const long n4 = n >> 2;
     const long stride = (long)gridDim.x * blockDim.x;
@@ -94,8 +101,22 @@ int dg_adam(float *p, const float *g, float *m, float *v, int64_t n, float lr, f
     if (n == 0) return DG_OK;
     unsigned grid = (unsigned)std::max<long>(1, std::min<long>(dg_cdiv(n / 4 + 1, 256), 4096));
     hipLaunchKernelGGL(dg::k_adam, dim3(grid), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (long)n, lr, beta1,
-                       beta2, eps, grad_scale, iter_dev);
+                       beta2, eps, grad_scale, iter_dev, 0L, 1.f, 0);
     DG_LAUNCHED("adam");
+    return DG_OK;
+}
+
+int dg_adam_sched(float *p, const float *g, float *m, float *v, int64_t n, float lr, int64_t decay_steps,
+                  float decay_rate, int staircase, float beta1, float beta2, float eps, float grad_scale,
+                  const int32_t *iter_dev, dg_stream_t stream) {
+    DG_ARG(p && g && m && v, "NULL tensor");
+    DG_ARG(n >= 0, "negative size");
+    DG_ARG((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0, "adam buffers must be 16B aligned");
+    if (n == 0) return DG_OK;
+    unsigned grid = (unsigned)std::max<long>(1, std::min<long>(dg_cdiv(n / 4 + 1, 256), 4096));
+    hipLaunchKernelGGL(dg::k_adam, dim3(grid), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (long)n, lr, beta1,
+                       beta2, eps, grad_scale, iter_dev, (long)decay_steps, decay_rate, staircase);
+    DG_LAUNCHED("adam_sched");
     return DG_OK;
 }
 

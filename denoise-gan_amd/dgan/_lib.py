@@ -46,6 +46,31 @@ _SIGS = {
     "dg_channel_concat": (c_int, [c_int64, _P, c_int, c_int, _P, c_int, c_int, _P, c_int, _P]),
     "dg_fill": (c_int, [_P, c_int64, c_float, _P]),
     "dg_strided_copy": (c_int, [c_int64, c_int, _P, c_int, _P, c_int, _P]),
+    "dg_adam_sched": (c_int, [_P, _P, _P, _P, c_int64, c_float, c_int64, c_float, c_int, c_float, c_float, c_float,
+                              c_float, _P, _P]),
+    "dg_prelu_workspace_size": (c_int, [c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_size_t)]),
+    "dg_prelu_fwd": (c_int, [c_int, c_int, c_int, c_int, c_int, _P, c_int, _P, _P, c_int, _P]),
+    "dg_prelu_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, _P, c_int, _P, _P, c_int, _P, c_int, c_float, _P,
+                             c_float, _P, c_size_t, _P]),
+    "dg_add": (c_int, [c_int64, c_int, _P, c_int, _P, c_int, _P, c_int, _P]),
+    "dg_accumulate": (c_int, [c_int64, c_int, _P, c_int, _P, c_int, c_float, _P]),
+    "dg_act_fwd": (c_int, [c_int64, c_int, _P, c_int, c_int, c_float, _P, c_int, _P]),
+    "dg_maxpool2_fwd": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P]),
+    "dg_maxpool2_bwd": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, c_float, _P]),
+    "dg_upsample2_relu_fwd": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P]),
+    "dg_upsample2_relu_bwd": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, c_float, _P]),
+    "dg_dwconv3_workspace_size": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_size_t)]),
+    "dg_dwconv3_fwd": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, _P, _P, c_int, _P]),
+    "dg_dwconv3_bwd_data": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, _P, c_int, c_float, _P]),
+    "dg_dwconv3_bwd_filter": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, _P, c_float, _P,
+                                      c_size_t, _P]),
+    "dg_vgg_preprocess_fwd": (c_int, [c_int64, _P, c_int, _P, c_int, _P]),
+    "dg_vgg_preprocess_bwd": (c_int, [c_int64, _P, c_int, _P, c_int, c_float, _P]),
+    "dg_mse_workspace_size": (c_int, [ctypes.POINTER(c_size_t)]),
+    "dg_mse": (c_int, [c_int64, c_int, _P, c_int, _P, c_int, c_float, _P, _P, c_int, c_float, _P, c_size_t, _P]),
+    "dg_gan_loss_workspace_size": (c_int, [ctypes.POINTER(c_size_t)]),
+    "dg_gan_loss": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, _P, c_int, ctypes.POINTER(c_float),
+                            _P, _P, _P, c_int, _P, _P, _P, _P, c_size_t, _P]),
 }
 
 EXPORTED = tuple(_SIGS)

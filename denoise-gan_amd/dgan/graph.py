@@ -1,0 +1,607 @@
+"""Layer-graph executor for the SRGAN / FastSRGAN / Autoencoder networks and
+the frozen VGG19 feature extractor, on libdgan.
+
+The reference builds these networks as Keras functional models and lets
+GradientTape differentiate them (srgan.py:129-272, fsrgan.py:99-258,
+autoencoder.py:89-229, train_*.py train_step).  Here a model is a small
+static graph of fused layer nodes built once (`Graph`), and `GraphPlan`
+turns it into a fixed forward + backward schedule for one input shape:
+
+  * every node is one libdgan call (Conv2D with its bias and activation
+    fused into the GEMM epilogue, BN with its activation fused into the
+    apply pass, PReLU with depth_to_space fused, ...);
+  * activations are NHWC fp32 buffers whose pixel stride is rounded up to a
+    multiple of 4 floats (16-byte aligned rows for the vector paths);
+  * channel concatenation (autoencoder.py:134-138) is zero-copy: the members
+    are written straight into channel slices of the concat buffer and their
+    gradients accumulate there in place;
+  * a tensor with several consumers (residual skips) accumulates its
+    gradient with beta = 1 after the first writer, decided at plan time;
+  * trainable variables live in one flat arena (`nets.Arena`) laid out in
+    backward-completion order, so Adam is one launch and DP buckets become
+    final front to back.
+
+Nothing here computes on the host: PyTorch only allocates device memory.
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import ops
+from .nets import Arena, BNState
+
+# ---------------------------------------------------------------------------
+# graph definition
+# ---------------------------------------------------------------------------
+
+
+class Tensor:
+    __slots__ = ("id", "C", "node")
+
+    def __init__(self, tid, C, node):
+        self.id, self.C, self.node = tid, C, node
+
+    def __repr__(self):
+        return f"T{self.id}(C={self.C}, from={self.node.kind}:{self.node.name})"
+
+
+class Node:
+    __slots__ = ("kind", "name", "ins", "out", "attrs", "idx")
+
+    def __init__(self, kind, name, ins, attrs, idx):
+        self.kind, self.name, self.ins, self.attrs, self.idx = kind, name, list(ins), dict(attrs), idx
+        self.out = None
+
+
+class Graph:
+    """A Keras-functional-style network description (NHWC, channels only;
+    spatial sizes are resolved per input shape by GraphPlan)."""
+
+    def __init__(self, name, in_ch=3):
+        self.name = name
+        self.nodes = []
+        self.vars = []          # (name, shape, init) in creation (Keras trainable_variables) order
+        self.bn_layers = {}     # name -> channels
+        self._names = {}
+        self.input = self._node("input", "input", [], in_ch)
+        self.output = None
+
+    def _uname(self, base):
+        k = self._names.get(base, 0)
+        self._names[base] = k + 1
+        return base if k == 0 else f"{base}_{k}"
+
+    def _node(self, kind, name, ins, C, **attrs):
+        n = Node(kind, name, ins, attrs, len(self.nodes))
+        n.out = Tensor(len(self.nodes), C, n)
+        self.nodes.append(n)
+        return n.out
+
+    def _var(self, name, shape, init):
+        self.vars.append((name, tuple(int(s) for s in shape), init))
+
+    # layers ---------------------------------------------------------------
+    def conv(self, x, filters, kernel, strides=1, padding="same", use_bias=True, act=None, alpha=0.3,
+             kernel_init=("glorot_uniform",), name=None):
+        """keras.layers.Conv2D (HWIO kernel), bias and activation fused."""
+        name = self._uname(name or "conv2d")
+        self._var(f"{name}/kernel", (kernel, kernel, x.C, filters), kernel_init)
+        if use_bias:
+            self._var(f"{name}/bias", (filters,), ("zeros",))
+        return self._node("conv", name, [x], filters, k=kernel, s=strides, padding=padding, bias=use_bias,
+                          act=act, alpha=alpha)
+
+    def bn(self, x, momentum=0.99, epsilon=1e-3, act=None, alpha=0.3, gamma_init=("ones",), name=None):
+        """keras.layers.BatchNormalization (+ the activation that follows it, fused)."""
+        name = self._uname(name or "batch_normalization")
+        self._var(f"{name}/gamma", (x.C,), gamma_init)
+        self._var(f"{name}/beta", (x.C,), ("zeros",))
+        self.bn_layers[name] = x.C
+        return self._node("bn", name, [x], x.C, momentum=momentum, eps=epsilon, act=act, alpha=alpha)
+
+    def prelu(self, x, block=1, name=None):
+        """keras.layers.PReLU(shared_axes=[1, 2]), after tf.nn.depth_to_space(x, block) when block == 2."""
+        if x.C % (block * block):
+            raise ValueError("depth_to_space needs channels divisible by block^2")
+        C = x.C // (block * block)
+        name = self._uname(name or "p_re_lu")
+        self._var(f"{name}/alpha", (1, 1, C), ("zeros",))
+        return self._node("prelu", name, [x], C, block=block)
+
+    def add(self, a, b, name=None):
+        if a.C != b.C:
+            raise ValueError("Add needs equal channels")
+        return self._node("add", self._uname(name or "add"), [a, b], a.C)
+
+    def concat(self, a, b, name=None):
+        return self._node("concat", self._uname(name or "concatenate"), [a, b], a.C + b.C)
+
+    def maxpool(self, x, name=None):
+        return self._node("maxpool", self._uname(name or "max_pooling2d"), [x], x.C)
+
+    def upsample_relu(self, x, name=None):
+        return self._node("upsample", self._uname(name or "up_sampling2d"), [x], x.C)
+
+    def dwconv(self, x, use_bias=True, kernel_init=("glorot_uniform",), name=None):
+        """keras.layers.DepthwiseConv2D(3, strides 1, 'same')."""
+        name = self._uname(name or "depthwise_conv2d")
+        self._var(f"{name}/depthwise_kernel", (3, 3, x.C, 1), kernel_init)
+        if use_bias:
+            self._var(f"{name}/bias", (x.C,), ("zeros",))
+        return self._node("dwconv", name, [x], x.C, bias=use_bias)
+
+    def act(self, x, act, alpha=0.3, name=None):
+        return self._node("act", self._uname(name or "activation"), [x], x.C, act=act, alpha=alpha)
+
+    def set_output(self, t):
+        self.output = t
+        return self
+
+    # derived ----------------------------------------------------------------
+    def var_list(self):
+        return [(n, s) for n, s, _ in self.vars]
+
+    def layout_order(self):
+        """Backward-completion order: variables of the last layer first."""
+        return [n for n, _, _ in reversed(self.vars)]
+
+    def consumers(self):
+        out = {n.out.id: [] for n in self.nodes}
+        for n in self.nodes:
+            for t in n.ins:
+                out[t.id].append(n)
+        return out
+
+
+# ---------------------------------------------------------------------------
+# Keras-style initialisers from a seeded numpy PCG64 stream
+# ---------------------------------------------------------------------------
+def _fans(shape):
+    if len(shape) == 4:
+        rf = shape[0] * shape[1]
+        return shape[2] * rf, shape[3] * rf
+    if len(shape) == 2:
+        return shape[0], shape[1]
+    return int(np.prod(shape)), int(np.prod(shape))
+
+
+def _trunc_normal(rng, shape, std):
+    out = rng.standard_normal(shape)
+    bad = np.abs(out) > 2.0
+    while bad.any():
+        out[bad] = rng.standard_normal(int(bad.sum()))
+        bad = np.abs(out) > 2.0
+    return out * std
+
+
+def init_value(rng, shape, init):
+    kind = init[0]
+    if kind == "zeros":
+        return np.zeros(shape, np.float32)
+    if kind == "ones":
+        return np.ones(shape, np.float32)
+    if kind == "normal":  # tf.random_normal_initializer(mean, stddev)
+        return (init[1] + init[2] * rng.standard_normal(shape)).astype(np.float32)
+    fan_in, fan_out = _fans(shape)
+    if kind == "glorot_uniform":
+        lim = math.sqrt(6.0 / (fan_in + fan_out))
+        return rng.uniform(-lim, lim, shape).astype(np.float32)
+    if kind == "he_normal":  # VarianceScaling(2, fan_in, truncated_normal)
+        return _trunc_normal(rng, shape, math.sqrt(2.0 / fan_in) / 0.87962566103423978).astype(np.float32)
+    if kind == "lecun_normal":
+        return _trunc_normal(rng, shape, math.sqrt(1.0 / fan_in) / 0.87962566103423978).astype(np.float32)
+    if kind == "he_normal_plain":  # untruncated N(0, 2/fan_in): seeded stand-in for pretrained VGG weights
+        return (rng.standard_normal(shape) * math.sqrt(2.0 / fan_in)).astype(np.float32)
+    raise ValueError(f"unknown initialiser {init!r}")
+
+
+def init_graph_variables(graph, seed):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    return {n: init_value(rng, s, init) for n, s, init in graph.vars}
+
+
+# ---------------------------------------------------------------------------
+# static plan
+# ---------------------------------------------------------------------------
+def _ld(C):
+    return -(-C // 4) * 4
+
+
+def _buf(N, H, W, C, device):
+    """NHWC buffer with a 16-byte-multiple pixel stride; returns the [..., :C] view."""
+    ld = _ld(C)
+    t = torch.empty((N, H, W, ld), dtype=torch.float32, device=device)
+    return t if ld == C else t[..., :C]
+
+
+class GraphPlan:
+    """Forward/backward schedule of a Graph for input [N, H, W, Cin].
+
+    slots: independent activation sets (e.g. D(real) and D(fake), or VGG on
+    G(x) and on the target) whose backwards run after all forwards.
+    param_grads: False for frozen networks (VGG19) -- only input gradients."""
+
+    def __init__(self, graph, N, H, W, arena, bn_state, device, slots=1, train=True, param_grads=True):
+        self.g = graph
+        self.arena, self.bn = arena, bn_state
+        self.device = device
+        self.N = N
+        self.train = train
+        self.param_grads = param_grads
+        nodes = graph.nodes
+        cons = graph.consumers()
+        # ---- shape inference + descriptors ----
+        shp = {}
+        self.desc = {}
+        shp[graph.input.id] = (N, H, W, graph.input.C)
+        for n in nodes[1:]:
+            x = shp[n.ins[0].id]
+            _, h, w, c = x
+            if n.kind == "conv":
+                d = ops.ConvDesc(N, h, w, c, n.out.C, n.attrs["k"], n.attrs["s"], n.attrs["padding"])
+                self.desc[n.idx] = d
+                shp[n.out.id] = d.out_shape
+            elif n.kind == "prelu":
+                b = n.attrs["block"]
+                shp[n.out.id] = (N, h * b, w * b, n.out.C)
+            elif n.kind == "maxpool":
+                shp[n.out.id] = (N, h // 2, w // 2, c)
+            elif n.kind == "upsample":
+                shp[n.out.id] = (N, 2 * h, 2 * w, c)
+            elif n.kind == "concat":
+                y = shp[n.ins[1].id]
+                if y[1:3] != x[1:3]:
+                    raise ValueError(f"concat {n.name}: spatial mismatch {x} vs {y}")
+                shp[n.out.id] = (N, h, w, n.out.C)
+            elif n.kind == "add":
+                y = shp[n.ins[1].id]
+                if y != x:
+                    raise ValueError(f"add {n.name}: shape mismatch {x} vs {y}")
+                shp[n.out.id] = x
+            else:  # bn, dwconv, act
+                shp[n.out.id] = x
+        self.shape = shp
+        self.out_shape = shp[graph.output.id]
+        # ---- zero-copy concat membership ----
+        # member t of concat node c becomes a channel slice of c's buffer when t is
+        # produced by a node (not the graph input), belongs to one concat only, and
+        # every other consumer of t precedes c's consumers (their gradient
+        # contributions then accumulate after c's consumer has written the slice).
+        self.slice_of = {}   # tensor id -> (concat tensor id, channel offset)
+        for n in nodes:
+            if n.kind != "concat":
+                continue
+            off = 0
+            first_cons = min((m.idx for m in cons[n.out.id]), default=len(nodes))
+            for t in n.ins:
+                ok = (t.id != graph.input.id and t.id not in self.slice_of and t.id != graph.output.id
+                      and all(m.idx < first_cons for m in cons[t.id]))
+                if ok:
+                    self.slice_of[t.id] = (n.out.id, off)
+                off += t.C
+        # ---- activation buffers per slot ----
+        self.slots = []
+        for _ in range(slots):
+            self.slots.append(self._alloc_set(nodes, shp))
+        self.saved = []
+        for _ in range(slots):
+            s = {}
+            for n in nodes:
+                if n.kind == "bn":
+                    s[n.name] = (torch.empty(n.out.C, device=device), torch.empty(n.out.C, device=device))
+            self.saved.append(s)
+        # ---- gradient buffers (shared by slots) + beta schedule ----
+        if train:
+            self.grad = self._alloc_set(nodes, shp)
+            self._schedule(nodes, cons)
+            mx = 0
+            for n in nodes[1:]:
+                if n.kind in ("conv", "bn", "act"):
+                    s0 = shp[n.out.id]
+                    mx = max(mx, int(np.prod(s0[:3])) * _ld(s0[3]))
+            self.scratch = torch.empty(max(mx, 4), dtype=torch.float32, device=device)
+        # ---- workspace ----
+        ws = [0]
+        for n in nodes[1:]:
+            sx = shp[n.ins[0].id]
+            if n.kind == "conv":
+                ws.append(self.desc[n.idx].max_ws())
+            elif n.kind == "bn":
+                ws.append(ops.bn_workspace_bytes(int(np.prod(sx[:3])), sx[3]))
+            elif n.kind == "prelu":
+                b = n.attrs["block"]
+                ws.append(ops.prelu_workspace_bytes(sx[0], sx[1], sx[2], n.out.C, b))
+            elif n.kind == "dwconv":
+                ws.append(ops.dwconv3_workspace_bytes(*sx))
+        self.ws_bytes = max(ws)
+
+    def _alloc_set(self, nodes, shp):
+        """tensor id -> NHWC view (graph input excluded: supplied per call)."""
+        bufs = {}
+        for n in nodes[1:]:
+            if n.out.id in self.slice_of:
+                continue
+            bufs[n.out.id] = _buf(*shp[n.out.id], self.device)
+        for tid, (cid, off) in self.slice_of.items():
+            C = shp[tid][3]
+            bufs[tid] = bufs[cid][..., off:off + C]
+        return bufs
+
+    def _schedule(self, nodes, cons):
+        """beta (0 = first writer, 1 = accumulate) of every input-gradient write, in backward order."""
+        written = set()
+        self.beta = {}
+        gin = self.g.input.id
+
+        def mark(tid):
+            b = 1.0 if tid in written else 0.0
+            written.add(tid)
+            return b
+
+        for n in reversed(nodes[1:]):
+            if n.kind == "concat":
+                # the concat buffer's gradient (written by its consumer) is the members' gradient
+                for t in n.ins:
+                    if t.id in self.slice_of and self.slice_of[t.id][0] == n.out.id:
+                        if t.id in written:
+                            raise RuntimeError(f"concat {n.name}: member gradient written before the concat's")
+                        written.add(t.id)
+                    else:
+                        self.beta[(n.idx, t.id)] = mark(t.id)
+                continue
+            for t in n.ins:
+                self.beta[(n.idx, t.id)] = mark(t.id)
+        self.input_first_beta = None  # graph input: the caller's beta applies to its first write
+        self._in_writes = [k for k in self.beta if k[1] == gin]
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, x, slot=0, training=True, out=None, ws=None):
+        """x: NHWC device view [N,H,W,Cin]; returns the output view (or writes into `out`)."""
+        g = self.g
+        A = self.arena
+        s = self.slots[slot]
+        s[g.input.id] = x
+        if out is not None:
+            s[g.output.id] = out
+        for n in g.nodes[1:]:
+            xin = s[n.ins[0].id]
+            y = s[n.out.id]
+            k = n.kind
+            if k == "conv":
+                d = self.desc[n.idx]
+                bias = A.param(f"{n.name}/bias") if n.attrs["bias"] else None
+                d.fwd(xin, A.param(f"{n.name}/kernel"), y, bias=bias, act=n.attrs["act"],
+                      alpha=n.attrs["alpha"], ws=ws)
+            elif k == "bn":
+                mean, inv = self.saved[slot][n.name]
+                if training:
+                    ops.bn_fwd_train(xin, A.param(f"{n.name}/gamma"), A.param(f"{n.name}/beta"), mean, inv,
+                                     self.bn.mean[n.name], self.bn.var[n.name], y, act=n.attrs["act"],
+                                     alpha=n.attrs["alpha"], momentum=n.attrs["momentum"], eps=n.attrs["eps"],
+                                     ws=ws)
+                else:
+                    ops.bn_fwd_infer(xin, A.param(f"{n.name}/gamma"), A.param(f"{n.name}/beta"),
+                                     self.bn.mean[n.name], self.bn.var[n.name], y, act=n.attrs["act"],
+                                     alpha=n.attrs["alpha"], eps=n.attrs["eps"])
+            elif k == "prelu":
+                ops.prelu_fwd(xin, A.param(f"{n.name}/alpha"), y, block=n.attrs["block"])
+            elif k == "add":
+                ops.add(xin, s[n.ins[1].id], y)
+            elif k == "concat":
+                off = 0
+                for t in n.ins:
+                    if self.slice_of.get(t.id, (None,))[0] != n.out.id:
+                        ops.strided_copy(s[t.id], y[..., off:off + t.C])
+                    off += t.C
+            elif k == "maxpool":
+                ops.maxpool2_fwd(xin, y)
+            elif k == "upsample":
+                ops.upsample2_relu_fwd(xin, y)
+            elif k == "dwconv":
+                bias = A.param(f"{n.name}/bias") if n.attrs["bias"] else None
+                ops.dwconv3_fwd(xin, A.param(f"{n.name}/depthwise_kernel"), y, bias=bias)
+            elif k == "act":
+                ops.act_fwd(xin, y, n.attrs["act"], n.attrs["alpha"])
+            else:
+                raise ValueError(k)
+        return s[g.output.id]
+
+    # --------------------------------------------------------------- backward
+    def _scratch(self, shape):
+        N, H, W, C = shape
+        ld = _ld(C)
+        v = self.scratch[:N * H * W * ld].view(N, H, W, ld)
+        return v if ld == C else v[..., :C]
+
+    def backward(self, dout, slot=0, param_beta=0.0, input_grad=None, input_beta=0.0, ws=None, on_grads_ready=None,
+                 params=None):
+        """dout: gradient of the graph output.  Parameter gradients go to the
+        arena grad buffer (g = new + param_beta*g) unless param_grads (or the
+        per-call `params`) is off; input_grad (NHWC view) receives dL/d(input)
+        (+ input_beta*old)."""
+        g = self.g
+        A = self.arena
+        s = self.slots[slot]
+        gr = dict(self.grad)
+        gr[g.output.id] = dout
+        gin = g.input.id
+        if input_grad is not None:
+            gr[gin] = input_grad
+        pg = self.param_grads if params is None else bool(params)
+        in_seen = [False]
+
+        def beta_of(n, t):
+            if t.id == gin:
+                if in_seen[0]:
+                    return 1.0
+                in_seen[0] = True
+                return input_beta
+            return self.beta[(n.idx, t.id)]
+
+        def need(t):
+            return t.id != gin or input_grad is not None
+
+        for n in reversed(g.nodes[1:]):
+            k = n.kind
+            t_in = n.ins[0]
+            dz = gr[n.out.id]
+            if k == "conv":
+                d = self.desc[n.idx]
+                act = n.attrs["act"]
+                if ops.act_id(act) != 0:
+                    dy = self._scratch(self.shape[n.out.id])
+                    ops.act_bwd(dz, s[n.out.id], dy, act, n.attrs["alpha"])
+                else:
+                    dy = dz
+                if pg:
+                    db = A.grad_of(f"{n.name}/bias") if n.attrs["bias"] else None
+                    d.bwd_filter(s[t_in.id], dy, A.grad_of(f"{n.name}/kernel"), dbias=db, beta=param_beta, ws=ws)
+                if need(t_in):
+                    d.bwd_data(dy, A.param(f"{n.name}/kernel"), gr[t_in.id], beta=beta_of(n, t_in), ws=ws)
+            elif k == "bn":
+                mean, inv = self.saved[slot][n.name]
+                b = beta_of(n, t_in)
+                tgt = gr[t_in.id] if b == 0.0 else self._scratch(self.shape[t_in.id])
+                ops.bn_bwd(dz, s[n.out.id], s[t_in.id], A.param(f"{n.name}/gamma"), mean, inv, tgt,
+                           A.grad_of(f"{n.name}/gamma") if pg else None, A.grad_of(f"{n.name}/beta") if pg else None,
+                           act=n.attrs["act"], alpha=n.attrs["alpha"], beta=param_beta, ws=ws)
+                if b != 0.0:
+                    ops.accumulate(tgt, gr[t_in.id], b)
+            elif k == "prelu":
+                ops.prelu_bwd(s[t_in.id], A.param(f"{n.name}/alpha"), dz, gr[t_in.id],
+                              dalpha=A.grad_of(f"{n.name}/alpha") if pg else None, block=n.attrs["block"],
+                              beta=beta_of(n, t_in), alpha_beta=param_beta, ws=ws)
+            elif k == "add":
+                for t in n.ins:
+                    if need(t):
+                        ops.accumulate(dz, gr[t.id], beta_of(n, t))
+            elif k == "concat":
+                off = 0
+                for t in n.ins:
+                    if self.slice_of.get(t.id, (None,))[0] != n.out.id and need(t):
+                        ops.accumulate(dz[..., off:off + t.C], gr[t.id], beta_of(n, t))
+                    off += t.C
+            elif k == "maxpool":
+                if need(t_in):
+                    ops.maxpool2_bwd(s[t_in.id], dz, gr[t_in.id], beta=beta_of(n, t_in))
+            elif k == "upsample":
+                if need(t_in):
+                    ops.upsample2_relu_bwd(s[t_in.id], dz, gr[t_in.id], beta=beta_of(n, t_in))
+            elif k == "dwconv":
+                if pg:
+                    db = A.grad_of(f"{n.name}/bias") if n.attrs["bias"] else None
+                    ops.dwconv3_bwd_filter(s[t_in.id], dz, A.grad_of(f"{n.name}/depthwise_kernel"), dbias=db,
+                                           beta=param_beta, ws=ws)
+                if need(t_in):
+                    ops.dwconv3_bwd_data(dz, A.param(f"{n.name}/depthwise_kernel"), gr[t_in.id],
+                                         beta=beta_of(n, t_in))
+            elif k == "act":
+                if need(t_in):
+                    b = beta_of(n, t_in)
+                    tgt = gr[t_in.id] if b == 0.0 else self._scratch(self.shape[t_in.id])
+                    ops.act_bwd(dz, s[n.out.id], tgt, n.attrs["act"], n.attrs["alpha"])
+                    if b != 0.0:
+                        ops.accumulate(tgt, gr[t_in.id], b)
+            if pg and on_grads_ready is not None and k in ("conv", "bn", "prelu", "dwconv"):
+                on_grads_ready(n.name)
+
+
+# ---------------------------------------------------------------------------
+# Keras-shaped network object over a Graph
+# ---------------------------------------------------------------------------
+class GraphNetwork:
+    """What the reference's drivers touch on a tf.keras.Model: call,
+    trainable_variables, count_params, summary, save / load_weights,
+    get_weights / set_weights."""
+
+    def __init__(self, graph, seed=1234, device=None, kind=None, trainable=True):
+        from .models import default_device
+        self.graph = graph
+        self.name = graph.name
+        self.kind = kind or graph.name
+        self.device = device or default_device()
+        self.arena = Arena(graph.var_list(), self.device, graph.layout_order())
+        self.bn = BNState(dict(graph.bn_layers), self.device)
+        self.arena.load(init_graph_variables(graph, seed))
+        self.trainable = trainable
+        self._plans = {}
+
+    @property
+    def trainable_variables(self):
+        if not self.trainable:
+            return []
+        return [self.arena.param(n) for n, _ in self.arena.var_list]
+
+    @property
+    def non_trainable_variables(self):
+        out = [] if self.trainable else [self.arena.param(n) for n, _ in self.arena.var_list]
+        for k in self.bn.mean:
+            out += [self.bn.mean[k], self.bn.var[k]]
+        return out
+
+    @property
+    def variables(self):
+        return self.trainable_variables + self.non_trainable_variables
+
+    def count_params(self):
+        return self.arena.count + sum(int(t.numel()) for k in self.bn.mean for t in (self.bn.mean[k], self.bn.var[k]))
+
+    def summary(self, print_fn=print):
+        print_fn(f'Model: "{self.name}"')
+        for n, s in self.arena.var_list:
+            print_fn(f"  {n:<40s} {str(tuple(s)):<22s} {int(np.prod(s)):>12,d}")
+        print_fn(f"Total params: {self.count_params():,d}")
+        print_fn(f"Trainable params: {self.arena.count if self.trainable else 0:,d}")
+
+    def plan(self, N, H, W, slots=1, train=False, param_grads=True):
+        key = (N, H, W, slots, train, param_grads)
+        if key not in self._plans:
+            self._plans[key] = GraphPlan(self.graph, N, H, W, self.arena, self.bn, self.device, slots=slots,
+                                         train=train, param_grads=param_grads)
+        return self._plans[key]
+
+    def __call__(self, x, training=False):
+        from .models import to_device
+        x = to_device(x, self.device)
+        N, H, W, _ = x.shape
+        p = self.plan(N, H, W)
+        ws = ops.Workspace(self.device)
+        ws.get(p.ws_bytes)
+        y = p.forward(x, slot=0, training=training, ws=ws)
+        return y.contiguous().clone()
+
+    # weights -------------------------------------------------------------
+    def state_dict(self):
+        d = dict(self.arena.export())
+        d.update(self.bn.export())
+        return d
+
+    def load_state_dict(self, d):
+        self.arena.load({n: d[n] for n, _ in self.arena.var_list if n in d})
+        self.bn.load(d)
+
+    def get_weights(self):
+        w = self.arena.export()
+        bn = self.bn.export()
+        return [w[n] for n, _ in self.arena.var_list] + [bn[k] for k in sorted(bn)]
+
+    def set_weights(self, weights):
+        names = [n for n, _ in self.arena.var_list]
+        self.arena.load(dict(zip(names, weights[:len(names)])))
+        bnk = sorted(self.bn.export())
+        self.bn.load(dict(zip(bnk, weights[len(names):])))
+
+    def save(self, path):
+        import json
+        import os
+        os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
+        base = path[:-4] if path.endswith(".npz") else path
+        np.savez(base + ".npz", **self.state_dict())
+        with open(base + ".json", "w") as f:
+            json.dump({"model": self.kind, "name": self.name}, f)
+
+    def load_weights(self, path):
+        p = path if path.endswith(".npz") else path + ".npz"
+        with np.load(p, allow_pickle=False) as z:
+            self.load_state_dict({k: z[k] for k in z.files})

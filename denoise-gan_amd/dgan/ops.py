@@ -11,7 +11,7 @@ import torch
 
 from ._lib import call, lib, DGError
 
-ACT = {"none": 0, "linear": 0, None: 0, "lrelu": 1, "leaky_relu": 1, "relu": 2, "tanh": 3}
+ACT = {"none": 0, "linear": 0, None: 0, "lrelu": 1, "leaky_relu": 1, "relu": 2, "tanh": 3, "sigmoid": 4}
 OP_FWD, OP_BWD_DATA, OP_BWD_FILTER = 0, 1, 2
 
 
@@ -355,3 +355,161 @@ def strided_copy(src, dst):
     C = src.shape[-1]
     call("dg_strided_copy", _rows(src), C, _p(src), pix_ld(src, C), _p(dst), pix_ld(dst, C), _stream())
     return dst
+
+
+def adam_sched(p, g, m, v, lr, decay_steps, decay_rate, staircase, beta1, beta2, eps, iter_dev, grad_scale=1.0):
+    """Keras Adam under ExponentialDecay(lr, decay_steps, decay_rate, staircase) (srgan.py:34-46)."""
+    call("dg_adam_sched", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), int(decay_steps), float(decay_rate),
+         int(bool(staircase)), float(beta1), float(beta2), float(eps), float(grad_scale), _p(iter_dev), _stream())
+
+
+# ---------------------------------------------------------------------------
+# SRGAN / FastSRGAN / Autoencoder / VGG19 layers (csrc/layers.hip)
+# ---------------------------------------------------------------------------
+def _nhwc(t):
+    if t.dim() != 4:
+        raise DGError(f"expected an NHWC tensor, got shape {tuple(t.shape)}")
+    return t.shape
+
+
+def prelu_workspace_bytes(N, H, W, C, block):
+    n = ctypes.c_size_t()
+    call("dg_prelu_workspace_size", N, H, W, C, block, ctypes.byref(n))
+    return n.value
+
+
+def prelu_fwd(y, alpha, z, block=1):
+    """z = PReLU(depth_to_space(y, block)); y [N,H,W,C*block^2] -> z [N,H*block,W*block,C]."""
+    N, H, W, CB = _nhwc(y)
+    C = CB // (block * block)
+    call("dg_prelu_fwd", N, H, W, C, block, _p(y), pix_ld(y, CB), _p(alpha), _p(z), pix_ld(z, C), _stream())
+    return z
+
+
+def prelu_bwd(y, alpha, dz, dy, dalpha=None, block=1, beta=0.0, alpha_beta=0.0, ws=None):
+    N, H, W, CB = _nhwc(y)
+    C = CB // (block * block)
+    ws = ws or default_workspace()
+    buf, n = ws.get(prelu_workspace_bytes(N, H, W, C, block))
+    call("dg_prelu_bwd", N, H, W, C, block, _p(y), pix_ld(y, CB), _p(alpha), _p(dz), pix_ld(dz, C), _p(dy),
+         pix_ld(dy, CB), float(beta), _p(dalpha), float(alpha_beta), _p(buf), n, _stream())
+    return dy
+
+
+def add(a, b, out):
+    C = a.shape[-1]
+    call("dg_add", _rows(a), C, _p(a), pix_ld(a, C), _p(b), pix_ld(b, C), _p(out), pix_ld(out, C), _stream())
+    return out
+
+
+def accumulate(src, dst, beta=1.0):
+    C = src.shape[-1]
+    call("dg_accumulate", _rows(src), C, _p(src), pix_ld(src, C), _p(dst), pix_ld(dst, C), float(beta), _stream())
+    return dst
+
+
+def act_fwd(x, z, act, alpha=0.3):
+    C = x.shape[-1]
+    call("dg_act_fwd", _rows(x), C, _p(x), pix_ld(x, C), act_id(act), float(alpha), _p(z), pix_ld(z, C), _stream())
+    return z
+
+
+def maxpool2_fwd(x, y):
+    N, H, W, C = _nhwc(x)
+    call("dg_maxpool2_fwd", N, H, W, C, _p(x), pix_ld(x, C), _p(y), pix_ld(y, C), _stream())
+    return y
+
+
+def maxpool2_bwd(x, dy, dx, beta=0.0):
+    N, H, W, C = _nhwc(x)
+    call("dg_maxpool2_bwd", N, H, W, C, _p(x), pix_ld(x, C), _p(dy), pix_ld(dy, C), _p(dx), pix_ld(dx, C),
+         float(beta), _stream())
+    return dx
+
+
+def upsample2_relu_fwd(x, z):
+    N, H, W, C = _nhwc(x)
+    call("dg_upsample2_relu_fwd", N, H, W, C, _p(x), pix_ld(x, C), _p(z), pix_ld(z, C), _stream())
+    return z
+
+
+def upsample2_relu_bwd(x, dz, dx, beta=0.0):
+    N, H, W, C = _nhwc(x)
+    call("dg_upsample2_relu_bwd", N, H, W, C, _p(x), pix_ld(x, C), _p(dz), pix_ld(dz, C), _p(dx), pix_ld(dx, C),
+         float(beta), _stream())
+    return dx
+
+
+def dwconv3_workspace_bytes(N, H, W, C):
+    n = ctypes.c_size_t()
+    call("dg_dwconv3_workspace_size", N, H, W, C, ctypes.byref(n))
+    return n.value
+
+
+def dwconv3_fwd(x, k, y, bias=None):
+    N, H, W, C = _nhwc(x)
+    call("dg_dwconv3_fwd", N, H, W, C, _p(x), pix_ld(x, C), _p(k), _p(bias), _p(y), pix_ld(y, C), _stream())
+    return y
+
+
+def dwconv3_bwd_data(dy, k, dx, beta=0.0):
+    N, H, W, C = _nhwc(dy)
+    call("dg_dwconv3_bwd_data", N, H, W, C, _p(dy), pix_ld(dy, C), _p(k), _p(dx), pix_ld(dx, C), float(beta),
+         _stream())
+    return dx
+
+
+def dwconv3_bwd_filter(x, dy, dk, dbias=None, beta=0.0, ws=None):
+    N, H, W, C = _nhwc(x)
+    ws = ws or default_workspace()
+    buf, n = ws.get(dwconv3_workspace_bytes(N, H, W, C))
+    call("dg_dwconv3_bwd_filter", N, H, W, C, _p(x), pix_ld(x, C), _p(dy), pix_ld(dy, C), _p(dk), _p(dbias),
+         float(beta), _p(buf), n, _stream())
+    return dk
+
+
+def vgg_preprocess_fwd(x, z):
+    call("dg_vgg_preprocess_fwd", _rows(x), _p(x), pix_ld(x, 3), _p(z), pix_ld(z, 3), _stream())
+    return z
+
+
+def vgg_preprocess_bwd(dz, dx, beta=0.0):
+    call("dg_vgg_preprocess_bwd", _rows(dz), _p(dz), pix_ld(dz, 3), _p(dx), pix_ld(dx, 3), float(beta), _stream())
+    return dx
+
+
+def mse_workspace_bytes():
+    n = ctypes.c_size_t()
+    call("dg_mse_workspace_size", ctypes.byref(n))
+    return n.value
+
+
+def mse(a, b, out, scale=1.0, da=None, grad_weight=1.0, ws=None):
+    """out[0] = mean((scale*a - scale*b)^2); da = grad_weight * d out / d a."""
+    C = a.shape[-1]
+    ws = ws or default_workspace()
+    buf, n = ws.get(mse_workspace_bytes())
+    call("dg_mse", _rows(a), C, _p(a), pix_ld(a, C), _p(b), pix_ld(b, C), float(scale), _p(out), _p(da),
+         pix_ld(da, C) if da is not None else C, float(grad_weight), _p(buf), n, _stream())
+    return out
+
+
+def gan_loss_workspace_bytes():
+    n = ctypes.c_size_t()
+    call("dg_gan_loss_workspace_size", ctypes.byref(n))
+    return n.value
+
+
+def gan_loss(gen, tgt, logit_real, logit_fake, out, coef, content=None, dgen=None, dlogit_real_d=None,
+             dlogit_fake_d=None, dlogit_fake_g=None, ws=None):
+    """coef = (w_adv, w_var, disc_scale, t_mae, t_mse, t_content, t_var); out[7] =
+    (gen_total, adv, mae, mse, content, disc, var)."""
+    B, H, W, C = gen.shape
+    ws = ws or default_workspace()
+    buf, n = ws.get(gan_loss_workspace_bytes())
+    carr = (ctypes.c_float * 7)(*[float(v) for v in coef])
+    call("dg_gan_loss", B, H, W, C, _p(gen), pix_ld(gen, C), _p(tgt), pix_ld(tgt, C), _p(logit_real),
+         _p(logit_fake), logit_fake.numel(), carr, _p(content), _p(out), _p(dgen),
+         pix_ld(dgen, C) if dgen is not None else C, _p(dlogit_real_d), _p(dlogit_fake_d), _p(dlogit_fake_g), _p(buf),
+         n, _stream())
+    return out

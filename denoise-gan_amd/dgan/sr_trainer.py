@@ -1,0 +1,172 @@
+"""Fused training steps of the SRGAN / FastSRGAN / Autoencoder families
+(train_srgan.py:61-118, train_fsrgan.py:61-120, train_autoencoder.py:66-112)
+on libdgan, and the VGG19 content loss shared with pix2pix.
+
+One call = the reference's traced `train_step`:
+  G(x); D(y) [slot 0], D(G(x)) [slot 1]; VGG19 on preprocess(G(x)) and
+  preprocess(y) -> content MSE / 12.75; adv / mae / mse / tv / disc losses;
+  the disc-loss backward through both D passes; the gen-loss backward
+  through D(fake) and through VGG(G(x)) into G; Adam (ExponentialDecay,
+  TTUR) on G and D.  Both gradients see the same pre-update weights, as in
+  the reference's single persistent tape.
+
+All launches go to the current stream with pre-sized buffers, so a step can
+be captured in one HIP graph.
+"""
+import torch
+
+from . import ops
+from .graph import GraphNetwork
+from .zoo import vgg19_features
+
+FEAT_SCALE = 1.0 / 12.75   # srgan.py:74-75
+
+
+class ScheduleConfig:
+    """keras.optimizers.schedules.ExponentialDecay + Adam hyper-parameters."""
+
+    def __init__(self, lr, decay_steps=100000, decay_rate=0.1, staircase=True, beta_1=0.9, beta_2=0.999,
+                 epsilon=1e-7):
+        self.lr, self.decay_steps, self.decay_rate, self.staircase = lr, decay_steps, decay_rate, staircase
+        self.beta_1, self.beta_2, self.epsilon = beta_1, beta_2, epsilon
+
+    def __call__(self, step):
+        e = step / self.decay_steps
+        if self.staircase:
+            e = float(int(e))
+        return self.lr * self.decay_rate ** e
+
+
+def apply_adam(arena, cfg, grad_scale=1.0):
+    if isinstance(cfg, ScheduleConfig):
+        ops.adam_sched(arena.data, arena.grad, arena.m, arena.v, cfg.lr, cfg.decay_steps, cfg.decay_rate,
+                       cfg.staircase, cfg.beta_1, cfg.beta_2, cfg.epsilon, arena.iterations, grad_scale=grad_scale)
+    else:
+        ops.adam(arena.data, arena.grad, arena.m, arena.v, cfg.lr, cfg.beta_1, cfg.beta_2, cfg.epsilon,
+                 arena.iterations, grad_scale=grad_scale)
+    ops.counter_add(arena.iterations, 1)
+
+
+class VGGNetwork(GraphNetwork):
+    """Frozen VGG19 feature extractor (block5_conv4).  ImageNet weights are a
+    network download in the reference (keras.applications.VGG19(weights=
+    "imagenet")); offline they load from a local .npz with Keras layer names
+    (`vgg_weights`), else seeded He-normal weights stand in."""
+
+    def __init__(self, weights=None, seed=4242, width=1, device=None):
+        super().__init__(vgg19_features(width), seed=seed, device=device, kind="vgg19", trainable=False)
+        self.pretrained = False
+        if weights:
+            self.load_weights(weights)
+            self.pretrained = True
+
+
+class ContentLoss:
+    """VGG19 content loss of one (gen, target) shape: value into a device
+    scalar and, when requested, its gradient w.r.t. gen accumulated into a
+    caller buffer (srgan.py:70-76, pix2pix.py:45-51)."""
+
+    def __init__(self, vgg, N, H, W, device, train=True):
+        self.vgg = vgg
+        self.plan = vgg.plan(N, H, W, slots=2, train=train, param_grads=False)
+        e = lambda s: torch.empty(s, dtype=torch.float32, device=device)
+        self.pre = [e((N, H, W, 3)), e((N, H, W, 3))]
+        self.dpre = e((N, H, W, 3)) if train else None
+        self.dfeat = e(self.plan.out_shape) if train else None
+        self.value = torch.zeros(1, dtype=torch.float32, device=device)
+        self.ws_bytes = max(self.plan.ws_bytes, ops.mse_workspace_bytes())
+
+    def forward(self, gen, tgt, grad_weight=1.0, ws=None):
+        ops.vgg_preprocess_fwd(gen, self.pre[0])
+        ops.vgg_preprocess_fwd(tgt, self.pre[1])
+        fg = self.plan.forward(self.pre[0], slot=0, training=False, ws=ws)
+        ft = self.plan.forward(self.pre[1], slot=1, training=False, ws=ws)
+        # MeanSquaredError()(target_features, gen_features): grad w.r.t. gen features
+        ops.mse(fg, ft, self.value, scale=FEAT_SCALE, da=self.dfeat, grad_weight=grad_weight, ws=ws)
+        return self.value
+
+    def backward(self, dgen, beta=1.0, ws=None):
+        """dgen += d content / d gen (through VGG and preprocess_input)."""
+        self.plan.backward(self.dfeat, slot=0, input_grad=self.dpre, input_beta=0.0, ws=ws, params=False)
+        ops.vgg_preprocess_bwd(self.dpre, dgen, beta=beta)
+
+
+# coefficient sets of dg_gan_loss: (w_adv, w_var, disc_scale, t_mae, t_mse, t_content, t_var)
+COEF = {
+    # train_srgan.py:87-96: gen = content + adv + 0*mse + mae + 0*var; disc = real + fake
+    "srgan": (1e-3, 1e-5, 1.0, 1.0, 0.0, 1.0, 0.0),
+    # train_fsrgan.py:88-96: gen = content + adv + 0*mse + mae; disc = 0.5*(valid + fake)
+    "fsrgan": (1e-3, 1e-5, 0.5, 1.0, 0.0, 1.0, 0.0),
+    # train_autoencoder.py:88-100: perceptual = content + adv + 0*mse + mae; disc = valid + fake
+    "autoencoder": (1e-3, 1e-5, 1.0, 1.0, 0.0, 1.0, 0.0),
+}
+
+
+class SRTrainer:
+    """Static plan of one SR-family training step for x [N,h,w,3] -> y [N,H,W,3]."""
+
+    def __init__(self, G, D, vgg, N, in_hw, out_hw, device, coef, g_opt, d_opt, grad_sync=None):
+        self.G, self.D, self.vgg = G, D, vgg
+        self.N = N
+        h, w = in_hw
+        H, W = out_hw
+        self.coef = tuple(coef)
+        self.g_opt, self.d_opt = g_opt, d_opt
+        self.grad_sync = grad_sync
+        self.Gp = G.plan(N, h, w, slots=1, train=True)
+        if tuple(self.Gp.out_shape) != (N, H, W, 3):
+            raise ValueError(f"generator output {self.Gp.out_shape} != target {(N, H, W, 3)}")
+        self.Dp = D.plan(N, H, W, slots=2, train=True)
+        e = lambda s: torch.empty(s, dtype=torch.float32, device=device)
+        ls = self.Dp.out_shape
+        self.dzr, self.dzf_d, self.dzf_g = e(ls), e(ls), e(ls)
+        self.dgen = e((N, H, W, 3))
+        self.loss = torch.zeros(7, dtype=torch.float32, device=device)
+        self.content = ContentLoss(vgg, N, H, W, device) if vgg is not None else None
+        wsb = [self.Gp.ws_bytes, self.Dp.ws_bytes, ops.gan_loss_workspace_bytes()]
+        if self.content:
+            wsb.append(self.content.ws_bytes)
+        self.ws = ops.Workspace(device)
+        self.ws.get(max(wsb))
+
+    @property
+    def gen_output(self):
+        return self.Gp.slots[0][self.G.graph.output.id]
+
+    def step(self, x, y, apply=True):
+        """x [N,h,w,3], y [N,H,W,3] device fp32 in [-1, 1].  Returns the 7 loss
+        values (gen_total, adv, mae, mse, content, disc, var) on the device."""
+        x = x if x.is_contiguous() else x.contiguous()
+        y = y if y.is_contiguous() else y.contiguous()
+        ws = self.ws
+        Gp, Dp = self.Gp, self.Dp
+        # ---- forward (train_srgan.py:76-80) ---------------------------------
+        gen = Gp.forward(x, slot=0, training=True, ws=ws)
+        zr = Dp.forward(y, slot=0, training=True, ws=ws)
+        zf = Dp.forward(gen, slot=1, training=True, ws=ws)
+        content = None
+        if self.content is not None:
+            content = self.content.forward(gen, y, grad_weight=self.coef[5], ws=ws)
+        # ---- losses and their gradients (train_srgan.py:84-96) -------------
+        ops.gan_loss(gen, y, zr, zf, self.loss, self.coef, content=content, dgen=self.dgen, dlogit_real_d=self.dzr,
+                     dlogit_fake_d=self.dzf_d, dlogit_fake_g=self.dzf_g, ws=ws)
+        sync = self.grad_sync
+        # ---- disc gradients (train_srgan.py:105-106) ------------------------
+        Dp.backward(self.dzr, slot=0, param_beta=0.0, ws=ws)
+        Dp.backward(self.dzf_d, slot=1, param_beta=1.0, ws=ws)
+        if sync:
+            sync.start("D")
+        # ---- gen gradients: through D(fake) and VGG(G(x)) into G ------------
+        Dp.backward(self.dzf_g, slot=1, params=False, input_grad=self.dgen, input_beta=1.0, ws=ws)
+        if self.content is not None:
+            self.content.backward(self.dgen, beta=1.0, ws=ws)
+        Gp.backward(self.dgen, slot=0, param_beta=0.0, ws=ws,
+                    on_grads_ready=(sync.ready_G if sync else None))
+        if sync:
+            sync.finish()
+        # ---- apply_gradients (train_srgan.py:113-114) -----------------------
+        if apply:
+            scale = sync.grad_scale if sync else 1.0
+            apply_adam(self.G.arena, self.g_opt, scale)
+            apply_adam(self.D.arena, self.d_opt, scale)
+        return self.loss

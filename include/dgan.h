@@ -38,7 +38,7 @@ typedef struct dg_conv_desc_s *dg_conv_t;  /* shapes immutable once created */
 enum { DG_OK = 0, DG_ERR_ARG = 1, DG_ERR_HIP = 2, DG_ERR_WORKSPACE = 3, DG_ERR_UNSUPPORTED = 4 };
 
 /* fused activations (Keras defaults: LeakyReLU alpha=0.3, pix2pix.py:121) */
-enum { DG_ACT_NONE = 0, DG_ACT_LRELU = 1, DG_ACT_RELU = 2, DG_ACT_TANH = 3 };
+enum { DG_ACT_NONE = 0, DG_ACT_LRELU = 1, DG_ACT_RELU = 2, DG_ACT_TANH = 3, DG_ACT_SIGMOID = 4 };
 
 /* ops for dg_conv_workspace_size */
 enum { DG_OP_FWD = 0, DG_OP_BWD_DATA = 1, DG_OP_BWD_FILTER = 2 };
@@ -152,6 +152,14 @@ int dg_adam(float *p, const float *g, float *m, float *v, int64_t n,
             float lr, float beta1, float beta2, float eps, float grad_scale,
             const int32_t *iter_dev, dg_stream_t stream);
 int dg_counter_add(int32_t *counter_dev, int32_t inc, dg_stream_t stream);
+/* Adam under keras.optimizers.schedules.ExponentialDecay (srgan.py:34-46,
+ * fsrgan.py:30-43, autoencoder.py:26-37): the learning rate of the update
+ * with iterations = *iter_dev is lr * decay_rate^(it / decay_steps) (floor
+ * of the exponent when staircase).  decay_steps <= 0 means a constant lr. */
+int dg_adam_sched(float *p, const float *g, float *m, float *v, int64_t n,
+                  float lr, int64_t decay_steps, float decay_rate, int staircase,
+                  float beta1, float beta2, float eps, float grad_scale,
+                  const int32_t *iter_dev, dg_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * Data movement helpers.
@@ -163,6 +171,71 @@ int dg_channel_concat(int64_t npix, const float *a, int lda, int ca, const float
                       float *out, int ldo, dg_stream_t stream);
 int dg_fill(float *p, int64_t n, float value, dg_stream_t stream);
 int dg_strided_copy(int64_t npix, int C, const float *src, int lds, float *dst, int ldd, dg_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Layers of the SRGAN / FastSRGAN / Autoencoder models and of the frozen
+ * VGG19 feature extractor.  Input-gradient outputs take `beta`
+ * (dx = new + beta*dx) so a tensor with several consumers (residual
+ * skips, concat members) accumulates its gradient in place.
+ * ---------------------------------------------------------------------- */
+/* PReLU(shared_axes=[1,2]) (srgan.py:139, :152), optionally preceded by
+ * tf.nn.depth_to_space(., block=2) (srgan.py:138, fsrgan.py:198):
+ * y [N,H,W,C*block^2] -> z [N,H*block,W*block,C]; alpha[C]. */
+int dg_prelu_workspace_size(int N, int H, int W, int C, int block, size_t *bytes);
+int dg_prelu_fwd(int N, int H, int W, int C, int block, const float *y, int ldy, const float *alpha,
+                 float *z, int ldz, dg_stream_t stream);
+/* dy = dL/dy + beta*dy ; dalpha = dL/dalpha + alpha_beta*dalpha (dalpha may be NULL) */
+int dg_prelu_bwd(int N, int H, int W, int C, int block, const float *y, int ldy, const float *alpha,
+                 const float *dz, int lddz, float *dy, int lddy, float beta,
+                 float *dalpha, float alpha_beta, void *ws, size_t ws_bytes, dg_stream_t stream);
+/* keras.layers.Add (srgan.py:165): out = a + b */
+int dg_add(int64_t npix, int C, const float *a, int lda, const float *b, int ldb, float *out, int ldo,
+           dg_stream_t stream);
+/* dst = src + beta*dst (gradient fan-in) */
+int dg_accumulate(int64_t npix, int C, const float *src, int lds, float *dst, int ldd, float beta,
+                  dg_stream_t stream);
+/* z = act(x) (e.g. the sigmoid of the autoencoder discriminator's output, autoencoder.py:226) */
+int dg_act_fwd(int64_t npix, int C, const float *x, int ldx, int act, float alpha, float *z, int ldz,
+               dg_stream_t stream);
+/* MaxPool2D(2, strides 2) (autoencoder.py:111-115, VGG19 block pools): [N,H,W,C] -> [N,H/2,W/2,C] */
+int dg_maxpool2_fwd(int N, int H, int W, int C, const float *x, int ldx, float *y, int ldy, dg_stream_t stream);
+int dg_maxpool2_bwd(int N, int H, int W, int C, const float *x, int ldx, const float *dy, int lddy,
+                    float *dx, int lddx, float beta, dg_stream_t stream);
+/* UpSampling2D(2, 'nearest') + relu (autoencoder.py:117-131): [N,H,W,C] -> [N,2H,2W,C] */
+int dg_upsample2_relu_fwd(int N, int H, int W, int C, const float *x, int ldx, float *z, int ldz,
+                          dg_stream_t stream);
+int dg_upsample2_relu_bwd(int N, int H, int W, int C, const float *x, int ldx, const float *dz, int lddz,
+                          float *dx, int lddx, float beta, dg_stream_t stream);
+/* DepthwiseConv2D(3, strides 1, 'same', use_bias) (fsrgan.py:162-167); k [3,3,C] */
+int dg_dwconv3_workspace_size(int N, int H, int W, int C, size_t *bytes);
+int dg_dwconv3_fwd(int N, int H, int W, int C, const float *x, int ldx, const float *k, const float *bias,
+                   float *y, int ldy, dg_stream_t stream);
+int dg_dwconv3_bwd_data(int N, int H, int W, int C, const float *dy, int lddy, const float *k,
+                        float *dx, int lddx, float beta, dg_stream_t stream);
+int dg_dwconv3_bwd_filter(int N, int H, int W, int C, const float *x, int ldx, const float *dy, int lddy,
+                          float *dk, float *dbias, float beta, void *ws, size_t ws_bytes, dg_stream_t stream);
+/* vgg19.preprocess_input(((x + 1) * 255) / 2) (srgan.py:71-72): RGB->BGR, minus the caffe means */
+int dg_vgg_preprocess_fwd(int64_t npix, const float *x, int ldx, float *z, int ldz, dg_stream_t stream);
+int dg_vgg_preprocess_bwd(int64_t npix, const float *dz, int lddz, float *dx, int lddx, float beta,
+                          dg_stream_t stream);
+/* out[0] = mean((scale*a - scale*b)^2) (MeanSquaredError of VGG features / 12.75,
+ * srgan.py:74-76); da = grad_weight * d out / d a (may be NULL) */
+int dg_mse_workspace_size(size_t *bytes);
+int dg_mse(int64_t npix, int C, const float *a, int lda, const float *b, int ldb, float scale, float *out,
+           float *da, int ldda, float grad_weight, void *ws, size_t ws_bytes, dg_stream_t stream);
+/* SR-GAN loss set (train_srgan.py:84-96, train_fsrgan.py:86-96, train_autoencoder.py:84-100).
+ * coef[7] = {w_adv, w_var, disc_scale, t_mae, t_mse, t_content, t_var}:
+ *   adv = w_adv*BCE_logits(1, fake); mae, mse raw; var = w_var*mean_b TV(y - g);
+ *   disc = disc_scale*(BCE_logits(1, real) + BCE_logits(0, fake));
+ *   gen_total = adv + t_mae*mae + t_mse*mse + t_content*content + t_var*var.
+ * out[7] = {gen_total, adv, mae, mse, content, disc, var}.  dgen = d gen_total / d g
+ * through the image terms only; the logit gradients are those of disc (d) and adv (g). */
+int dg_gan_loss_workspace_size(size_t *bytes);
+int dg_gan_loss(int B, int H, int W, int C, const float *gen, int ldgen, const float *tgt, int ldtgt,
+                const float *logit_real, const float *logit_fake, int n_logits, const float *coef,
+                const float *content_value, float *out, float *dgen, int lddgen,
+                float *dlogit_real_d, float *dlogit_fake_d, float *dlogit_fake_g,
+                void *ws, size_t ws_bytes, dg_stream_t stream);
 
 #ifdef __cplusplus
 }

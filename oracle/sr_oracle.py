@@ -1,0 +1,342 @@
+"""CPU oracle for the SRGAN / FastSRGAN / Autoencoder training steps and the
+VGG19 content loss — TEST INFRASTRUCTURE ONLY.
+
+A float64 torch-CPU restatement (forward written by hand from the reference
+sources, gradients by autograd).  Only tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg may use it, and only as the checker; the product
+path (dgan/, libdgan.so) never imports it.  It does not import dgan either:
+the only thing it shares with the product is the variable-naming scheme
+("<layer>/<kernel|bias|gamma|beta|alpha|depthwise_kernel>") so a test can
+hand both the same weights.
+
+PARITY STATUS: parity unpinned against TensorFlow itself (TensorFlow is not
+installable here and the reference ships no fixtures).  The
+TF semantics restated below are pinned by known-answer tests in
+tests/test_sr_oracle.py; the layer conventions shared with the pix2pix
+oracle (padding, BN, BCE, TV, Adam) are the ones oracle/p2p_oracle.py
+documents and tests.
+
+What it restates (file:line in /root/reference):
+  SRGAN G         srgan.py:129-188   conv-BN(gamma~N(1,.02))-PReLU, 16 x [conv-BN-ReLU-conv-BN + skip],
+                                      conv-BN + long skip, scale//2 x [conv3 256 -> depth_to_space 2 -> PReLU],
+                                      conv1x1(3) + tanh
+  SR D            srgan.py:232-272 = fsrgan.py:216-258 (autoencoder.py:188-229 adds a sigmoid)
+  FastSRGAN G     fsrgan.py:99-214   inverted residual blocks (fsrgan.py:112-177)
+  Autoencoder G   autoencoder.py:89-185
+  VGG19           keras.applications.VGG19 to block5_conv4; preprocess_input caffe mode
+  content loss    srgan.py:69-76     MSE(vgg(pre(hr))/12.75, vgg(pre(sr))/12.75)
+  steps           train_srgan.py:61-118, train_fsrgan.py:61-120, train_autoencoder.py:66-112
+  Adam + ExponentialDecay(lr, 100000, 0.1, staircase), D lr x5 (srgan.py:34-49)
+TF semantics (beyond those of p2p_oracle):
+  S1 PReLU(shared_axes=[1,2]) = relu(x) - alpha * relu(-x), alpha per channel
+  S2 tf.nn.depth_to_space NHWC block b: out[n, h*b+i, w*b+j, c] = in[n, h, w, (i*b+j)*C + c]
+  S3 DepthwiseConv2D 3x3 'same' stride 1: per-channel correlation, kernel [3,3,C,1]
+  S4 MaxPool2D(2,2): max over 2x2 windows; UpSampling2D(2) nearest: replication
+  S5 vgg19.preprocess_input (caffe): RGB->BGR, minus (103.939, 116.779, 123.68)
+  S6 Keras BinaryCrossentropy() on a Sigmoid output in graph mode = BCE with the logits
+  S7 ExponentialDecay staircase: lr * rate^floor(iterations / steps), iterations before the update
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+BN_EPS = 1e-3
+VGG_MEAN_BGR = (103.939, 116.779, 123.68)
+
+
+# --------------------------------------------------------------------------
+# layers (NHWC tensors, Keras kernel layouts)
+# --------------------------------------------------------------------------
+def tf_same_pads(size, k, s):
+    out = -(-size // s)
+    total = max((out - 1) * s + k - size, 0)
+    return total // 2, total - total // 2
+
+
+def conv(x, w, b=None, s=1):
+    """Conv2D 'same': x NHWC, w HWIO."""
+    k = w.shape[0]
+    xt = x.permute(0, 3, 1, 2)
+    pt, pb = tf_same_pads(xt.shape[2], k, s)
+    pl, pr = tf_same_pads(xt.shape[3], k, s)
+    xt = F.pad(xt, (pl, pr, pt, pb))
+    y = F.conv2d(xt, w.permute(3, 2, 0, 1), bias=b, stride=s)
+    return y.permute(0, 2, 3, 1)
+
+
+def dwconv3(x, k, b=None):
+    """S3: DepthwiseConv2D(3, 'same', stride 1); k [3,3,C,1]."""
+    C = x.shape[-1]
+    xt = F.pad(x.permute(0, 3, 1, 2), (1, 1, 1, 1))
+    wt = k[..., 0].permute(2, 0, 1).unsqueeze(1)  # [C,1,3,3]
+    y = F.conv2d(xt, wt, bias=b, groups=C)
+    return y.permute(0, 2, 3, 1)
+
+
+class BNStats:
+    """Moving statistics, updated like TF's fused BN (unbiased variance)."""
+
+    def __init__(self):
+        self.mean, self.var = {}, {}
+
+
+def bn(x, gamma, beta, name, stats, momentum=0.99, eps=BN_EPS, training=True):
+    if not training:
+        m = torch.as_tensor(stats.mean[name])
+        v = torch.as_tensor(stats.var[name])
+        return (x - m) / torch.sqrt(v + eps) * gamma + beta
+    mu = x.mean(dim=(0, 1, 2))
+    var = ((x - mu) ** 2).mean(dim=(0, 1, 2))
+    n = x.shape[0] * x.shape[1] * x.shape[2]
+    C = x.shape[-1]
+    m0 = stats.mean.get(name, np.zeros(C))
+    v0 = stats.var.get(name, np.ones(C))
+    mu_d = mu.detach().numpy()
+    var_u = var.detach().numpy() * n / max(n - 1, 1)
+    stats.mean[name] = m0 * momentum + mu_d * (1 - momentum)
+    stats.var[name] = v0 * momentum + var_u * (1 - momentum)
+    return (x - mu) / torch.sqrt(var + eps) * gamma + beta
+
+
+def prelu(x, alpha):
+    """S1."""
+    a = alpha.reshape(-1)
+    return F.relu(x) - a * F.relu(-x)
+
+
+def depth_to_space(x, b):
+    """S2."""
+    N, H, W, CB = x.shape
+    C = CB // (b * b)
+    y = x.reshape(N, H, W, b, b, C).permute(0, 1, 3, 2, 4, 5)
+    return y.reshape(N, H * b, W * b, C)
+
+
+def maxpool2(x):
+    N, H, W, C = x.shape
+    x = x[:, :H // 2 * 2, :W // 2 * 2]
+    return x.reshape(N, H // 2, 2, W // 2, 2, C).amax(dim=(2, 4))
+
+
+def upsample2(x):
+    return x.repeat_interleave(2, dim=1).repeat_interleave(2, dim=2)
+
+
+def lrelu(x, a):
+    return torch.where(x > 0, x, a * x)
+
+
+# --------------------------------------------------------------------------
+# networks
+# --------------------------------------------------------------------------
+def srgan_generator(P, x, stats, scale=4, n_blocks=16, training=True):
+    """srgan.py:129-188."""
+    n = conv(x, P["conv2d/kernel"])
+    n = bn(n, P["batch_normalization/gamma"], P["batch_normalization/beta"], "batch_normalization", stats,
+           training=training)
+    n = prelu(n, P["p_re_lu/alpha"])
+    temp = n
+    for i in range(n_blocks):
+        nn_ = conv(n, P[f"block_{i}_conv1/kernel"])
+        nn_ = F.relu(bn(nn_, P[f"block_{i}_bn1/gamma"], P[f"block_{i}_bn1/beta"], f"block_{i}_bn1", stats,
+                        training=training))
+        nn_ = conv(nn_, P[f"block_{i}_conv2/kernel"])
+        nn_ = bn(nn_, P[f"block_{i}_bn2/gamma"], P[f"block_{i}_bn2/beta"], f"block_{i}_bn2", stats,
+                 training=training)
+        n = n + nn_
+    n = conv(n, P["conv2d_post/kernel"])
+    n = bn(n, P["batch_normalization_post/gamma"], P["batch_normalization_post/beta"], "batch_normalization_post",
+           stats, training=training)
+    n = n + temp
+    for i in range(scale // 2):
+        n = conv(n, P[f"deconv_{i}_conv/kernel"], P[f"deconv_{i}_conv/bias"])
+        n = prelu(depth_to_space(n, 2), P[f"deconv_{i}_p_re_lu/alpha"])
+    return torch.tanh(conv(n, P["conv2d_out/kernel"], P["conv2d_out/bias"]))
+
+
+def sr_discriminator(P, x, stats, df=32, training=True):
+    """srgan.py:232-272 (logits)."""
+    spec = [(df, 1, False), (df, 2, True), (df, 1, True), (df, 2, True),
+            (df * 2, 1, True), (df * 2, 2, True), (df * 2, 1, True), (df * 2, 2, True)]
+    h = x
+    for i, (f, s, use_bn) in enumerate(spec):
+        h = conv(h, P[f"d{i + 1}_conv/kernel"], P[f"d{i + 1}_conv/bias"], s)
+        if use_bn:
+            h = bn(h, P[f"d{i + 1}_bn/gamma"], P[f"d{i + 1}_bn/beta"], f"d{i + 1}_bn", stats, momentum=0.8,
+                   training=training)
+        h = lrelu(h, 0.2)
+    return conv(h, P["logits/kernel"], P["logits/bias"])
+
+
+def fsrgan_generator(P, x, stats, gf=32, n_blocks=6, training=True):
+    """fsrgan.py:99-214."""
+    def B(h, name, momentum=0.99):
+        return bn(h, P[f"{name}/gamma"], P[f"{name}/beta"], name, stats, momentum=momentum, training=training)
+
+    c1 = prelu(B(conv(x, P["conv2d/kernel"], P["conv2d/bias"]), "batch_normalization"), P["p_re_lu/alpha"])
+    r = c1
+    for bid in range(n_blocks):
+        inp = r
+        h = r
+        if bid:
+            pre = f"block_{bid}_"
+            h = conv(h, P[pre + "expand/kernel"], P[pre + "expand/bias"])
+            h = F.relu(B(h, pre + "expand_BN", 0.999))
+        else:
+            pre = "expanded_conv_"
+        h = dwconv3(h, P[pre + "depthwise/depthwise_kernel"], P[pre + "depthwise/bias"])
+        h = F.relu(B(h, pre + "depthwise_BN", 0.999))
+        h = conv(h, P[pre + "project/kernel"], P[pre + "project/bias"])
+        h = B(h, pre + "project_BN", 0.999)
+        r = inp + h if inp.shape[-1] == h.shape[-1] else h
+    c2 = B(conv(r, P["conv2d_post/kernel"], P["conv2d_post/bias"]), "batch_normalization_post") + c1
+    u = c2
+    for i in range(2):
+        u = conv(u, P[f"deconv_{i}_conv/kernel"], P[f"deconv_{i}_conv/bias"])
+        u = prelu(depth_to_space(u, 2), P[f"deconv_{i}_p_re_lu/alpha"])
+    return torch.tanh(conv(u, P["conv2d_out/kernel"], P["conv2d_out/bias"]))
+
+
+def autoencoder_generator(P, x):
+    """autoencoder.py:89-185."""
+    def c(h, name, act=F.relu):
+        return act(conv(h, P[f"{name}/kernel"], P[f"{name}/bias"]))
+
+    h = c(c(x, "conv1"), "conv1b")
+    pool1 = maxpool2(h)
+    pool2 = maxpool2(c(pool1, "conv2"))
+    pool3 = maxpool2(c(pool2, "conv3"))
+    pool4 = maxpool2(c(pool3, "conv4"))
+    pool5 = maxpool2(c(pool4, "conv5"))
+    h = pool5
+    for lvl, skip in zip((6, 7, 8, 9), (pool4, pool3, pool2, pool1)):
+        h = torch.cat([F.relu(upsample2(h)), skip], dim=3)
+        h = c(c(h, f"conv{lvl}"), f"conv{lvl}b")
+    h = torch.cat([F.relu(upsample2(h)), x], dim=3)
+    h = c(c(h, "conv10"), "conv10b")
+    return c(h, "conv11", torch.tanh)
+
+
+VGG19_BLOCKS = [(64, 2), (128, 2), (256, 4), (512, 4), (512, 4)]
+
+
+def vgg19(P, x):
+    """VGG19 to block5_conv4 (post-ReLU); x already preprocessed."""
+    h = x
+    for b, (_, n) in enumerate(VGG19_BLOCKS):
+        for i in range(n):
+            name = f"block{b + 1}_conv{i + 1}"
+            h = F.relu(conv(h, P[f"{name}/kernel"], P[f"{name}/bias"]))
+        if b < 4:
+            h = maxpool2(h)
+    return h
+
+
+def vgg_preprocess(img):
+    """S5 applied to ((img + 1) * 255) / 2 (srgan.py:71-72)."""
+    x = ((img + 1.0) * 255.0) / 2.0
+    x = x.flip(-1)
+    return x - torch.tensor(VGG_MEAN_BGR, dtype=x.dtype)
+
+
+def content_loss(PV, hr, sr):
+    """srgan.py:69-76."""
+    fs = vgg19(PV, vgg_preprocess(sr)) / 12.75
+    fh = vgg19(PV, vgg_preprocess(hr)) / 12.75
+    return ((fh - fs) ** 2).mean()
+
+
+# --------------------------------------------------------------------------
+# losses and steps
+# --------------------------------------------------------------------------
+def bce_logits(z, y):
+    return (torch.clamp(z, min=0) - z * y + torch.log1p(torch.exp(-z.abs()))).mean()
+
+
+def total_variation(img):
+    """tf.image.total_variation: per image sum |dh| + |dw|."""
+    dh = (img[:, 1:] - img[:, :-1]).abs().sum(dim=(1, 2, 3))
+    dw = (img[:, :, 1:] - img[:, :, :-1]).abs().sum(dim=(1, 2, 3))
+    return dh + dw
+
+
+def exp_decay(lr, it, steps=100000, rate=0.1, staircase=True):
+    """S7."""
+    e = it / steps
+    return lr * rate ** (math.floor(e) if staircase else e)
+
+
+def adam_update(p, g, m, v, t, lr, b1=0.9, b2=0.999, eps=1e-7):
+    """TF ApplyAdam (see p2p_oracle item 8); t = iterations + 1."""
+    lr_t = lr * math.sqrt(1 - b2 ** t) / (1 - b1 ** t)
+    m = m + (g - m) * (1 - b1)
+    v = v + (g * g - v) * (1 - b2)
+    p = p - m * lr_t / (np.sqrt(v) + eps)
+    return p, m, v
+
+
+class SRState:
+    """Oracle-side copy of one SR model: weights (float64), BN stats, Adam slots."""
+
+    def __init__(self, kind, PG, PD, PV=None, scale=4, lr=1e-3, n_blocks=16):
+        self.kind = kind
+        self.PG = {k: np.asarray(v, np.float64) for k, v in PG.items()}
+        self.PD = {k: np.asarray(v, np.float64) for k, v in PD.items()}
+        self.PV = None if PV is None else {k: np.asarray(v, np.float64) for k, v in PV.items()}
+        self.scale, self.lr, self.n_blocks = scale, lr, n_blocks
+        self.Gs, self.Ds = BNStats(), BNStats()
+        self.mG = {k: np.zeros_like(v) for k, v in self.PG.items()}
+        self.vG = {k: np.zeros_like(v) for k, v in self.PG.items()}
+        self.mD = {k: np.zeros_like(v) for k, v in self.PD.items()}
+        self.vD = {k: np.zeros_like(v) for k, v in self.PD.items()}
+        self.iterations = 0
+
+    def generator(self, P, x, training=True):
+        if self.kind == "srgan":
+            return srgan_generator(P, x, self.Gs, self.scale, self.n_blocks, training=training)
+        if self.kind == "fsrgan":
+            return fsrgan_generator(P, x, self.Gs, training=training)
+        return autoencoder_generator(P, x)
+
+
+def train_step(st, x, y, apply=True):
+    """One step of train_srgan.py:61-118 / train_fsrgan.py:61-120 /
+    train_autoencoder.py:66-112 (all three share the gen-loss composition
+    content + adv + 0*mse + mae; FSRGAN halves the disc loss).
+    Returns dict(losses=(gen_total, adv, mae, mse, content, disc, var),
+    gen, gG, gD)."""
+    PG = {k: torch.tensor(v, requires_grad=True) for k, v in st.PG.items()}
+    PD = {k: torch.tensor(v, requires_grad=True) for k, v in st.PD.items()}
+    PV = None if st.PV is None else {k: torch.tensor(v) for k, v in st.PV.items()}
+    xt = torch.tensor(np.asarray(x, np.float64))
+    yt = torch.tensor(np.asarray(y, np.float64))
+    gen = st.generator(PG, xt)
+    zr = sr_discriminator(PD, yt, st.Ds)
+    zf = sr_discriminator(PD, gen, st.Ds)
+    cont = content_loss(PV, yt, gen) if PV is not None else torch.zeros((), dtype=torch.float64)
+    adv = 1e-3 * bce_logits(zf, 1.0)
+    mse = ((yt - gen) ** 2).mean()
+    mae = (yt - gen).abs().mean()
+    var = 1e-5 * total_variation(yt - gen).mean()
+    gen_loss = cont + adv + 0 * mse + mae
+    disc = bce_logits(zr, 1.0) + bce_logits(zf, 0.0)
+    if st.kind == "fsrgan":
+        disc = 0.5 * disc
+    gG = torch.autograd.grad(gen_loss, list(PG.values()), retain_graph=True)
+    gD = torch.autograd.grad(disc, list(PD.values()))
+    gG = {k: g.numpy() for k, g in zip(PG, gG)}
+    gD = {k: g.numpy() for k, g in zip(PD, gD)}
+    out = dict(losses=tuple(float(v) for v in (gen_loss, adv, mae, mse, cont, disc, var)),
+               gen=gen.detach().numpy(), gG=gG, gD=gD)
+    if apply:
+        t = st.iterations + 1
+        lrg = exp_decay(st.lr, st.iterations)
+        lrd = exp_decay(st.lr * 5, st.iterations)
+        for k in st.PG:
+            st.PG[k], st.mG[k], st.vG[k] = adam_update(st.PG[k], gG[k], st.mG[k], st.vG[k], t, lrg)
+        for k in st.PD:
+            st.PD[k], st.mD[k], st.vD[k] = adam_update(st.PD[k], gD[k], st.mD[k], st.vD[k], t, lrd)
+        st.iterations += 1
+    return out

@@ -1,0 +1,397 @@
+"""SR-family layers and training steps on the HIP path vs the CPU oracles.
+
+Layer kernels (csrc/layers.hip) are checked against torch fp64 autograd of
+the oracle's restatement of each TF op (oracle/sr_oracle.py S1-S7); the
+fused training steps of SRGAN / FastSRGAN / Autoencoder (dgan.sr_trainer)
+against oracle.sr_oracle.train_step on the same weights and synthetic
+inputs, VGG19 content loss included (seeded stand-in weights).
+
+Tolerances (fp32 vs fp64): layers 1e-5 relative to the output scale; full
+steps: the 7 loss values to 2e-5 relative, generator output |dPSNR| < 0.01 dB
+and max-abs 1e-4, every gradient within 1e-4 + 2e-4 * max|g_ref| of the
+oracle (BASELINE.json north_star's max-abs 1e-4 bar, widened by the
+gradient's own scale where VGG features make it O(1)).
+"""
+import math
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import sr_oracle as S
+
+gpu = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _t(a):
+    return torch.as_tensor(np.asarray(a, np.float32)).to(DEV)
+
+
+def _close(got, ref, rtol=1e-5, atol=0.0, what=""):
+    got = got.detach().double().cpu().numpy() if torch.is_tensor(got) else np.asarray(got, np.float64)
+    ref = ref.detach().double().cpu().numpy() if torch.is_tensor(ref) else np.asarray(ref, np.float64)
+    assert got.shape == ref.shape, (what, got.shape, ref.shape)
+    err = np.abs(got - ref).max() if got.size else 0.0
+    scale = np.abs(ref).max() if ref.size else 0.0
+    assert err <= atol + rtol * scale, f"{what}: max abs err {err:.3e} vs scale {scale:.3e}"
+    return err
+
+
+def _padded(shape, C_ld=None):
+    """NHWC device buffer whose pixel stride exceeds C (exercises ld handling)."""
+    N, H, W, C = shape
+    ld = C_ld or C + 4
+    return torch.zeros((N, H, W, ld), device=DEV)[..., :C]
+
+
+# -------------------------------------------------------------------------
+# layers
+# -------------------------------------------------------------------------
+@gpu
+@pytest.mark.parametrize("block", [1, 2])
+def test_prelu_depth_to_space(block):
+    from dgan import ops
+    rng = np.random.default_rng(block)
+    N, H, W, C = 2, 5, 7, 12
+    y = rng.standard_normal((N, H, W, C * block * block))
+    y[0, 0, 0, :3] = 0.0  # exact zeros: gradient 0 (relu' at 0)
+    a = rng.standard_normal((1, 1, C)) * 0.3
+    dz = rng.standard_normal((N, H * block, W * block, C))
+    yt = torch.tensor(y, requires_grad=True)
+    at = torch.tensor(a, requires_grad=True)
+    zt = S.prelu(S.depth_to_space(yt, block) if block > 1 else yt, at)
+    zt.backward(torch.tensor(dz))
+    yd, ad, dzd = _t(y), _t(a), _t(dz)
+    z = _padded((N, H * block, W * block, C))
+    ops.prelu_fwd(yd, ad, z, block=block)
+    dy = _padded(yd.shape)
+    da = torch.zeros_like(ad)
+    ops.prelu_bwd(yd, ad, dzd, dy, dalpha=da, block=block)
+    torch.cuda.synchronize()
+    _close(z, zt, 1e-6, what="prelu fwd")
+    _close(dy, yt.grad, 1e-6, what="prelu dy")
+    _close(da, at.grad, 1e-5, what="prelu dalpha")
+
+
+@gpu
+def test_depthwise_conv_fwd_bwd():
+    from dgan import ops
+    rng = np.random.default_rng(7)
+    N, H, W, C = 2, 9, 11, 70
+    x = rng.standard_normal((N, H, W, C))
+    k = rng.standard_normal((3, 3, C, 1)) * 0.3
+    b = rng.standard_normal(C)
+    dy = rng.standard_normal((N, H, W, C))
+    xt, kt, bt = (torch.tensor(v, requires_grad=True) for v in (x, k, b))
+    yt = S.dwconv3(xt, kt, bt)
+    yt.backward(torch.tensor(dy))
+    xd, kd, bd, dyd = _t(x), _t(k), _t(b), _t(dy)
+    y = _padded((N, H, W, C))
+    ops.dwconv3_fwd(xd, kd, y, bias=bd)
+    dx = _padded((N, H, W, C))
+    dx.fill_(1.0)
+    ops.dwconv3_bwd_data(dyd, kd, dx, beta=1.0)   # accumulate onto ones
+    dk = torch.zeros_like(kd)
+    db = torch.zeros_like(bd)
+    ops.dwconv3_bwd_filter(xd, dyd, dk, dbias=db)
+    torch.cuda.synchronize()
+    _close(y, yt, 1e-6, what="dw fwd")
+    _close(dx, xt.grad + 1.0, 1e-6, what="dw dx")
+    _close(dk, kt.grad, 2e-6, what="dw dk")
+    _close(db, bt.grad, 2e-6, what="dw db")
+
+
+@gpu
+def test_maxpool_upsample_fwd_bwd():
+    from dgan import ops
+    rng = np.random.default_rng(3)
+    N, H, W, C = 2, 8, 6, 9
+    x = rng.standard_normal((N, H, W, C))
+    xt = torch.tensor(x, requires_grad=True)
+    pt = S.maxpool2(xt)
+    dp = rng.standard_normal(pt.shape)
+    pt.backward(torch.tensor(dp))
+    xd = _t(x)
+    p = _padded(tuple(pt.shape))
+    ops.maxpool2_fwd(xd, p)
+    dx = _padded((N, H, W, C))
+    ops.maxpool2_bwd(xd, _t(dp), dx)
+    # upsample + relu
+    ut_in = torch.tensor(x, requires_grad=True)
+    ut = torch.relu(S.upsample2(ut_in))
+    du = rng.standard_normal(ut.shape)
+    ut.backward(torch.tensor(du))
+    u = _padded(tuple(ut.shape))
+    ops.upsample2_relu_fwd(xd, u)
+    dxu = _padded((N, H, W, C))
+    ops.upsample2_relu_bwd(xd, _t(du), dxu)
+    torch.cuda.synchronize()
+    _close(p, pt, 0, what="maxpool fwd")
+    _close(dx, xt.grad, 0, what="maxpool bwd")
+    _close(u, ut, 0, what="upsample fwd")
+    _close(dxu, ut_in.grad, 1e-6, what="upsample bwd")
+
+
+@gpu
+def test_vgg_preprocess_and_content_mse():
+    from dgan import ops
+    rng = np.random.default_rng(5)
+    img = rng.uniform(-1, 1, (2, 4, 5, 3))
+    it = torch.tensor(img, requires_grad=True)
+    zt = S.vgg_preprocess(it)
+    dz = rng.standard_normal(zt.shape)
+    zt.backward(torch.tensor(dz))
+    z = _padded((2, 4, 5, 3))
+    ops.vgg_preprocess_fwd(_t(img), z)
+    dimg = torch.ones((2, 4, 5, 3), device=DEV)
+    ops.vgg_preprocess_bwd(_t(dz), dimg, beta=1.0)
+    a = rng.standard_normal((3, 2, 2, 40)) * 50
+    b = rng.standard_normal((3, 2, 2, 40)) * 50
+    at = torch.tensor(a, requires_grad=True)
+    mt = (((torch.tensor(b) - at) / 12.75) ** 2).mean()
+    mt.backward()
+    out = torch.zeros(1, device=DEV)
+    da = torch.zeros((3, 2, 2, 40), device=DEV)
+    ops.mse(_t(a), _t(b), out, scale=1 / 12.75, da=da, grad_weight=1.0)
+    torch.cuda.synchronize()
+    _close(z, zt, 1e-6, what="preprocess fwd")
+    _close(dimg, it.grad + 1.0, 1e-6, what="preprocess bwd")
+    _close(out[0], mt, 1e-6, what="mse value")
+    _close(da, at.grad, 1e-6, what="mse grad")
+
+
+@gpu
+def test_gan_loss_set_matches_oracle():
+    from dgan import ops
+    rng = np.random.default_rng(11)
+    B, H, W = 3, 12, 10
+    g = np.tanh(rng.standard_normal((B, H, W, 3)))
+    y = np.tanh(rng.standard_normal((B, H, W, 3)))
+    zr = rng.standard_normal((B, 2, 2, 1)) * 3
+    zf = rng.standard_normal((B, 2, 2, 1)) * 3
+    for coef in [(1e-3, 1e-5, 1.0, 1.0, 0.0, 1.0, 0.0), (1e-3, 1e-5, 0.5, 0.7, 0.3, 1.0, 2.0)]:
+        gt = torch.tensor(g, requires_grad=True)
+        zrt = torch.tensor(zr, requires_grad=True)
+        zft = torch.tensor(zf, requires_grad=True)
+        yt = torch.tensor(y)
+        cont = torch.tensor(0.25, dtype=torch.float64)
+        adv = coef[0] * S.bce_logits(zft, 1.0)
+        mae = (yt - gt).abs().mean()
+        mse = ((yt - gt) ** 2).mean()
+        var = coef[1] * S.total_variation(yt - gt).mean()
+        total = adv + coef[3] * mae + coef[4] * mse + coef[5] * cont + coef[6] * var
+        disc = coef[2] * (S.bce_logits(zrt, 1.0) + S.bce_logits(zft, 0.0))
+        dgen_img = torch.autograd.grad(total - adv, gt, retain_graph=True)[0]
+        dzf_g = torch.autograd.grad(adv, zft, retain_graph=True)[0]
+        dzr_d, dzf_d = torch.autograd.grad(disc, [zrt, zft])
+        out = torch.zeros(7, device=DEV)
+        dgen = torch.zeros((B, H, W, 3), device=DEV)
+        d1, d2, d3 = (torch.zeros((B, 2, 2, 1), device=DEV) for _ in range(3))
+        ops.gan_loss(_t(g), _t(y), _t(zr), _t(zf), out, coef, content=_t([0.25]), dgen=dgen, dlogit_real_d=d1,
+                     dlogit_fake_d=d2, dlogit_fake_g=d3)
+        torch.cuda.synchronize()
+        want = [total, adv, mae, mse, cont, disc, var]
+        for i, w in enumerate(want):
+            _close(out[i], w, 2e-6, atol=1e-9, what=f"loss[{i}]")
+        _close(dgen, dgen_img, 1e-5, what="dgen")
+        _close(d1, dzr_d, 1e-6, what="dzr_d")
+        _close(d2, dzf_d, 1e-6, what="dzf_d")
+        _close(d3, dzf_g, 1e-6, what="dzf_g")
+
+
+@gpu
+def test_adam_exponential_decay():
+    from dgan import ops
+    rng = np.random.default_rng(2)
+    n = 1001
+    p, g = rng.standard_normal(n), rng.standard_normal(n) * 1e-3
+    m, v = rng.standard_normal(n) * 1e-4, rng.uniform(0, 1e-6, n)
+    for it in (0, 99999, 100000, 250001):
+        dp, dg, dm, dv = _t(p), _t(g), _t(m), _t(v)
+        itd = torch.tensor([it], dtype=torch.int32, device=DEV)
+        ops.adam_sched(dp, dg, dm, dv, 1e-3, 100000, 0.1, True, 0.9, 0.999, 1e-7, itd)
+        rp, rm, rv = S.adam_update(p, g, m, v, it + 1, S.exp_decay(1e-3, it))
+        torch.cuda.synchronize()
+        _close(dp, rp, 1e-6, what=f"adam p it={it}")
+        # step size must reflect the decayed lr
+        step = np.abs(dp.cpu().numpy() - p.astype(np.float32)).max()
+        assert step <= S.exp_decay(1e-3, it) * 1.01 * math.sqrt(1 - 0.999 ** (it + 1)) / (1 - 0.9 ** (it + 1)) * 4
+
+
+# layer geometries of the SR family that the pix2pix conv tests do not cover
+SR_CONVS = [
+    # (name, N, H, W, Cin, Cout, k, s, bias, ld_in)
+    ("srgan.res", 2, 12, 12, 64, 64, 3, 1, False, None),
+    ("srgan.deconv", 2, 12, 12, 64, 256, 3, 1, True, None),
+    ("srgan.out1x1", 2, 24, 24, 64, 3, 1, 1, True, None),
+    ("fsrgan.expand", 2, 16, 16, 32, 192, 1, 1, True, None),
+    ("fsrgan.project", 2, 16, 16, 192, 32, 1, 1, True, None),
+    ("fsrgan.out3x3", 2, 32, 32, 32, 3, 3, 1, True, None),
+    ("d.s2", 2, 24, 24, 32, 32, 3, 2, True, None),
+    ("d.in3", 2, 24, 24, 3, 32, 3, 1, True, None),
+    ("d.logits", 2, 6, 6, 64, 1, 1, 1, True, None),
+    ("ae.conv2", 2, 16, 16, 32, 44, 3, 1, True, None),
+    ("ae.conv6", 2, 4, 4, 176, 152, 3, 1, True, None),
+    ("ae.conv8", 2, 8, 8, 156, 84, 3, 1, True, None),
+    ("ae.conv10", 2, 32, 32, 67, 64, 3, 1, True, 68),
+    ("ae.slice_in", 2, 8, 8, 76, 100, 3, 1, True, 176),
+    ("vgg.c11", 2, 16, 16, 3, 64, 3, 1, True, None),
+]
+
+
+@gpu
+@pytest.mark.parametrize("case", SR_CONVS, ids=[c[0] for c in SR_CONVS])
+def test_sr_conv_geometries(case):
+    from torch_ref import conv2d_ref
+    from dgan.ops import ConvDesc
+    name, N, H, W, Ci, Co, k, s, bias, ld_in = case
+    torch.manual_seed(zlib.crc32(name.encode()))
+    d = ConvDesc(N, H, W, Ci, Co, k, s, "same")
+    x = torch.randn(N, H, W, Ci, dtype=torch.float64)
+    w = torch.randn(*d.weight_shape, dtype=torch.float64) * 0.05
+    b = torch.randn(Co, dtype=torch.float64) if bias else None
+    dy = torch.randn(N, d.Ho, d.Wo, Co, dtype=torch.float64)
+    xr, wr = x.clone().requires_grad_(), w.clone().requires_grad_()
+    br = b.clone().requires_grad_() if bias else None
+    yr = conv2d_ref(xr, wr, s, d.pads, br)
+    yr.backward(dy)
+    xg = _padded((N, H, W, Ci), ld_in or -(-Ci // 4) * 4)
+    xg.copy_(x.float())
+    wg = w.float().to(DEV)
+    bg = b.float().to(DEV) if bias else None
+    y = _padded((N, d.Ho, d.Wo, Co), -(-Co // 4) * 4)
+    d.fwd(xg, wg, y, bias=bg)
+    dx = _padded((N, H, W, Ci), ld_in or -(-Ci // 4) * 4)
+    d.bwd_data(dy.float().to(DEV), wg, dx)
+    dw = torch.zeros_like(wg)
+    db = torch.zeros(Co, device=DEV) if bias else None
+    d.bwd_filter(xg, dy.float().to(DEV), dw, dbias=db)
+    torch.cuda.synchronize()
+    K = k * k * max(Ci, Co)
+    tol = 1e-5 * max(1.0, math.sqrt(K / 1024))
+    _close(y, yr, tol, what="fwd")
+    _close(dx, xr.grad, tol, what="bwd_data")
+    _close(dw, wr.grad, tol * 4, what="bwd_filter")
+    if bias:
+        _close(db, br.grad, 1e-5, what="dbias")
+
+
+# -------------------------------------------------------------------------
+# full training steps
+# -------------------------------------------------------------------------
+class Args:
+    def __init__(self, **kw):
+        self.crop_size = 32
+        self.scale = 4
+        self.fp16 = 0
+        self.lr = 1e-3
+        self.retrain = 0
+        self.seed = 21
+        self.__dict__.update(kw)
+
+
+def psnr(img, ref):
+    a = (np.asarray(img, np.float64) + 1) / 2
+    b = (np.asarray(ref, np.float64) + 1) / 2
+    return 10 * math.log10(1.0 / np.mean((a - b) ** 2))
+
+
+def _grads_close(arena, ref, label, rtol=2e-4, atol=1e-4):
+    worst = 0.0
+    for name, g_ref in ref.items():
+        g = arena.grad_of(name).detach().double().cpu().numpy()
+        err = float(np.abs(g - g_ref).max())
+        tol = atol + rtol * float(np.abs(g_ref).max())
+        assert err <= tol, f"{label} {name}: max-abs grad diff {err:.3e} > {tol:.3e} (ref max {np.abs(g_ref).max():.3e})"
+        worst = max(worst, err)
+    return worst
+
+
+def _synthetic(N, H, W, scale, seed):
+    from dataloader import synthetic_pair
+    x, y = synthetic_pair(N, H, seed=seed)
+    if scale > 1:
+        x = np.ascontiguousarray(x[:, ::scale, ::scale, :])
+    return x, y
+
+
+def _run_step_parity(model_cls, kind, N, H, scale, steps=1, **kw):
+    m = model_cls(Args(crop_size=H, scale=scale, **kw))
+    st = S.SRState(kind, m.generator.arena.export(), m.discriminator.arena.export(),
+                   m.vgg.arena.export() if m.vgg is not None else None, scale=scale, lr=1e-3)
+    res = None
+    for it in range(steps):
+        x, y = _synthetic(N, H, H, scale, seed=50 + it)
+        ref = S.train_step(st, x, y, apply=True)
+        tr = m.trainer(x.shape, y.shape)
+        loss = tr.step(torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV), apply=(it < steps - 1))
+        torch.cuda.synchronize()
+        got = loss.cpu().double().numpy()
+        want = np.array(ref["losses"])
+        rt = 2e-5 if it == 0 else 5e-4
+        assert np.allclose(got, want, rtol=rt, atol=1e-8), (it, got, want)
+        res = (m, tr, ref, x, y)
+    m, tr, ref, x, y = res
+    gen = tr.gen_output.detach().cpu().numpy()
+    if steps == 1:
+        assert abs(psnr(gen, y) - psnr(ref["gen"], y)) < 0.01
+        assert np.abs(gen - ref["gen"]).max() < 1e-4
+        _grads_close(m.generator.arena, ref["gG"], "G")
+        _grads_close(m.discriminator.arena, ref["gD"], "D")
+    return m, st
+
+
+@gpu
+def test_srgan_step_parity():
+    from srgan import SRGAN
+    m, st = _run_step_parity(SRGAN, "srgan", N=2, H=32, scale=4)
+    # BN moving statistics after G(x), D(y), D(G(x))
+    bn_g = m.generator.bn.export()
+    for k, v in st.Gs.mean.items():
+        assert np.allclose(bn_g[f"{k}/moving_mean"], v, rtol=1e-4, atol=1e-5), k
+    bn_d = m.discriminator.bn.export()
+    for k, v in st.Ds.var.items():
+        assert np.allclose(bn_d[f"{k}/moving_variance"], v, rtol=1e-4, atol=1e-5), k
+
+
+@gpu
+def test_fsrgan_step_parity():
+    from fsrgan import FastSRGAN
+    _run_step_parity(FastSRGAN, "fsrgan", N=2, H=64, scale=4)
+
+
+@gpu
+def test_autoencoder_step_parity():
+    from autoencoder import Autoencoder
+    _run_step_parity(Autoencoder, "autoencoder", N=4, H=64, scale=1)
+
+
+@gpu
+def test_srgan_two_steps_track_oracle():
+    """Adam with ExponentialDecay and TTUR (D lr x5): step-2 losses track the oracle."""
+    from srgan import SRGAN
+    _run_step_parity(SRGAN, "srgan", N=2, H=32, scale=4, steps=2)
+
+
+@gpu
+def test_sr_train_step_tuples():
+    import train_autoencoder
+    import train_fsrgan
+    import train_srgan
+    from autoencoder import Autoencoder
+    from fsrgan import FastSRGAN
+    from srgan import SRGAN
+    for mod, cls, H, scale, n in ((train_srgan, SRGAN, 32, 4, 7), (train_fsrgan, FastSRGAN, 32, 4, 8),
+                                  (train_autoencoder, Autoencoder, 32, 1, 5)):
+        m = cls(Args(crop_size=H, scale=scale, vgg_width=8))
+        x, y = _synthetic(2, H, H, scale, seed=1)
+        out = mod.train_step(m, x, y)
+        assert len(out) == n and all(torch.isfinite(v).item() for v in out)
+        g = m.generator(x, training=False)
+        assert tuple(g.shape) == (2, H, H, 3)
+        d = m.discriminator(y, training=False)
+        assert d.shape[-1] == 1
+        if cls is Autoencoder:
+            assert float(d.min()) >= 0.0 and float(d.max()) <= 1.0  # sigmoid output
