@@ -205,7 +205,9 @@ def init_graph_variables(graph, seed):
 # static plan
 # ---------------------------------------------------------------------------
 def _ld(C):
-    return -(-C // 4) * 4
+    """Pixel stride of an activation buffer: channel counts >= 4 round up to a
+    multiple of 4 floats (16-byte rows); narrow tensors (logits, images) stay dense."""
+    return C if C < 4 else -(-C // 4) * 4
 
 
 def _buf(N, H, W, C, device):

@@ -31,7 +31,7 @@ TF semantics (beyond those of p2p_oracle):
   S1 PReLU(shared_axes=[1,2]) = relu(x) - alpha * relu(-x), alpha per channel
   S2 tf.nn.depth_to_space NHWC block b: out[n, h*b+i, w*b+j, c] = in[n, h, w, (i*b+j)*C + c]
   S3 DepthwiseConv2D 3x3 'same' stride 1: per-channel correlation, kernel [3,3,C,1]
-  S4 MaxPool2D(2,2): max over 2x2 windows; UpSampling2D(2) nearest: replication
+  S4 MaxPool2D(2,2): max over 2x2 windows, gradient to the first maximum; UpSampling2D(2) nearest: replication
   S5 vgg19.preprocess_input (caffe): RGB->BGR, minus (103.939, 116.779, 123.68)
   S6 Keras BinaryCrossentropy() on a Sigmoid output in graph mode = BCE with the logits
   S7 ExponentialDecay staircase: lr * rate^floor(iterations / steps), iterations before the update
@@ -115,9 +115,14 @@ def depth_to_space(x, b):
 
 
 def maxpool2(x):
+    """S4: the gradient goes to ONE element per window, the first maximum in
+    row-major window order (TF MaxPoolGrad routes to the forward argmax;
+    torch's amax would split it between tied elements)."""
     N, H, W, C = x.shape
     x = x[:, :H // 2 * 2, :W // 2 * 2]
-    return x.reshape(N, H // 2, 2, W // 2, 2, C).amax(dim=(2, 4))
+    win = x.reshape(N, H // 2, 2, W // 2, 2, C).permute(0, 1, 3, 5, 2, 4).reshape(N, H // 2, W // 2, C, 4)
+    idx = win.detach().argmax(dim=-1, keepdim=True)  # first occurrence of the max
+    return win.gather(-1, idx)[..., 0]
 
 
 def upsample2(x):
@@ -324,12 +329,13 @@ def train_step(st, x, y, apply=True):
     disc = bce_logits(zr, 1.0) + bce_logits(zf, 0.0)
     if st.kind == "fsrgan":
         disc = 0.5 * disc
+    dgen = torch.autograd.grad(gen_loss, gen, retain_graph=True)[0]
     gG = torch.autograd.grad(gen_loss, list(PG.values()), retain_graph=True)
     gD = torch.autograd.grad(disc, list(PD.values()))
     gG = {k: g.numpy() for k, g in zip(PG, gG)}
     gD = {k: g.numpy() for k, g in zip(PD, gD)}
     out = dict(losses=tuple(float(v) for v in (gen_loss, adv, mae, mse, cont, disc, var)),
-               gen=gen.detach().numpy(), gG=gG, gD=gD)
+               gen=gen.detach().numpy(), dgen=dgen.numpy(), gG=gG, gD=gD)
     if apply:
         t = st.iterations + 1
         lrg = exp_decay(st.lr, st.iterations)

