@@ -8,8 +8,11 @@ training images/sec, pix2pix 256x256 bs16 per GPU, 1/2/4/8 GPUs).
 One step = the reference's train_step (train_pix2pix.py:33-71) on 16 synthetic
 256x256 noisy/clean pairs per GPU already resident in HBM: G(x), the identity
 pass G(y), D real + fake, L1/L2/TV/GAN/identity losses, both gradients, the
-data-parallel gradient all-reduce (N>1) and Keras-Adam on G and D.  The VGG19
-content term is 0 (ImageNet weights unavailable offline).  fp32 tensors
+data-parallel gradient all-reduce (N>1) and Keras-Adam on G and D, plus the
+VGG19 content loss (pix2pix.py:45-51: VGG19-to-block5_conv4 forward on G(x)
+and on y, backward into G(x)) with seeded stand-in weights (ImageNet weights
+are a download; same FLOPs and shapes).  `--no-content` drops the VGG term;
+at N=1 the same run also reports that content-free step as `core`.  fp32 tensors
 throughout; the conv GEMMs use the library's default conv math, bf16x6
 (fp32 operands split exactly into three bf16 pieces, the six significant
 piece products accumulated in fp32 -- fp32-accurate); set
@@ -65,6 +68,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-identity", action="store_true")
+    ap.add_argument("--no-content", action="store_true", help="drop the VGG19 content term")
+    ap.add_argument("--no-core", action="store_true", help="skip the content-free secondary measurement")
     ap.add_argument("--profile-only", action="store_true", help="skip roofline/cpu legs (for rocprofv3 runs)")
     args = ap.parse_args()
 
@@ -83,65 +88,72 @@ def main():
     from pix2pix import Pix2Pix
     from dgan import ops
 
-    model = Pix2Pix(Args(crop_size=args.size, retrain=0, width=1, seed=1234, dropout_seed=rank,
-                         identity_loss=0 if args.no_identity else 1))
-    if distributed:
-        from dgan.dist import setup_data_parallel
-        setup_data_parallel(model)
+    def build(content):
+        m = Pix2Pix(Args(crop_size=args.size, retrain=0, width=1, seed=1234, dropout_seed=rank,
+                         identity_loss=0 if args.no_identity else 1, content_loss=int(content)))
+        if distributed:
+            from dgan.dist import setup_data_parallel
+            setup_data_parallel(m)
+        return m
+
     x_np, y_np = synthetic_batch(args.batch, args.size, seed=1000 + rank)
     x = torch.from_numpy(x_np).to(dev)
     y = torch.from_numpy(y_np).to(dev)
-    trainer = model.trainer(x.shape)
-    conv_math = "bf16x6" if trainer.G.ldesc.math == ops.MATH_BF16X6 else "fp32"
-
-    # ---- warmup (also plans/JIT-free: everything is prebuilt) ------------
-    for _ in range(max(1, args.warmup // 2)):
-        trainer.step(x, y)
-    torch.cuda.synchronize()
-
-    graph = None
     use_graph = not args.no_graph and not distributed
-    if use_graph:
-        try:
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                trainer.step(x, y)
-            torch.cuda.current_stream().wait_stream(s)
-            torch.cuda.synchronize()
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                trainer.step(x, y)
-            torch.cuda.synchronize()
-        except Exception as e:  # report, fall back to eager launches
-            print(f"[bench] graph capture failed ({e}); eager launches", file=sys.stderr)
-            graph = None
 
-    def step():
-        if graph is not None:
-            graph.replay()
-        else:
+    def measure(content):
+        model = build(content)
+        trainer = model.trainer(x.shape)
+        for _ in range(max(1, args.warmup // 2)):
             trainer.step(x, y)
+        torch.cuda.synchronize()
+        graph = None
+        if use_graph:
+            try:
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(s):
+                    trainer.step(x, y)
+                torch.cuda.current_stream().wait_stream(s)
+                torch.cuda.synchronize()
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    trainer.step(x, y)
+                torch.cuda.synchronize()
+            except Exception as e:  # report, fall back to eager launches
+                print(f"[bench] graph capture failed ({e}); eager launches", file=sys.stderr)
+                graph = None
 
-    for _ in range(args.warmup - max(1, args.warmup // 2)):
-        step()
-    torch.cuda.synchronize()
+        def step():
+            if graph is not None:
+                graph.replay()
+            else:
+                trainer.step(x, y)
 
-    # ---- timed region ------------------------------------------------------
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if distributed:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        for _ in range(args.warmup - max(1, args.warmup // 2)):
+            step()
+        torch.cuda.synchronize()
+        # ---- timed region: barrier + sync on both sides, max over ranks ----
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if distributed:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return model, trainer, graph, elapsed
+
+    content = not args.no_content
+    model, trainer, graph, elapsed = measure(content)
+    hip_graph = graph is not None
+    conv_math = "bf16x6" if trainer.G.ldesc.math == ops.MATH_BF16X6 else "fp32"
     losses = trainer.loss.cpu().numpy()
     ms_per_step = elapsed / args.steps * 1e3
     images = world * args.batch * args.steps
@@ -173,10 +185,17 @@ def main():
             for r in sorted(recs, key=lambda r: -r["ms"])[:40]:
                 print(json.dumps({**r, "tflops": r["flops"] / (r["ms"] * 1e-3) / 1e12}), file=sys.stderr)
 
+    core = None
+    if content and world == 1 and not args.no_core and not args.profile_only:
+        _, _, _, el_core = measure(False)
+        core = {"value": round(images / el_core, 2), "ms_per_step": round(el_core / args.steps * 1e3, 3),
+                "workload": "the same step without the VGG19 content term (pix2pix.py:87 weight 0)"}
+
     # ---- CPU baseline: torch fp32 restatement, rank 0, N=1 only -------------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_only:
-        cpu = cpu_baseline(args.size, args.cpu_seconds, identity=not args.no_identity)
+        cpu = cpu_baseline(args.size, args.cpu_seconds, identity=not args.no_identity,
+                           vgg=model.vgg.arena.export() if model.vgg is not None else None)
 
     if rank == 0:
         out = {
@@ -195,13 +214,15 @@ def main():
             "data": "synthetic (seeded noisy/clean 256x256 pairs resident in HBM; random-init weights)",
             "config": {"workload": "pix2pix train_step (train_pix2pix.py:33-71): G(x)+G(y) identity pass, D real+fake, "
                                    "GAN/L1/L2/TV/identity losses, D and G gradients, Keras Adam G and D; "
-                                   "VGG content term 0 (no ImageNet weights offline)",
+                                   + ("VGG19 content loss (seeded stand-in weights: ImageNet weights are a download)"
+                                      if content else "VGG content term 0"),
                        "model": "pix2pix U-Net G (54.4M) + PatchGAN D (2.77M)",
                        "global_batch": world * args.batch, "batch_per_gpu": args.batch, "image_size": args.size,
-                       "parallelism": f"dp{world}", "hip_graph": graph is not None,
+                       "parallelism": f"dp{world}", "hip_graph": hip_graph,
                        "identity_pass": not args.no_identity,
                        "conv_gflop_per_image": round(step_flops / args.batch / 1e9, 2) if step_flops else None},
             "losses": [round(float(v), 6) for v in losses],
+            "core": core,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
@@ -210,7 +231,7 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(size, seconds, identity=True):
+def cpu_baseline(size, seconds, identity=True, vgg=None):
     """The oracle's torch-fp32 restatement of the same step on the host cores."""
     from oracle import torch_p2p as T
     from oracle import p2p_oracle as O
@@ -219,7 +240,7 @@ def cpu_baseline(size, seconds, identity=True):
     bs = 2
     G = O.init_variables(O.g_variables(1), 1234)
     D = O.init_variables(O.d_variables(1), 1235)
-    step = T.make_fp32_step(G, D)
+    step = T.make_fp32_step(G, D, PV=vgg)
     x, y = O.synthetic_pair(bs, size, seed=7)
     step(x, y)  # warm-up
     n = 0
@@ -232,7 +253,8 @@ def cpu_baseline(size, seconds, identity=True):
     el = time.perf_counter() - t0
     return {"value": round(n * bs / el, 3), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"{n} steps x {bs} images at {size}x{size}, torch fp32 CPU autograd restatement "
-                      f"(oracle/torch_p2p.py) incl. identity pass and Keras-Adam; {el:.1f}s"}
+                      f"(oracle/torch_p2p.py) incl. identity pass, {'VGG19 content loss, ' if vgg else ''}"
+                      f"Keras-Adam; {el:.1f}s"}
 
 
 if __name__ == "__main__":

@@ -27,7 +27,7 @@ class AdamConfig:
 class Pix2PixTrainer:
     def __init__(self, g_arena, g_bn, d_arena, d_bn, N, H, W, device, width=1, identity=True,
                  loss_weights=ops.LOSS_WEIGHTS_REF, drop_rate=DROP_RATE, drop_seed=0, g_opt=None, d_opt=None,
-                 grad_sync=None):
+                 grad_sync=None, vgg=None):
         self.gA, self.dA = g_arena, d_arena
         self.N, self.H, self.W = N, H, W
         self.identity = identity
@@ -44,8 +44,14 @@ class Pix2PixTrainer:
         self.dident = e((N, H, W, 3)) if identity else None
         self.dzr, self.dzf_d, self.dzf_g = e(lshape), e(lshape), e(lshape)
         self.loss = torch.zeros(8, dtype=torch.float32, device=device)
+        # VGG19 content loss (pix2pix.py:45-51, :87): frozen feature extractor on G(x) and y
+        self.content = None
+        if vgg is not None and self.weights[5] != 0.0:
+            from .sr_trainer import ContentLoss
+            self.content = ContentLoss(vgg, N, H, W, device)
         ws_bytes = max(self.G.ws_bytes, self.D.ws_bytes,
-                       ops.p2p_loss_workspace_bytes(N, H, W, 3, lshape[0] * lshape[1] * lshape[2]))
+                       ops.p2p_loss_workspace_bytes(N, H, W, 3, lshape[0] * lshape[1] * lshape[2]),
+                       self.content.ws_bytes if self.content else 0)
         self.ws = ops.Workspace(device)
         self.ws.get(ws_bytes)
 
@@ -72,12 +78,16 @@ class Pix2PixTrainer:
                       step_dev=step_dev)
         zr = D.forward(slot=0, ws=ws)
         zf = D.forward(slot=1, ws=ws)
+        content = None
+        if self.content is not None:
+            # content_loss(target, gen) = MSE(vgg(pre(y))/12.75, vgg(pre(G(x)))/12.75) (pix2pix.py:45-51)
+            content = self.content.forward(gen, y, grad_weight=self.weights[5], ws=ws)
         # ---- losses + their gradients (pix2pix.py:74-103) ----------------
         dinp = D.dinp
         ops.fill(dinp, 0.0)
-        ops.p2p_loss(gen, y, zr, zf, self.loss, ident=self.ident, weights=self.weights, dgen=dinp[..., 3:],
-                     dident=self.dident, dlogit_real_d=self.dzr, dlogit_fake_d=self.dzf_d, dlogit_fake_g=self.dzf_g,
-                     ws=ws)
+        ops.p2p_loss(gen, y, zr, zf, self.loss, ident=self.ident, weights=self.weights, content=content,
+                     dgen=dinp[..., 3:], dident=self.dident, dlogit_real_d=self.dzr, dlogit_fake_d=self.dzf_d,
+                     dlogit_fake_g=self.dzf_g, ws=ws)
         sync = self.grad_sync
         # ---- disc_tape.gradient (train_pix2pix.py:65) ---------------------
         D.backward(self.dzr, slot=0, param_grads=True, beta=0.0, ws=ws)
@@ -86,6 +96,8 @@ class Pix2PixTrainer:
             sync.start("D")
         # ---- gen_tape.gradient (train_pix2pix.py:64): through D(fake) into G
         D.backward(self.dzf_g, slot=1, param_grads=False, input_grad=dinp, input_beta=1.0, ws=ws)
+        if self.content is not None:
+            self.content.backward(dinp[..., 3:], beta=1.0, ws=ws)
         if self.identity:
             G.backward(self.dident, slot=1, beta=0.0, ws=ws, drop_rate=self.drop_rate)
         G.backward(dinp[..., 3:], slot=0, beta=1.0 if self.identity else 0.0, ws=ws, drop_rate=self.drop_rate,

@@ -17,19 +17,23 @@ Reference surface kept:
   .discriminator_loss(real, fake)     scalar                           (:96-103)
 
 Differences that cannot be avoided offline (documented in DESIGN.md):
-  * VGG19 ImageNet weights (pix2pix.py:59) are a network download; `.vgg`
-    is None and content_loss returns 0, i.e. the content term weighs 0.
+  * VGG19 ImageNet weights (pix2pix.py:59) are a network download.  `.vgg`
+    is the same VGG19-to-block5_conv4 network on libdgan; it loads local
+    weights from args.vgg_weights (.npz, Keras layer names) when given, else
+    seeded He-normal stand-in weights.  args.content_loss=0 drops the term.
   * Dropout masks come from a counter-based hash (reproducible on the CPU
     oracle) instead of TF's RNG stream.
 Extra (MI355X-specific) knobs, read from args when present:
   args.width (test-only channel divisor, default 1), args.seed,
-  args.dropout_seed, args.identity_loss (default 1).
+  args.dropout_seed, args.identity_loss (default 1), args.content_loss
+  (default 1), args.vgg_weights, args.vgg_width (test-only).
 """
 import torch
 
 from dgan import ops
 from dgan.models import Adam, Discriminator, Generator, default_device, to_device
 from dgan.trainer import Pix2PixTrainer
+from dgan.sr_trainer import ContentLoss, VGGNetwork
 
 
 class _MSE:
@@ -71,8 +75,6 @@ class Pix2Pix(object):
         self.gen_optimizer = Adam(2e-4, beta_1=0.5)
         self.disc_optimizer = Adam(2e-4, beta_1=0.5)
 
-        # VGG19(weights="imagenet") is a remote download (pix2pix.py:59): unavailable offline.
-        self.vgg = None
 
         self.gf = 32
         self.df = 32
@@ -83,6 +85,13 @@ class Pix2Pix(object):
         self.identity = bool(int(getattr(args, "identity_loss", 1)))
         self.dropout_rate = float(getattr(args, "dropout_rate", 0.5))
         self.loss_weights = tuple(getattr(args, "loss_weights", ops.LOSS_WEIGHTS_REF))
+        self.use_content = bool(int(getattr(args, "content_loss", 1)))
+        if not self.use_content:
+            self.loss_weights = self.loss_weights[:5] + (0.0,)
+        # VGG19(weights="imagenet") (pix2pix.py:53-67) is a remote download: local .npz or seeded stand-in
+        self.vgg = VGGNetwork(weights=getattr(args, "vgg_weights", None), seed=self.seed + 7,
+                              width=int(getattr(args, "vgg_width", 1)), device=self.device) if self.use_content else None
+        self._content = {}
         self.generator, self.discriminator = self.build_gan()
         self.gen_optimizer.bind(self.generator.arena)
         self.disc_optimizer.bind(self.discriminator.arena)
@@ -91,19 +100,28 @@ class Pix2Pix(object):
 
     # ------------------------------------------------------------------
     def content_loss(self, target, gen_output):
-        """VGG19 content loss (pix2pix.py:45-51).  ImageNet weights are not
-        available offline, so the term is 0 (documented deviation)."""
-        return torch.zeros((), dtype=torch.float32, device=self.device)
+        """MSE(vgg(pre(target))/12.75, vgg(pre(gen))/12.75) (pix2pix.py:45-51)."""
+        if self.vgg is None:
+            return torch.zeros((), dtype=torch.float32, device=self.device)
+        tgt, gen = to_device(target, self.device), to_device(gen_output, self.device)
+        N, H, W, _ = gen.shape
+        if (N, H, W) not in self._content:
+            self._content[(N, H, W)] = ContentLoss(self.vgg, N, H, W, self.device, train=False)
+        c = self._content[(N, H, W)]
+        ws = ops.Workspace(self.device)
+        ws.get(c.ws_bytes)
+        return c.forward(gen, tgt, ws=ws)[0].clone()
 
     def build_vgg(self):
-        return None
+        return self.vgg
 
     def _loss_values(self, gen, tgt, ident, real, fake):
         out = torch.empty(8, dtype=torch.float32, device=self.device)
         gen, tgt = to_device(gen, self.device), to_device(tgt, self.device)
         real, fake = to_device(real, self.device), to_device(fake, self.device)
+        cont = self.content_loss(tgt, gen).reshape(1) if self.vgg is not None else None
         ops.p2p_loss(gen, tgt, real, fake, out, ident=None if ident is None else to_device(ident, self.device),
-                     weights=self.loss_weights)
+                     weights=self.loss_weights, content=cont)
         return out
 
     def generator_loss(self, disc_generated_output, gen_output, target):
@@ -132,7 +150,7 @@ class Pix2Pix(object):
                 self.generator.arena, self.generator.bn, self.discriminator.arena, self.discriminator.bn, N, H, W,
                 self.device, width=self.width, identity=self.identity, loss_weights=self.loss_weights,
                 drop_rate=self.dropout_rate, drop_seed=self.dropout_seed, g_opt=_opt_cfg(self.gen_optimizer),
-                d_opt=_opt_cfg(self.disc_optimizer), grad_sync=self.grad_sync)
+                d_opt=_opt_cfg(self.disc_optimizer), grad_sync=self.grad_sync, vgg=self.vgg)
         return self._trainers[key]
 
 

@@ -93,9 +93,16 @@ def _bce(z, y):
     return (torch.clamp(z, min=0) - z * y + torch.log1p(torch.exp(-z.abs()))).mean()
 
 
+def _content(PV, yt, gen):
+    """VGG19 content loss (pix2pix.py:45-51) on NCHW tensors, via oracle/sr_oracle.py's restatement."""
+    from . import sr_oracle as S
+    return S.content_loss(PV, yt.permute(0, 2, 3, 1), gen.permute(0, 2, 3, 1))
+
+
 def step_grads(Gnp, Dnp, x, y, width=1, drop_rate=0.5, drop_seed=0, step=0, identity=True, weights=None,
-               dtype=torch.float64):
-    """One train_step's losses and gradients (no optimizer) -> (tuple8, gG, gD) as numpy float64."""
+               dtype=torch.float64, PV=None):
+    """One train_step's losses and gradients (no optimizer) -> (tuple8, gG, gD) as numpy float64.
+    PV: VGG19 weights for the content term (None: the term is 0)."""
     w = dict(O.LOSS_WEIGHTS) if weights is None else weights
     G = {k: torch.tensor(v, dtype=dtype, requires_grad=True) for k, v in Gnp.items()}
     D = {k: torch.tensor(v, dtype=dtype, requires_grad=True) for k, v in Dnp.items()}
@@ -113,7 +120,10 @@ def step_grads(Gnp, Dnp, x, y, width=1, drop_rate=0.5, drop_seed=0, step=0, iden
         idl = w["identity"] * (generator(G, yt, width, drop_rate, drop_seed, step, 1) - yt).abs().mean()
     else:
         idl = torch.zeros((), dtype=dtype)
-    cont = torch.zeros((), dtype=dtype)
+    if PV is not None:
+        cont = w["content"] * _content({k: torch.tensor(v, dtype=dtype) for k, v in PV.items()}, yt, gen)
+    else:
+        cont = torch.zeros((), dtype=dtype)
     total = gan + l2 + cont + tv + l1 + idl
     disc = _bce(zr, 1.0) + _bce(zf, 0.0)
     gG = torch.autograd.grad(total, list(G.values()), retain_graph=True)
@@ -123,8 +133,10 @@ def step_grads(Gnp, Dnp, x, y, width=1, drop_rate=0.5, drop_seed=0, step=0, iden
             gen.detach().permute(0, 2, 3, 1).double().numpy())
 
 
-def make_fp32_step(Gnp, Dnp, width=1, lr=2e-4, b1=0.5, b2=0.999, eps=1e-7):
-    """A full fp32 CPU training step (fwd, both backwards, Keras-Adam) for the CPU baseline timing."""
+def make_fp32_step(Gnp, Dnp, width=1, lr=2e-4, b1=0.5, b2=0.999, eps=1e-7, PV=None):
+    """A full fp32 CPU training step (fwd, both backwards, Keras-Adam; VGG19 content loss when PV is
+    given) for the CPU baseline timing."""
+    PVt = None if PV is None else {k: torch.tensor(v, dtype=torch.float32) for k, v in PV.items()}
     G = {k: torch.tensor(v, dtype=torch.float32, requires_grad=True) for k, v in Gnp.items()}
     D = {k: torch.tensor(v, dtype=torch.float32, requires_grad=True) for k, v in Dnp.items()}
     opt_state = {"t": 0, "m": {}, "v": {}}
@@ -150,6 +162,8 @@ def make_fp32_step(Gnp, Dnp, width=1, lr=2e-4, b1=0.5, b2=0.999, eps=1e-7):
         total = (1e-3 * _bce(zf, 1.0) + (d * d).mean() + 1e-5 * (
             (d[:, :, 1:] - d[:, :, :-1]).abs().sum() + (d[:, :, :, 1:] - d[:, :, :, :-1]).abs().sum()) / d.shape[0]
                  + d.abs().mean() + (generator(G, yt, width, 0.5, 0, opt_state["t"], 1) - yt).abs().mean())
+        if PVt is not None:
+            total = total + _content(PVt, yt, gen)
         disc = _bce(zr, 1.0) + _bce(zf, 0.0)
         gG = torch.autograd.grad(total, list(G.values()), retain_graph=True)
         gD = torch.autograd.grad(disc, list(D.values()))

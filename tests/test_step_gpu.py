@@ -21,6 +21,7 @@ class Args:
     def __init__(self, **kw):
         self.crop_size = 256
         self.retrain = 0
+        self.content_loss = 0   # the p2p oracle restates the step without the VGG term (tested below)
         self.__dict__.update(kw)
 
 
@@ -156,3 +157,35 @@ def test_generator_inference_uses_moving_stats():
     states = m.generator.bn.export()
     ref, _ = O.generator_forward(params, x, width, training=False, states=states)
     assert np.abs(got.cpu().numpy() - ref).max() < 1e-5
+
+
+@gpu
+def test_step_parity_with_vgg_content():
+    """The reference-equivalent step incl. the VGG19 content loss (pix2pix.py:45-51, :87; seeded
+    stand-in VGG weights, channel width /8 to keep the fp64 CPU oracle fast) vs the torch fp64
+    autograd restatement (oracle/torch_p2p.py + oracle/sr_oracle.py's VGG19).  Losses to 1e-5;
+    gradients: relative L2 per variable < 2e-2 (the VGG input gradient is piecewise smooth; see
+    tests/test_sr_gpu.py::_grads_close_l2) and max-abs < 1e-4 where the content-free part dominates."""
+    from oracle import torch_p2p as T
+    from pix2pix import Pix2Pix
+    width, seed = 16, 5
+    m = Pix2Pix(Args(width=width, seed=seed, dropout_rate=0.0, content_loss=1, vgg_width=8))
+    G = m.generator.arena.export()
+    D = m.discriminator.arena.export()
+    PV = m.vgg.arena.export()
+    x, y = O.synthetic_pair(2, 256, seed=21)
+    vals, gG, gD, gen_ref = T.step_grads(G, D, x, y, width=width, drop_rate=0.0, PV=PV)
+    tr = m.trainer(x.shape)
+    loss = tr.step(torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda(), apply=False)
+    torch.cuda.synchronize()
+    got = loss.cpu().double().numpy()
+    assert got[4] > 0.0
+    assert np.allclose(got, np.array(vals), rtol=1e-5, atol=1e-7), (got, vals)
+    gen = tr.gen_output.cpu().numpy()
+    assert abs(psnr(gen, y) - psnr(gen_ref, y)) < 0.01
+    for arena, ref in ((m.generator.arena, gG), (m.discriminator.arena, gD)):
+        for name, g_ref in ref.items():
+            g = arena.grad_of(name).detach().double().cpu().numpy()
+            den = np.linalg.norm(g_ref)
+            if den > 1e-12:
+                assert np.linalg.norm(g - g_ref) / den < 2e-2, name
