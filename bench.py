@@ -182,7 +182,7 @@ def main():
                     "conv_launch_ms_per_step": round(conv_ms, 3), "conv_gflop_per_step": round(conv_flops / 1e9, 1),
                     "step_frac": round(conv_flops / (ms_per_step * 1e-3) / peak, 4)}
         if rank == 0 and os.environ.get("DG_BENCH_DETAIL"):
-            for r in sorted(recs, key=lambda r: -r["ms"])[:40]:
+            for r in sorted(recs, key=lambda r: -r["ms"])[:int(os.environ.get("DG_BENCH_DETAIL_N", "60"))]:
                 print(json.dumps({**r, "tflops": r["flops"] / (r["ms"] * 1e-3) / 1e12}), file=sys.stderr)
 
     core = None

@@ -425,19 +425,20 @@ k_splitk_reduce(const GemmArgs p, int V4) {
                 for (int q = 0; q < 4; ++q) v[q] += __shfl_xor(v[q], o);
             }
             if (lane != 0) continue;
-            long off;
+            long pix;
             if constexpr (MODE == MODE_DGRAD) {
                 int ww = row % ph.Wp; int t = row / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
-                off = ((long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw) * p.ldc;
+                pix = (long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw;
             } else {
-                off = (long)row * p.ldc;
+                pix = row;
             }
+            const long off = pix * p.ldc;
             f32x4 o;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 float x = v[q];
                 if (p.bias) x += p.bias[col + q];
-                o[q] = act_fwd(x, p.act, p.alpha);
+                o[q] = epi_mask(p, pix, col + q, act_fwd(x, p.act, p.alpha));
             }
             f32x4 *dst = reinterpret_cast<f32x4 *>(p.C + off + col);
             if (p.beta != 0.f) o += p.beta * (*dst);
@@ -451,15 +452,16 @@ k_splitk_reduce(const GemmArgs p, int V4) {
         int col = (int)(e - (long)row * p.N);
         float v = 0.f;
         for (int s = 0; s < p.splits; ++s) v += base[s * plane + (long)row * p.N + col];
-        long off;
+        long pix;
         if constexpr (MODE == MODE_DGRAD) {
             int ww = row % ph.Wp; int t = row / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
-            off = ((long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw) * p.ldc;
+            pix = (long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw;
         } else {
-            off = (long)row * p.ldc;
+            pix = row;
         }
+        const long off = pix * p.ldc;
         if (p.bias) v += p.bias[col];
-        v = act_fwd(v, p.act, p.alpha);
+        v = epi_mask(p, pix, col, act_fwd(v, p.act, p.alpha));
         if (p.beta != 0.f) v += p.beta * p.C[off + col];
         p.C[off + col] = v;
     }
@@ -509,7 +511,7 @@ k_narrow_fwd(const GemmArgs p) {
         for (int co = 0; co < Co; ++co) {
             float v = acc[co];
             if (p.bias) v += p.bias[co];
-            v = act_fwd(v, p.act, p.alpha);
+            v = epi_mask(p, m, co, act_fwd(v, p.act, p.alpha));
             long off = (long)m * p.ldc + co;
             if (p.beta != 0.f) v += p.beta * p.C[off];
             p.C[off] = v;
@@ -572,11 +574,12 @@ k_narrow_dgrad(const GemmArgs p, int w_in_lds) {
             }
         }
     }
-    long off = ((long)(n * g.H + h) * g.W + w) * p.ldc;
+    const long pix = (long)(n * g.H + h) * g.W + w;
+    long off = pix * p.ldc;
     for (int ci = 0; ci < Ci; ++ci) {
         float v = acc[ci];
         if (p.bias) v += p.bias[ci];
-        v = act_fwd(v, p.act, p.alpha);
+        v = epi_mask(p, pix, ci, act_fwd(v, p.act, p.alpha));
         if (p.beta != 0.f) v += p.beta * p.C[off + ci];
         p.C[off + ci] = v;
     }
@@ -637,13 +640,13 @@ __global__ void k_colsum_final(const float *partial, int nblk, int C, float *out
 
 // ---- recast helpers (see Recast) -------------------------------------------
 __global__ void __launch_bounds__(256)
-k_transpose(const float *__restrict__ src, int R, int Cc, float *__restrict__ dst) {
-    // dst[c][r] = src[r][c]
-    const long total = (long)R * Cc;
+k_transpose(const float *__restrict__ src, int R, int Cc, float *__restrict__ dst, int Rp) {
+    // dst[c][r] = src[r][c] for r < R, 0 for R <= r < Rp (row stride Rp)
+    const long total = (long)Rp * Cc;
     for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-        int c = (int)(e / R);
-        int r = (int)(e - (long)c * R);
-        dst[e] = src[(long)r * Cc + c];
+        int c = (int)(e / Rp);
+        int r = (int)(e - (long)c * Rp);
+        dst[e] = r < R ? src[(long)r * Cc + c] : 0.f;
     }
 }
 
@@ -665,7 +668,7 @@ k_recast_fwd_gather(const GemmArgs p, const float *__restrict__ V, int nv) {
         }
     }
     if (p.bias) v += p.bias[0];
-    v = act_fwd(v, p.act, p.alpha);
+    v = epi_mask(p, m, 0, act_fwd(v, p.act, p.alpha));
     long off = (long)m * p.ldc;
     if (p.beta != 0.f) v += p.beta * p.C[off];
     p.C[off] = v;
@@ -697,7 +700,7 @@ k_recast_col2im(const GemmArgs p, const float *__restrict__ V, int nv) {
             }
         }
         if (p.bias) v += p.bias[ci];
-        v = act_fwd(v, p.act, p.alpha);
+        v = epi_mask(p, pix, ci, act_fwd(v, p.act, p.alpha));
         long off = pix * p.ldc + ci;
         if (p.beta != 0.f) v += p.beta * p.C[off];
         p.C[off] = v;
@@ -777,6 +780,7 @@ struct Recast {
     ConvGeom g1;        // its geometry (N=1, H=1, W=pixels)
     OpPlan p1;          // its plan
     int nv;             // columns of V / G
+    int nvp;            // row stride of V (nv rounded up so the 1x1 GEMM stays on the bf16x6 path)
     size_t wt_off, v_off, slab_off, bytes;
 };
 
@@ -934,7 +938,7 @@ static void plan_recast(dg_conv_desc_s *d, int op) {
     if (mode == MODE_FWD) {
         if (g.Co != 1 || g.Ci % 32 || ntap % 4 || ntap < 8) return;
         long P = (long)g.N * g.H * g.W;
-        rc.nv = ntap; rc.mode1 = MODE_FWD;
+        rc.nv = ntap; rc.nvp = ntap; rc.mode1 = MODE_FWD;
         rc.g1 = geom_1x1(P, g.Ci, ntap);
         rc.p1 = make_plan(rc.g1, MODE_FWD, d->math);
         rc.wt_off = 0;
@@ -942,18 +946,19 @@ static void plan_recast(dg_conv_desc_s *d, int op) {
         rc.slab_off = al256(rc.v_off + (size_t)P * ntap * 4);
     } else if (mode == MODE_DGRAD) {
         const int nv = ntap * g.Ci;
-        if (g.Co % 32 || nv % 4 || nv < 8) return;
+        if (g.Co % 32 || nv < 8) return;
+        const int nvp = (nv + 15) & ~15;  // zero-padded columns (e.g. VGG block1_conv1: 3x3x3 = 27 -> 32)
         long P = (long)g.N * g.Ho * g.Wo;
-        rc.nv = nv; rc.mode1 = MODE_FWD;
-        rc.g1 = geom_1x1(P, g.Co, nv);
+        rc.nv = nv; rc.nvp = nvp; rc.mode1 = MODE_FWD;
+        rc.g1 = geom_1x1(P, g.Co, nvp);
         rc.p1 = make_plan(rc.g1, MODE_FWD, d->math);
         rc.wt_off = 0;
-        rc.v_off = al256((size_t)g.Co * nv * 4);
-        rc.slab_off = al256(rc.v_off + (size_t)P * nv * 4);
+        rc.v_off = al256((size_t)g.Co * nvp * 4);
+        rc.slab_off = al256(rc.v_off + (size_t)P * nvp * 4);
     } else {
         if (g.Co != 1 || g.Ci % 4 || g.Ci < 8 || ntap % 4) return;
         long P = (long)g.N * g.H * g.W;
-        rc.nv = ntap; rc.mode1 = MODE_WGRAD;
+        rc.nv = ntap; rc.nvp = ntap; rc.mode1 = MODE_WGRAD;
         rc.g1 = geom_1x1(P, ntap, g.Ci);
         rc.p1 = make_plan(rc.g1, MODE_WGRAD, d->math);
         rc.wt_off = 0;
@@ -1034,7 +1039,7 @@ static int run_recast(const dg_conv_desc_s *d, int op, const GemmArgs &a0, char 
     if (rc.mode1 == MODE_FWD && engine_mode(d, op) == MODE_FWD) {
         // Co == 1: V = x . wt, wt[ci][(i,j)] = w[(i,j)][ci]
         hipLaunchKernelGGL(k_transpose, dim3(std::min<unsigned>(dg_cdiv((long)rc.nv * g.Ci, 256), 1024)), dim3(256), 0, s,
-                           a0.B, rc.nv, g.Ci, wt);
+                           a0.B, rc.nv, g.Ci, wt, rc.nv);
         DG_LAUNCHED("recast_transpose");
         GemmArgs a = make_args(rc.g1, rc.p1, a0.A, a0.lda, wt, rc.nv, V, rc.nv, nullptr, 0.f, DG_ACT_NONE, 0.f, slab);
         int r = run_gemm(MODE_FWD, rc.p1, a, s);
@@ -1045,15 +1050,15 @@ static int run_recast(const dg_conv_desc_s *d, int op, const GemmArgs &a0, char 
     }
     if (rc.mode1 == MODE_FWD) {
         // DGRAD, Ci <= 8: V = dy . wt, wt[co][(i,j,ci)] = w[(i,j,ci)][co]; dx = col2im(V)
-        hipLaunchKernelGGL(k_transpose, dim3(std::min<unsigned>(dg_cdiv((long)rc.nv * g.Co, 256), 1024)), dim3(256), 0, s,
-                           a0.B, rc.nv, g.Co, wt);
+        hipLaunchKernelGGL(k_transpose, dim3(std::min<unsigned>(dg_cdiv((long)rc.nvp * g.Co, 256), 1024)), dim3(256), 0, s,
+                           a0.B, rc.nv, g.Co, wt, rc.nvp);
         DG_LAUNCHED("recast_transpose");
-        GemmArgs a = make_args(rc.g1, rc.p1, a0.A, a0.lda, wt, rc.nv, V, rc.nv, nullptr, 0.f, DG_ACT_NONE, 0.f, slab);
+        GemmArgs a = make_args(rc.g1, rc.p1, a0.A, a0.lda, wt, rc.nvp, V, rc.nvp, nullptr, 0.f, DG_ACT_NONE, 0.f, slab);
         int r = run_gemm(MODE_FWD, rc.p1, a, s);
         if (r != DG_OK) return r;
         long total = (long)g.N * g.H * g.W * g.Ci;
         hipLaunchKernelGGL(k_recast_col2im, dim3((unsigned)std::min<long>(dg_cdiv(total, 256), 8192)), dim3(256), 0, s,
-                           a0, V, rc.nv);
+                           a0, V, rc.nvp);
         DG_LAUNCHED("recast_col2im");
         return DG_OK;
     }
@@ -1068,13 +1073,15 @@ static int run_recast(const dg_conv_desc_s *d, int op, const GemmArgs &a0, char 
 
 static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, const float *B, int ldb,
                       float *C, int ldc, const float *bias, float beta, int act, float alpha,
-                      void *ws, size_t ws_bytes, hipStream_t s) {
+                      void *ws, size_t ws_bytes, hipStream_t s, const float *mz = nullptr, int ldmz = 0,
+                      int mact = DG_ACT_NONE, float malpha = 0.f) {
     const int mode = engine_mode(d, op);
     const OpPlan &pl = d->plan[op];
     const size_t need = d->rc[op].on ? d->rc[op].bytes : pl.gemm_bytes;
     DG_ARG(ws_bytes >= need, "workspace too small: need %zu bytes, got %zu", need, ws_bytes);
     DG_ARG(need == 0 || ws != nullptr, "workspace pointer is NULL");
     GemmArgs a = make_args(d->g, pl, A, lda, B, ldb, C, ldc, bias, beta, act, alpha, ws);
+    a.mz = mz; a.ldmz = ldmz; a.mact = mact; a.malpha = malpha;
     if (pl.M == 0 || pl.N == 0) return DG_OK;
     if (d->rc[op].on) {
         DG_ARG(lda % 4 == 0 && ((uintptr_t)A & 15) == 0, "recast path needs lda%%4==0 and 16B-aligned A");
@@ -1293,6 +1300,16 @@ int dg_conv_bwd_data(dg_conv_t d, const float *dy, int lddy, const float *w, flo
     DG_ARG(lddy >= d->Cout && lddx >= d->Cin, "pixel stride smaller than channels");
     return dg::run_engine(d, DG_OP_BWD_DATA, dy, lddy, w, d->transpose ? d->g.Co : 0, dx, lddx, nullptr, beta,
                           DG_ACT_NONE, 0.f, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int dg_conv_bwd_data_masked(dg_conv_t d, const float *dy, int lddy, const float *w, float *dx, int lddx,
+                            float beta, const float *z, int ldz, int act, float alpha, void *ws, size_t ws_bytes,
+                            dg_stream_t stream) {
+    DG_ARG(d && dy && w && dx && z, "NULL tensor");
+    DG_ARG(lddy >= d->Cout && lddx >= d->Cin && ldz >= d->Cin, "pixel stride smaller than channels");
+    DG_ARG(act >= DG_ACT_NONE && act <= DG_ACT_SIGMOID, "unknown activation %d", act);
+    return dg::run_engine(d, DG_OP_BWD_DATA, dy, lddy, w, d->transpose ? d->g.Co : 0, dx, lddx, nullptr, beta,
+                          DG_ACT_NONE, 0.f, ws, ws_bytes, (hipStream_t)stream, z, ldz, act, alpha);
 }
 
 int dg_conv_bwd_filter(dg_conv_t d, const float *x, int ldx, const float *dy, int lddy, float *dw, float *dbias,

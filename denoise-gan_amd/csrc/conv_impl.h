@@ -30,7 +30,14 @@ struct GemmArgs {
     unsigned a_bytes, b_bytes;  // extents of A and B for the buffer-resource range check
     unsigned mg_wo, mg_ho;      // multiply-shift division by g.Wo / g.Ho (bf16x6 WGRAD)
     int sh_wo, sh_ho;
+    // optional gradient mask of the output (dg_conv_bwd_data_masked):
+    // C = (result * act'(mz)) + beta*C, act' expressed through the activation's output mz
+    const float *mz; int ldmz; int mact; float malpha;
 };
+
+__device__ __forceinline__ float epi_mask(const GemmArgs &p, long pix, int col, float v) {
+    return p.mz ? v * act_grad_from_out(p.mz[pix * p.ldmz + col], p.mact, p.malpha) : v;
+}
 
 // Branch-free operand loads: raw buffer loads through a resource whose range
 // check returns 0 for an out-of-range offset, so padding taps and ragged tile
@@ -111,15 +118,17 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs &p, f32x16 (&acc)[T
                 if (p.splits > 1) {
                     p.slab[((long)(phase * p.splits + split) * p.M + row) * p.N + col] = v;
                 } else {
-                    long off;
+                    long pix;
                     if constexpr (MODE == MODE_DGRAD) {
                         int ww = row % ph.Wp; int t = row / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
-                        off = ((long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw) * p.ldc;
+                        pix = (long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw;
                     } else {
-                        off = (long)row * p.ldc;
+                        pix = row;
                     }
+                    const long off = pix * p.ldc;
                     if (p.bias) v += p.bias[col];
                     v = act_fwd(v, p.act, p.alpha);
+                    v = epi_mask(p, pix, col, v);
                     if (p.beta != 0.f) v += p.beta * p.C[off + col];
                     p.C[off + col] = v;
                 }
@@ -148,15 +157,17 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
                 if (p.splits > 1) {
                     p.slab[((long)(phase * p.splits + split) * p.M + row) * p.N + col] = v;
                 } else {
-                    long off;
+                    long pix;
                     if constexpr (MODE == MODE_DGRAD) {
                         int ww = row % ph.Wp; int t = row / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
-                        off = ((long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw) * p.ldc;
+                        pix = (long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw;
                     } else {
-                        off = (long)row * p.ldc;
+                        pix = row;
                     }
+                    const long off = pix * p.ldc;
                     if (p.bias) v += p.bias[col];
                     v = act_fwd(v, p.act, p.alpha);
+                    v = epi_mask(p, pix, col, v);
                     if (p.beta != 0.f) v += p.beta * p.C[off + col];
                     p.C[off + col] = v;
                 }

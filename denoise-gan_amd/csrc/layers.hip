@@ -185,32 +185,51 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd(int N, int H, int W, int C,
     }
 }
 
+// one thread per (window, channel): the window's four input gradients; rows/cols past
+// 2*Ho / 2*Wo (odd sizes) get their zero gradient from the tail pass below
 __global__ void __launch_bounds__(256) k_maxpool_bwd(int N, int H, int W, int C, const float *x, int ldx,
-                                                    const float *dy, int lddy, float *dx, int lddx, float beta) {
+                                                    const float *dy, int lddy, float *dx, int lddx, float beta,
+                                                    int act, float alpha) {
     const int Ho = H / 2, Wo = W / 2;
+    const long total = (long)N * Ho * Wo * C;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long op = e / C;
+        const int c = (int)(e - op * C);
+        const int wo = (int)(op % Wo);
+        const long t = op / Wo;
+        const int ho = (int)(t % Ho);
+        const long n = t / Ho;
+        const long p0 = (n * H + 2 * ho) * W + 2 * wo;
+        const long pp[4] = {p0, p0 + 1, p0 + W, p0 + W + 1};
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = x[pp[q] * ldx + c];
+        int am = 0;
+#pragma unroll
+        for (int q = 1; q < 4; ++q)
+            if (v[q] > v[am]) am = q;
+        const float gy = dy[op * lddy + c];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float g = q == am ? gy * act_grad_from_out(v[q], act, alpha) : 0.f;
+            float *o = dx + pp[q] * lddx + c;
+            *o = beta != 0.f ? g + beta * *o : g;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_maxpool_bwd_tail(int N, int H, int W, int C, float *dx, int lddx,
+                                                         float beta) {
+    const int H2 = H / 2 * 2, W2 = W / 2 * 2;
     const long total = (long)N * H * W * C;
     for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
         const long ip = e / C;
         const int c = (int)(e - ip * C);
         const int w = (int)(ip % W);
-        const long t = ip / W;
-        const int h = (int)(t % H);
-        const long n = t / H;
-        float g = 0.f;
-        const int ho = h >> 1, wo = w >> 1;
-        if (ho < Ho && wo < Wo) {
-            const long p0 = (n * H + 2 * ho) * W + 2 * wo;
-            const float v[4] = {x[p0 * ldx + c], x[(p0 + 1) * ldx + c], x[(p0 + W) * ldx + c],
-                                x[(p0 + W + 1) * ldx + c]};
-            int am = 0;
-#pragma unroll
-            for (int q = 1; q < 4; ++q)
-                if (v[q] > v[am]) am = q;
-            const int mine = (h & 1) * 2 + (w & 1);
-            if (am == mine) g = dy[((n * Ho + ho) * Wo + wo) * lddy + c];
-        }
+        const int h = (int)((ip / W) % H);
+        if (h < H2 && w < W2) continue;
         float *o = dx + ip * lddx + c;
-        *o = beta != 0.f ? g + beta * *o : g;
+        *o = beta != 0.f ? beta * *o : 0.f;
     }
 }
 
@@ -628,13 +647,19 @@ int dg_maxpool2_fwd(int N, int H, int W, int C, const float *x, int ldx, float *
 }
 
 int dg_maxpool2_bwd(int N, int H, int W, int C, const float *x, int ldx, const float *dy, int lddy, float *dx,
-                    int lddx, float beta, dg_stream_t stream) {
+                    int lddx, float beta, int act, float alpha, dg_stream_t stream) {
     DG_ARG(x && dy && dx, "NULL tensor");
     DG_ARG(N > 0 && H >= 2 && W >= 2 && C > 0 && ldx >= C && lddy >= C && lddx >= C, "bad shape");
-    const long total = (long)N * H * W * C;
+    DG_ARG(act >= DG_ACT_NONE && act <= DG_ACT_SIGMOID, "unknown activation %d", act);
+    const long total = (long)N * (H / 2) * (W / 2) * C;
     hipLaunchKernelGGL(dg::k_maxpool_bwd, dim3(dg::lgrid(total)), dim3(256), 0, (hipStream_t)stream, N, H, W, C, x, ldx,
-                       dy, lddy, dx, lddx, beta);
+                       dy, lddy, dx, lddx, beta, act, alpha);
     DG_LAUNCHED("maxpool_bwd");
+    if ((H & 1) || (W & 1)) {
+        hipLaunchKernelGGL(dg::k_maxpool_bwd_tail, dim3(dg::lgrid((long)N * H * W * C)), dim3(256), 0,
+                           (hipStream_t)stream, N, H, W, C, dx, lddx, beta);
+        DG_LAUNCHED("maxpool_bwd_tail");
+    }
     return DG_OK;
 }
 

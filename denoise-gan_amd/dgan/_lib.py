@@ -56,7 +56,10 @@ _SIGS = {
     "dg_accumulate": (c_int, [c_int64, c_int, _P, c_int, _P, c_int, c_float, _P]),
     "dg_act_fwd": (c_int, [c_int64, c_int, _P, c_int, c_int, c_float, _P, c_int, _P]),
     "dg_maxpool2_fwd": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P]),
-    "dg_maxpool2_bwd": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, c_float, _P]),
+    "dg_maxpool2_bwd": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, c_float, c_int, c_float,
+                                _P]),
+    "dg_conv_bwd_data_masked": (c_int, [c_void_p, _P, c_int, _P, _P, c_int, c_float, _P, c_int, c_int, c_float, _P,
+                                        c_size_t, _P]),
     "dg_upsample2_relu_fwd": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P]),
     "dg_upsample2_relu_bwd": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, c_float, _P]),
     "dg_dwconv3_workspace_size": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_size_t)]),

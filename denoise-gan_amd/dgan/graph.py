@@ -282,6 +282,21 @@ class GraphPlan:
                 if ok:
                     self.slice_of[t.id] = (n.out.id, off)
                 off += t.C
+        # ---- fused activation gradients ----
+        # a conv whose activation output feeds exactly one consumer that can fold
+        # act'(z) into the gradient it writes (a conv's masked bwd_data epilogue, a
+        # max-pool's routing pass, or -- for ReLU -- the nearest-upsample+ReLU
+        # backward, whose x > 0 mask is the same) skips its own act_bwd pass.
+        self.premask = set()
+        for n in nodes[1:]:
+            if n.kind != "conv" or ops.act_id(n.attrs["act"]) == 0 or n.out.id == graph.output.id:
+                continue
+            cs = cons[n.out.id]
+            if len(cs) != 1 or n.out.id in self.slice_of:
+                continue
+            c = cs[0]
+            if c.kind in ("conv", "maxpool") or (c.kind == "upsample" and ops.act_id(n.attrs["act"]) == 2):
+                self.premask.add(n.out.id)
         # ---- activation buffers per slot ----
         self.slots = []
         for _ in range(slots):
@@ -451,16 +466,21 @@ class GraphPlan:
             if k == "conv":
                 d = self.desc[n.idx]
                 act = n.attrs["act"]
-                if ops.act_id(act) != 0:
+                if ops.act_id(act) != 0 and n.out.id not in self.premask:
                     dy = self._scratch(self.shape[n.out.id])
                     ops.act_bwd(dz, s[n.out.id], dy, act, n.attrs["alpha"])
                 else:
-                    dy = dz
+                    dy = dz   # (already multiplied by act'(z) by the consumer when premasked)
                 if pg:
                     db = A.grad_of(f"{n.name}/bias") if n.attrs["bias"] else None
                     d.bwd_filter(s[t_in.id], dy, A.grad_of(f"{n.name}/kernel"), dbias=db, beta=param_beta, ws=ws)
                 if need(t_in):
-                    d.bwd_data(dy, A.param(f"{n.name}/kernel"), gr[t_in.id], beta=beta_of(n, t_in), ws=ws)
+                    if t_in.id in self.premask:
+                        pa = t_in.node.attrs
+                        d.bwd_data_masked(dy, A.param(f"{n.name}/kernel"), gr[t_in.id], s[t_in.id], pa["act"],
+                                          pa["alpha"], beta=beta_of(n, t_in), ws=ws)
+                    else:
+                        d.bwd_data(dy, A.param(f"{n.name}/kernel"), gr[t_in.id], beta=beta_of(n, t_in), ws=ws)
             elif k == "bn":
                 mean, inv = self.saved[slot][n.name]
                 b = beta_of(n, t_in)
@@ -486,7 +506,9 @@ class GraphPlan:
                     off += t.C
             elif k == "maxpool":
                 if need(t_in):
-                    ops.maxpool2_bwd(s[t_in.id], dz, gr[t_in.id], beta=beta_of(n, t_in))
+                    pa = t_in.node.attrs if t_in.id in self.premask else {"act": "none", "alpha": 0.0}
+                    ops.maxpool2_bwd(s[t_in.id], dz, gr[t_in.id], beta=beta_of(n, t_in), act=pa["act"],
+                                     alpha=pa["alpha"])
             elif k == "upsample":
                 if need(t_in):
                     ops.upsample2_relu_bwd(s[t_in.id], dz, gr[t_in.id], beta=beta_of(n, t_in))

@@ -197,6 +197,16 @@ class ConvDesc:
         _prof_end(ev, self, "bwd_data")
         return dx
 
+    def bwd_data_masked(self, dy, w, dx, z, act, alpha=0.3, beta=0.0, ws=None):
+        """dx = dL/dx * act'(z) + beta*dx, z = the activation output this conv read as input."""
+        lddy, lddx = pix_ld(dy, self.Cout), pix_ld(dx, self.Cin)
+        wp, wn = self._ws(OP_BWD_DATA, ws)
+        ev = _prof_begin()
+        call("dg_conv_bwd_data_masked", self._h, _p(dy), lddy, _p(w), _p(dx), lddx, float(beta), _p(z),
+             pix_ld(z, self.Cin), act_id(act), float(alpha), wp, wn, _stream())
+        _prof_end(ev, self, "bwd_data")
+        return dx
+
     def bwd_filter(self, x, dy, dw, dbias=None, beta=0.0, ws=None):
         ldx, lddy = pix_ld(x, self.Cin), pix_ld(dy, self.Cout)
         wp, wn = self._ws(OP_BWD_FILTER, ws)
@@ -420,10 +430,11 @@ def maxpool2_fwd(x, y):
     return y
 
 
-def maxpool2_bwd(x, dy, dx, beta=0.0):
+def maxpool2_bwd(x, dy, dx, beta=0.0, act="none", alpha=0.3):
+    """dx = routed dy * act'(x) + beta*dx (act: the activation whose output x is)."""
     N, H, W, C = _nhwc(x)
     call("dg_maxpool2_bwd", N, H, W, C, _p(x), pix_ld(x, C), _p(dy), pix_ld(dy, C), _p(dx), pix_ld(dx, C),
-         float(beta), _stream())
+         float(beta), act_id(act), float(alpha), _stream())
     return dx
 
 

@@ -84,6 +84,12 @@ int dg_conv_fwd(dg_conv_t d, const float *x, int ldx, const float *w, const floa
 int dg_conv_bwd_data(dg_conv_t d, const float *dy, int lddy, const float *w,
                      float *dx, int lddx, float beta,
                      void *ws, size_t ws_bytes, dg_stream_t stream);
+/* dx = (dL/dx) * act'(z) + beta * dx: the input gradient with the gradient of the
+ * activation that PRODUCED the input (z = act(.), e.g. Conv2D(activation='relu')
+ * feeding this conv, VGG19 / autoencoder.py:97-101) folded into the epilogue. */
+int dg_conv_bwd_data_masked(dg_conv_t d, const float *dy, int lddy, const float *w,
+                            float *dx, int lddx, float beta, const float *z, int ldz, int act, float alpha,
+                            void *ws, size_t ws_bytes, dg_stream_t stream);
 /* dw = dL/dw + beta * dw ; dbias = sum(dy) + beta * dbias  (dbias may be NULL) */
 int dg_conv_bwd_filter(dg_conv_t d, const float *x, int ldx, const float *dy, int lddy,
                        float *dw, float *dbias, float beta,
@@ -199,8 +205,10 @@ int dg_act_fwd(int64_t npix, int C, const float *x, int ldx, int act, float alph
                dg_stream_t stream);
 /* MaxPool2D(2, strides 2) (autoencoder.py:111-115, VGG19 block pools): [N,H,W,C] -> [N,H/2,W/2,C] */
 int dg_maxpool2_fwd(int N, int H, int W, int C, const float *x, int ldx, float *y, int ldy, dg_stream_t stream);
+/* dx = routed dy * act'(x) + beta*dx; act (through x = the activation's output) folds the
+ * gradient of the activation that produced the pool input (DG_ACT_NONE: plain MaxPoolGrad) */
 int dg_maxpool2_bwd(int N, int H, int W, int C, const float *x, int ldx, const float *dy, int lddy,
-                    float *dx, int lddx, float beta, dg_stream_t stream);
+                    float *dx, int lddx, float beta, int act, float alpha, dg_stream_t stream);
 /* UpSampling2D(2, 'nearest') + relu (autoencoder.py:117-131): [N,H,W,C] -> [N,2H,2W,C] */
 int dg_upsample2_relu_fwd(int N, int H, int W, int C, const float *x, int ldx, float *z, int ldz,
                           dg_stream_t stream);
