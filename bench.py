@@ -168,12 +168,21 @@ def main():
         torch.cuda.synchronize()
         recs = prof.summary()
         conv_flops = sum(r["flops"] for r in recs)
+        conv_alg_bytes = sum(r["bytes"] for r in recs)
         conv_ms = sum(r["ms"] for r in recs)
         step_flops = conv_flops
         achieved = conv_flops / (conv_ms * 1e-3)
         peak = X6_PEAK if conv_math == "bf16x6" else FP32_MFMA_PEAK
+        traffic = None
+        tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        if os.path.exists(tpath) and content:
+            with open(tpath) as f:
+                traffic = round(json.load(f)["conv_engine_bytes_per_step"], 0)
         roofline = {"bound": "mfma", "achieved": round(achieved / 1e12, 2), "peak": round(peak / 1e12, 1),
-                    "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                    "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                    "traffic_unit": "HBM bytes per step over the conv-engine launches (rocprofv3 PMC, "
+                                    "profiles/pmc_traffic.json; algorithmic operand bytes per step: "
+                                    f"{round(conv_alg_bytes / 1e9, 2)} GB)",
                     "kernel": "dg conv engine (k_conv_gemm_x6 / k_conv_gemm + split passes + narrow + split-K "
                               "reduce), all conv launches of one step",
                     "peak_basis": ("bf16 dense MFMA peak / 6 (six bf16 piece products per fp32 product)"

@@ -179,6 +179,13 @@ class ConvDesc:
             return 2 * self.N * self.H * self.W * self.Cin * self.kh * self.kw * self.Cout
         return 2 * self.N * self.Ho * self.Wo * self.Cout * self.kh * self.kw * self.Cin
 
+    def op_bytes(self, op):
+        """Algorithmic HBM bytes of one call: each fp32 operand read once, the output written once."""
+        xin = self.N * self.H * self.W * self.Cin
+        yout = self.N * self.Ho * self.Wo * self.Cout
+        w = self.kh * self.kw * self.Cin * self.Cout
+        return 4 * (xin + yout + w)
+
     def fwd(self, x, w, y, bias=None, act="none", alpha=0.3, beta=0.0, ws=None):
         ldx, ldy = pix_ld(x, self.Cin), pix_ld(y, self.Cout)
         wp, wn = self._ws(OP_FWD, ws)
@@ -244,7 +251,7 @@ class ConvProfile:
         out = []
         for e0, e1, d, op in self.records:
             out.append(dict(op=op, transpose=d.transpose, shape=(d.N, d.H, d.W, d.Cin, d.Cout, d.kh, d.sh),
-                            flops=d.flops, ms=e0.elapsed_time(e1)))
+                            flops=d.flops, bytes=d.op_bytes(op), ms=e0.elapsed_time(e1)))
         return out
 
 

@@ -5,7 +5,8 @@ doubled: on gfx950 it reports half the bytes of 16-B-per-lane streaming
 reads (MI355X_MICROARCH.md, HBM section), the access width of the conv
 engine's operand loads (buffer_load ... lds dwordx4) and split passes.
 
-usage: pmc_traffic.py FETCH_CSV WRITE_CSV STEPS"""
+usage: pmc_traffic.py FETCH_CSV WRITE_CSV STEPS [OUT_JSON]"""
+import json
 import csv
 import sys
 from collections import defaultdict
@@ -26,7 +27,7 @@ def load(path, counter):
     return per, n
 
 
-def main(fetch_csv, write_csv, steps):
+def main(fetch_csv, write_csv, steps, out_json=None):
     steps = int(steps)
     fe, _ = load(fetch_csv, "FETCH_SIZE")
     wr, _ = load(write_csv, "WRITE_SIZE")
@@ -41,7 +42,14 @@ def main(fetch_csv, write_csv, steps):
         rows[k.split("(")[0][-60:]][1] += v / steps
     for k, (f, w) in sorted(rows.items(), key=lambda kv: -(kv[1][0] + kv[1][1]))[:25]:
         print(f"  {k:60s} read {f / 1e9:8.3f} GB  write {w / 1e9:8.3f} GB")
+    if out_json:
+        with open(out_json, "w") as f:
+            json.dump({"conv_engine_bytes_per_step": (tot_f + tot_w) / steps, "read_bytes_per_step": tot_f / steps,
+                       "write_bytes_per_step": tot_w / steps, "steps": steps,
+                       "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 16B/lane correction) and --pmc WRITE_SIZE "
+                                 "in separate passes over bench.py --profile-only --no-graph; kernels "
+                                 + ", ".join(CONV)}, f, indent=1)
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])
