@@ -491,6 +491,8 @@ void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t
         DG_X6(3, 64, 64, 2, 2, 3)
         DG_X6(4, 256, 128, 4, 2, 2)
         DG_X6(5, 128, 256, 2, 4, 2)
+        DG_X6(6, 256, 64, 4, 1, 2)
+        DG_X6(7, 64, 256, 1, 4, 2)
     }
 #undef DG_X6
 }

@@ -185,76 +185,80 @@ def _empty(shape, device):
 class GeneratorPlan:
     """Static forward/backward schedule of the U-Net for one input shape.
 
-    slots: independent activation sets (slot 0 = G(x), slot 1 = G(target)
-    for the identity loss, pix2pix.py:90) so both backwards can run after
-    both forwards, as the two GradientTapes do."""
+    halves: independent images sets batched into ONE pass (half 0 = G(x),
+    half 1 = G(target) for the identity loss, pix2pix.py:90).  The convs run
+    once over all halves*N images -- twice the GEMM rows of two separate
+    passes, which fills the chip on the deep layers -- while BatchNorm
+    (statistics, moving averages, dropout masks) is applied per half, exactly
+    as the reference's two separate generator calls."""
 
-    def __init__(self, N, H, W, width, arena, bn_state, device, slots=1, train=True):
+    def __init__(self, N, H, W, width, arena, bn_state, device, halves=1, train=True):
         self.N, self.H, self.W, self.width = N, H, W, width
+        self.halves = halves
+        NT = N * halves
+        self.NT = NT
         self.arena, self.bn = arena, bn_state
         self.device = device
         self.downs, self.ups, self.last = g_layer_specs(width)
         self.train = train
-        if H % 256 or W % 256:
+        if H % (1 << 8) or W % (1 << 8):
             # 8 stride-2 blocks need H, W divisible by 2^8 for the skip shapes to line up
-            if H % (1 << 8) or W % (1 << 8):
-                raise ValueError(f"pix2pix generator needs H, W divisible by 256, got {H}x{W}")
-        # descriptors
+            raise ValueError(f"pix2pix generator needs H, W divisible by 256, got {H}x{W}")
+        # descriptors over all halves
         self.ddesc, self.udesc = [], []
         h, w = H, W
         self.down_hw = []
         for name, ci, co, _ in self.downs:
-            d = ConvDesc(N, h, w, ci, co, 4, 2, "same")
+            d = ConvDesc(NT, h, w, ci, co, 4, 2, "same")
             self.ddesc.append(d)
             h, w = d.Ho, d.Wo
             self.down_hw.append((h, w))
         for name, ci, co, _ in self.ups:
-            d = ConvDesc(N, h, w, ci, co, 4, 2, "same", transpose=True)
+            d = ConvDesc(NT, h, w, ci, co, 4, 2, "same", transpose=True)
             self.udesc.append(d)
             h, w = d.Ho, d.Wo
-        self.ldesc = ConvDesc(N, h, w, self.last[1], self.last[2], 4, 2, "same", transpose=True)
+        self.ldesc = ConvDesc(NT, h, w, self.last[1], self.last[2], 4, 2, "same", transpose=True)
         self.out_shape = self.ldesc.out_shape
-        # activations per slot
-        self.slots = []
-        for _ in range(slots):
-            s = {}
-            s["cat"] = []
-            for u, (name, ci, co, _) in enumerate(self.ups):
-                d = self.udesc[u]
-                skip_c = self.downs[6 - u][2]
-                s["cat"].append(_empty((N, d.Ho, d.Wo, co + skip_c), device))
-            s["z8"] = _empty((N,) + self.down_hw[7] + (self.downs[7][2],), device)
-            s["yd"] = [(_empty((N,) + self.down_hw[i] + (self.downs[i][2],), device) if self.downs[i][3] else None)
-                       for i in range(8)]
-            s["yu"] = [_empty(self.udesc[u].out_shape, device) for u in range(7)]
-            s["mean"] = {}
-            s["inv"] = {}
-            for name, _, co, bn in self.downs + [(n, a, b, True) for n, a, b, _ in self.ups]:
-                if bn:
-                    s["mean"][name] = _empty((co,), device)
-                    s["inv"][name] = _empty((co,), device)
-            s["x"] = None
-            s["out"] = None
-            self.slots.append(s)
-        # gradient buffers (shared by slots: backwards run one after another)
+        # activations
+        s = {}
+        s["cat"] = []
+        for u, (name, ci, co, _) in enumerate(self.ups):
+            d = self.udesc[u]
+            skip_c = self.downs[6 - u][2]
+            s["cat"].append(_empty((NT, d.Ho, d.Wo, co + skip_c), device))
+        s["z8"] = _empty((NT,) + self.down_hw[7] + (self.downs[7][2],), device)
+        s["yd"] = [(_empty((NT,) + self.down_hw[i] + (self.downs[i][2],), device) if self.downs[i][3] else None)
+                   for i in range(8)]
+        s["yu"] = [_empty(self.udesc[u].out_shape, device) for u in range(7)]
+        s["mean"] = {}
+        s["inv"] = {}
+        for name, _, co, bn in self.downs + [(n, a, b, True) for n, a, b, _ in self.ups]:
+            if bn:
+                s["mean"][name] = [_empty((co,), device) for _ in range(halves)]
+                s["inv"][name] = [_empty((co,), device) for _ in range(halves)]
+        s["x"] = None
+        s["out"] = None
+        self.s = s
+        # gradient buffers
         if train:
-            self.dcat = [torch.empty_like(c) for c in self.slots[0]["cat"]]
-            self.dz8 = torch.empty_like(self.slots[0]["z8"])
+            self.dcat = [torch.empty_like(c) for c in s["cat"]]
+            self.dz8 = torch.empty_like(s["z8"])
             maxdy = max([d.N * d.Ho * d.Wo * d.Cout for d in self.ddesc + self.udesc + [self.ldesc]])
             self.dy = _empty((maxdy,), device)
-        sizes = [d.max_ws() for d in self.ddesc + self.udesc + [self.ldesc]]
-        for name, _, co, bn in self.downs:
-            pass
-        self.ws_bytes = max(sizes + [self._bn_ws_max()])
+        self.ws_bytes = max([d.max_ws() for d in self.ddesc + self.udesc + [self.ldesc]] + [self._bn_ws_max()])
+
+    @property
+    def slots(self):
+        return [self.s]
 
     def _bn_ws_max(self):
         m = 0
-        for i, (name, ci, co, bn) in enumerate(self.downs):
-            d = self.ddesc[i]
-            m = max(m, ops.bn_workspace_bytes(d.N * d.Ho * d.Wo, co))
-        for u, d in enumerate(self.udesc):
-            m = max(m, ops.bn_workspace_bytes(d.N * d.Ho * d.Wo, d.Cout))
+        for d in self.ddesc + self.udesc:
+            m = max(m, ops.bn_workspace_bytes(self.N * d.Ho * d.Wo, d.Cout))
         return m
+
+    def _half(self, t, h):
+        return t[h * self.N:(h + 1) * self.N]
 
     # views ---------------------------------------------------------------
     def z_view(self, s, l):
@@ -276,8 +280,8 @@ class GeneratorPlan:
 
     # forward --------------------------------------------------------------
     def forward(self, x, out, slot=0, training=True, ws=None, drop_rate=DROP_RATE, drop_seed=0, step_dev=None):
-        """x [N,H,W,3] view; writes tanh output into `out` (any NHWC view)."""
-        s = self.slots[slot]
+        """x [halves*N,H,W,3] view; writes the tanh output into `out` (any NHWC view of that batch)."""
+        s = self.s
         s["x"], s["out"] = x, out
         A = self.arena
         h = x
@@ -297,27 +301,41 @@ class GeneratorPlan:
             d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws)
             z = s["cat"][u][..., :co]
             rate = drop_rate if (drop and training) else 0.0
-            self._bn_fwd(s, name, y, z, "relu", training, ws, rate, dropout_seed(drop_seed, u, slot), step_dev)
+            self._bn_fwd(s, name, y, z, "relu", training, ws, rate, lambda hv: dropout_seed(drop_seed, u, hv),
+                         step_dev)
             h = s["cat"][u]
         self.ldesc.fwd(h, A.param("last/kernel"), out, bias=A.param("last/bias"), act="tanh", ws=ws)
         return out
 
-    def _bn_fwd(self, s, name, y, z, act, training, ws, drop_rate=0.0, seed=0, step_dev=None):
+    def _bn_fwd(self, s, name, y, z, act, training, ws, drop_rate=0.0, seed_of=None, step_dev=None):
         A = self.arena
-        if training:
-            ops.bn_fwd_train(y, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), s["mean"][name], s["inv"][name],
-                             self.bn.mean[name], self.bn.var[name], z, act=act, alpha=ALPHA, momentum=BN_MOMENTUM,
-                             eps=BN_EPS, drop_rate=drop_rate, drop_seed=seed, step_dev=step_dev, ws=ws)
-        else:
-            ops.bn_fwd_infer(y, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.bn.mean[name],
-                             self.bn.var[name], z, act=act, alpha=ALPHA, eps=BN_EPS)
+        for hv in range(self.halves):
+            yh, zh = self._half(y, hv), self._half(z, hv)
+            if training:
+                ops.bn_fwd_train(yh, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), s["mean"][name][hv],
+                                 s["inv"][name][hv], self.bn.mean[name], self.bn.var[name], zh, act=act, alpha=ALPHA,
+                                 momentum=BN_MOMENTUM, eps=BN_EPS, drop_rate=drop_rate,
+                                 drop_seed=seed_of(hv) if seed_of else 0, step_dev=step_dev, ws=ws)
+            else:
+                ops.bn_fwd_infer(yh, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.bn.mean[name],
+                                 self.bn.var[name], zh, act=act, alpha=ALPHA, eps=BN_EPS)
+
+    def _bn_bwd(self, s, name, dz, z, y, dy, act, beta, ws, drop_rate=0.0):
+        """BN backward per half; the gamma/beta gradients of the halves accumulate."""
+        A = self.arena
+        for hv in range(self.halves):
+            ops.bn_bwd(self._half(dz, hv), self._half(z, hv), self._half(y, hv), A.param(f"{name}/gamma"),
+                       s["mean"][name][hv], s["inv"][name][hv], self._half(dy, hv), A.grad_of(f"{name}/gamma"),
+                       A.grad_of(f"{name}/beta"), act=act, alpha=ALPHA, drop_rate=drop_rate,
+                       beta=beta if hv == 0 else 1.0, ws=ws)
 
     # backward ---------------------------------------------------------------
     def backward(self, dout, slot=0, beta=0.0, ws=None, drop_rate=DROP_RATE, on_grads_ready=None):
-        """dout: grad of the tanh output (NHWC view).  Weight grads go to the
-        arena grad buffer: g = new + beta * g.  `on_grads_ready(name)` is
-        called after each layer's gradients are enqueued (bucketed all-reduce)."""
-        s = self.slots[slot]
+        """dout: grad of the tanh output over all halves (NHWC view).  Weight
+        grads go to the arena grad buffer: g = new + beta * g (summed over the
+        halves).  `on_grads_ready(name)` is called after each layer's
+        gradients are enqueued (bucketed all-reduce)."""
+        s = self.s
         A = self.arena
         dl = self.ldesc
         dpre = self._dy(dl, dl.Cout)
@@ -330,9 +348,8 @@ class GeneratorPlan:
             name, ci, co, drop = self.ups[u]
             d = self.udesc[u]
             dy = self._dy(d, co)
-            ops.bn_bwd(self.dcat[u][..., :co], s["cat"][u][..., :co], s["yu"][u], A.param(f"{name}/gamma"),
-                       s["mean"][name], s["inv"][name], dy, A.grad_of(f"{name}/gamma"), A.grad_of(f"{name}/beta"),
-                       act="relu", alpha=ALPHA, drop_rate=drop_rate if drop else 0.0, beta=beta, ws=ws)
+            self._bn_bwd(s, name, self.dcat[u][..., :co], s["cat"][u][..., :co], s["yu"][u], dy, "relu", beta, ws,
+                         drop_rate=drop_rate if drop else 0.0)
             hin = s["z8"] if u == 0 else s["cat"][u - 1]
             dhin = self.dz8 if u == 0 else self.dcat[u - 1]
             d.bwd_filter(hin, dy, A.grad_of(f"{name}/kernel"), beta=beta, ws=ws)
@@ -346,9 +363,7 @@ class GeneratorPlan:
             z = self.z_view(s, l)
             dy = self._dy(d, co)
             if bn:
-                ops.bn_bwd(dz, z, s["yd"][l], A.param(f"{name}/gamma"), s["mean"][name], s["inv"][name], dy,
-                           A.grad_of(f"{name}/gamma"), A.grad_of(f"{name}/beta"), act="lrelu", alpha=ALPHA,
-                           beta=beta, ws=ws)
+                self._bn_bwd(s, name, dz, z, s["yd"][l], dy, "lrelu", beta, ws)
             else:
                 ops.act_bwd(dz, z, dy, "lrelu", ALPHA)
             hin = s["x"] if l == 0 else self.z_view(s, l - 1)
@@ -386,99 +401,128 @@ def d_layout_order(width=1):
 # PatchGAN discriminator plan (pix2pix.py:194-220)
 # ---------------------------------------------------------------------------
 class DiscriminatorPlan:
-    """slot 0 = D([x, y]) (real), slot 1 = D([x, G(x)]) (fake); every slot owns
-    its 6-channel input buffer `inp[slot]`."""
+    """PatchGAN schedule.  halves=2 batches D([x, y]) (half 0, real) and
+    D([x, G(x)]) (half 1, fake) into one pass over 2N images: the convs run
+    once over both, BatchNorm per half (the reference's two separate calls);
+    the parameter backward of both passes is one backward over 2N rows (the
+    gradients of the two calls sum), and the input-gradient-only backward of
+    the fake half runs on N-image descriptors over views of the same
+    buffers.  `inp` is the [halves*N, H, W, 6] input buffer."""
 
-    def __init__(self, N, H, W, width, arena, bn_state, device, slots=2, train=True):
+    def __init__(self, N, H, W, width, arena, bn_state, device, halves=1, train=True):
         self.N, self.H, self.W = N, H, W
+        self.halves = halves
+        NT = N * halves
         self.arena, self.bn = arena, bn_state
         self.specs = d_layer_specs(width)
-        self.desc = []
-        h, w = H, W
-        for name, ci, co, _ in self.specs:
-            if name.startswith("down"):
-                d = ConvDesc(N, h, w, ci, co, 4, 2, "same")
-            else:  # ZeroPadding2D() + Conv2D(k4, s1, 'valid') == explicit pad 1
-                d = ConvDesc(N, h, w, ci, co, 4, 1, (1, 1, 1, 1))
-            self.desc.append(d)
-            h, w = d.Ho, d.Wo
+
+        def descs(n):
+            out = []
+            h, w = H, W
+            for name, ci, co, _ in self.specs:
+                if name.startswith("down"):
+                    d = ConvDesc(n, h, w, ci, co, 4, 2, "same")
+                else:  # ZeroPadding2D() + Conv2D(k4, s1, 'valid') == explicit pad 1
+                    d = ConvDesc(n, h, w, ci, co, 4, 1, (1, 1, 1, 1))
+                out.append(d)
+                h, w = d.Ho, d.Wo
+            return out
+
+        self.desc = descs(NT)
+        self.desc_half = descs(N) if (train and halves > 1) else self.desc
         self.out_shape = self.desc[-1].out_shape
-        self.slots = []
-        for _ in range(slots):
-            s = {"inp": _empty((N, H, W, self.specs[0][1]), device)}
-            s["y"] = [(_empty(d.out_shape, device) if sp[3] else None) for d, sp in zip(self.desc, self.specs)]
-            s["z"] = [_empty(d.out_shape, device) for d in self.desc[:-1]]
-            s["logits"] = _empty(self.out_shape, device)
-            s["mean"] = {sp[0]: _empty((sp[2],), device) for sp in self.specs if sp[3]}
-            s["inv"] = {sp[0]: _empty((sp[2],), device) for sp in self.specs if sp[3]}
-            self.slots.append(s)
+        self.inp = _empty((NT, H, W, self.specs[0][1]), device)
+        self.y = [(_empty(d.out_shape, device) if sp[3] else None) for d, sp in zip(self.desc, self.specs)]
+        self.z = [_empty(d.out_shape, device) for d in self.desc[:-1]]
+        self.logits = _empty(self.out_shape, device)
+        self.mean = {sp[0]: [_empty((sp[2],), device) for _ in range(halves)] for sp in self.specs if sp[3]}
+        self.inv = {sp[0]: [_empty((sp[2],), device) for _ in range(halves)] for sp in self.specs if sp[3]}
         if train:
             self.dz = [_empty(d.out_shape, device) for d in self.desc[:-1]]
             maxdy = max(d.N * d.Ho * d.Wo * d.Cout for d in self.desc)
             self.dy = _empty((maxdy,), device)
-            self.dinp = _empty((N, H, W, self.specs[0][1]), device)
-        self.ws_bytes = max([d.max_ws() for d in self.desc] +
-                            [ops.bn_workspace_bytes(d.N * d.Ho * d.Wo, d.Cout) for d in self.desc])
+        self.ws_bytes = max([d.max_ws() for d in self.desc + self.desc_half] +
+                            [ops.bn_workspace_bytes(N * d.Ho * d.Wo, d.Cout) for d in self.desc])
+
+    @property
+    def slots(self):
+        return [{"inp": self.inp, "logits": self.logits}]
+
+    def _half(self, t, h):
+        return t[h * self.N:(h + 1) * self.N]
 
     def _dy(self, d):
         return self.dy[: d.N * d.Ho * d.Wo * d.Cout].view(d.N, d.Ho, d.Wo, d.Cout)
 
     def forward(self, slot=0, training=True, ws=None):
-        s = self.slots[slot]
         A = self.arena
-        h = s["inp"]
+        h = self.inp
         for i, (name, ci, co, bn) in enumerate(self.specs):
             d = self.desc[i]
             if name == "last":
-                d.fwd(h, A.param("last/kernel"), s["logits"], bias=A.param("last/bias"), ws=ws)
-                return s["logits"]
-            z = s["z"][i]
+                d.fwd(h, A.param("last/kernel"), self.logits, bias=A.param("last/bias"), ws=ws)
+                return self.logits
+            z = self.z[i]
             if not bn:
                 d.fwd(h, A.param(f"{name}/kernel"), z, act="lrelu", alpha=ALPHA, ws=ws)
             else:
-                y = s["y"][i]
+                y = self.y[i]
                 d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws)
-                if training:
-                    ops.bn_fwd_train(y, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), s["mean"][name],
-                                     s["inv"][name], self.bn.mean[name], self.bn.var[name], z, act="lrelu",
-                                     alpha=ALPHA, momentum=BN_MOMENTUM, eps=BN_EPS, ws=ws)
-                else:
-                    ops.bn_fwd_infer(y, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.bn.mean[name],
-                                     self.bn.var[name], z, act="lrelu", alpha=ALPHA, eps=BN_EPS)
+                for hv in range(self.halves):
+                    yh, zh = self._half(y, hv), self._half(z, hv)
+                    if training:
+                        ops.bn_fwd_train(yh, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.mean[name][hv],
+                                         self.inv[name][hv], self.bn.mean[name], self.bn.var[name], zh, act="lrelu",
+                                         alpha=ALPHA, momentum=BN_MOMENTUM, eps=BN_EPS, ws=ws)
+                    else:
+                        ops.bn_fwd_infer(yh, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.bn.mean[name],
+                                         self.bn.var[name], zh, act="lrelu", alpha=ALPHA, eps=BN_EPS)
             h = z
 
     def backward(self, dlogits, slot=0, param_grads=True, beta=0.0, input_grad=None, input_beta=0.0, ws=None,
-                 on_grads_ready=None):
-        """Backward through D for one slot.  param_grads: accumulate weight grads
-        (g = new + beta*g); input_grad: NHWC view receiving dL/d(input) (+input_beta*old)."""
-        s = self.slots[slot]
+                 on_grads_ready=None, half=None):
+        """Backward through D.  half=None: over all halves (dlogits [halves*N]);
+        half=h: over that half only (dlogits [N]), e.g. the G-path gradient
+        through D(fake).  param_grads: accumulate weight grads (g = new +
+        beta*g, summed over the halves covered); input_grad: NHWC view
+        receiving dL/d(input) (+input_beta*old)."""
         A = self.arena
+        hs = range(self.halves) if half is None else [half]
+        desc = self.desc if half is None else self.desc_half
+
+        def sub(t):  # the rows of t this pass covers
+            return t if half is None else self._half(t, half)
+
         dh = dlogits
         n = len(self.specs)
         for i in range(n - 1, -1, -1):
             name, ci, co, bn = self.specs[i]
-            d = self.desc[i]
+            d = desc[i]
             if name == "last":
                 dy = dh
                 if param_grads:
-                    d.bwd_filter(s["z"][i - 1], dy, A.grad_of("last/kernel"), dbias=A.grad_of("last/bias"),
+                    d.bwd_filter(sub(self.z[i - 1]), dy, A.grad_of("last/kernel"), dbias=A.grad_of("last/bias"),
                                  beta=beta, ws=ws)
             else:
                 dy = self._dy(d)
                 if bn:
-                    ops.bn_bwd(dh, s["z"][i], s["y"][i], A.param(f"{name}/gamma"), s["mean"][name], s["inv"][name],
-                               dy, A.grad_of(f"{name}/gamma") if param_grads else None,
-                               A.grad_of(f"{name}/beta") if param_grads else None, act="lrelu", alpha=ALPHA,
-                               beta=beta, ws=ws)
+                    for k, hv in enumerate(hs):
+                        rows = slice(k * self.N, (k + 1) * self.N)
+                        ops.bn_bwd(dh[rows], self._half(self.z[i], hv), self._half(self.y[i], hv),
+                                   A.param(f"{name}/gamma"), self.mean[name][hv], self.inv[name][hv], dy[rows],
+                                   A.grad_of(f"{name}/gamma") if param_grads else None,
+                                   A.grad_of(f"{name}/beta") if param_grads else None, act="lrelu", alpha=ALPHA,
+                                   beta=beta if k == 0 else 1.0, ws=ws)
                 else:
-                    ops.act_bwd(dh, s["z"][i], dy, "lrelu", ALPHA)
+                    ops.act_bwd(dh, sub(self.z[i]), dy, "lrelu", ALPHA)
                 if param_grads:
-                    hin = s["inp"] if i == 0 else s["z"][i - 1]
+                    hin = sub(self.inp) if i == 0 else sub(self.z[i - 1])
                     d.bwd_filter(hin, dy, A.grad_of(f"{name}/kernel"), beta=beta, ws=ws)
             if param_grads and on_grads_ready:
                 on_grads_ready(name)
             if i > 0:
-                d.bwd_data(dy, A.param(f"{name}/kernel"), self.dz[i - 1], ws=ws)
-                dh = self.dz[i - 1]
+                dz = sub(self.dz[i - 1])
+                d.bwd_data(dy, A.param(f"{name}/kernel"), dz, ws=ws)
+                dh = dz
             elif input_grad is not None:
                 d.bwd_data(dy, A.param(f"{name}/kernel"), input_grad, beta=input_beta, ws=ws)

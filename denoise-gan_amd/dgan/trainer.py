@@ -25,6 +25,17 @@ class AdamConfig:
 
 
 class Pix2PixTrainer:
+    """One fused pix2pix step for x, y [N,H,W,3].
+
+    The two generator calls (G(x) and the identity pass G(y)) run as ONE
+    U-Net pass over 2N images, and the two discriminator calls (real, fake)
+    as one PatchGAN pass over 2N images; BatchNorm statistics, moving
+    averages and dropout stay per call (GeneratorPlan / DiscriminatorPlan
+    `halves`).  Backward: one G pass over both halves (their gradients sum,
+    as the reference's single gen_tape does over the two calls), one D pass
+    over both halves for the disc gradients, and the G-path gradient through
+    D(fake) on the fake half only."""
+
     def __init__(self, g_arena, g_bn, d_arena, d_bn, N, H, W, device, width=1, identity=True,
                  loss_weights=ops.LOSS_WEIGHTS_REF, drop_rate=DROP_RATE, drop_seed=0, g_opt=None, d_opt=None,
                  grad_sync=None, vgg=None):
@@ -36,13 +47,17 @@ class Pix2PixTrainer:
         self.g_opt = g_opt or AdamConfig()
         self.d_opt = d_opt or AdamConfig()
         self.grad_sync = grad_sync
-        self.G = GeneratorPlan(N, H, W, width, g_arena, g_bn, device, slots=2 if identity else 1, train=True)
-        self.D = DiscriminatorPlan(N, H, W, width, d_arena, d_bn, device, slots=2, train=True)
-        lshape = self.D.out_shape
+        gh = 2 if identity else 1
+        self.G = GeneratorPlan(N, H, W, width, g_arena, g_bn, device, halves=gh, train=True)
+        self.D = DiscriminatorPlan(N, H, W, width, d_arena, d_bn, device, halves=2, train=True)
+        lshape = (N,) + tuple(self.D.out_shape[1:])
         e = lambda shape: torch.empty(shape, dtype=torch.float32, device=device)
-        self.ident = e((N, H, W, 3)) if identity else None
-        self.dident = e((N, H, W, 3)) if identity else None
-        self.dzr, self.dzf_d, self.dzf_g = e(lshape), e(lshape), e(lshape)
+        self.gin = e((gh * N, H, W, 3)) if identity else None   # [x; y]
+        self.gout = e((gh * N, H, W, 3))                        # [G(x); G(y)]
+        self.dgout = e((gh * N, H, W, 3))                       # [dL/dG(x); dL/dG(y)]
+        self.dlog = e(self.D.out_shape)                         # [dzr_d; dzf_d]
+        self.dzf_g = e(lshape)
+        self.dinp = e((N, H, W, 6))                             # dL/d D([x, G(x)]) of the G path
         self.loss = torch.zeros(8, dtype=torch.float32, device=device)
         # VGG19 content loss (pix2pix.py:45-51, :87): frozen feature extractor on G(x) and y
         self.content = None
@@ -57,8 +72,8 @@ class Pix2PixTrainer:
 
     @property
     def gen_output(self):
-        """G(x) of the last step: a view into the fake half of D's input."""
-        return self.D.slots[1]["inp"][..., 3:]
+        """G(x) of the last step."""
+        return self.gout[:self.N]
 
     def step(self, x, y, apply=True):
         """x, y: device NHWC [N,H,W,3] fp32 in [-1, 1].  Returns the 8 losses (device, no sync)."""
@@ -66,41 +81,46 @@ class Pix2PixTrainer:
         y = y if y.is_contiguous() else y.contiguous()
         ws = self.ws
         G, D = self.G, self.D
-        real_in, fake_in = D.slots[0]["inp"], D.slots[1]["inp"]
-        gen = fake_in[..., 3:]
+        N = self.N
+        inp = D.inp
+        real_in, fake_in = inp[:N], inp[N:]
         step_dev = self.gA.iterations
         # ---- forward (pix2pix.py:44-48 and the identity pass :90) -----------
         ops.channel_concat(x, y, real_in)                 # concatenate([inp, tar]) (pix2pix.py:200)
         ops.strided_copy(x, fake_in[..., :3])
-        G.forward(x, gen, slot=0, ws=ws, drop_rate=self.drop_rate, drop_seed=self.drop_seed, step_dev=step_dev)
         if self.identity:
-            G.forward(y, self.ident, slot=1, ws=ws, drop_rate=self.drop_rate, drop_seed=self.drop_seed,
-                      step_dev=step_dev)
-        zr = D.forward(slot=0, ws=ws)
-        zf = D.forward(slot=1, ws=ws)
+            ops.strided_copy(x, self.gin[:N])
+            ops.strided_copy(y, self.gin[N:])
+            gin = self.gin
+        else:
+            gin = x
+        G.forward(gin, self.gout, ws=ws, drop_rate=self.drop_rate, drop_seed=self.drop_seed, step_dev=step_dev)
+        gen = self.gout[:N]
+        ident = self.gout[N:] if self.identity else None
+        ops.strided_copy(gen, fake_in[..., 3:])
+        logits = D.forward(ws=ws)
+        zr, zf = logits[:N], logits[N:]
         content = None
         if self.content is not None:
             # content_loss(target, gen) = MSE(vgg(pre(y))/12.75, vgg(pre(G(x)))/12.75) (pix2pix.py:45-51)
             content = self.content.forward(gen, y, grad_weight=self.weights[5], ws=ws)
         # ---- losses + their gradients (pix2pix.py:74-103) ----------------
-        dinp = D.dinp
-        ops.fill(dinp, 0.0)
-        ops.p2p_loss(gen, y, zr, zf, self.loss, ident=self.ident, weights=self.weights, content=content,
-                     dgen=dinp[..., 3:], dident=self.dident, dlogit_real_d=self.dzr, dlogit_fake_d=self.dzf_d,
-                     dlogit_fake_g=self.dzf_g, ws=ws)
+        dgen = self.dgout[:N]
+        ops.p2p_loss(gen, y, zr, zf, self.loss, ident=ident, weights=self.weights, content=content,
+                     dgen=dgen, dident=self.dgout[N:] if self.identity else None, dlogit_real_d=self.dlog[:N],
+                     dlogit_fake_d=self.dlog[N:], dlogit_fake_g=self.dzf_g, ws=ws)
         sync = self.grad_sync
-        # ---- disc_tape.gradient (train_pix2pix.py:65) ---------------------
-        D.backward(self.dzr, slot=0, param_grads=True, beta=0.0, ws=ws)
-        D.backward(self.dzf_d, slot=1, param_grads=True, beta=1.0, ws=ws)
+        # ---- disc_tape.gradient (train_pix2pix.py:65): both D calls in one pass
+        D.backward(self.dlog, param_grads=True, beta=0.0, ws=ws)
         if sync:
             sync.start("D")
-        # ---- gen_tape.gradient (train_pix2pix.py:64): through D(fake) into G
-        D.backward(self.dzf_g, slot=1, param_grads=False, input_grad=dinp, input_beta=1.0, ws=ws)
+        # ---- gen_tape.gradient (train_pix2pix.py:64): through D(fake) into G(x)
+        D.backward(self.dzf_g, half=1, param_grads=False, input_grad=self.dinp, input_beta=0.0, ws=ws)
+        ops.accumulate(self.dinp[..., 3:], dgen, 1.0)
         if self.content is not None:
-            self.content.backward(dinp[..., 3:], beta=1.0, ws=ws)
-        if self.identity:
-            G.backward(self.dident, slot=1, beta=0.0, ws=ws, drop_rate=self.drop_rate)
-        G.backward(dinp[..., 3:], slot=0, beta=1.0 if self.identity else 0.0, ws=ws, drop_rate=self.drop_rate,
+            self.content.backward(dgen, beta=1.0, ws=ws)
+        # both generator calls (G(x), G(y)) in one backward: their gradients sum
+        G.backward(self.dgout, beta=0.0, ws=ws, drop_rate=self.drop_rate,
                    on_grads_ready=(sync.ready_G if sync else None))
         if sync:
             sync.finish()

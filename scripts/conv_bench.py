@@ -36,6 +36,16 @@ LAYERS = [
     ("D.down3", 64, 64, 128, 256, 4, 2, "same", False, (2, 3, 2)),
     ("D.conv", 32, 32, 256, 512, 4, 1, (1, 1, 1, 1), False, (2, 3, 2)),
     ("D.last", 31, 31, 512, 1, 4, 1, (1, 1, 1, 1), False, (2, 3, 2)),
+    # VGG19 to block5_conv4 on 256x256 (content loss: fwd on G(x) and y, bwd_data on G(x))
+    ("V.b1c1", 256, 256, 3, 64, 3, 1, "same", False, (2, 1, 0)),
+    ("V.b1c2", 256, 256, 64, 64, 3, 1, "same", False, (2, 1, 0)),
+    ("V.b2c1", 128, 128, 64, 128, 3, 1, "same", False, (2, 1, 0)),
+    ("V.b2c2", 128, 128, 128, 128, 3, 1, "same", False, (2, 1, 0)),
+    ("V.b3c1", 64, 64, 128, 256, 3, 1, "same", False, (2, 1, 0)),
+    ("V.b3cx", 64, 64, 256, 256, 3, 1, "same", False, (6, 3, 0)),
+    ("V.b4c1", 32, 32, 256, 512, 3, 1, "same", False, (2, 1, 0)),
+    ("V.b4cx", 32, 32, 512, 512, 3, 1, "same", False, (6, 3, 0)),
+    ("V.b5cx", 16, 16, 512, 512, 3, 1, "same", False, (8, 4, 0)),
 ]
 
 
