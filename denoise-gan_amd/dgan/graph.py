@@ -222,9 +222,13 @@ class GraphPlan:
 
     slots: independent activation sets (e.g. D(real) and D(fake), or VGG on
     G(x) and on the target) whose backwards run after all forwards.
-    param_grads: False for frozen networks (VGG19) -- only input gradients."""
+    param_grads: False for frozen networks (VGG19) -- only input gradients.
+    alias: a plan of the same graph over a larger batch whose slot-0
+    activations this plan's slot 0 views (its first N images): e.g. a
+    backward over one half of a batched forward."""
 
-    def __init__(self, graph, N, H, W, arena, bn_state, device, slots=1, train=True, param_grads=True):
+    def __init__(self, graph, N, H, W, arena, bn_state, device, slots=1, train=True, param_grads=True,
+                 alias=None):
         self.g = graph
         self.arena, self.bn = arena, bn_state
         self.device = device
@@ -299,8 +303,11 @@ class GraphPlan:
                 self.premask.add(n.out.id)
         # ---- activation buffers per slot ----
         self.slots = []
-        for _ in range(slots):
-            self.slots.append(self._alloc_set(nodes, shp))
+        for k in range(slots):
+            if alias is not None and k == 0:
+                self.slots.append({tid: t[:N] for tid, t in alias.slots[0].items() if tid != graph.input.id})
+            else:
+                self.slots.append(self._alloc_set(nodes, shp))
         self.saved = []
         for _ in range(slots):
             s = {}
@@ -578,11 +585,11 @@ class GraphNetwork:
         print_fn(f"Total params: {self.count_params():,d}")
         print_fn(f"Trainable params: {self.arena.count if self.trainable else 0:,d}")
 
-    def plan(self, N, H, W, slots=1, train=False, param_grads=True):
-        key = (N, H, W, slots, train, param_grads)
+    def plan(self, N, H, W, slots=1, train=False, param_grads=True, alias=None):
+        key = (N, H, W, slots, train, param_grads, id(alias) if alias is not None else None)
         if key not in self._plans:
             self._plans[key] = GraphPlan(self.graph, N, H, W, self.arena, self.bn, self.device, slots=slots,
-                                         train=train, param_grads=param_grads)
+                                         train=train, param_grads=param_grads, alias=alias)
         return self._plans[key]
 
     def __call__(self, x, training=False):

@@ -64,30 +64,38 @@ class VGGNetwork(GraphNetwork):
 class ContentLoss:
     """VGG19 content loss of one (gen, target) shape: value into a device
     scalar and, when requested, its gradient w.r.t. gen accumulated into a
-    caller buffer (srgan.py:70-76, pix2pix.py:45-51)."""
+    caller buffer (srgan.py:70-76, pix2pix.py:45-51).
+
+    The two VGG19 calls (on G(x) and on the target) run as ONE forward over
+    2N images (twice the GEMM rows per conv); the backward runs over the G(x)
+    half only, on an N-image plan whose activations are views of the first
+    half of the batched forward's buffers."""
 
     def __init__(self, vgg, N, H, W, device, train=True):
         self.vgg = vgg
-        self.plan = vgg.plan(N, H, W, slots=2, train=train, param_grads=False)
+        self.N = N
+        self.fplan = vgg.plan(2 * N, H, W, slots=1, train=False, param_grads=False)
+        self.bplan = vgg.plan(N, H, W, slots=1, train=True, param_grads=False, alias=self.fplan) if train else None
         e = lambda s: torch.empty(s, dtype=torch.float32, device=device)
-        self.pre = [e((N, H, W, 3)), e((N, H, W, 3))]
+        self.pre = e((2 * N, H, W, 3))                    # [pre(gen); pre(target)]
         self.dpre = e((N, H, W, 3)) if train else None
-        self.dfeat = e(self.plan.out_shape) if train else None
+        self.dfeat = e((N,) + tuple(self.fplan.out_shape[1:])) if train else None
         self.value = torch.zeros(1, dtype=torch.float32, device=device)
-        self.ws_bytes = max(self.plan.ws_bytes, ops.mse_workspace_bytes())
+        self.ws_bytes = max(self.fplan.ws_bytes, self.bplan.ws_bytes if train else 0, ops.mse_workspace_bytes())
 
     def forward(self, gen, tgt, grad_weight=1.0, ws=None):
-        ops.vgg_preprocess_fwd(gen, self.pre[0])
-        ops.vgg_preprocess_fwd(tgt, self.pre[1])
-        fg = self.plan.forward(self.pre[0], slot=0, training=False, ws=ws)
-        ft = self.plan.forward(self.pre[1], slot=1, training=False, ws=ws)
+        N = self.N
+        ops.vgg_preprocess_fwd(gen, self.pre[:N])
+        ops.vgg_preprocess_fwd(tgt, self.pre[N:])
+        f = self.fplan.forward(self.pre, slot=0, training=False, ws=ws)
         # MeanSquaredError()(target_features, gen_features): grad w.r.t. gen features
-        ops.mse(fg, ft, self.value, scale=FEAT_SCALE, da=self.dfeat, grad_weight=grad_weight, ws=ws)
+        ops.mse(f[:N], f[N:], self.value, scale=FEAT_SCALE, da=self.dfeat, grad_weight=grad_weight, ws=ws)
         return self.value
 
     def backward(self, dgen, beta=1.0, ws=None):
         """dgen += d content / d gen (through VGG and preprocess_input)."""
-        self.plan.backward(self.dfeat, slot=0, input_grad=self.dpre, input_beta=0.0, ws=ws, params=False)
+        self.bplan.slots[0][self.vgg.graph.input.id] = self.pre[:self.N]
+        self.bplan.backward(self.dfeat, slot=0, input_grad=self.dpre, input_beta=0.0, ws=ws, params=False)
         ops.vgg_preprocess_bwd(self.dpre, dgen, beta=beta)
 
 
