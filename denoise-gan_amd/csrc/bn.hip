@@ -23,6 +23,9 @@ struct BnPlan {
 };
 
 static BnPlan bn_plan(long M, int C) {
+    // row chunks of >= 64 rows, at most 256 (measured: more, shorter chunks
+    // slow the partial passes down); the finalize kernels spread a channel's
+    // R partials over 32 lanes
     (void)C;
     BnPlan p;
     long r = std::min<long>(256, std::max<long>(1, (M + 63) / 64));
@@ -119,39 +122,45 @@ k_bn_stats_partial(const float *__restrict__ y, int ld, long M, int C, long rows
     }
 }
 
-// finalize: block = 16 channels x 16 lanes; two parallel passes over the R chunk
-// partials (Chan's combine as sums: mean = sum n_i mean_i / n, M2 = sum M2_i + n_i (mean_i - mean)^2)
+// finalize: block = 8 channels x 32 lanes; two parallel passes over the R chunk
+// partials (Chan's combine as sums: mean = sum n_i mean_i / n, M2 = sum M2_i + n_i (mean_i - mean)^2);
+// the 32 lane sums of a channel are combined in a fixed order (deterministic)
+constexpr int FIN_C = 8, FIN_L = 32;
+
+__device__ __forceinline__ float lane_sum32(float v, float *sh, int cl, int ln) {
+    sh[ln * FIN_C + cl] = v;
+    __syncthreads();
+    float s = 0.f;
+    for (int l = 0; l < FIN_L; ++l) s += sh[l * FIN_C + cl];
+    __syncthreads();
+    return s;
+}
+
 __global__ void __launch_bounds__(256)
 k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, int C, const float *gamma,
                  const float *beta, float *save_mean, float *save_invstd, float *mm, float *mv, float momentum,
                  float eps, float *scale, float *shift) {
-    __shared__ float s0[256], s1[256];
-    const int cl = threadIdx.x & 15, ln = threadIdx.x >> 4;
-    const int c = blockIdx.x * 16 + cl;
+    __shared__ float sh[256];
+    const int cl = threadIdx.x % FIN_C, ln = threadIdx.x / FIN_C;
+    const int c = blockIdx.x * FIN_C + cl;
     float sn = 0.f, sm = 0.f;
     if (c < C)
-        for (int r = ln; r < R; r += 16) {
+        for (int r = ln; r < R; r += FIN_L) {
             const float n = pn[(long)r * C + c];
             sn += n;
             sm += n * pmean[(long)r * C + c];
         }
-    s0[threadIdx.x] = sn; s1[threadIdx.x] = sm;
-    __syncthreads();
-    float n = 0.f, msum = 0.f;
-    for (int l = 0; l < 16; ++l) { n += s0[cl + 16 * l]; msum += s1[cl + 16 * l]; }
+    const float n = lane_sum32(sn, sh, cl, ln);
+    const float msum = lane_sum32(sm, sh, cl, ln);
     const float mu = n > 0.f ? msum / n : 0.f;
-    __syncthreads();
     float q = 0.f;
     if (c < C)
-        for (int r = ln; r < R; r += 16) {
+        for (int r = ln; r < R; r += FIN_L) {
             const float d = pmean[(long)r * C + c] - mu;
             q += pm2[(long)r * C + c] + pn[(long)r * C + c] * d * d;
         }
-    s0[threadIdx.x] = q;
-    __syncthreads();
+    const float m2 = lane_sum32(q, sh, cl, ln);
     if (ln != 0 || c >= C) return;
-    float m2 = 0.f;
-    for (int l = 0; l < 16; ++l) m2 += s0[cl + 16 * l];
     const float var = n > 0.f ? m2 / n : 0.f;
     const float inv = 1.f / sqrtf(var + eps);
     if (save_mean) save_mean[c] = mu;
@@ -261,17 +270,15 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
 __global__ void __launch_bounds__(256)
 k_bn_bwd_final(const float *p1, const float *p2, int R, int C, long M, const float *gamma, const float *mean,
                const float *invstd, float *dgamma, float *dbeta, float beta, float *coef) {
-    __shared__ float s0[256], s1[256];
-    const int cl = threadIdx.x & 15, ln = threadIdx.x >> 4;
-    const int c = blockIdx.x * 16 + cl;
+    __shared__ float sh[256];
+    const int cl = threadIdx.x % FIN_C, ln = threadIdx.x / FIN_C;
+    const int c = blockIdx.x * FIN_C + cl;
     float a1 = 0.f, a2 = 0.f;
     if (c < C)
-        for (int r = ln; r < R; r += 16) { a1 += p1[(long)r * C + c]; a2 += p2[(long)r * C + c]; }
-    s0[threadIdx.x] = a1; s1[threadIdx.x] = a2;
-    __syncthreads();
+        for (int r = ln; r < R; r += FIN_L) { a1 += p1[(long)r * C + c]; a2 += p2[(long)r * C + c]; }
+    a1 = lane_sum32(a1, sh, cl, ln);
+    a2 = lane_sum32(a2, sh, cl, ln);
     if (ln != 0 || c >= C) return;
-    a1 = 0.f; a2 = 0.f;
-    for (int l = 0; l < 16; ++l) { a1 += s0[cl + 16 * l]; a2 += s1[cl + 16 * l]; }
     if (dbeta) dbeta[c] = a1 + (beta != 0.f ? beta * dbeta[c] : 0.f);
     if (dgamma) dgamma[c] = a2 + (beta != 0.f ? beta * dgamma[c] : 0.f);
     // dy = k1 (dbn - m1 - xhat m2), xhat = (y - mean) invstd  ==>  dy = A dbn + B (y - mean) + D
@@ -372,7 +379,7 @@ int dg_bn_fwd_train(int M, int C, const float *y, int ldy, const float *gamma, c
                            pg.cpb, pn, pmean, pm2);
     }
     DG_LAUNCHED("bn_stats_partial");
-    hipLaunchKernelGGL(dg::k_bn_stats_final, dim3(dg_cdiv(C, 16)), dim3(256), 0, s, pn, pmean, pm2, bp.R, C, gamma,
+    hipLaunchKernelGGL(dg::k_bn_stats_final, dim3(dg_cdiv(C, dg::FIN_C)), dim3(256), 0, s, pn, pmean, pm2, bp.R, C, gamma,
                        beta, save_mean, save_invstd, moving_mean, moving_var, momentum, eps, scale, shift);
     DG_LAUNCHED("bn_stats_final");
     if (dg::vec4_ok(C, {{y, ldy}, {z, ldz}}))
@@ -423,7 +430,7 @@ int dg_bn_bwd(int M, int C, const float *dz, int lddz, const float *z, int ldz, 
                            (long)M, C, bp.rows, pg.cpb, save_mean, save_invstd, act, alpha, dscale, p1, p2);
     }
     DG_LAUNCHED("bn_bwd_partial");
-    hipLaunchKernelGGL(dg::k_bn_bwd_final, dim3(dg_cdiv(C, 16)), dim3(256), 0, s, p1, p2, bp.R, C, (long)M, gamma,
+    hipLaunchKernelGGL(dg::k_bn_bwd_final, dim3(dg_cdiv(C, dg::FIN_C)), dim3(256), 0, s, p1, p2, bp.R, C, (long)M, gamma,
                        save_mean, save_invstd, dgamma, dbeta, beta, coef);
     DG_LAUNCHED("bn_bwd_final");
     if (dg::vec4_ok(C, {{dz, lddz}, {z, ldz}, {y, ldy}, {dy, lddy}}))

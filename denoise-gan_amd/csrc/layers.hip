@@ -439,11 +439,25 @@ __global__ void __launch_bounds__(256) k_mse_partial(long npix, int C, const flo
     if (threadIdx.x == 0) part[blockIdx.x] = r;
 }
 
-__global__ void k_mse_final(const float *part, int nb, float inv_n, float *out) {
-    if (threadIdx.x != 0) return;
-    float s = 0.f;
-    for (int i = 0; i < nb; ++i) s += part[i];
-    out[0] = s * inv_n;
+// fixed-order block sum over 256 threads (tree in LDS): deterministic
+__device__ __forceinline__ float tree_sum256(float v, float *sh) {
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+        __syncthreads();
+    }
+    const float r = sh[0];
+    __syncthreads();
+    return r;
+}
+
+__global__ void __launch_bounds__(256) k_mse_final(const float *part, int nb, float inv_n, float *out) {
+    __shared__ float sh[256];
+    float v = 0.f;
+    for (int i = threadIdx.x; i < nb; i += 256) v += part[i];
+    const float s = tree_sum256(v, sh);
+    if (threadIdx.x == 0) out[0] = s * inv_n;
 }
 
 // --------------------------------------------------------------------------
@@ -529,15 +543,17 @@ __global__ void __launch_bounds__(256) k_ganloss_logits(const GanLossArgs a) {
     r = block_sum256(f1, red); if (threadIdx.x == 0) a.part_log[blockIdx.x * 3 + 2] = r;
 }
 
-__global__ void k_ganloss_final(const GanLossArgs a) {
+__global__ void __launch_bounds__(256) k_ganloss_final(const GanLossArgs a) {
+    __shared__ float sh[256];
+    float v[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int b = threadIdx.x; b < GL_IMG_BLOCKS; b += 256)
+        for (int q = 0; q < 3; ++q) v[q] += a.part_img[b * 3 + q];
+    for (int b = threadIdx.x; b < GL_LOG_BLOCKS; b += 256)
+        for (int q = 0; q < 3; ++q) v[3 + q] += a.part_log[b * 3 + q];
+    float t[6];
+    for (int q = 0; q < 6; ++q) t[q] = tree_sum256(v[q], sh);
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    float l1 = 0.f, l2 = 0.f, tv = 0.f, r1 = 0.f, f0 = 0.f, f1 = 0.f;
-    for (int b = 0; b < GL_IMG_BLOCKS; ++b) {
-        l1 += a.part_img[b * 3 + 0]; l2 += a.part_img[b * 3 + 1]; tv += a.part_img[b * 3 + 2];
-    }
-    for (int b = 0; b < GL_LOG_BLOCKS; ++b) {
-        r1 += a.part_log[b * 3 + 0]; f0 += a.part_log[b * 3 + 1]; f1 += a.part_log[b * 3 + 2];
-    }
+    const float l1 = t[0], l2 = t[1], tv = t[2], r1 = t[3], f0 = t[4], f1 = t[5];
     const float n = (float)((long)a.B * a.H * a.W * a.C);
     const float nl = (float)a.nlog;
     const float adv = a.w_adv * (f1 / nl);
@@ -774,7 +790,7 @@ int dg_mse(int64_t npix, int C, const float *a, int lda, const float *b, int ldb
     hipLaunchKernelGGL(dg::k_mse_partial, dim3(dg::MSE_BLOCKS), dim3(256), 0, s, (long)npix, C, a, lda, b, ldb, scale,
                        grad_weight, inv_n, da, ldda, (float *)ws);
     DG_LAUNCHED("mse_partial");
-    hipLaunchKernelGGL(dg::k_mse_final, dim3(1), dim3(64), 0, s, (const float *)ws, dg::MSE_BLOCKS, inv_n, out);
+    hipLaunchKernelGGL(dg::k_mse_final, dim3(1), dim3(256), 0, s, (const float *)ws, dg::MSE_BLOCKS, inv_n, out);
     DG_LAUNCHED("mse_final");
     return DG_OK;
 }
@@ -811,7 +827,7 @@ int dg_gan_loss(int B, int H, int W, int C, const float *gen, int ldgen, const f
     DG_LAUNCHED("gan_loss_img");
     hipLaunchKernelGGL(dg::k_ganloss_logits, dim3(dg::GL_LOG_BLOCKS), dim3(256), 0, s, a);
     DG_LAUNCHED("gan_loss_logits");
-    hipLaunchKernelGGL(dg::k_ganloss_final, dim3(1), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(dg::k_ganloss_final, dim3(1), dim3(256), 0, s, a);
     DG_LAUNCHED("gan_loss_final");
     return DG_OK;
 }

@@ -121,14 +121,30 @@ __global__ void __launch_bounds__(256) k_loss_logits(const LossArgs a) {
     r = block_sum(s_f1, red); if (threadIdx.x == 0) a.part_log[blockIdx.x * 3 + 2] = r;
 }
 
-__global__ void k_loss_final(const LossArgs a, int nimg_blocks, int nlog_blocks) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    float l1 = 0.f, l2 = 0.f, tv = 0.f, id = 0.f, r1 = 0.f, f0 = 0.f, f1 = 0.f;
-    for (int b = 0; b < nimg_blocks; ++b) {
-        l1 += a.part_img[b * 4 + 0]; l2 += a.part_img[b * 4 + 1];
-        tv += a.part_img[b * 4 + 2]; id += a.part_img[b * 4 + 3];
+// fixed-order block sum over 256 threads (tree in LDS): deterministic
+__device__ __forceinline__ float tree_sum256(float v, float *sh) {
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+        __syncthreads();
     }
-    for (int b = 0; b < nlog_blocks; ++b) { r1 += a.part_log[b * 3 + 0]; f0 += a.part_log[b * 3 + 1]; f1 += a.part_log[b * 3 + 2]; }
+    const float r = sh[0];
+    __syncthreads();
+    return r;
+}
+
+__global__ void __launch_bounds__(256) k_loss_final(const LossArgs a, int nimg_blocks, int nlog_blocks) {
+    __shared__ float sh[256];
+    float v[7] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int b = threadIdx.x; b < nimg_blocks; b += 256)
+        for (int q = 0; q < 4; ++q) v[q] += a.part_img[b * 4 + q];
+    for (int b = threadIdx.x; b < nlog_blocks; b += 256)
+        for (int q = 0; q < 3; ++q) v[4 + q] += a.part_log[b * 3 + q];
+    float t[7];
+    for (int q = 0; q < 7; ++q) t[q] = tree_sum256(v[q], sh);
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const float l1 = t[0], l2 = t[1], tv = t[2], id = t[3], r1 = t[4], f0 = t[5], f1 = t[6];
     const float n = (float)((long)a.B * a.H * a.W * a.C);
     const float nl = (float)a.nlog;
     const float gan = a.w_gan * f1 / nl;
@@ -187,7 +203,7 @@ int dg_p2p_loss(int B, int H, int W, int C, const float *gen, int ldgen, const f
     DG_LAUNCHED("loss_img");
     hipLaunchKernelGGL(dg::k_loss_logits, dim3(dg::LOSS_LOGIT_BLOCKS), dim3(256), 0, s, a);
     DG_LAUNCHED("loss_logits");
-    hipLaunchKernelGGL(dg::k_loss_final, dim3(1), dim3(64), 0, s, a, dg::LOSS_IMG_BLOCKS, dg::LOSS_LOGIT_BLOCKS);
+    hipLaunchKernelGGL(dg::k_loss_final, dim3(1), dim3(256), 0, s, a, dg::LOSS_IMG_BLOCKS, dg::LOSS_LOGIT_BLOCKS);
     DG_LAUNCHED("loss_final");
     return DG_OK;
 }
