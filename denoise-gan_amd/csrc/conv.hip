@@ -749,7 +749,6 @@ constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 static const TileCfg kX6Cfgs[] = {
     {128, 128, 2, 2, 16, 2, 2, 1.00}, {128, 64, 2, 2, 16, 2, 2, 1.15}, {64, 128, 2, 2, 16, 2, 2, 1.15},
     {64, 64, 2, 2, 16, 3, 4, 1.40},   {256, 128, 4, 2, 16, 2, 1, 1.00}, {128, 256, 2, 4, 16, 2, 1, 1.00},
-    {256, 64, 4, 1, 16, 2, 1, 1.00},  {64, 256, 1, 4, 16, 2, 1, 1.00},
 };
 constexpr int kNumX6Cfgs = sizeof(kX6Cfgs) / sizeof(kX6Cfgs[0]);
 
@@ -894,7 +893,8 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         x6_ok = g.Ci % 16 == 0 && g.Co % 16 == 0;
         ra = (long)g.N * g.H * g.W; ca = g.Ci; rb = (long)g.N * g.Ho * g.Wo; cb = g.Co;
     }
-    x6_ok = x6_ok && math == DG_MATH_BF16X6 && 6.0 * ra * ca < 2.0e9 && 6.0 * rb * cb < 2.0e9;
+    // (the bf16x6 kernel keeps a per-row bitmask of valid taps: at most 32 taps)
+    x6_ok = x6_ok && math == DG_MATH_BF16X6 && 6.0 * ra * ca < 2.0e9 && 6.0 * rb * cb < 2.0e9 && g.kh * g.kw <= 32;
     if (x6_ok) {
         OpPlan p6 = pl;
         double t6 = choose_tiles(p6, kX6Cfgs, kNumX6Cfgs, 2516.6e12 / 6.0, "DG_FORCE_X6CFG", nullptr);

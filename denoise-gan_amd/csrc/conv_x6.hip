@@ -139,6 +139,14 @@ k_split3(const float *__restrict__ src, int ld, long rows, int C, unsigned short
     }
 }
 
+// wait until at most N of this wave's DMAs are in flight (compile-time N: no
+// runtime switch in the K-tile body)
+template <int N>
+__device__ __forceinline__ void wait_dma_c() {
+    static_assert(N >= 0 && N <= 63, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // The GEMM.  A and B of GemmArgs point at the operands' packed bf16 planes
 // (k_split3 output); lda / ldb are their column counts C (rows are 3C
 // elements), a_bytes / b_bytes their extents.
@@ -235,11 +243,17 @@ k_conv_gemm_x6(const GemmArgs p) {
         bsl[j].live = d < B_SL;
     }
     // DMA instructions this wave issues per K-tile (wave-uniform)
+    // when every wave owns the same number of slots (A_SL, B_SL multiples of
+    // NW) liveness and the DMA count are compile-time, which keeps the K-tile
+    // body branch-free so the scheduler can interleave its DMA / LDS / VALU
+    // work with the MFMAs
+    constexpr bool A_ALL = (A_SL % NW) == 0, B_ALL = (B_SL % NW) == 0;
     int nmine = 0;
 #pragma unroll
-    for (int j = 0; j < A_NJ; ++j) nmine += asl[j].live;
+    for (int j = 0; j < A_NJ; ++j) nmine += (A_ALL || asl[j].live);
 #pragma unroll
-    for (int j = 0; j < B_NJ; ++j) nmine += bsl[j].live;
+    for (int j = 0; j < B_NJ; ++j) nmine += (B_ALL || bsl[j].live);
+    if constexpr (A_ALL && B_ALL) nmine = A_NJ + B_NJ;
 
     // A geometry per slot.  KC (FWD / DGRAD): the output pixel of row r.
     // WGRAD (RC): the (tap, ci) of columns c..c+7 and their packed offset.
@@ -282,8 +296,58 @@ k_conv_gemm_x6(const GemmArgs p) {
         int kk = kbeg / BK; wk_chunk = kk / (TA * TB); int t = kk - wk_chunk * TA * TB;
         wk_a = t / TB; wk_b = t - wk_a * TB;
     }
-    auto walk_next = [&]() {
-        if (++wk_b == TB) { wk_b = 0; if (++wk_a == TA) { wk_a = 0; ++wk_chunk; } }
+    // FWD / DGRAD: per-slot byte offsets at tap (0, 0) of chunk 0 plus a
+    // bitmask of the taps whose source pixel lies inside the image, so the
+    // K-tile issue is one add of a wave-uniform delta and one mask test per
+    // slot (no per-tile index multiplies).
+    int abase[A_NJ], amask[A_NJ], bbase[B_NJ];
+    bool bok[B_NJ];
+    if constexpr (MODE != MODE_WGRAD) {
+#pragma unroll
+        for (int j = 0; j < A_NJ; ++j) {
+            abase[j] = 0; amask[j] = 0;
+            if (arow_n[j] < 0) continue;
+            if constexpr (MODE == MODE_FWD) {
+                abase[j] = (((arow_n[j] * g.H + arow_h[j]) * g.W + arow_w[j]) * (3 * p.lda) + 16 * asl[j].plane +
+                            8 * asl[j].c) * 2;
+                for (int a = 0; a < TA; ++a)
+                    for (int b = 0; b < TB; ++b) {
+                        const int hi = arow_h[j] + a, wi = arow_w[j] + b;
+                        if ((unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W) amask[j] |= 1 << (a * TB + b);
+                    }
+            } else {
+                abase[j] = (((arow_n[j] * g.Ho + arow_h[j]) * g.Wo + arow_w[j]) * (3 * p.lda) + 16 * asl[j].plane +
+                            8 * asl[j].c) * 2;
+                for (int a = 0; a < TA; ++a)
+                    for (int b = 0; b < TB; ++b) {
+                        const int i = ph.i0h + a * g.sh, jj = ph.i0w + b * g.sw;
+                        const int ho = arow_h[j] - a, wo = arow_w[j] - b;
+                        if (i < g.kh && jj < g.kw && (unsigned)ho < (unsigned)g.Ho && (unsigned)wo < (unsigned)g.Wo)
+                            amask[j] |= 1 << (a * TB + b);
+                    }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < B_NJ; ++j) {
+            if constexpr (MODE == MODE_FWD) {  // RC weights: k-row r, columns c..c+7
+                const int col = n0 + bsl[j].c;
+                bok[j] = col < p.N;
+                bbase[j] = (bsl[j].r * (3 * p.ldb) + (col >> 4) * 48 + 16 * bsl[j].plane + (col & 8)) * 2;
+            } else {                           // KC weights: row ci
+                const int ci = n0 + bsl[j].r;
+                bok[j] = ci < p.N;
+                bbase[j] = (ci * (3 * p.ldb) + 16 * bsl[j].plane + 8 * bsl[j].c) * 2;
+            }
+        }
+    }
+    auto walk_next = [&]() {  // branch-free (selects)
+        const int nb = wk_b + 1;
+        const bool wb = nb == TB;
+        const int na = wk_a + (wb ? 1 : 0);
+        const bool wa = na == TA;
+        wk_b = wb ? 0 : nb;
+        wk_a = wa ? 0 : na;
+        wk_chunk += wa ? 1 : 0;
     };
 
     const rsrc_t rA = make_rsrc((const float *)p.A, p.a_bytes);
@@ -299,24 +363,31 @@ k_conv_gemm_x6(const GemmArgs p) {
     auto issue_tile = [&](int k0, char *sm) {
         char *As = sm;
         char *Bs = As + 3 * APL;
+        // wave-uniform parts of this K-tile's offsets (tap (wk_a, wk_b) of chunk wk_chunk)
+        int a_delta = 0, b_delta = 0, tap_bit = 0;
+        bool b_tap_ok = true;
+        if constexpr (MODE == MODE_FWD) {
+            a_delta = ((wk_a * g.W + wk_b) * (3 * p.lda) + wk_chunk * 48) * 2;
+            b_delta = (((wk_a * g.kw + wk_b) * g.Ci + wk_chunk * BK) * (3 * p.ldb)) * 2;
+            tap_bit = wk_a * TB + wk_b;
+        } else if constexpr (MODE == MODE_DGRAD) {
+            a_delta = (wk_chunk * 48 - (wk_a * g.Wo + wk_b) * (3 * p.lda)) * 2;
+            const int i = ph.i0h + wk_a * g.sh, jj = ph.i0w + wk_b * g.sw;
+            b_tap_ok = i < g.kh && jj < g.kw;
+            b_delta = ((b_tap_ok ? (i * g.kw + jj) * g.Ci * (3 * p.ldb) : 0) + wk_chunk * 48) * 2;
+            tap_bit = wk_a * TB + wk_b;
+        }
+        (void)a_delta; (void)b_delta; (void)tap_bit; (void)b_tap_ok;
 #pragma unroll
         for (int j = 0; j < A_NJ; ++j) {
-            if (!asl[j].live) continue;
+            if constexpr (!A_ALL) { if (!asl[j].live) continue; }
             const int d = wid + NW * j, per = BM / 32;
             char *dst = As + asl[j].plane * APL + (d - asl[j].plane * per) * 1024;
             unsigned off;
             bool ok;
-            if constexpr (MODE == MODE_FWD) {
-                const int hi = arow_h[j] + wk_a, wi = arow_w[j] + wk_b;
-                ok = arow_n[j] >= 0 && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
-                off = ((unsigned)((arow_n[j] * g.H + hi) * g.W + wi) * (3 * p.lda) + wk_chunk * 48 +
-                       16 * asl[j].plane + 8 * asl[j].c) * 2u;
-            } else if constexpr (MODE == MODE_DGRAD) {
-                const int i = ph.i0h + wk_a * g.sh, jj = ph.i0w + wk_b * g.sw;
-                const int ho = arow_h[j] - wk_a, wo = arow_w[j] - wk_b;
-                ok = i < g.kh && jj < g.kw && arow_n[j] >= 0 && (unsigned)ho < (unsigned)g.Ho && (unsigned)wo < (unsigned)g.Wo;
-                off = ((unsigned)((arow_n[j] * g.Ho + ho) * g.Wo + wo) * (3 * p.lda) + wk_chunk * 48 +
-                       16 * asl[j].plane + 8 * asl[j].c) * 2u;
+            if constexpr (MODE != MODE_WGRAD) {
+                ok = (amask[j] >> tap_bit) & 1;
+                off = (unsigned)(abase[j] + a_delta);
             } else {
                 const unsigned pix = (unsigned)(k0 + asl[j].r);
                 const unsigned t = fdiv(pix, p.mg_wo, p.sh_wo); const int wo = (int)(pix - t * g.Wo);
@@ -329,22 +400,17 @@ k_conv_gemm_x6(const GemmArgs p) {
         }
 #pragma unroll
         for (int j = 0; j < B_NJ; ++j) {
-            if (!bsl[j].live) continue;
+            if constexpr (!B_ALL) { if (!bsl[j].live) continue; }
             const int d = wid + NW * j, per = BN / 32;
             char *dst = Bs + bsl[j].plane * BPL + (d - bsl[j].plane * per) * 1024;
             unsigned off;
             bool ok;
             if constexpr (MODE == MODE_FWD) {  // w[k][co], k = (tap, ci); RC: k-row r, columns c..c+7
-                const int col = n0 + bsl[j].c;
-                const unsigned k = (unsigned)((wk_a * g.kw + wk_b) * g.Ci + wk_chunk * BK + bsl[j].r);
-                ok = col < p.N;
-                off = (k * (3 * p.ldb) + (col >> 4) * 48 + 16 * bsl[j].plane + (col & 8)) * 2u;
+                ok = bok[j];
+                off = (unsigned)(bbase[j] + b_delta);
             } else if constexpr (MODE == MODE_DGRAD) {  // w[i,j,ci,co]: KC rows ci
-                const int i = ph.i0h + wk_a * g.sh, jj = ph.i0w + wk_b * g.sw;
-                const int ci = n0 + bsl[j].r;
-                ok = i < g.kh && jj < g.kw && ci < p.N;
-                off = ((unsigned)((i * g.kw + jj) * g.Ci + ci) * (3 * p.ldb) + wk_chunk * 48 + 16 * bsl[j].plane +
-                       8 * bsl[j].c) * 2u;
+                ok = bok[j] && b_tap_ok;
+                off = (unsigned)(bbase[j] + b_delta);
             } else {  // WGRAD: dy rows (pixels) contiguous along co
                 const int col = n0 + bsl[j].c;
                 const int pix = k0 + bsl[j].r;
@@ -447,7 +513,8 @@ k_conv_gemm_x6(const GemmArgs p) {
 #pragma unroll
             for (int b = 0; b < TN; ++b)
                 acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahl[a], b3[b], acc[a][b], 0, 0, 0);
-        wait_dma(nmine);
+        if constexpr (A_ALL && B_ALL) wait_dma_c<A_NJ + B_NJ>();
+        else wait_dma(nmine);
         barrier();
     };
     issue_tile(kbeg, smem0);
@@ -491,8 +558,6 @@ void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t
         DG_X6(3, 64, 64, 2, 2, 3)
         DG_X6(4, 256, 128, 4, 2, 2)
         DG_X6(5, 128, 256, 2, 4, 2)
-        DG_X6(6, 256, 64, 4, 1, 2)
-        DG_X6(7, 64, 256, 1, 4, 2)
     }
 #undef DG_X6
 }

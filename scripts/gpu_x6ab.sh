@@ -1,7 +1,8 @@
 set -o pipefail
 mkdir -p gpurun_out
-L=${L:-"G.down2,G.down4,G.up4,G.up6,G.up7,D.down2,D.conv"}
-for c in ${CFGS:-0 4 5}; do
-  DG_LAYERS=$L DG_FORCE_X6CFG=$c timeout -k 10 300 python scripts/conv_bench.py > gpurun_out/x6ab_$c.log 2>&1 || exit 2
-done
-echo rc=0
+export TMPDIR=/tmp
+export DG_REPS=5
+timeout -k 10 300 python scripts/conv_bench.py > gpurun_out/cfg_new.log 2>&1 && \
+timeout -k 10 900 python -u -m pytest tests/test_conv_gpu.py tests/test_step_gpu.py -q -m gpu -x --timeout 300 --timeout-method thread > gpurun_out/t.log 2>&1 && \
+timeout -k 10 600 python bench.py --steps 30 --warmup 8 --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err
+echo rc=$?
