@@ -150,9 +150,10 @@ __device__ __forceinline__ void wait_dma_c() {
 // The GEMM.  A and B of GemmArgs point at the operands' packed bf16 planes
 // (k_split3 output); lda / ldb are their column counts C (rows are 3C
 // elements), a_bytes / b_bytes their extents.
-template <int MODE, int BM, int BN, int WGM, int WGN, int MINW>
+template <int MODE, int BM, int BN, int WGM, int WGN, int MINW, int NBUF = 3>
 __global__ void __launch_bounds__(64 * WGM * WGN, MINW)
 k_conv_gemm_x6(const GemmArgs p) {
+    static_assert(NBUF == 3 || NBUF == 4, "3 or 4 LDS buffers (2 or 3 K-tiles in flight)");
     constexpr int BK = 16;
     constexpr bool A_KC = (MODE != MODE_WGRAD);
     constexpr bool B_KC = (MODE == MODE_DGRAD);
@@ -175,6 +176,7 @@ k_conv_gemm_x6(const GemmArgs p) {
     __shared__ __attribute__((aligned(16))) char smem0[BUF];
     __shared__ __attribute__((aligned(16))) char smem1[BUF];
     __shared__ __attribute__((aligned(16))) char smem2[BUF];
+    __shared__ __attribute__((aligned(16))) char smem3[NBUF == 4 ? BUF : 16];
 
     const ConvGeom &g = p.g;
     const int tid = threadIdx.x;
@@ -488,16 +490,17 @@ k_conv_gemm_x6(const GemmArgs p) {
         }
     };
 
-    // Three LDS buffers, two K-tiles in flight: iteration kt reads the
-    // fragments of tile kt, issues the DMA of tile kt+2 into the buffer tile
-    // kt-1 used (every wave passed the barrier after reading it), runs the
-    // MFMAs of tile kt, then waits until only tile kt+2's DMAs are outstanding
-    // and crosses the barrier.  DMAs past nk fetch harmless data into the
-    // idle buffer.
-    auto ktile = [&](int kt, const char *cur, char *nxt2) {
+    // NBUF LDS buffers, AHEAD = NBUF-1 K-tiles in flight: iteration kt reads
+    // the fragments of tile kt, issues the DMA of tile kt+AHEAD into the
+    // buffer tile kt-1 used (every wave passed the barrier after reading it),
+    // runs the MFMAs of tile kt, then waits until only the DMAs of tiles
+    // kt+2 .. kt+AHEAD are outstanding and crosses the barrier.  DMAs past nk
+    // fetch harmless data into idle buffers.
+    constexpr int AHEAD = NBUF - 1;
+    auto ktile = [&](int kt, const char *cur, char *nxt) {
         bf16x8 ahm[TM], ahl[TM], b1[TN], b2[TN], b3[TN];
         read_frags(cur, ahm, ahl, b1, b2, b3);
-        issue_tile(kbeg + (kt + 2) * BK, nxt2);
+        issue_tile(kbeg + (kt + AHEAD) * BK, nxt);
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -513,22 +516,35 @@ k_conv_gemm_x6(const GemmArgs p) {
 #pragma unroll
             for (int b = 0; b < TN; ++b)
                 acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahl[a], b3[b], acc[a][b], 0, 0, 0);
-        if constexpr (A_ALL && B_ALL) wait_dma_c<A_NJ + B_NJ>();
-        else wait_dma(nmine);
+        if constexpr (A_ALL && B_ALL) wait_dma_c<(AHEAD - 1) * (A_NJ + B_NJ)>();
+        else wait_dma((AHEAD - 1) * nmine);
         barrier();
     };
     issue_tile(kbeg, smem0);
     issue_tile(kbeg + BK, smem1);
-    wait_dma(nmine);
+    if constexpr (NBUF == 4) issue_tile(kbeg + 2 * BK, smem2);
+    wait_dma((AHEAD - 1) * nmine);
     barrier();
     int kt = 0;
-    for (; kt + 2 < nk; kt += 3) {
-        ktile(kt, smem0, smem2);
-        ktile(kt + 1, smem1, smem0);
-        ktile(kt + 2, smem2, smem1);
+    if constexpr (NBUF == 3) {
+        for (; kt + 2 < nk; kt += 3) {
+            ktile(kt, smem0, smem2);
+            ktile(kt + 1, smem1, smem0);
+            ktile(kt + 2, smem2, smem1);
+        }
+        if (kt < nk) ktile(kt, smem0, smem2);
+        if (kt + 1 < nk) ktile(kt + 1, smem1, smem0);
+    } else {
+        for (; kt + 3 < nk; kt += 4) {
+            ktile(kt, smem0, smem3);
+            ktile(kt + 1, smem1, smem0);
+            ktile(kt + 2, smem2, smem1);
+            ktile(kt + 3, smem3, smem2);
+        }
+        if (kt < nk) ktile(kt, smem0, smem3);
+        if (kt + 1 < nk) ktile(kt + 1, smem1, smem0);
+        if (kt + 2 < nk) ktile(kt + 2, smem2, smem1);
     }
-    if (kt < nk) ktile(kt, smem0, smem2);
-    if (kt + 1 < nk) ktile(kt + 1, smem1, smem0);
     wait_dma(0);
 
     conv_epilogue16<MODE, TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, Mrows, ph, phase, split, lane);
@@ -543,21 +559,21 @@ void launch_split3(const float *src, int ld, long rows, int C, unsigned short *d
 
 // tile configs of the bf16x6 kernel (index = kX6Cfgs in conv.hip)
 void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s) {
-#define DG_X6(C, BM_, BN_, WM_, WN_, MW_)                                                                       \
+#define DG_X6(C, BM_, BN_, WM_, WN_, MW_, NB_)                                                                  \
     case C: {                                                                                                   \
         const dim3 blk(64 * WM_ * WN_);                                                                         \
-        if (mode == MODE_FWD) hipLaunchKernelGGL((k_conv_gemm_x6<MODE_FWD, BM_, BN_, WM_, WN_, MW_>), grid, blk, 0, s, a); \
-        else if (mode == MODE_DGRAD) hipLaunchKernelGGL((k_conv_gemm_x6<MODE_DGRAD, BM_, BN_, WM_, WN_, MW_>), grid, blk, 0, s, a); \
-        else hipLaunchKernelGGL((k_conv_gemm_x6<MODE_WGRAD, BM_, BN_, WM_, WN_, MW_>), grid, blk, 0, s, a); \
+        if (mode == MODE_FWD) hipLaunchKernelGGL((k_conv_gemm_x6<MODE_FWD, BM_, BN_, WM_, WN_, MW_, NB_>), grid, blk, 0, s, a); \
+        else if (mode == MODE_DGRAD) hipLaunchKernelGGL((k_conv_gemm_x6<MODE_DGRAD, BM_, BN_, WM_, WN_, MW_, NB_>), grid, blk, 0, s, a); \
+        else hipLaunchKernelGGL((k_conv_gemm_x6<MODE_WGRAD, BM_, BN_, WM_, WN_, MW_, NB_>), grid, blk, 0, s, a); \
         break;                                                                                                  \
     }
     switch (cfg) {
-        DG_X6(0, 128, 128, 2, 2, 2)
-        DG_X6(1, 128, 64, 2, 2, 2)
-        DG_X6(2, 64, 128, 2, 2, 2)
-        DG_X6(3, 64, 64, 2, 2, 3)
-        DG_X6(4, 256, 128, 4, 2, 2)
-        DG_X6(5, 128, 256, 2, 4, 2)
+        DG_X6(0, 128, 128, 2, 2, 2, 3)
+        DG_X6(1, 128, 64, 2, 2, 2, 3)
+        DG_X6(2, 64, 128, 2, 2, 2, 3)
+        DG_X6(3, 64, 64, 2, 2, 3, 3)
+        DG_X6(4, 256, 128, 4, 2, 2, 3)
+        DG_X6(5, 128, 256, 2, 4, 2, 3)
     }
 #undef DG_X6
 }
