@@ -1027,7 +1027,14 @@ static GemmArgs make_args(const ConvGeom &g, const OpPlan &pl, const float *A, i
     return a;
 }
 
-static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a, hipStream_t s);
+// caller-held bf16x6 planes of the two engine operands (dg_conv_planes_t mapped
+// onto A / B of one op): NULL = split into the workspace; ready = already split
+struct PlaneRefs {
+    void *a, *b;
+    int a_ready, b_ready;
+};
+
+static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a, hipStream_t s, const PlaneRefs *pr = nullptr);
 static int finish_splitk(int mode, const OpPlan &pl, const GemmArgs &a, hipStream_t s);
 
 // narrow op through its recast (1x1 MFMA GEMM + gather)
@@ -1075,7 +1082,7 @@ static int run_recast(const dg_conv_desc_s *d, int op, const GemmArgs &a0, char 
 static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, const float *B, int ldb,
                       float *C, int ldc, const float *bias, float beta, int act, float alpha,
                       void *ws, size_t ws_bytes, hipStream_t s, const float *mz = nullptr, int ldmz = 0,
-                      int mact = DG_ACT_NONE, float malpha = 0.f) {
+                      int mact = DG_ACT_NONE, float malpha = 0.f, const PlaneRefs *pr = nullptr) {
     const int mode = engine_mode(d, op);
     const OpPlan &pl = d->plan[op];
     const size_t need = d->rc[op].on ? d->rc[op].bytes : pl.gemm_bytes;
@@ -1107,10 +1114,10 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
         }
         return DG_OK;
     }
-    return run_gemm(mode, pl, a, s);
+    return run_gemm(mode, pl, a, s, pr);
 }
 
-static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_t s) {
+static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_t s, const PlaneRefs *pr) {
     GemmArgs a = a_in;
     const float *A = a.A, *B = a.B;
     const int lda = a.lda, ldb = a.ldb;
@@ -1141,10 +1148,16 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
         unsigned short *pb = (unsigned short *)(ws + pl.x6_b_off);
         const long pas = pl.x6_ra * pl.x6_ca, pbs = pl.x6_rb * pl.x6_cb;
         const int ldbw = (mode == MODE_DGRAD) ? a.g.Co : ldb;  // DGRAD B is the dense weight tensor
-        launch_split3(A, lda, pl.x6_ra, pl.x6_ca, pa, s);
-        DG_LAUNCHED("split3_a");
-        launch_split3(B, ldbw, pl.x6_rb, pl.x6_cb, pb, s);
-        DG_LAUNCHED("split3_b");
+        if (pr && pr->a) pa = (unsigned short *)pr->a;
+        if (pr && pr->b) pb = (unsigned short *)pr->b;
+        if (!(pr && pr->a && pr->a_ready)) {
+            launch_split3(A, lda, pl.x6_ra, pl.x6_ca, pa, s);
+            DG_LAUNCHED("split3_a");
+        }
+        if (!(pr && pr->b && pr->b_ready)) {
+            launch_split3(B, ldbw, pl.x6_rb, pl.x6_cb, pb, s);
+            DG_LAUNCHED("split3_b");
+        }
         a.A = (const float *)pa; a.lda = pl.x6_ca; a.a_bytes = (unsigned)(3 * pas * 2);
         fastdiv_magic((unsigned)a.g.Wo, a.mg_wo, a.sh_wo);
         fastdiv_magic((unsigned)a.g.Ho, a.mg_ho, a.sh_ho);
@@ -1205,6 +1218,44 @@ static int run_colsum(const float *dy, int ld, long M, int C, float *out, float 
     DG_LAUNCHED("colsum_partial");
     hipLaunchKernelGGL(k_colsum_final, dim3(dg_cdiv(C, 256)), dim3(256), 0, s, ws, nblk, C, out, beta);
     DG_LAUNCHED("colsum_final");
+    return DG_OK;
+}
+
+// layer tensors (DG_TENSOR_*) read as engine operands A and B by op
+static void op_tensors(const dg_conv_desc_s *d, int op, int &ta, int &tb) {
+    if (op == DG_OP_FWD) { ta = DG_TENSOR_X; tb = DG_TENSOR_W; }
+    else if (op == DG_OP_BWD_DATA) { ta = DG_TENSOR_DY; tb = DG_TENSOR_W; }
+    else if (!d->transpose) { ta = DG_TENSOR_X; tb = DG_TENSOR_DY; }
+    else { ta = DG_TENSOR_DY; tb = DG_TENSOR_X; }  // conv view of a transposed layer: A = its output grad
+}
+
+static size_t tensor_plane_bytes(const dg_conv_desc_s *d, int t) {
+    if (t == DG_TENSOR_X) return (size_t)6 * d->N * d->H * d->W * d->Cin;
+    if (t == DG_TENSOR_DY) return (size_t)6 * d->N * d->Ho * d->Wo * d->Cout;
+    return (size_t)6 * d->g.kh * d->g.kw * d->Cin * d->Cout;
+}
+
+// tensors op reads as bf16x6 planes (0 for fp32 / narrow / recast plans)
+static int op_plane_mask(const dg_conv_desc_s *d, int op) {
+    const OpPlan &pl = d->plan[op];
+    if (!pl.x6 || pl.narrow || d->rc[op].on || pl.M == 0 || pl.N == 0) return 0;
+    int ta, tb;
+    op_tensors(d, op, ta, tb);
+    return ta | tb;
+}
+
+// dg_conv_planes_t -> the op's PlaneRefs (out = nullptr when the op takes no planes)
+static int plane_refs(const dg_conv_desc_s *d, int op, const dg_conv_planes_t *p, PlaneRefs &r,
+                      const PlaneRefs *&out) {
+    out = nullptr;
+    if (!p || !op_plane_mask(d, op)) return DG_OK;
+    int ta, tb;
+    op_tensors(d, op, ta, tb);
+    auto buf = [&](int t) -> void * { return t == DG_TENSOR_X ? p->x : (t == DG_TENSOR_DY ? p->dy : p->w); };
+    r.a = buf(ta); r.b = buf(tb);
+    r.a_ready = (p->ready & ta) != 0; r.b_ready = (p->ready & tb) != 0;
+    DG_ARG(((((uintptr_t)r.a) | ((uintptr_t)r.b)) & 15) == 0, "plane buffers must be 16-byte aligned");
+    out = &r;
     return DG_OK;
 }
 
@@ -1287,47 +1338,90 @@ int dg_conv_workspace_size(dg_conv_t d, int op, size_t *bytes) {
     return DG_OK;
 }
 
-int dg_conv_fwd(dg_conv_t d, const float *x, int ldx, const float *w, const float *bias, float *y, int ldy,
-                float beta, int act, float alpha, void *ws, size_t ws_bytes, dg_stream_t stream) {
+int dg_conv_planes_size(dg_conv_t d, int tensor, size_t *bytes) {
+    DG_ARG(d && bytes, "NULL argument");
+    DG_ARG(tensor == DG_TENSOR_X || tensor == DG_TENSOR_DY || tensor == DG_TENSOR_W, "bad tensor id %d", tensor);
+    *bytes = dg::tensor_plane_bytes(d, tensor);
+    return DG_OK;
+}
+
+int dg_conv_op_planes(dg_conv_t d, int op, int *tensors) {
+    DG_ARG(d && tensors, "NULL argument");
+    DG_ARG(op >= 0 && op < 3, "bad op %d", op);
+    *tensors = dg::op_plane_mask(d, op);
+    return DG_OK;
+}
+
+int dg_conv_fwd_pl(dg_conv_t d, const float *x, int ldx, const float *w, const float *bias, float *y, int ldy,
+                   float beta, int act, float alpha, const dg_conv_planes_t *planes, void *ws, size_t ws_bytes,
+                   dg_stream_t stream) {
     DG_ARG(d && x && w && y, "NULL tensor");
     DG_ARG(ldx >= d->Cin && ldy >= d->Cout, "pixel stride smaller than channels");
+    dg::PlaneRefs r{};
+    const dg::PlaneRefs *pr;
+    int e = dg::plane_refs(d, DG_OP_FWD, planes, r, pr);
+    if (e != DG_OK) return e;
     return dg::run_engine(d, DG_OP_FWD, x, ldx, w, d->transpose ? 0 : d->Cout, y, ldy, bias, beta, act, alpha, ws,
-                          ws_bytes, (hipStream_t)stream);
+                          ws_bytes, (hipStream_t)stream, nullptr, 0, DG_ACT_NONE, 0.f, pr);
+}
+
+int dg_conv_fwd(dg_conv_t d, const float *x, int ldx, const float *w, const float *bias, float *y, int ldy,
+                float beta, int act, float alpha, void *ws, size_t ws_bytes, dg_stream_t stream) {
+    return dg_conv_fwd_pl(d, x, ldx, w, bias, y, ldy, beta, act, alpha, nullptr, ws, ws_bytes, stream);
+}
+
+int dg_conv_bwd_data_pl(dg_conv_t d, const float *dy, int lddy, const float *w, float *dx, int lddx, float beta,
+                        const float *z, int ldz, int act, float alpha, const dg_conv_planes_t *planes, void *ws,
+                        size_t ws_bytes, dg_stream_t stream) {
+    DG_ARG(d && dy && w && dx, "NULL tensor");
+    DG_ARG(lddy >= d->Cout && lddx >= d->Cin, "pixel stride smaller than channels");
+    DG_ARG(!z || ldz >= d->Cin, "pixel stride smaller than channels");
+    DG_ARG(act >= DG_ACT_NONE && act <= DG_ACT_SIGMOID, "unknown activation %d", act);
+    dg::PlaneRefs r{};
+    const dg::PlaneRefs *pr;
+    int e = dg::plane_refs(d, DG_OP_BWD_DATA, planes, r, pr);
+    if (e != DG_OK) return e;
+    return dg::run_engine(d, DG_OP_BWD_DATA, dy, lddy, w, d->transpose ? d->g.Co : 0, dx, lddx, nullptr, beta,
+                          DG_ACT_NONE, 0.f, ws, ws_bytes, (hipStream_t)stream, z, z ? ldz : 0,
+                          z ? act : DG_ACT_NONE, alpha, pr);
 }
 
 int dg_conv_bwd_data(dg_conv_t d, const float *dy, int lddy, const float *w, float *dx, int lddx, float beta,
                      void *ws, size_t ws_bytes, dg_stream_t stream) {
-    DG_ARG(d && dy && w && dx, "NULL tensor");
-    DG_ARG(lddy >= d->Cout && lddx >= d->Cin, "pixel stride smaller than channels");
-    return dg::run_engine(d, DG_OP_BWD_DATA, dy, lddy, w, d->transpose ? d->g.Co : 0, dx, lddx, nullptr, beta,
-                          DG_ACT_NONE, 0.f, ws, ws_bytes, (hipStream_t)stream);
+    return dg_conv_bwd_data_pl(d, dy, lddy, w, dx, lddx, beta, nullptr, 0, DG_ACT_NONE, 0.f, nullptr, ws, ws_bytes,
+                               stream);
 }
 
 int dg_conv_bwd_data_masked(dg_conv_t d, const float *dy, int lddy, const float *w, float *dx, int lddx,
                             float beta, const float *z, int ldz, int act, float alpha, void *ws, size_t ws_bytes,
                             dg_stream_t stream) {
-    DG_ARG(d && dy && w && dx && z, "NULL tensor");
-    DG_ARG(lddy >= d->Cout && lddx >= d->Cin && ldz >= d->Cin, "pixel stride smaller than channels");
-    DG_ARG(act >= DG_ACT_NONE && act <= DG_ACT_SIGMOID, "unknown activation %d", act);
-    return dg::run_engine(d, DG_OP_BWD_DATA, dy, lddy, w, d->transpose ? d->g.Co : 0, dx, lddx, nullptr, beta,
-                          DG_ACT_NONE, 0.f, ws, ws_bytes, (hipStream_t)stream, z, ldz, act, alpha);
+    DG_ARG(z, "NULL tensor");
+    return dg_conv_bwd_data_pl(d, dy, lddy, w, dx, lddx, beta, z, ldz, act, alpha, nullptr, ws, ws_bytes, stream);
 }
 
 int dg_conv_bwd_filter(dg_conv_t d, const float *x, int ldx, const float *dy, int lddy, float *dw, float *dbias,
                        float beta, void *ws, size_t ws_bytes, dg_stream_t stream) {
+    return dg_conv_bwd_filter_pl(d, x, ldx, dy, lddy, dw, dbias, beta, nullptr, ws, ws_bytes, stream);
+}
+
+int dg_conv_bwd_filter_pl(dg_conv_t d, const float *x, int ldx, const float *dy, int lddy, float *dw, float *dbias,
+                          float beta, const dg_conv_planes_t *planes, void *ws, size_t ws_bytes, dg_stream_t stream) {
     DG_ARG(d && x && dy && dw, "NULL tensor");
     DG_ARG(ldx >= d->Cin && lddy >= d->Cout, "pixel stride smaller than channels");
     const dg::OpPlan &pl = d->plan[DG_OP_BWD_FILTER];
     DG_ARG(ws_bytes >= pl.ws_bytes && ws != nullptr, "workspace too small: need %zu bytes", pl.ws_bytes);
     size_t slab_bytes = pl.colsum_off;
-    int rc;
+    dg::PlaneRefs r{};
+    const dg::PlaneRefs *pr;
+    int rc = dg::plane_refs(d, DG_OP_BWD_FILTER, planes, r, pr);
+    if (rc != DG_OK) return rc;
     // conv view: A = conv input, B = conv output grad
     if (!d->transpose)
         rc = dg::run_engine(d, DG_OP_BWD_FILTER, x, ldx, dy, lddy, dw, d->g.Co, nullptr, beta, DG_ACT_NONE, 0.f, ws,
-                            slab_bytes, (hipStream_t)stream);
+                            slab_bytes, (hipStream_t)stream, nullptr, 0, DG_ACT_NONE, 0.f, pr);
     else
         rc = dg::run_engine(d, DG_OP_BWD_FILTER, dy, lddy, x, ldx, dw, d->g.Co, nullptr, beta, DG_ACT_NONE, 0.f, ws,
-                            slab_bytes, (hipStream_t)stream);
+                            slab_bytes, (hipStream_t)stream, nullptr, 0, DG_ACT_NONE, 0.f, pr);
     if (rc != DG_OK) return rc;
     if (dbias) {
         long M = (long)d->N * d->Ho * d->Wo;

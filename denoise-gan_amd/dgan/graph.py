@@ -325,6 +325,35 @@ class GraphPlan:
                     s0 = shp[n.out.id]
                     mx = max(mx, int(np.prod(s0[:3])) * _ld(s0[3]))
             self.scratch = torch.empty(max(mx, 4), dtype=torch.float32, device=device)
+        # ---- bf16x6 operand planes shared between the ops of a conv ----
+        # w: one buffer per conv of the NETWORK (arena.wplanes), shared by all
+        # its plans (e.g. the VGG19 forward over 2N images and the backward over
+        # N); x: per slot, split by fwd and kept for bwd_filter (trainable plans
+        # that own their activations); dy: one scratch per plan.
+        wplanes = getattr(arena, "wplanes", None)
+        if wplanes is None:
+            wplanes = arena.wplanes = {}
+        conv_nodes = [n for n in nodes[1:] if n.kind == "conv"]
+        descs = [self.desc[n.idx] for n in conv_nodes]
+        keep_x = train and param_grads and alias is None
+        self.cplanes = []
+        for k in range(slots):
+            wb = []
+            for n, d in zip(conv_nodes, descs):
+                if (d.plane_mask[0] | d.plane_mask[1]) & ops.TENSOR_W:
+                    if n.name not in wplanes:
+                        wplanes[n.name] = ops.PlaneBuf(d.plane_bytes(ops.TENSOR_W), device)
+                    wb.append(wplanes[n.name])
+                else:
+                    wb.append(None)
+            ps = ops.plan_planes(descs, device, keep_x=keep_x, wbufs=wb)
+            if not train:
+                for p in ps:
+                    p.dy = None
+            if k > 0 and train:
+                for p, p0 in zip(ps, self.cplanes[0].values()):
+                    p.dy = p0.dy   # one dy scratch per plan
+            self.cplanes.append({n.idx: p for n, p in zip(conv_nodes, ps)})
         # ---- workspace ----
         ws = [0]
         for n in nodes[1:]:
@@ -395,8 +424,10 @@ class GraphPlan:
             if k == "conv":
                 d = self.desc[n.idx]
                 bias = A.param(f"{n.name}/bias") if n.attrs["bias"] else None
+                P = self.cplanes[slot][n.idx]
+                P.invalidate(ops.TENSOR_X | ops.TENSOR_W)
                 d.fwd(xin, A.param(f"{n.name}/kernel"), y, bias=bias, act=n.attrs["act"],
-                      alpha=n.attrs["alpha"], ws=ws)
+                      alpha=n.attrs["alpha"], ws=ws, planes=P)
             elif k == "bn":
                 mean, inv = self.saved[slot][n.name]
                 if training:
@@ -478,16 +509,20 @@ class GraphPlan:
                     ops.act_bwd(dz, s[n.out.id], dy, act, n.attrs["alpha"])
                 else:
                     dy = dz   # (already multiplied by act'(z) by the consumer when premasked)
+                P = self.cplanes[slot][n.idx]
+                P.invalidate(ops.TENSOR_DY)
                 if pg:
                     db = A.grad_of(f"{n.name}/bias") if n.attrs["bias"] else None
-                    d.bwd_filter(s[t_in.id], dy, A.grad_of(f"{n.name}/kernel"), dbias=db, beta=param_beta, ws=ws)
+                    d.bwd_filter(s[t_in.id], dy, A.grad_of(f"{n.name}/kernel"), dbias=db, beta=param_beta, ws=ws,
+                                 planes=P)
                 if need(t_in):
                     if t_in.id in self.premask:
                         pa = t_in.node.attrs
                         d.bwd_data_masked(dy, A.param(f"{n.name}/kernel"), gr[t_in.id], s[t_in.id], pa["act"],
-                                          pa["alpha"], beta=beta_of(n, t_in), ws=ws)
+                                          pa["alpha"], beta=beta_of(n, t_in), ws=ws, planes=P)
                     else:
-                        d.bwd_data(dy, A.param(f"{n.name}/kernel"), gr[t_in.id], beta=beta_of(n, t_in), ws=ws)
+                        d.bwd_data(dy, A.param(f"{n.name}/kernel"), gr[t_in.id], beta=beta_of(n, t_in), ws=ws,
+                                   planes=P)
             elif k == "bn":
                 mean, inv = self.saved[slot][n.name]
                 b = beta_of(n, t_in)

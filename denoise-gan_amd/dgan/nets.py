@@ -245,6 +245,10 @@ class GeneratorPlan:
             self.dz8 = torch.empty_like(s["z8"])
             maxdy = max([d.N * d.Ho * d.Wo * d.Cout for d in self.ddesc + self.udesc + [self.ldesc]])
             self.dy = _empty((maxdy,), device)
+        # bf16x6 operand planes shared by the ops of each layer (x: fwd ->
+        # bwd_filter, w: fwd -> bwd_data, dy: bwd_filter -> bwd_data)
+        descs = self.ddesc + self.udesc + [self.ldesc]
+        self.planes = ops.plan_planes(descs, device) if train else [None] * len(descs)
         self.ws_bytes = max([d.max_ws() for d in self.ddesc + self.udesc + [self.ldesc]] + [self._bn_ws_max()])
 
     @property
@@ -284,28 +288,42 @@ class GeneratorPlan:
         s = self.s
         s["x"], s["out"] = x, out
         A = self.arena
+        P = self._fwd_planes()
         h = x
         for l, (name, ci, co, bn) in enumerate(self.downs):
             d = self.ddesc[l]
             z = self.z_view(s, l)
             if not bn:
-                d.fwd(h, A.param(f"{name}/kernel"), z, act="lrelu", alpha=ALPHA, ws=ws)
+                d.fwd(h, A.param(f"{name}/kernel"), z, act="lrelu", alpha=ALPHA, ws=ws, planes=P[l])
             else:
                 y = s["yd"][l]
-                d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws)
+                d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws, planes=P[l])
                 self._bn_fwd(s, name, y, z, "lrelu", training, ws)
             h = z
         for u, (name, ci, co, drop) in enumerate(self.ups):
             d = self.udesc[u]
             y = s["yu"][u]
-            d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws)
+            d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws, planes=P[8 + u])
             z = s["cat"][u][..., :co]
             rate = drop_rate if (drop and training) else 0.0
             self._bn_fwd(s, name, y, z, "relu", training, ws, rate, lambda hv: dropout_seed(drop_seed, u, hv),
                          step_dev)
             h = s["cat"][u]
-        self.ldesc.fwd(h, A.param("last/kernel"), out, bias=A.param("last/bias"), act="tanh", ws=ws)
+        self.ldesc.fwd(h, A.param("last/kernel"), out, bias=A.param("last/bias"), act="tanh", ws=ws, planes=P[15])
         return out
+
+    def _fwd_planes(self):
+        """The layer planes with x and w invalidated (a forward re-splits both)."""
+        for p in self.planes:
+            if p is not None:
+                p.invalidate(ops.TENSOR_X | ops.TENSOR_W)
+        return self.planes
+
+    def _bwd_planes(self, i):
+        p = self.planes[i]
+        if p is not None:
+            p.invalidate(ops.TENSOR_DY)
+        return p
 
     def _bn_fwd(self, s, name, y, z, act, training, ws, drop_rate=0.0, seed_of=None, step_dev=None):
         A = self.arena
@@ -340,8 +358,10 @@ class GeneratorPlan:
         dl = self.ldesc
         dpre = self._dy(dl, dl.Cout)
         ops.act_bwd(dout, s["out"], dpre, "tanh")
-        dl.bwd_filter(s["cat"][6], dpre, A.grad_of("last/kernel"), dbias=A.grad_of("last/bias"), beta=beta, ws=ws)
-        dl.bwd_data(dpre, A.param("last/kernel"), self.dcat[6], ws=ws)
+        P = self._bwd_planes(15)
+        dl.bwd_filter(s["cat"][6], dpre, A.grad_of("last/kernel"), dbias=A.grad_of("last/bias"), beta=beta, ws=ws,
+                      planes=P)
+        dl.bwd_data(dpre, A.param("last/kernel"), self.dcat[6], ws=ws, planes=P)
         if on_grads_ready:
             on_grads_ready("last")
         for u in range(6, -1, -1):
@@ -352,8 +372,9 @@ class GeneratorPlan:
                          drop_rate=drop_rate if drop else 0.0)
             hin = s["z8"] if u == 0 else s["cat"][u - 1]
             dhin = self.dz8 if u == 0 else self.dcat[u - 1]
-            d.bwd_filter(hin, dy, A.grad_of(f"{name}/kernel"), beta=beta, ws=ws)
-            d.bwd_data(dy, A.param(f"{name}/kernel"), dhin, ws=ws)
+            P = self._bwd_planes(8 + u)
+            d.bwd_filter(hin, dy, A.grad_of(f"{name}/kernel"), beta=beta, ws=ws, planes=P)
+            d.bwd_data(dy, A.param(f"{name}/kernel"), dhin, ws=ws, planes=P)
             if on_grads_ready:
                 on_grads_ready(name)
         for l in range(7, -1, -1):
@@ -367,10 +388,11 @@ class GeneratorPlan:
             else:
                 ops.act_bwd(dz, z, dy, "lrelu", ALPHA)
             hin = s["x"] if l == 0 else self.z_view(s, l - 1)
-            d.bwd_filter(hin, dy, A.grad_of(f"{name}/kernel"), beta=beta, ws=ws)
+            P = self._bwd_planes(l)
+            d.bwd_filter(hin, dy, A.grad_of(f"{name}/kernel"), beta=beta, ws=ws, planes=P)
             if l > 0:
                 # accumulate into the skip-gradient already sitting in the concat grad buffer
-                d.bwd_data(dy, A.param(f"{name}/kernel"), self.dz_view(l - 1), beta=1.0, ws=ws)
+                d.bwd_data(dy, A.param(f"{name}/kernel"), self.dz_view(l - 1), beta=1.0, ws=ws, planes=P)
             if on_grads_ready:
                 on_grads_ready(name)
 
@@ -441,6 +463,15 @@ class DiscriminatorPlan:
             self.dz = [_empty(d.out_shape, device) for d in self.desc[:-1]]
             maxdy = max(d.N * d.Ho * d.Wo * d.Cout for d in self.desc)
             self.dy = _empty((maxdy,), device)
+        # bf16x6 operand planes (see GeneratorPlan); the half-batch backward
+        # shares the weight planes and splits its own dy
+        if train:
+            self.planes = ops.plan_planes(self.desc, device)
+            self.planes_half = (ops.plan_planes(self.desc_half, device, keep_x=False,
+                                                wbufs=[p.w for p in self.planes])
+                                if self.desc_half is not self.desc else self.planes)
+        else:
+            self.planes = self.planes_half = [None] * len(self.desc)
         self.ws_bytes = max([d.max_ws() for d in self.desc + self.desc_half] +
                             [ops.bn_workspace_bytes(N * d.Ho * d.Wo, d.Cout) for d in self.desc])
 
@@ -457,17 +488,21 @@ class DiscriminatorPlan:
     def forward(self, slot=0, training=True, ws=None):
         A = self.arena
         h = self.inp
+        for p in self.planes:
+            if p is not None:
+                p.invalidate(ops.TENSOR_X | ops.TENSOR_W)
         for i, (name, ci, co, bn) in enumerate(self.specs):
             d = self.desc[i]
+            P = self.planes[i]
             if name == "last":
-                d.fwd(h, A.param("last/kernel"), self.logits, bias=A.param("last/bias"), ws=ws)
+                d.fwd(h, A.param("last/kernel"), self.logits, bias=A.param("last/bias"), ws=ws, planes=P)
                 return self.logits
             z = self.z[i]
             if not bn:
-                d.fwd(h, A.param(f"{name}/kernel"), z, act="lrelu", alpha=ALPHA, ws=ws)
+                d.fwd(h, A.param(f"{name}/kernel"), z, act="lrelu", alpha=ALPHA, ws=ws, planes=P)
             else:
                 y = self.y[i]
-                d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws)
+                d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws, planes=P)
                 for hv in range(self.halves):
                     yh, zh = self._half(y, hv), self._half(z, hv)
                     if training:
@@ -493,16 +528,20 @@ class DiscriminatorPlan:
         def sub(t):  # the rows of t this pass covers
             return t if half is None else self._half(t, half)
 
+        planes = self.planes if half is None else self.planes_half
         dh = dlogits
         n = len(self.specs)
         for i in range(n - 1, -1, -1):
             name, ci, co, bn = self.specs[i]
             d = desc[i]
+            P = planes[i]
+            if P is not None:
+                P.invalidate(ops.TENSOR_DY)
             if name == "last":
                 dy = dh
                 if param_grads:
                     d.bwd_filter(sub(self.z[i - 1]), dy, A.grad_of("last/kernel"), dbias=A.grad_of("last/bias"),
-                                 beta=beta, ws=ws)
+                                 beta=beta, ws=ws, planes=P)
             else:
                 dy = self._dy(d)
                 if bn:
@@ -517,12 +556,12 @@ class DiscriminatorPlan:
                     ops.act_bwd(dh, sub(self.z[i]), dy, "lrelu", ALPHA)
                 if param_grads:
                     hin = sub(self.inp) if i == 0 else sub(self.z[i - 1])
-                    d.bwd_filter(hin, dy, A.grad_of(f"{name}/kernel"), beta=beta, ws=ws)
+                    d.bwd_filter(hin, dy, A.grad_of(f"{name}/kernel"), beta=beta, ws=ws, planes=P)
             if param_grads and on_grads_ready:
                 on_grads_ready(name)
             if i > 0:
                 dz = sub(self.dz[i - 1])
-                d.bwd_data(dy, A.param(f"{name}/kernel"), dz, ws=ws)
+                d.bwd_data(dy, A.param(f"{name}/kernel"), dz, ws=ws, planes=P)
                 dh = dz
             elif input_grad is not None:
-                d.bwd_data(dy, A.param(f"{name}/kernel"), input_grad, beta=input_beta, ws=ws)
+                d.bwd_data(dy, A.param(f"{name}/kernel"), input_grad, beta=input_beta, ws=ws, planes=P)

@@ -95,6 +95,106 @@ def default_workspace():
 MATH_FP32, MATH_BF16X6 = 0, 1
 MATH_MODES = {"fp32": MATH_FP32, "bf16x6": MATH_BF16X6}
 
+# layer tensors of dg_conv_planes_t (include/dgan.h DG_TENSOR_*)
+TENSOR_X, TENSOR_DY, TENSOR_W = 1, 2, 4
+
+
+class _PlanesC(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_void_p), ("dy", ctypes.c_void_p), ("w", ctypes.c_void_p), ("ready", ctypes.c_int)]
+
+
+class PlaneBuf:
+    """A device buffer of bf16x6 planes and whether it holds the split of the
+    tensor it stands for.  One PlaneBuf may serve several ConvPlanes: the
+    weight planes of a network read by several plans, or one output-gradient
+    scratch reused layer after layer."""
+
+    __slots__ = ("buf", "ready")
+
+    def __init__(self, nbytes, device=None):
+        self.buf = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device or "cuda")
+        self.ready = False
+
+    def view(self, nbytes):
+        """A PlaneBuf sharing the first nbytes of this one (own ready flag)."""
+        v = PlaneBuf.__new__(PlaneBuf)
+        v.buf, v.ready = self.buf[:max(int(nbytes), 16)], False
+        return v
+
+
+class ConvPlanes:
+    """Caller-held bf16x6 planes of one conv layer's tensors (dg_conv_planes_t).
+
+    x / dy / w: PlaneBuf or None.  A conv wrapper called with planes marks
+    a buffer ready after its op split that tensor into it; callers
+    `invalidate` the tensors that change -- a new forward input or weights,
+    a new output gradient."""
+
+    __slots__ = ("x", "dy", "w")
+
+    def __init__(self, x=None, dy=None, w=None):
+        self.x, self.dy, self.w = x, dy, w
+
+    @classmethod
+    def for_desc(cls, d, x=False, dy=False, w=False, device=None):
+        """Fresh buffers for the tensors of descriptor d that are asked for and
+        that at least one op of d reads as planes."""
+        used = d.plane_mask[0] | d.plane_mask[1] | d.plane_mask[2]
+
+        def buf(t, want):
+            return PlaneBuf(d.plane_bytes(t), device) if want and (used & t) else None
+
+        return cls(buf(TENSOR_X, x), buf(TENSOR_DY, dy), buf(TENSOR_W, w))
+
+    def _bufs(self):
+        return ((TENSOR_X, self.x), (TENSOR_DY, self.dy), (TENSOR_W, self.w))
+
+    @property
+    def ready(self):
+        return sum(t for t, b in self._bufs() if b is not None and b.ready)
+
+    def invalidate(self, bits):
+        for t, b in self._bufs():
+            if b is not None and (bits & t):
+                b.ready = False
+
+    def _filled(self, bits):
+        for t, b in self._bufs():
+            if b is not None and (bits & t):
+                b.ready = True
+
+    def _c(self):
+        ptr = lambda b: None if b is None else b.buf.data_ptr()
+        return _PlanesC(ptr(self.x), ptr(self.dy), ptr(self.w), self.ready)
+
+    def _have(self):
+        return sum(t for t, b in self._bufs() if b is not None)
+
+
+def plan_planes(descs, device=None, keep_x=True, wbufs=None):
+    """One ConvPlanes per descriptor of a training schedule (forward, then
+    per layer bwd_filter -> bwd_data):
+      x  -- its own buffer per layer, split by fwd and kept for bwd_filter
+            (when both read x as planes and keep_x);
+      w  -- split by fwd, reused by bwd_data (wbufs[i]: a PlaneBuf shared
+            with other plans of the same weights);
+      dy -- one scratch shared by all layers, split by bwd_filter, reused by
+            bwd_data of the same layer.
+    The schedule invalidates x and w before each fwd and dy before each
+    layer's backward."""
+    masks = [d.plane_mask for d in descs]
+    dy_need = [d.plane_bytes(TENSOR_DY) if (m[1] & m[2] & TENSOR_DY) else 0 for d, m in zip(descs, masks)]
+    dy_buf = PlaneBuf(max(dy_need), device) if dy_need and max(dy_need) else None
+    out = []
+    for i, (d, m) in enumerate(zip(descs, masks)):
+        x = PlaneBuf(d.plane_bytes(TENSOR_X), device) if keep_x and (m[0] & m[2] & TENSOR_X) else None
+        w = None
+        if (m[0] | m[1]) & TENSOR_W:
+            w = wbufs[i] if wbufs is not None and wbufs[i] is not None else PlaneBuf(d.plane_bytes(TENSOR_W), device)
+        dy = dy_buf.view(dy_need[i]) if dy_need[i] else None
+        out.append(ConvPlanes(x, dy, w))
+    return out
+
 
 class ConvDesc:
     """A Conv2D / Conv2DTranspose layer geometry (immutable), libdgan descriptor.
@@ -144,10 +244,26 @@ class ConvDesc:
         call("dg_conv_get_math", h, ctypes.byref(m))
         self.math = m.value
         self.ws = []
+        self.plane_mask = []   # per op: TENSOR_* bits it reads as bf16x6 planes
         for op in (OP_FWD, OP_BWD_DATA, OP_BWD_FILTER):
             n = ctypes.c_size_t()
             call("dg_conv_workspace_size", h, op, ctypes.byref(n))
             self.ws.append(n.value)
+            m = ctypes.c_int()
+            call("dg_conv_op_planes", h, op, ctypes.byref(m))
+            self.plane_mask.append(m.value)
+
+    def plane_bytes(self, tensor):
+        n = ctypes.c_size_t()
+        call("dg_conv_planes_size", self._h, tensor, ctypes.byref(n))
+        return n.value
+
+    def _pl(self, op, planes):
+        """(struct pointer, bits this op fills) for a ConvPlanes (None -> no planes)."""
+        if planes is None or not self.plane_mask[op]:
+            return None, 0
+        st = planes._c()
+        return ctypes.byref(st), self.plane_mask[op] & planes._have()
 
     def __del__(self):
         try:
@@ -186,41 +302,50 @@ class ConvDesc:
         w = self.kh * self.kw * self.Cin * self.Cout
         return 4 * (xin + yout + w)
 
-    def fwd(self, x, w, y, bias=None, act="none", alpha=0.3, beta=0.0, ws=None):
+    # planes: optional ConvPlanes (bf16x6 operand planes shared between the
+    # ops of this layer, include/dgan.h dg_conv_planes_t)
+    def fwd(self, x, w, y, bias=None, act="none", alpha=0.3, beta=0.0, ws=None, planes=None):
         ldx, ldy = pix_ld(x, self.Cin), pix_ld(y, self.Cout)
         wp, wn = self._ws(OP_FWD, ws)
+        pp, fills = self._pl(OP_FWD, planes)
         ev = _prof_begin()
-        call("dg_conv_fwd", self._h, _p(x), ldx, _p(w), _p(bias), _p(y), ldy,
-             float(beta), act_id(act), float(alpha), wp, wn, _stream())
+        call("dg_conv_fwd_pl", self._h, _p(x), ldx, _p(w), _p(bias), _p(y), ldy,
+             float(beta), act_id(act), float(alpha), pp, wp, wn, _stream())
         _prof_end(ev, self, "fwd")
+        if fills:
+            planes._filled(fills)
         return y
 
-    def bwd_data(self, dy, w, dx, beta=0.0, ws=None):
-        lddy, lddx = pix_ld(dy, self.Cout), pix_ld(dx, self.Cin)
-        wp, wn = self._ws(OP_BWD_DATA, ws)
-        ev = _prof_begin()
-        call("dg_conv_bwd_data", self._h, _p(dy), lddy, _p(w), _p(dx), lddx,
-             float(beta), wp, wn, _stream())
-        _prof_end(ev, self, "bwd_data")
-        return dx
+    def bwd_data(self, dy, w, dx, beta=0.0, ws=None, planes=None):
+        return self._bwd_data(dy, w, dx, None, 0, 0.0, beta, ws, planes)
 
-    def bwd_data_masked(self, dy, w, dx, z, act, alpha=0.3, beta=0.0, ws=None):
+    def bwd_data_masked(self, dy, w, dx, z, act, alpha=0.3, beta=0.0, ws=None, planes=None):
         """dx = dL/dx * act'(z) + beta*dx, z = the activation output this conv read as input."""
+        return self._bwd_data(dy, w, dx, z, act_id(act), alpha, beta, ws, planes)
+
+    def _bwd_data(self, dy, w, dx, z, act, alpha, beta, ws, planes):
         lddy, lddx = pix_ld(dy, self.Cout), pix_ld(dx, self.Cin)
+        ldz = pix_ld(z, self.Cin) if z is not None else 0
         wp, wn = self._ws(OP_BWD_DATA, ws)
+        pp, fills = self._pl(OP_BWD_DATA, planes)
         ev = _prof_begin()
-        call("dg_conv_bwd_data_masked", self._h, _p(dy), lddy, _p(w), _p(dx), lddx, float(beta), _p(z),
-             pix_ld(z, self.Cin), act_id(act), float(alpha), wp, wn, _stream())
+        call("dg_conv_bwd_data_pl", self._h, _p(dy), lddy, _p(w), _p(dx), lddx, float(beta), _p(z), ldz, act,
+             float(alpha), pp, wp, wn, _stream())
         _prof_end(ev, self, "bwd_data")
+        if fills:
+            planes._filled(fills)
         return dx
 
-    def bwd_filter(self, x, dy, dw, dbias=None, beta=0.0, ws=None):
+    def bwd_filter(self, x, dy, dw, dbias=None, beta=0.0, ws=None, planes=None):
         ldx, lddy = pix_ld(x, self.Cin), pix_ld(dy, self.Cout)
         wp, wn = self._ws(OP_BWD_FILTER, ws)
+        pp, fills = self._pl(OP_BWD_FILTER, planes)
         ev = _prof_begin()
-        call("dg_conv_bwd_filter", self._h, _p(x), ldx, _p(dy), lddy, _p(dw),
-             _p(dbias), float(beta), wp, wn, _stream())
+        call("dg_conv_bwd_filter_pl", self._h, _p(x), ldx, _p(dy), lddy, _p(dw),
+             _p(dbias), float(beta), pp, wp, wn, _stream())
         _prof_end(ev, self, "bwd_filter")
+        if fills:
+            planes._filled(fills)
         return dw
 
 

@@ -95,6 +95,36 @@ int dg_conv_bwd_filter(dg_conv_t d, const float *x, int ldx, const float *dy, in
                        float *dw, float *dbias, float beta,
                        void *ws, size_t ws_bytes, dg_stream_t stream);
 
+/* Caller-held bf16x6 operand planes.  Under DG_MATH_BF16X6 every GEMM first
+ * splits its two fp32 operands into bf16 hi/mid/lo planes (6 B per element);
+ * the planes are a function of the tensor alone, so one split can serve every
+ * op that reads the tensor: x by fwd and bwd_filter, dy by bwd_filter and
+ * bwd_data, w by fwd and bwd_data.  A dg_conv_planes_t names a buffer
+ * (dg_conv_planes_size bytes, 16-byte aligned) per tensor; an op that reads
+ * a tensor as planes (dg_conv_op_planes) splits it into the given buffer, or,
+ * when the tensor's bit is set in `ready`, reads the planes already there
+ * without touching the fp32 tensor.  NULL buffers fall back to the workspace.
+ * The caller owns validity: set a ready bit only after an op whose
+ * dg_conv_op_planes mask holds that tensor has run on the same stream, and
+ * clear it when the tensor changes. */
+enum { DG_TENSOR_X = 1, DG_TENSOR_DY = 2, DG_TENSOR_W = 4 };
+typedef struct dg_conv_planes {
+    void *x, *dy, *w;  /* plane buffers (NULL: split into the workspace) */
+    int ready;         /* DG_TENSOR_* bits whose buffer already holds the split */
+} dg_conv_planes_t;
+int dg_conv_planes_size(dg_conv_t d, int tensor, size_t *bytes);
+int dg_conv_op_planes(dg_conv_t d, int op, int *tensors);
+int dg_conv_fwd_pl(dg_conv_t d, const float *x, int ldx, const float *w, const float *bias,
+                   float *y, int ldy, float beta, int act, float alpha,
+                   const dg_conv_planes_t *planes, void *ws, size_t ws_bytes, dg_stream_t stream);
+/* z == NULL: dg_conv_bwd_data; else dg_conv_bwd_data_masked */
+int dg_conv_bwd_data_pl(dg_conv_t d, const float *dy, int lddy, const float *w,
+                        float *dx, int lddx, float beta, const float *z, int ldz, int act, float alpha,
+                        const dg_conv_planes_t *planes, void *ws, size_t ws_bytes, dg_stream_t stream);
+int dg_conv_bwd_filter_pl(dg_conv_t d, const float *x, int ldx, const float *dy, int lddy,
+                          float *dw, float *dbias, float beta,
+                          const dg_conv_planes_t *planes, void *ws, size_t ws_bytes, dg_stream_t stream);
+
 /* ------------------------------------------------------------------------
  * BatchNormalization, training semantics of Keras' fused kernel
  * (pix2pix.py:119, :135, :211): batch statistics over the M = N*H*W rows,
