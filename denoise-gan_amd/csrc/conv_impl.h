@@ -143,27 +143,31 @@ template <int MODE, int TM, int TN>
 __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[TM][TN], int rbase, int cbase,
                                                 int Mrows, const PhaseInfo &ph, int phase, int split, int lane) {
     const ConvGeom &g = p.g;
+    // rows outer, columns inner: the DGRAD phase-row -> pixel map (integer
+    // divisions) is computed once per row, not once per element; unit-stride
+    // DGRAD (one phase covering the image) maps row -> pixel identically
+    const bool ident = MODE != MODE_DGRAD || (g.sh == 1 && g.sw == 1);
 #pragma unroll
     for (int a = 0; a < TM; ++a) {
 #pragma unroll
-        for (int b = 0; b < TN; ++b) {
-            const int col = cbase + b * 16 + (lane & 15);
-            if (col >= p.N) continue;
+        for (int r = 0; r < 4; ++r) {
+            const int row = rbase + a * 16 + 4 * (lane >> 4) + r;
+            if (row >= Mrows) continue;
+            long pix = row;
+            if constexpr (MODE == MODE_DGRAD) {
+                if (!ident && p.splits == 1) {
+                    int ww = row % ph.Wp; int t = row / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
+                    pix = (long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw;
+                }
+            }
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = rbase + a * 16 + 4 * (lane >> 4) + r;
-                if (row >= Mrows) continue;
+            for (int b = 0; b < TN; ++b) {
+                const int col = cbase + b * 16 + (lane & 15);
+                if (col >= p.N) continue;
                 float v = acc[a][b][r];
                 if (p.splits > 1) {
                     p.slab[((long)(phase * p.splits + split) * p.M + row) * p.N + col] = v;
                 } else {
-                    long pix;
-                    if constexpr (MODE == MODE_DGRAD) {
-                        int ww = row % ph.Wp; int t = row / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
-                        pix = (long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw;
-                    } else {
-                        pix = row;
-                    }
                     const long off = pix * p.ldc;
                     if (p.bias) v += p.bias[col];
                     v = act_fwd(v, p.act, p.alpha);
