@@ -138,43 +138,85 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs &p, f32x16 (&acc)[T
 }
 
 // The same for 16x16 accumulator tiles (v_mfma_f32_16x16x32_bf16 C layout:
-// col = lane&15, row = 4(lane>>4) + r).
+// col = lane&15, row = 4(lane>>4) + r), staged through LDS: the wave writes
+// 16 rows of its tile at a time into `stage` (16 x (16*TN + 4) floats, its
+// own region) and reads them back row-contiguous, so every global access is
+// 16 bytes per lane (C, the split-K slab, beta*C and the gradient mask) and
+// the row -> pixel map is computed once per row per lane.
 template <int MODE, int TM, int TN>
 __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[TM][TN], int rbase, int cbase,
-                                                int Mrows, const PhaseInfo &ph, int phase, int split, int lane) {
+                                                int Mrows, const PhaseInfo &ph, int phase, int split, int lane,
+                                                float *stage) {
+    constexpr int WTN = 16 * TN;
+    constexpr int LD = WTN + 4;   // padded staging row (floats): conflict-free writes
+    constexpr int C4 = WTN / 4;   // float4 per row
+    constexpr int RPP = 64 / C4;  // rows per pass of the wave
+    static_assert(64 % C4 == 0 && 16 % RPP == 0, "wave tile width");
     const ConvGeom &g = p.g;
-    // rows outer, columns inner: the DGRAD phase-row -> pixel map (integer
-    // divisions) is computed once per row, not once per element; unit-stride
-    // DGRAD (one phase covering the image) maps row -> pixel identically
     const bool ident = MODE != MODE_DGRAD || (g.sh == 1 && g.sw == 1);
+    const bool cvec = ((p.ldc & 3) == 0) && ((((uintptr_t)p.C) & 15) == 0);
+    const bool mvec = ((p.ldmz & 3) == 0) && ((((uintptr_t)p.mz) & 15) == 0);
+    const bool svec = ((p.N & 3) == 0) && ((((uintptr_t)p.slab) & 15) == 0);
+    const int c4 = lane % C4;
+    const int col = cbase + c4 * 4;
+    const bool full = col + 3 < p.N;
 #pragma unroll
     for (int a = 0; a < TM; ++a) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int row = rbase + a * 16 + 4 * (lane >> 4) + r;
-            if (row >= Mrows) continue;
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) stage[(4 * (lane >> 4) + r) * LD + b * 16 + (lane & 15)] = acc[a][b][r];
+#pragma unroll
+        for (int pass = 0; pass < 16 / RPP; ++pass) {
+            const int rl = pass * RPP + lane / C4;
+            const f32x4 v = *reinterpret_cast<const f32x4 *>(stage + rl * LD + c4 * 4);
+            const int row = rbase + a * 16 + rl;
+            if (row >= Mrows || col >= p.N) continue;
+            if (p.splits > 1) {
+                float *dst = p.slab + ((long)(phase * p.splits + split) * p.M + row) * p.N + col;
+                if (svec && full) {
+                    *reinterpret_cast<f32x4 *>(dst) = v;
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        if (col + q < p.N) dst[q] = v[q];
+                }
+                continue;
+            }
             long pix = row;
             if constexpr (MODE == MODE_DGRAD) {
-                if (!ident && p.splits == 1) {
+                if (!ident) {
                     int ww = row % ph.Wp; int t = row / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
                     pix = (long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw;
                 }
             }
+            float *dst = p.C + pix * p.ldc + col;
+            f32x4 o = v;
+            if (p.bias) {
 #pragma unroll
-            for (int b = 0; b < TN; ++b) {
-                const int col = cbase + b * 16 + (lane & 15);
-                if (col >= p.N) continue;
-                float v = acc[a][b][r];
-                if (p.splits > 1) {
-                    p.slab[((long)(phase * p.splits + split) * p.M + row) * p.N + col] = v;
+                for (int q = 0; q < 4; ++q) o[q] += (col + q < p.N) ? p.bias[col + q] : 0.f;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = act_fwd(o[q], p.act, p.alpha);
+            if (p.mz) {
+                const float *mz = p.mz + pix * p.ldmz + col;
+                f32x4 z;
+                if (mvec && full) {
+                    z = *reinterpret_cast<const f32x4 *>(mz);
                 } else {
-                    const long off = pix * p.ldc;
-                    if (p.bias) v += p.bias[col];
-                    v = act_fwd(v, p.act, p.alpha);
-                    v = epi_mask(p, pix, col, v);
-                    if (p.beta != 0.f) v += p.beta * p.C[off + col];
-                    p.C[off + col] = v;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) z[q] = (col + q < p.N) ? mz[q] : 0.f;
                 }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) o[q] *= act_grad_from_out(z[q], p.mact, p.malpha);
+            }
+            if (cvec && full) {
+                if (p.beta != 0.f) o += p.beta * *reinterpret_cast<const f32x4 *>(dst);
+                *reinterpret_cast<f32x4 *>(dst) = o;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (col + q < p.N) dst[q] = p.beta != 0.f ? o[q] + p.beta * dst[q] : o[q];
             }
         }
     }

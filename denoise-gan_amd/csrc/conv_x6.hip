@@ -177,6 +177,9 @@ k_conv_gemm_x6(const GemmArgs p) {
     __shared__ __attribute__((aligned(16))) char smem1[BUF];
     __shared__ __attribute__((aligned(16))) char smem2[BUF];
     __shared__ __attribute__((aligned(16))) char smem3[NBUF == 4 ? BUF : 16];
+    // landing block of the DMAs of dead slots (their source offset is out of
+    // range, so nothing is fetched; never read)
+    __shared__ __attribute__((aligned(16))) char smem_dead[1024];
 
     const ConvGeom &g = p.g;
     const int tid = threadIdx.x;
@@ -244,18 +247,14 @@ k_conv_gemm_x6(const GemmArgs p) {
         bsl[j] = slot_of(d < B_SL ? d : 0, B_KC, BN);
         bsl[j].live = d < B_SL;
     }
-    // DMA instructions this wave issues per K-tile (wave-uniform)
-    // when every wave owns the same number of slots (A_SL, B_SL multiples of
-    // NW) liveness and the DMA count are compile-time, which keeps the K-tile
-    // body branch-free so the scheduler can interleave its DMA / LDS / VALU
-    // work with the MFMAs
+    // Every wave issues A_NJ + B_NJ DMAs per K-tile: when a slot count is not
+    // a multiple of NW the dead slots of a wave still issue one, with an
+    // out-of-range source into a dummy LDS block.  The DMA count and the
+    // s_waitcnt values are then compile-time and the K-tile body has no
+    // branches, so the scheduler can interleave its DMA / LDS / VALU work
+    // with the MFMAs.
     constexpr bool A_ALL = (A_SL % NW) == 0, B_ALL = (B_SL % NW) == 0;
-    int nmine = 0;
-#pragma unroll
-    for (int j = 0; j < A_NJ; ++j) nmine += (A_ALL || asl[j].live);
-#pragma unroll
-    for (int j = 0; j < B_NJ; ++j) nmine += (B_ALL || bsl[j].live);
-    if constexpr (A_ALL && B_ALL) nmine = A_NJ + B_NJ;
+    constexpr int NMINE = A_NJ + B_NJ;
 
     // A geometry per slot.  KC (FWD / DGRAD): the output pixel of row r.
     // WGRAD (RC): the (tap, ci) of columns c..c+7 and their packed offset.
@@ -382,14 +381,19 @@ k_conv_gemm_x6(const GemmArgs p) {
         (void)a_delta; (void)b_delta; (void)tap_bit; (void)b_tap_ok;
 #pragma unroll
         for (int j = 0; j < A_NJ; ++j) {
-            if constexpr (!A_ALL) { if (!asl[j].live) continue; }
             const int d = wid + NW * j, per = BM / 32;
             char *dst = As + asl[j].plane * APL + (d - asl[j].plane * per) * 1024;
+            if constexpr (!A_ALL) dst = asl[j].live ? dst : smem_dead;
             unsigned off;
             bool ok;
             if constexpr (MODE != MODE_WGRAD) {
                 ok = (amask[j] >> tap_bit) & 1;
                 off = (unsigned)(abase[j] + a_delta);
+#if DG_EXP == 1
+                if constexpr (MODE == MODE_FWD) { if (tap_bit != 0) continue; }
+#elif DG_EXP == 2
+                if constexpr (MODE == MODE_FWD) ok = ok && tap_bit == 0;
+#endif
             } else {
                 const unsigned pix = (unsigned)(k0 + asl[j].r);
                 const unsigned t = fdiv(pix, p.mg_wo, p.sh_wo); const int wo = (int)(pix - t * g.Wo);
@@ -398,13 +402,14 @@ k_conv_gemm_x6(const GemmArgs p) {
                 ok = arow_n[j] >= 0 && (int)pix < kend && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
                 off = ((unsigned)(((int)n * g.H + hi) * g.W + wi) * (3 * p.lda) + wg_ci[j]) * 2u;
             }
+            if constexpr (!A_ALL) ok = ok && asl[j].live;
             dma(rA, dst, ok ? off : DG_OOB);
         }
 #pragma unroll
         for (int j = 0; j < B_NJ; ++j) {
-            if constexpr (!B_ALL) { if (!bsl[j].live) continue; }
             const int d = wid + NW * j, per = BN / 32;
             char *dst = Bs + bsl[j].plane * BPL + (d - bsl[j].plane * per) * 1024;
+            if constexpr (!B_ALL) dst = bsl[j].live ? dst : smem_dead;
             unsigned off;
             bool ok;
             if constexpr (MODE == MODE_FWD) {  // w[k][co], k = (tap, ci); RC: k-row r, columns c..c+7
@@ -419,28 +424,10 @@ k_conv_gemm_x6(const GemmArgs p) {
                 ok = col < p.N && pix < kend;
                 off = ((unsigned)pix * (3 * p.ldb) + (col >> 4) * 48 + 16 * bsl[j].plane + (col & 8)) * 2u;
             }
+            if constexpr (!B_ALL) ok = ok && bsl[j].live;
             dma(rB, dst, ok ? off : DG_OOB);
         }
         if constexpr (MODE != MODE_WGRAD) walk_next();
-    };
-    // wait until at most n of this wave's DMAs are in flight (n wave-uniform)
-    auto wait_dma = [](int n) {
-        switch (n) {
-        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-        case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-        case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-        case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-        }
     };
     // barrier without the vmcnt(0) drain of __syncthreads (DMAs stay in flight)
     auto barrier = []() {
@@ -516,14 +503,13 @@ k_conv_gemm_x6(const GemmArgs p) {
 #pragma unroll
             for (int b = 0; b < TN; ++b)
                 acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahl[a], b3[b], acc[a][b], 0, 0, 0);
-        if constexpr (A_ALL && B_ALL) wait_dma_c<(AHEAD - 1) * (A_NJ + B_NJ)>();
-        else wait_dma((AHEAD - 1) * nmine);
+        wait_dma_c<(AHEAD - 1) * NMINE>();
         barrier();
     };
     issue_tile(kbeg, smem0);
     issue_tile(kbeg + BK, smem1);
     if constexpr (NBUF == 4) issue_tile(kbeg + 2 * BK, smem2);
-    wait_dma((AHEAD - 1) * nmine);
+    wait_dma_c<(AHEAD - 1) * NMINE>();
     barrier();
     int kt = 0;
     if constexpr (NBUF == 3) {
@@ -545,9 +531,14 @@ k_conv_gemm_x6(const GemmArgs p) {
         if (kt + 1 < nk) ktile(kt + 1, smem1, smem0);
         if (kt + 2 < nk) ktile(kt + 2, smem2, smem1);
     }
-    wait_dma(0);
-
-    conv_epilogue16<MODE, TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, Mrows, ph, phase, split, lane);
+    // every wave's DMAs (including the harmless ones past nk) have landed
+    // before smem0 becomes the epilogue's staging area
+    wait_dma_c<0>();
+    barrier();
+    constexpr int STAGE = 16 * (WTN + 4);  // floats per wave
+    static_assert(NW * STAGE * 4 <= BUF, "epilogue staging fits in one LDS buffer");
+    conv_epilogue16<MODE, TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, Mrows, ph, phase, split, lane,
+                                  reinterpret_cast<float *>(smem0) + wid * STAGE);
 }
 
 void launch_split3(const float *src, int ld, long rows, int C, unsigned short *dst, hipStream_t s) {
@@ -574,6 +565,8 @@ void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t
         DG_X6(3, 64, 64, 2, 2, 3, 3)
         DG_X6(4, 256, 128, 4, 2, 2, 3)
         DG_X6(5, 128, 256, 2, 4, 2, 3)
+        DG_X6(6, 256, 64, 4, 1, 1, 3)
+        DG_X6(7, 256, 64, 4, 2, 1, 3)
     }
 #undef DG_X6
 }
