@@ -749,7 +749,6 @@ constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 static const TileCfg kX6Cfgs[] = {
     {128, 128, 2, 2, 16, 2, 2, 1.00}, {128, 64, 2, 2, 16, 2, 2, 1.15}, {64, 128, 2, 2, 16, 2, 2, 1.15},
     {64, 64, 2, 2, 16, 3, 4, 1.40},   {256, 128, 4, 2, 16, 2, 1, 1.00}, {128, 256, 2, 4, 16, 2, 1, 1.00},
-    {256, 64, 4, 1, 16, 1, 1, 9.00},  {256, 64, 4, 2, 16, 1, 1, 9.00},
 };
 constexpr int kNumX6Cfgs = sizeof(kX6Cfgs) / sizeof(kX6Cfgs[0]);
 

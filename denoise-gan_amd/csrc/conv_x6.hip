@@ -389,11 +389,6 @@ k_conv_gemm_x6(const GemmArgs p) {
             if constexpr (MODE != MODE_WGRAD) {
                 ok = (amask[j] >> tap_bit) & 1;
                 off = (unsigned)(abase[j] + a_delta);
-#if DG_EXP == 1
-                if constexpr (MODE == MODE_FWD) { if (tap_bit != 0) continue; }
-#elif DG_EXP == 2
-                if constexpr (MODE == MODE_FWD) ok = ok && tap_bit == 0;
-#endif
             } else {
                 const unsigned pix = (unsigned)(k0 + asl[j].r);
                 const unsigned t = fdiv(pix, p.mg_wo, p.sh_wo); const int wo = (int)(pix - t * g.Wo);
@@ -565,8 +560,6 @@ void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t
         DG_X6(3, 64, 64, 2, 2, 3, 3)
         DG_X6(4, 256, 128, 4, 2, 2, 3)
         DG_X6(5, 128, 256, 2, 4, 2, 3)
-        DG_X6(6, 256, 64, 4, 1, 1, 3)
-        DG_X6(7, 256, 64, 4, 2, 1, 3)
     }
 #undef DG_X6
 }
