@@ -92,7 +92,23 @@ k_bn_stats_partial(const float *__restrict__ y, int ld, long M, int C, long rows
     const bool cok = c0 < C;
     if (cok) {
         loadv<V>(y + r0 * ld + c0, K);
-        for (long r = r0 + rl; r < r1; r += RL) {
+        // U rows' loads in flight per lane, summed in row order (deterministic)
+        constexpr int U = 8;
+        long r = r0 + rl;
+        for (; r + (U - 1) * RL < r1; r += U * RL) {
+            float v[U][V];
+#pragma unroll
+            for (int u = 0; u < U; ++u) loadv<V>(y + (r + u * RL) * ld + c0, v[u]);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int q = 0; q < V; ++q) {
+                    float d = v[u][q] - K[q];
+                    s1[q] += d;
+                    s2[q] += d * d;
+                }
+        }
+        for (; r < r1; r += RL) {
             float v[V];
             loadv<V>(y + r * ld + c0, v);
 #pragma unroll
@@ -237,17 +253,34 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
     if (cok) {
         loadv<V>(mean + c0, mu);
         loadv<V>(invstd + c0, inv);
-        for (long r = r0 + rl; r < r1; r += RL) {
-            float dv[V], zv[V], yv[V];
-            loadv<V>(dz + r * lddz + c0, dv);
-            loadv<V>(z + r * ldz + c0, zv);
-            loadv<V>(y + r * ldy + c0, yv);
+        auto acc_row = [&](const float (&dv)[V], const float (&zv)[V], const float (&yv)[V]) {
 #pragma unroll
             for (int q = 0; q < V; ++q) {
                 float dbn = dv[q] * act_grad_from_out(zv[q], act, alpha) * dscale;
                 a1[q] += dbn;
                 a2[q] += dbn * (yv[q] - mu[q]) * inv[q];
             }
+        };
+        // U rows' loads in flight per lane, summed in row order (deterministic)
+        constexpr int U = 4;
+        long r = r0 + rl;
+        for (; r + (U - 1) * RL < r1; r += U * RL) {
+            float dv[U][V], zv[U][V], yv[U][V];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                loadv<V>(dz + (r + u * RL) * lddz + c0, dv[u]);
+                loadv<V>(z + (r + u * RL) * ldz + c0, zv[u]);
+                loadv<V>(y + (r + u * RL) * ldy + c0, yv[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc_row(dv[u], zv[u], yv[u]);
+        }
+        for (; r < r1; r += RL) {
+            float dv[V], zv[V], yv[V];
+            loadv<V>(dz + r * lddz + c0, dv);
+            loadv<V>(z + r * ldz + c0, zv);
+            loadv<V>(y + r * ldy + c0, yv);
+            acc_row(dv, zv, yv);
         }
     }
 #pragma unroll
