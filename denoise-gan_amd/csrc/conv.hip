@@ -768,6 +768,9 @@ struct OpPlan {
     long x6_ra, x6_rb;
     int x6_ca, x6_cb;
     size_t x6_a_off, x6_b_off;
+    // halo-tiled bf16x6 kernel (stride-1 3x3 FWD / DGRAD, conv_x6h.hip):
+    // cfg = its BN, tiles of 8 x 16 output pixels
+    int halo, htx, hty;
 };
 
 // A narrow op (GEMM N <= 8) recast as a 1x1-geometry MFMA GEMM plus a gather:
@@ -906,6 +909,24 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         }
     }
     if (!pl.x6) choose_tiles(pl, kCfgs, kNumCfgs, 157.3e12, "DG_FORCE_CFG", nullptr);
+    if (pl.x6 && (mode == MODE_FWD || mode == MODE_DGRAD) && g.kh == 3 && g.kw == 3 && g.sh == 1 && g.sw == 1 &&
+        pl.K % 144 == 0 && !getenv("DG_NO_HALO")) {
+        // each input pixel staged once per 16-channel chunk instead of once per tap
+        const int Hout = mode == MODE_FWD ? g.Ho : g.H, Wout = mode == MODE_FWD ? g.Wo : g.W;
+        pl.halo = 1;
+        pl.htx = (Wout + 15) / 16;
+        pl.hty = (Hout + 7) / 8;
+        pl.cfg = pl.N > 64 ? 128 : 64;
+        pl.mtiles = g.N * pl.htx * pl.hty;
+        pl.ntiles = (pl.N + pl.cfg - 1) / pl.cfg;
+        // split-K over channel chunks (at least two per split) until ~2 blocks per CU
+        const long nch = pl.K / 144, blocks = (long)pl.mtiles * pl.ntiles;
+        long splits = 1;
+        while (blocks * splits < 512 && splits * 4 <= nch) splits *= 2;
+        const long cps = (nch + splits - 1) / splits;
+        pl.kchunk = (int)(cps * 144);
+        pl.splits = (int)((nch + cps - 1) / cps);
+    }
     pl.vec = pl.x6 ? 1 : cfg_vec(g, mode, kCfgs[pl.cfg].bk);
     pl.slab_bytes = pl.splits > 1 ? (size_t)pl.nphase * pl.splits * pl.M * pl.N * sizeof(float) : 0;
     pl.ws_bytes = pl.slab_bytes;
@@ -1163,7 +1184,8 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
         fastdiv_magic((unsigned)a.g.Ho, a.mg_ho, a.sh_ho);
         a.B = (const float *)pb; a.ldb = pl.x6_cb; a.b_bytes = (unsigned)(3 * pbs * 2);
         dim3 grid(pl.mtiles * pl.ntiles, pl.nphase * pl.splits);
-        launch_gemm_x6(mode, pl.cfg, grid, a, s);
+        if (pl.halo) launch_gemm_x6h(mode, pl.cfg, grid, a, pl.htx, pl.hty, s);
+        else launch_gemm_x6(mode, pl.cfg, grid, a, s);
         DG_LAUNCHED("conv_gemm_x6");
         return finish_splitk(mode, pl, a, s);
     }

@@ -137,23 +137,27 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs &p, f32x16 (&acc)[T
     }
 }
 
+// Row of a GEMM tile -> (row of the split-K slab, output pixel); slab < 0
+// marks a row outside the output.
+struct RowPix {
+    long slab, pix;
+};
+
 // The same for 16x16 accumulator tiles (v_mfma_f32_16x16x32_bf16 C layout:
 // col = lane&15, row = 4(lane>>4) + r), staged through LDS: the wave writes
 // 16 rows of its tile at a time into `stage` (16 x (16*TN + 4) floats, its
 // own region) and reads them back row-contiguous, so every global access is
 // 16 bytes per lane (C, the split-K slab, beta*C and the gradient mask) and
-// the row -> pixel map is computed once per row per lane.
-template <int MODE, int TM, int TN>
+// the row -> pixel map (`rowmap(rbase + local row)` -> RowPix) is evaluated
+// once per row per lane.
+template <int MODE, int TM, int TN, class RowMap>
 __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[TM][TN], int rbase, int cbase,
-                                                int Mrows, const PhaseInfo &ph, int phase, int split, int lane,
-                                                float *stage) {
+                                                RowMap rowmap, int phase, int split, int lane, float *stage) {
     constexpr int WTN = 16 * TN;
     constexpr int LD = WTN + 4;   // padded staging row (floats): conflict-free writes
     constexpr int C4 = WTN / 4;   // float4 per row
     constexpr int RPP = 64 / C4;  // rows per pass of the wave
     static_assert(64 % C4 == 0 && 16 % RPP == 0, "wave tile width");
-    const ConvGeom &g = p.g;
-    const bool ident = MODE != MODE_DGRAD || (g.sh == 1 && g.sw == 1);
     const bool cvec = ((p.ldc & 3) == 0) && ((((uintptr_t)p.C) & 15) == 0);
     const bool mvec = ((p.ldmz & 3) == 0) && ((((uintptr_t)p.mz) & 15) == 0);
     const bool svec = ((p.N & 3) == 0) && ((((uintptr_t)p.slab) & 15) == 0);
@@ -170,10 +174,10 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
         for (int pass = 0; pass < 16 / RPP; ++pass) {
             const int rl = pass * RPP + lane / C4;
             const f32x4 v = *reinterpret_cast<const f32x4 *>(stage + rl * LD + c4 * 4);
-            const int row = rbase + a * 16 + rl;
-            if (row >= Mrows || col >= p.N) continue;
+            const RowPix rp = rowmap(rbase + a * 16 + rl);
+            if (rp.slab < 0 || col >= p.N) continue;
             if (p.splits > 1) {
-                float *dst = p.slab + ((long)(phase * p.splits + split) * p.M + row) * p.N + col;
+                float *dst = p.slab + ((long)(phase * p.splits + split) * p.M + rp.slab) * p.N + col;
                 if (svec && full) {
                     *reinterpret_cast<f32x4 *>(dst) = v;
                 } else {
@@ -183,13 +187,7 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
                 }
                 continue;
             }
-            long pix = row;
-            if constexpr (MODE == MODE_DGRAD) {
-                if (!ident) {
-                    int ww = row % ph.Wp; int t = row / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
-                    pix = (long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw;
-                }
-            }
+            const long pix = rp.pix;
             float *dst = p.C + pix * p.ldc + col;
             f32x4 o = v;
             if (p.bias) {
@@ -224,6 +222,8 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
 
 // launcher of the bf16x6 kernels (conv_x6.hip); cfg indexes kX6Cfgs
 void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s);
+// the halo-tiled bf16x6 kernel (conv_x6h.hip) for stride-1 3x3 FWD / DGRAD; bn = 64 | 128
+void launch_gemm_x6h(int mode, int bn, dim3 grid, const GemmArgs &a, int tiles_x, int tiles_y, hipStream_t s);
 // fp32 [rows][ld] (first C columns, C % 8 == 0) -> bf16 hi/mid/lo planes [rows][C]
 void launch_split3(const float *src, int ld, long rows, int C, unsigned short *dst, hipStream_t s);
 

@@ -14,97 +14,24 @@
 // MFMA time per FLOP (tests/test_conv_gpu.py holds both paths to the same
 // fp64-referenced tolerance).
 //
-// Tiling: WGM x WGN waves (4 or 8), block tile BM x BN x 16; each wave owns a
-// (BM/WGM) x (BN/WGN) tile of 32x32 accumulators (v_mfma_f32_32x32x16_bf16).
-// Operands are staged global -> registers and split into hi/mid/lo planes
-// while being written to LDS:
-//   KC operands (rows contiguous along k: FWD/DGRAD activations, DGRAD
-//   weights): [plane][row][16 k] image, 32-byte rows whose two 16-byte halves
-//   are XOR-swizzled by row bit 3; the 32x32x16 operand is one conflict-free
-//   ds_read_b128 per lane.
-//   RC operands (k-rows contiguous along the GEMM column: FWD weights, both
-//   WGRAD operands): [plane][16 k][cols] image, stored as loaded (8-byte
-//   writes of 4 columns) and transposed by the read -- two ds_read_b64_tr_b16
-//   per operand (4 k-rows each); 16-dword blocks XOR-swizzled by k so the four
-//   rows of one transposed read land on distinct banks.
-// Double-buffered LDS, one barrier per K-tile, the MFMA chain split around
-// the staging of the next tiles, as in k_conv_gemm.
-#include "conv_impl.h"
+// Operands arrive pre-split (k_split3 below, or caller-held planes): row r
+// of a plane tensor holds, per 16-channel group, hi[16] mid[16] lo[16].
+// Tiling: WGM x WGN waves (4 or 8), block tile BM x BN x 16 channels; each
+// wave owns a (BM/WGM) x (BN/WGN) tile of 16x16 accumulators
+// (v_mfma_f32_16x16x32_bf16, K = two 16-wide plane pieces).  K-tiles are
+// staged global -> LDS by LDS-DMA (buffer_load ... lds, 1 KiB per wave
+// instruction) into three buffers, two tiles in flight, one barrier per
+// K-tile:
+//   KC images (rows contiguous along k: FWD/DGRAD activations, DGRAD
+//   weights): [plane][row][16 k], read as one ds_read_b128 per lane;
+//   RC images (k-rows contiguous along the GEMM column: FWD weights, both
+//   WGRAD operands): [plane][16 k][cols], XOR-swizzled by k and read
+//   transposed (ds_read_b64_tr_b16).
+// The epilogue is staged through LDS (conv_impl.h conv_epilogue16).
+#include "conv_x6.h"
 #include <algorithm>
 
-#ifndef DG_X6_SCHED
-#define DG_X6_SCHED 1
-#endif
-#ifndef DG_X6_VPM
-#define DG_X6_VPM 3
-#endif
-
 namespace dg {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-
-// (lo_src -> bits 15:0, hi_src -> bits 31:16), round-to-nearest-even
-__device__ __forceinline__ unsigned cvt_pk_bf16(float lo_src, float hi_src) {
-    unsigned r;
-    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo_src), "v"(hi_src));
-    return r;
-}
-
-// exact three-way split of the pair (x0, x1) into packed bf16 planes
-__device__ __forceinline__ void split3(float x0, float x1, unsigned &h, unsigned &m, unsigned &l) {
-    h = cvt_pk_bf16(x0, x1);
-    const float r0 = x0 - __uint_as_float(h << 16);
-    const float r1 = x1 - __uint_as_float(h & 0xffff0000u);
-    m = cvt_pk_bf16(r0, r1);
-    const float s0 = r0 - __uint_as_float(m << 16);
-    const float s1 = r1 - __uint_as_float(m & 0xffff0000u);
-    l = cvt_pk_bf16(s0, s1);
-}
-
-// LDS plane images (bf16), read by v_mfma_f32_16x16x32_bf16 fragments whose
-// 32-wide K is two 16-wide plane pieces side by side (see the kernel):
-//   KC image [rows][16 k], 32-byte rows: lane l of a read takes row l&15 and
-//   the 8-k half (l>>4)&1 of plane (l>>5 ? P1 : P0) -- conflict-free as is.
-//   RC image [16 k][COLS], read transposed (ds_read_b64_tr_b16): the 8-dword
-//   blocks of k-row k are XOR-swizzled by f(k) so the eight k-rows one 32-lane
-//   half touches (k and k+8 for 4 consecutive k) land on distinct banks.
-// (Both verified exhaustively against the gfx950 bank model for 64/128/256.)
-__device__ __forceinline__ int x6_off(int row, int half) { return row * 32 + 16 * half; }
-
-template <int COLS>
-__device__ __forceinline__ int x6_rc_swz(int k) {  // in dwords
-    return COLS >= 128 ? 8 * ((k & 3) | (((k >> 3) & 1) << 2)) : 8 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
-}
-// byte offset of bf16 element (k, col) in a [16][COLS] plane image (col even)
-template <int COLS>
-__device__ __forceinline__ int x6_rc_off(int k, int col) {
-    return 4 * (k * (COLS / 2) + ((col >> 1) ^ x6_rc_swz<COLS>(k)));
-}
-
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-
-// 16x16x32 operand fragment of an RC image pair: lane l gets column
-// c0 + (l&15) at k = 8(l>>4) + 0..7 of the concatenated K, i.e. k-rows
-// 8((l>>4)&1) + 0..7 of plane P0 (l < 32) or P1 (l >= 32); two transposed reads
-template <int COLS>
-__device__ __forceinline__ bf16x8 x6_rc_frag(const char *p0, const char *p1, int c0, int lane) {
-    const int g = lane >> 4, i = lane & 15, q = i >> 2, pp = i & 3;
-    const char *pl = g < 2 ? p0 : p1;
-    const int col = c0 + 4 * pp, k = 8 * (g & 1) + q;
-    lds_s16x4 *a0 = (lds_s16x4 *)(pl + x6_rc_off<COLS>(k, col));
-    lds_s16x4 *a1 = (lds_s16x4 *)(pl + x6_rc_off<COLS>(k + 4, col));
-    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(a0);
-    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(a1);
-    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-}
-// the same from a KC image pair: one 16-byte read per lane
-__device__ __forceinline__ bf16x8 x6_kc_frag(const char *p0, const char *p1, int r0, int lane) {
-    const int g = lane >> 4;
-    return *reinterpret_cast<const bf16x8 *>((g < 2 ? p0 : p1) + x6_off(r0 + (lane & 15), g & 1));
-}
 
 // Split pass: fp32 [rows][ld] (first C columns, C % 16 == 0) -> the packed
 // bf16 plane layout of the bf16x6 GEMM: row r holds, per 16-column group j,
@@ -139,14 +66,6 @@ k_split3(const float *__restrict__ src, int ld, long rows, int C, unsigned short
     }
 }
 
-// wait until at most N of this wave's DMAs are in flight (compile-time N: no
-// runtime switch in the K-tile body)
-template <int N>
-__device__ __forceinline__ void wait_dma_c() {
-    static_assert(N >= 0 && N <= 63, "vmcnt range");
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
 // The GEMM.  A and B of GemmArgs point at the operands' packed bf16 planes
 // (k_split3 output); lda / ldb are their column counts C (rows are 3C
 // elements), a_bytes / b_bytes their extents.
@@ -177,9 +96,6 @@ k_conv_gemm_x6(const GemmArgs p) {
     __shared__ __attribute__((aligned(16))) char smem1[BUF];
     __shared__ __attribute__((aligned(16))) char smem2[BUF];
     __shared__ __attribute__((aligned(16))) char smem3[NBUF == 4 ? BUF : 16];
-    // landing block of the DMAs of dead slots (their source offset is out of
-    // range, so nothing is fetched; never read)
-    __shared__ __attribute__((aligned(16))) char smem_dead[1024];
 
     const ConvGeom &g = p.g;
     const int tid = threadIdx.x;
@@ -218,7 +134,7 @@ k_conv_gemm_x6(const GemmArgs p) {
     constexpr int A_SL = 3 * BM / 32, B_SL = 3 * BN / 32;          // slots per tile
     constexpr int A_NJ = (A_SL + NW - 1) / NW, B_NJ = (B_SL + NW - 1) / NW;
     struct Slot { int plane, r, c; bool live; };  // KC: row r, half c; RC: k-row r, column c
-    auto slot_of = [&](int d, bool kc, int X) {
+    auto slot_of = [&](int d, bool kc, int X) __attribute__((always_inline)) {
         Slot sl; const int per = X / 32;  // 1-KB blocks per plane image
         sl.plane = d / per;
         const int pos = (d - sl.plane * per) * 1024 + 16 * lane;
@@ -248,11 +164,12 @@ k_conv_gemm_x6(const GemmArgs p) {
         bsl[j].live = d < B_SL;
     }
     // Every wave issues A_NJ + B_NJ DMAs per K-tile: when a slot count is not
-    // a multiple of NW the dead slots of a wave still issue one, with an
-    // out-of-range source into a dummy LDS block.  The DMA count and the
-    // s_waitcnt values are then compile-time and the K-tile body has no
-    // branches, so the scheduler can interleave its DMA / LDS / VALU work
-    // with the MFMAs.
+    // a multiple of NW a wave's dead slots repeat slot 0's DMA (same source,
+    // same LDS bytes, same data), so the DMA count and the s_waitcnt values
+    // are compile-time, the K-tile body has no branches, and every DMA
+    // provably targets the buffer being filled -- a DMA into some other LDS
+    // object would make the compiler drain all DMAs (vmcnt(0)) before the
+    // next fragment read.
     constexpr bool A_ALL = (A_SL % NW) == 0, B_ALL = (B_SL % NW) == 0;
     constexpr int NMINE = A_NJ + B_NJ;
 
@@ -341,7 +258,7 @@ k_conv_gemm_x6(const GemmArgs p) {
             }
         }
     }
-    auto walk_next = [&]() {  // branch-free (selects)
+    auto walk_next = [&]() __attribute__((always_inline)) {  // branch-free (selects)
         const int nb = wk_b + 1;
         const bool wb = nb == TB;
         const int na = wk_a + (wb ? 1 : 0);
@@ -351,17 +268,14 @@ k_conv_gemm_x6(const GemmArgs p) {
         wk_chunk += wa ? 1 : 0;
     };
 
-    const rsrc_t rA = make_rsrc((const float *)p.A, p.a_bytes);
-    const rsrc_t rB = make_rsrc((const float *)p.B, p.b_bytes);
-    typedef __attribute__((address_space(3))) void lds_void;
-    auto dma = [](rsrc_t r, char *lds_base, unsigned off) {
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void *)lds_base, 16, off, 0, 0, 0);
-    };
+    const rsrc4_t rA = make_rsrc4(p.A, p.a_bytes);
+    const rsrc4_t rB = make_rsrc4(p.B, p.b_bytes);
+    auto dma = [](rsrc4_t r, char *lds_base, unsigned off) __attribute__((always_inline)) { dma16(r, lds_base, off); };
     // WGRAD: output pixel -> (n, ho, wo) by multiply-shift division
-    auto fdiv = [](unsigned n, unsigned mul, int shr) { return (__umulhi(n, mul) + n) >> shr; };
+    auto fdiv = [](unsigned n, unsigned mul, int shr) __attribute__((always_inline)) { return (__umulhi(n, mul) + n) >> shr; };
 
     // issue the DMA of the K-tile at k0 (the walker's tile) into LDS buffer sm
-    auto issue_tile = [&](int k0, char *sm) {
+    auto issue_tile = [&](int k0, char *sm) __attribute__((always_inline)) {
         char *As = sm;
         char *Bs = As + 3 * APL;
         // wave-uniform parts of this K-tile's offsets (tap (wk_a, wk_b) of chunk wk_chunk)
@@ -381,9 +295,8 @@ k_conv_gemm_x6(const GemmArgs p) {
         (void)a_delta; (void)b_delta; (void)tap_bit; (void)b_tap_ok;
 #pragma unroll
         for (int j = 0; j < A_NJ; ++j) {
-            const int d = wid + NW * j, per = BM / 32;
+            const int d = asl[j].live ? wid + NW * j : 0, per = BM / 32;
             char *dst = As + asl[j].plane * APL + (d - asl[j].plane * per) * 1024;
-            if constexpr (!A_ALL) dst = asl[j].live ? dst : smem_dead;
             unsigned off;
             bool ok;
             if constexpr (MODE != MODE_WGRAD) {
@@ -397,14 +310,12 @@ k_conv_gemm_x6(const GemmArgs p) {
                 ok = arow_n[j] >= 0 && (int)pix < kend && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
                 off = ((unsigned)(((int)n * g.H + hi) * g.W + wi) * (3 * p.lda) + wg_ci[j]) * 2u;
             }
-            if constexpr (!A_ALL) ok = ok && asl[j].live;
             dma(rA, dst, ok ? off : DG_OOB);
         }
 #pragma unroll
         for (int j = 0; j < B_NJ; ++j) {
-            const int d = wid + NW * j, per = BN / 32;
+            const int d = bsl[j].live ? wid + NW * j : 0, per = BN / 32;
             char *dst = Bs + bsl[j].plane * BPL + (d - bsl[j].plane * per) * 1024;
-            if constexpr (!B_ALL) dst = bsl[j].live ? dst : smem_dead;
             unsigned off;
             bool ok;
             if constexpr (MODE == MODE_FWD) {  // w[k][co], k = (tap, ci); RC: k-row r, columns c..c+7
@@ -419,13 +330,12 @@ k_conv_gemm_x6(const GemmArgs p) {
                 ok = col < p.N && pix < kend;
                 off = ((unsigned)pix * (3 * p.ldb) + (col >> 4) * 48 + 16 * bsl[j].plane + (col & 8)) * 2u;
             }
-            if constexpr (!B_ALL) ok = ok && bsl[j].live;
             dma(rB, dst, ok ? off : DG_OOB);
         }
         if constexpr (MODE != MODE_WGRAD) walk_next();
     };
     // barrier without the vmcnt(0) drain of __syncthreads (DMAs stay in flight)
-    auto barrier = []() {
+    auto barrier = []() __attribute__((always_inline)) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
@@ -443,7 +353,7 @@ k_conv_gemm_x6(const GemmArgs p) {
     //   [hi|mid].[hi;mid] = hi.hi + mid.mid,  [hi|mid].[mid;hi] = hi.mid + mid.hi,
     //   [hi|lo].[lo;hi]   = hi.lo + lo.hi.
     auto read_frags = [&](const char *sm, bf16x8 (&ahm)[TM], bf16x8 (&ahl)[TM], bf16x8 (&b1)[TN],
-                          bf16x8 (&b2)[TN], bf16x8 (&b3)[TN]) {
+                          bf16x8 (&b2)[TN], bf16x8 (&b3)[TN]) __attribute__((always_inline)) {
         const char *A0 = sm, *A1 = sm + APL, *A2 = sm + 2 * APL;
         const char *B0 = sm + 3 * APL, *B1 = B0 + BPL, *B2 = B0 + 2 * BPL;
 #pragma unroll
@@ -479,7 +389,7 @@ k_conv_gemm_x6(const GemmArgs p) {
     // kt+2 .. kt+AHEAD are outstanding and crosses the barrier.  DMAs past nk
     // fetch harmless data into idle buffers.
     constexpr int AHEAD = NBUF - 1;
-    auto ktile = [&](int kt, const char *cur, char *nxt) {
+    auto ktile = [&](int kt, const char *cur, char *nxt) __attribute__((always_inline)) {
         bf16x8 ahm[TM], ahl[TM], b1[TN], b2[TN], b3[TN];
         read_frags(cur, ahm, ahl, b1, b2, b3);
         issue_tile(kbeg + (kt + AHEAD) * BK, nxt);
@@ -501,38 +411,56 @@ k_conv_gemm_x6(const GemmArgs p) {
         wait_dma_c<(AHEAD - 1) * NMINE>();
         barrier();
     };
-    issue_tile(kbeg, smem0);
-    issue_tile(kbeg + BK, smem1);
-    if constexpr (NBUF == 4) issue_tile(kbeg + 2 * BK, smem2);
-    wait_dma_c<(AHEAD - 1) * NMINE>();
-    barrier();
-    int kt = 0;
-    if constexpr (NBUF == 3) {
-        for (; kt + 2 < nk; kt += 3) {
-            ktile(kt, smem0, smem2);
-            ktile(kt + 1, smem1, smem0);
-            ktile(kt + 2, smem2, smem1);
+    auto pipeline = [&](char *L0, char *L1, char *L2, char *L3) __attribute__((always_inline)) {
+        issue_tile(kbeg, L0);
+        issue_tile(kbeg + BK, L1);
+        if constexpr (NBUF == 4) issue_tile(kbeg + 2 * BK, L2);
+        wait_dma_c<(AHEAD - 1) * NMINE>();
+        barrier();
+        int kt = 0;
+        if constexpr (NBUF == 3) {
+            for (; kt + 2 < nk; kt += 3) {
+                ktile(kt, L0, L2);
+                ktile(kt + 1, L1, L0);
+                ktile(kt + 2, L2, L1);
+            }
+            if (kt < nk) ktile(kt, L0, L2);
+            if (kt + 1 < nk) ktile(kt + 1, L1, L0);
+        } else {
+            for (; kt + 3 < nk; kt += 4) {
+                ktile(kt, L0, L3);
+                ktile(kt + 1, L1, L0);
+                ktile(kt + 2, L2, L1);
+                ktile(kt + 3, L3, L2);
+            }
+            if (kt < nk) ktile(kt, L0, L3);
+            if (kt + 1 < nk) ktile(kt + 1, L1, L0);
+            if (kt + 2 < nk) ktile(kt + 2, L2, L1);
         }
-        if (kt < nk) ktile(kt, smem0, smem2);
-        if (kt + 1 < nk) ktile(kt + 1, smem1, smem0);
-    } else {
-        for (; kt + 3 < nk; kt += 4) {
-            ktile(kt, smem0, smem3);
-            ktile(kt + 1, smem1, smem0);
-            ktile(kt + 2, smem2, smem1);
-            ktile(kt + 3, smem3, smem2);
-        }
-        if (kt < nk) ktile(kt, smem0, smem3);
-        if (kt + 1 < nk) ktile(kt + 1, smem1, smem0);
-        if (kt + 2 < nk) ktile(kt + 2, smem2, smem1);
-    }
+    };
+    pipeline(smem0, smem1, smem2, smem3);
+
     // every wave's DMAs (including the harmless ones past nk) have landed
     // before smem0 becomes the epilogue's staging area
     wait_dma_c<0>();
     barrier();
     constexpr int STAGE = 16 * (WTN + 4);  // floats per wave
     static_assert(NW * STAGE * 4 <= BUF, "epilogue staging fits in one LDS buffer");
-    conv_epilogue16<MODE, TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, Mrows, ph, phase, split, lane,
+    // GEMM row -> output pixel (DGRAD: the phase's sub-grid; unit stride and
+    // FWD / WGRAD rows are pixels / filter rows); slab rows are GEMM rows
+    const bool ident = MODE != MODE_DGRAD || (g.sh == 1 && g.sw == 1);
+    auto rowmap = [&](int row) __attribute__((always_inline)) -> RowPix {
+        if (row >= Mrows) return RowPix{-1, -1};
+        long pix = row;
+        if constexpr (MODE == MODE_DGRAD) {
+            if (!ident && p.splits == 1) {
+                int ww = row % ph.Wp; int t = row / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
+                pix = (long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw;
+            }
+        }
+        return RowPix{row, pix};
+    };
+    conv_epilogue16<MODE, TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, rowmap, phase, split, lane,
                                   reinterpret_cast<float *>(smem0) + wid * STAGE);
 }
 

@@ -1,0 +1,275 @@
+// Halo-tiled bf16x6 implicit GEMM for stride-1 3x3 convolutions (gfx950):
+// the forward pass of a Conv2D(3, strides=1) and its input gradient -- every
+// VGG19 layer (pix2pix.py:53-67) and the 3x3 convs of the SR family.
+//
+// The generic bf16x6 kernel (conv_x6.hip) stages each K-tile (one filter tap
+// x 16 channels) as BM rows gathered from the activation planes, so each
+// input pixel crosses L2 -> LDS nine times per channel chunk.  Here a block
+// owns a PH x PW = 8 x 16 output patch (its 128 GEMM rows) and stages, per
+// 16-channel chunk, the (PH+2) x (PW+2) = 180-pixel input halo ONCE; the nine
+// taps of the chunk read shifted windows of it.  A fragment of 16 GEMM rows
+// is one patch row, i.e. 16 consecutive halo pixels, so a tap is a constant
+// LDS offset (an immediate on the ds_read) and needs no per-row validity
+// test: padding pixels are fetched out of range and land as zeros.
+//
+// Per block (4 waves, 2x2, wave tile 64 x BN/2 of 16x16 accumulators):
+//   LDS: 2 halo buffers (3 planes x 6 KiB: 180 px x 32 B padded to whole
+//   1-KiB DMAs) + 3 weight K-tile buffers (as conv_x6.hip) = 74.6 KB for
+//   BN = 128, so two blocks share a CU.
+//   Pipeline: weight K-tiles two ahead (three buffers); the halo of chunk
+//   c+1 is fetched during the first five K-tiles of chunk c, one 1-KiB piece
+//   per wave per K-tile, into the other halo buffer.  Every K-tile position
+//   within a chunk is unrolled, so the DMA count of each position -- and so
+//   each s_waitcnt -- is a compile-time constant.
+//   The epilogue maps patch rows to pixels (ragged patches at the image edge
+//   are masked) and is shared with conv_x6.hip (staged through LDS).
+//
+// FWD : y[n,ho,wo]  = sum_{a,b} x [n, ho-pt+a, wo-pl+b] . w[a,b]   (halo origin (-pt, -pl))
+// DGRAD: dx[n,h,w] = sum_{a,b} dy[n, h+pt-a, w+pl-b]  . w[a,b]^T  (origin (pt-2, pl-2), taps mirrored)
+#include "conv_x6.h"
+#include <algorithm>
+#include <type_traits>
+
+namespace dg {
+
+constexpr int HX_PH = 8, HX_PW = 16, HX_K = 3;
+constexpr int HX_HH = HX_PH + HX_K - 1, HX_HW = HX_PW + HX_K - 1;  // 10 x 18 halo
+constexpr int HX_HPX = HX_HH * HX_HW;                              // 180 pixels
+constexpr int HX_HPL = 6 * 1024;                                   // bytes per halo plane image
+constexpr int HX_HDMA = 3 * HX_HPL / 1024;                         // 18 one-KiB DMAs per halo
+static_assert(HX_HPX * 32 <= HX_HPL, "halo plane image");
+
+template <int MODE, int BN>
+__global__ void __launch_bounds__(256, 2)
+k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
+    static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "forward or input gradient");
+    constexpr int BK = 16, NW = 4;
+    constexpr int WTM = 64, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
+    constexpr bool B_KC = MODE == MODE_DGRAD;
+    constexpr int BPL = BN * 32 + 96, BBUF = 3 * BPL;
+    constexpr int B_SL = 3 * BN / 32, B_NJ = (B_SL + NW - 1) / NW;
+    constexpr int H_NJ = (HX_HDMA + NW - 1) / NW;  // halo pieces per wave (5)
+    static_assert(H_NJ < 9, "the halo of the next chunk is issued within one chunk's K-tiles");
+
+    __shared__ __attribute__((aligned(16))) char hal0[3 * HX_HPL];
+    __shared__ __attribute__((aligned(16))) char hal1[3 * HX_HPL];
+    __shared__ __attribute__((aligned(16))) char bs0[BBUF];
+    __shared__ __attribute__((aligned(16))) char bs1[BBUF];
+    __shared__ __attribute__((aligned(16))) char bs2[BBUF];
+
+    const ConvGeom &g = p.g;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid >> 1, wn = wid & 1;
+
+    int split, tile;
+    xcd_remap(split, tile);
+    const int mt = tile / p.ntiles;
+    const int nt = tile - mt * p.ntiles;
+    const int n0 = nt * BN;
+    const int tx = mt % tiles_x;
+    const int t_ = mt / tiles_x;
+    const int ty = t_ % tiles_y;
+    const int nimg = t_ / tiles_y;
+    // A source (FWD: x; DGRAD: dy) and output extents
+    const int Hin = MODE == MODE_FWD ? g.H : g.Ho, Win = MODE == MODE_FWD ? g.W : g.Wo;
+    const int Hout = MODE == MODE_FWD ? g.Ho : g.H, Wout = MODE == MODE_FWD ? g.Wo : g.W;
+    const int oy = ty * HX_PH + (MODE == MODE_FWD ? -g.pt : g.pt - (HX_K - 1));
+    const int ox = tx * HX_PW + (MODE == MODE_FWD ? -g.pl : g.pl - (HX_K - 1));
+    // channel chunks of this split (kchunk is a multiple of 9 taps x 16 channels)
+    const int nch = p.K / (9 * BK);
+    const int cbeg = split * (p.kchunk / (9 * BK));
+    const int cend = min(nch, cbeg + p.kchunk / (9 * BK));
+    if (cbeg >= cend) return;
+
+    const rsrc4_t rA = make_rsrc4(p.A, p.a_bytes);
+    const rsrc4_t rB = make_rsrc4(p.B, p.b_bytes);
+    auto dma = [](rsrc4_t r, char *lds_base, unsigned off) __attribute__((always_inline)) { dma16(r, lds_base, off); };
+    auto barrier = []() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+
+    // ---- halo pieces: wave piece s is DMA d = wid + NW*s of the 18 (plane,
+    // KiB) pieces (d >= 18 repeats piece d - 18: same bytes, same data, and
+    // every DMA provably targets the halo buffer); lane L of a piece fetches
+    // the 16-byte half-row q = 64k + L of its plane image (halo pixel q/2,
+    // channel half q&1).  hoff: byte offset at chunk 0, or -1 outside the
+    // image / past the 180 pixels.
+    int hoff[H_NJ], hdst[H_NJ];
+#pragma unroll
+    for (int s = 0; s < H_NJ; ++s) {
+        const int d = (wid + NW * s) % HX_HDMA;
+        const int pl = d / 6, kk = d - pl * 6;
+        hdst[s] = pl * HX_HPL + kk * 1024;
+        hoff[s] = -1;
+        const int q = kk * 64 + lane, hp = q >> 1, hh = q & 1;
+        if (hp < HX_HPX) {
+            const int hr = hp / HX_HW, hc = hp - hr * HX_HW;
+            const int iy = oy + hr, ix = ox + hc;
+            if ((unsigned)iy < (unsigned)Hin && (unsigned)ix < (unsigned)Win)
+                hoff[s] = ((((nimg * Hin + iy) * Win + ix) * (3 * p.lda)) + 16 * pl + 8 * hh) * 2;
+        }
+    }
+    auto issue_h = [&](int s, int chunk, char *hal) __attribute__((always_inline)) {
+        dma(rA, hal + hdst[s], hoff[s] >= 0 ? (unsigned)(hoff[s] + chunk * 96) : DG_OOB);
+    };
+
+    // ---- weight K-tile slots (as conv_x6.hip): FWD RC image [16 k][BN],
+    // DGRAD KC image [BN rows ci][16 k]
+    int bbase[B_NJ];
+    bool bok[B_NJ];
+    int bdst[B_NJ];
+#pragma unroll
+    for (int j = 0; j < B_NJ; ++j) {
+        const int d0 = wid + NW * j;
+        const int d = d0 < B_SL ? d0 : 0;  // a dead slot repeats slot 0's DMA
+        constexpr int per = BN / 32;
+        const int plane = d / per;
+        const int pos = (d - plane * per) * 1024 + 16 * lane;
+        bdst[j] = plane * BPL + (d - plane * per) * 1024;
+        if constexpr (!B_KC) {
+            const int r = pos / (2 * BN);
+            const int pdw = (pos - r * 2 * BN) >> 2;
+            const int swz = BN >= 128 ? 8 * ((r & 3) | (((r >> 3) & 1) << 2)) : 8 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
+            const int col = n0 + 2 * (pdw ^ swz);
+            bok[j] = col < p.N;
+            bbase[j] = (r * (3 * p.ldb) + (col >> 4) * 48 + 16 * plane + (col & 8)) * 2;
+        } else {
+            const int r = pos >> 5, c = (pos >> 4) & 1;
+            const int ci = n0 + r;
+            bok[j] = ci < p.N;
+            bbase[j] = (ci * (3 * p.ldb) + 16 * plane + 8 * c) * 2;
+        }
+    }
+    // tap t = 3a + b of chunk c: FWD rows (t*Ci + 16c) of w[(a,b,ci)][co];
+    // DGRAD rows ci of w[a,b] at co-chunk c
+    auto issue_b = [&](int t, int chunk, char *bs) __attribute__((always_inline)) {
+        int delta;
+        if constexpr (!B_KC) delta = ((t * g.Ci + chunk * BK) * (3 * p.ldb)) * 2;
+        else delta = (t * g.Ci * (3 * p.ldb) + chunk * 48) * 2;
+#pragma unroll
+        for (int j = 0; j < B_NJ; ++j) {
+            dma(rB, bs + bdst[j], bok[j] ? (unsigned)(bbase[j] + delta) : DG_OOB);
+        }
+    };
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // one K-tile: tap T of chunk `chunk` from halo `hc`, weights in bs[T % 3];
+    // issues halo piece T of chunk+1 into `hn` (T < H_NJ) and the weight tile
+    // two K-tiles ahead, then the MFMAs, then waits for the next weight tile
+    auto ktile = [&](auto TT, int chunk, const char *hc, char *hn) __attribute__((always_inline)) {
+        constexpr int T = decltype(TT)::value;
+        constexpr int ta = T / 3, tb = T % 3;
+        constexpr int da = MODE == MODE_FWD ? ta : HX_K - 1 - ta;
+        constexpr int db = MODE == MODE_FWD ? tb : HX_K - 1 - tb;
+        const char *bc = T % 3 == 0 ? bs0 : (T % 3 == 1 ? bs1 : bs2);
+        char *bn = (T + 2) % 3 == 0 ? bs0 : ((T + 2) % 3 == 1 ? bs1 : bs2);
+        bf16x8 ahm[TM], ahl[TM], b1[TN], b2[TN], b3[TN];
+        const char *H0 = hc, *H1 = hc + HX_HPL, *H2 = hc + 2 * HX_HPL;
+#pragma unroll
+        for (int a = 0; a < TM; ++a) {
+            const int r0 = (wm * TM + a + da) * HX_HW + db;
+            ahm[a] = x6_kc_frag(H0, H1, r0, lane);
+            ahl[a] = x6_kc_frag(H0, H2, r0, lane);
+        }
+        const char *B0 = bc, *B1 = bc + BPL, *B2 = bc + 2 * BPL;
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+            const int c0 = wn * WTN + b * 16;
+            if constexpr (B_KC) {
+                b1[b] = x6_kc_frag(B0, B1, c0, lane);
+                b2[b] = x6_kc_frag(B1, B0, c0, lane);
+                b3[b] = x6_kc_frag(B2, B0, c0, lane);
+            } else {
+                b1[b] = x6_rc_frag<BN>(B0, B1, c0, lane);
+                b2[b] = x6_rc_frag<BN>(B1, B0, c0, lane);
+                b3[b] = x6_rc_frag<BN>(B2, B0, c0, lane);
+            }
+        }
+        if constexpr (T < H_NJ) issue_h(T, chunk + 1, hn);
+        if constexpr (T + 2 < 9) issue_b(T + 2, chunk, bn);
+        else issue_b(T + 2 - 9, chunk + 1, bn);
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahm[a], b1[b], acc[a][b], 0, 0, 0);
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahm[a], b2[b], acc[a][b], 0, 0, 0);
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahl[a], b3[b], acc[a][b], 0, 0, 0);
+        // DMAs issued in this K-tile may stay in flight; everything older
+        // (the next weight tile, and at T = 8 the whole next halo) has landed
+        wait_dma_c<B_NJ + (T < H_NJ ? 1 : 0)>();
+        barrier();
+    };
+    auto chunk_tiles = [&](int chunk, const char *hc, char *hn) __attribute__((always_inline)) {
+        ktile(std::integral_constant<int, 0>{}, chunk, hc, hn);
+        ktile(std::integral_constant<int, 1>{}, chunk, hc, hn);
+        ktile(std::integral_constant<int, 2>{}, chunk, hc, hn);
+        ktile(std::integral_constant<int, 3>{}, chunk, hc, hn);
+        ktile(std::integral_constant<int, 4>{}, chunk, hc, hn);
+        ktile(std::integral_constant<int, 5>{}, chunk, hc, hn);
+        ktile(std::integral_constant<int, 6>{}, chunk, hc, hn);
+        ktile(std::integral_constant<int, 7>{}, chunk, hc, hn);
+        ktile(std::integral_constant<int, 8>{}, chunk, hc, hn);
+    };
+
+    // prologue: the whole halo of the first chunk and its first two weight tiles
+#pragma unroll
+    for (int s = 0; s < H_NJ; ++s) issue_h(s, cbeg, hal0);
+    issue_b(0, cbeg, bs0);
+    issue_b(1, cbeg, bs1);
+    wait_dma_c<B_NJ>();
+    barrier();
+    int c = cbeg;
+    for (; c + 1 < cend; c += 2) {
+        chunk_tiles(c, hal0, hal1);
+        chunk_tiles(c + 1, hal1, hal0);
+    }
+    if (c < cend) chunk_tiles(c, hal0, hal1);
+    // every wave's DMAs (including the harmless ones past the last chunk)
+    // have landed before hal0 becomes the epilogue's staging area
+    wait_dma_c<0>();
+    barrier();
+
+    constexpr int STAGE = 16 * (WTN + 4);
+    static_assert(NW * STAGE * 4 <= 3 * HX_HPL, "epilogue staging fits in a halo buffer");
+    // patch row -> output pixel; slab rows are pixels (the split-K reduce of
+    // FWD / unit-stride DGRAD maps slab row = pixel)
+    auto rowmap = [&](int row) __attribute__((always_inline)) -> RowPix {
+        const int ho = ty * HX_PH + (row >> 4), wo = tx * HX_PW + (row & 15);
+        if (ho >= Hout || wo >= Wout) return RowPix{-1, -1};
+        const long pix = ((long)nimg * Hout + ho) * Wout + wo;
+        return RowPix{pix, pix};
+    };
+    conv_epilogue16<MODE, TM, TN>(p, acc, wm * WTM, n0 + wn * WTN, rowmap, 0, split, lane,
+                                  reinterpret_cast<float *>(hal0) + wid * STAGE);
+}
+
+void launch_gemm_x6h(int mode, int bn, dim3 grid, const GemmArgs &a, int tiles_x, int tiles_y, hipStream_t s) {
+    const dim3 blk(256);
+    if (mode == MODE_FWD) {
+        if (bn == 128) hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_FWD, 128>), grid, blk, 0, s, a, tiles_x, tiles_y);
+        else hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_FWD, 64>), grid, blk, 0, s, a, tiles_x, tiles_y);
+    } else {
+        if (bn == 128) hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_DGRAD, 128>), grid, blk, 0, s, a, tiles_x, tiles_y);
+        else hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_DGRAD, 64>), grid, blk, 0, s, a, tiles_x, tiles_y);
+    }
+}
+
+}  // namespace dg

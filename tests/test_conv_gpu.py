@@ -95,6 +95,28 @@ def test_conv_layer(case, math_mode):
         assert err <= 1e-6 * dy.abs().sum(dim=(0, 1, 2)).max().item(), f"{name} dbias: {err:.3e}"
 
 
+# stride-1 3x3 layers on the halo-tiled bf16x6 kernel (csrc/conv_x6h.hip):
+# ragged 8x16 output patches (H, W not multiples of 8 / 16), 'valid' padding,
+# BN 64 and 128, and split-K over channel chunks (small images, many channels)
+HALO_CASES = [
+    ("h.ragged", 4, 40, 36, 64, 128, 3, 1, "same", False, True),
+    ("h.bn64", 2, 16, 16, 256, 64, 3, 1, "same", False, False),
+    ("h.splitk", 2, 8, 8, 512, 512, 3, 1, "same", False, False),
+    ("h.valid", 2, 20, 21, 64, 64, 3, 1, "valid", False, True),
+    ("h.tfpad", 3, 13, 29, 32, 48, 3, 1, (1, 1, 1, 1), False, False),
+]
+
+
+@gpu
+@pytest.mark.parametrize("case", HALO_CASES, ids=[c[0] for c in HALO_CASES])
+def test_conv_halo_kernel(case, monkeypatch):
+    # force the bf16x6 path (the planner keeps small GEMMs on the fp32 kernel);
+    # every stride-1 3x3 bf16x6 FWD / DGRAD plan runs on the halo kernel
+    monkeypatch.setenv("DG_FORCE_X6CFG", "0")
+    monkeypatch.delenv("DG_NO_HALO", raising=False)
+    test_conv_layer(case, "bf16x6")
+
+
 @gpu
 @pytest.mark.parametrize("math_mode", MATHS)
 def test_conv_strided_views_and_accumulate(math_mode):

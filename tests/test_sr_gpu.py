@@ -341,7 +341,11 @@ def _grads_close_l2(arena, ref, label, rtol=2e-2):
         g = arena.grad_of(name).detach().double().cpu().numpy()
         den = float(np.linalg.norm(g_ref))
         if den < 1e-12:
-            assert float(np.abs(g).max()) < 1e-6, (label, name)
+            # an exactly cancelling gradient (e.g. the bias of a conv feeding a
+            # BatchNorm): what remains is the fp32 rounding residual of a sum
+            # over every pixel, ~1e-6 here and dependent on the GEMM's
+            # summation order
+            assert float(np.abs(g).max()) < 5e-6, (label, name)
             continue
         rel = float(np.linalg.norm(g - g_ref)) / den
         assert rel < rtol, f"{label} {name}: relative L2 grad error {rel:.3e}"
