@@ -748,7 +748,7 @@ constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 // bf16x6 kernel configs (conv_x6.hip launch_gemm_x6), K-tile 16
 static const TileCfg kX6Cfgs[] = {
     {128, 128, 2, 2, 16, 2, 2, 1.00}, {128, 64, 2, 2, 16, 2, 2, 1.15}, {64, 128, 2, 2, 16, 2, 2, 1.15},
-    {64, 64, 2, 2, 16, 3, 4, 1.40},   {256, 128, 4, 2, 16, 2, 1, 1.00}, {128, 256, 2, 4, 16, 2, 1, 1.00},
+    {64, 64, 2, 2, 16, 3, 4, 1.40},   {256, 128, 4, 2, 16, 2, 1, 1.00}, {128, 256, 2, 4, 16, 2, 1, 0.90},
 };
 constexpr int kNumX6Cfgs = sizeof(kX6Cfgs) / sizeof(kX6Cfgs[0]);
 
@@ -817,6 +817,8 @@ static bool cfg_vec(const ConvGeom &g, int mode, int bk) {
 //   rounds x (blocks per CU x per-block MFMA work) / (CU peak x occupancy efficiency)
 // + split-K slab traffic, where blocks per CU = min(resident limit, blocks / 256).
 static double choose_tiles(OpPlan &pl, const TileCfg *cfgs, int ncfg, double peak, const char *force_env, void *) {
+    // DG_PLAN_V10=1: the v10 cost model (occupancy in blocks, 128x256 at eff 1.0), for A/B runs
+    static const bool v10 = getenv("DG_PLAN_V10") != nullptr;
     const double cu_flops = peak / 256.0;
     static const double occ_eff[] = {0.0, 0.62, 0.80, 0.88, 0.92};
     int forced = -1;
@@ -834,7 +836,10 @@ static double choose_tiles(OpPlan &pl, const TileCfg *cfgs, int ncfg, double pea
             long blocks = tiles * splits;
             long bpc = std::min<long>(t.bpc, (blocks + 255) / 256);
             double rounds = std::ceil((double)blocks / (256.0 * bpc));
-            double tc = rounds * bpc * 2.0 * t.bm * t.bn * kt_per * t.bk * t.eff / (cu_flops * occ_eff[bpc]);
+            // occupancy in 4-wave units: an 8-wave block counts as two
+            const long occ = v10 ? bpc : std::min<long>(4, bpc * (t.wgm * t.wgn) / 4);
+            const double eff = (v10 && cfgs == kX6Cfgs && c == 5) ? 1.0 : t.eff;
+            double tc = rounds * bpc * 2.0 * t.bm * t.bn * kt_per * t.bk * eff / (cu_flops * occ_eff[occ]);
             double ts = splits > 1 ? (double)splits * pl.nphase * pl.M * pl.N * 8.0 / 5.0e12 + 2e-6 : 0.0;
             if (tc + ts < best_t) { best_t = tc + ts; best = c; best_splits = splits; }
             if (blocks >= 1024) break;
@@ -842,6 +847,7 @@ static double choose_tiles(OpPlan &pl, const TileCfg *cfgs, int ncfg, double pea
     }
     if (best < 0) best = 0;
     pl.cfg = best;
+
     const TileCfg &t = cfgs[best];
     long ktiles = (pl.K + t.bk - 1) / t.bk;
     long kt_per = (ktiles + best_splits - 1) / best_splits;
@@ -937,6 +943,9 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         pl.ws_bytes = pl.x6_b_off + (size_t)6 * rb * cb;
     }
     pl.gemm_bytes = pl.ws_bytes;
+    if (getenv("DG_PLAN_DEBUG"))
+        fprintf(stderr, "[dg plan] mode %d M=%d N=%d K=%d -> %s cfg %d splits %d\n", mode, pl.M, pl.N, pl.K,
+                pl.halo ? "x6h" : (pl.x6 ? "x6" : "fp32"), pl.cfg, pl.splits);
     return pl;
 }
 
