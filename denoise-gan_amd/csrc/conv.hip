@@ -443,6 +443,7 @@ k_splitk_reduce(const GemmArgs p, int V4) {
             f32x4 *dst = reinterpret_cast<f32x4 *>(p.C + off + col);
             if (p.beta != 0.f) o += p.beta * (*dst);
             *dst = o;
+            if (p.yp) store_planes4(p.yp, p.ypC, pix, col, o);
         }
         return;
     }
@@ -464,6 +465,7 @@ k_splitk_reduce(const GemmArgs p, int V4) {
         v = epi_mask(p, pix, col, act_fwd(v, p.act, p.alpha));
         if (p.beta != 0.f) v += p.beta * p.C[off + col];
         p.C[off + col] = v;
+        if (p.yp) store_planes1(p.yp, p.ypC, pix, col, v);
     }
 }
 
@@ -1112,7 +1114,8 @@ static int run_recast(const dg_conv_desc_s *d, int op, const GemmArgs &a0, char 
 static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, const float *B, int ldb,
                       float *C, int ldc, const float *bias, float beta, int act, float alpha,
                       void *ws, size_t ws_bytes, hipStream_t s, const float *mz = nullptr, int ldmz = 0,
-                      int mact = DG_ACT_NONE, float malpha = 0.f, const PlaneRefs *pr = nullptr) {
+                      int mact = DG_ACT_NONE, float malpha = 0.f, const PlaneRefs *pr = nullptr,
+                      unsigned short *yp = nullptr) {
     const int mode = engine_mode(d, op);
     const OpPlan &pl = d->plan[op];
     const size_t need = d->rc[op].on ? d->rc[op].bytes : pl.gemm_bytes;
@@ -1121,6 +1124,15 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
     GemmArgs a = make_args(d->g, pl, A, lda, B, ldb, C, ldc, bias, beta, act, alpha, ws);
     a.mz = mz; a.ldmz = ldmz; a.mact = mact; a.malpha = malpha;
     if (pl.M == 0 || pl.N == 0) return DG_OK;
+    if (yp) {
+        // planes of the output beside it: the GEMM epilogues (fp32, bf16x6,
+        // split-K reduce) write them; the narrow / recast paths (output
+        // channels < 16, never plane-eligible) are refused
+        const int oc = mode == MODE_WGRAD ? 0 : (mode == MODE_FWD ? d->g.Co : d->g.Ci);
+        DG_ARG(oc % 16 == 0 && !pl.narrow && !d->rc[op].on, "output planes need a GEMM path and channels %% 16 == 0");
+        DG_ARG((((uintptr_t)yp) & 15) == 0, "plane buffers must be 16-byte aligned");
+        a.yp = yp; a.ypC = oc;
+    }
     if (d->rc[op].on) {
         DG_ARG(lda % 4 == 0 && ((uintptr_t)A & 15) == 0, "recast path needs lda%%4==0 and 16B-aligned A");
         return run_recast(d, op, a, (char *)ws, s);
@@ -1393,7 +1405,8 @@ int dg_conv_fwd_pl(dg_conv_t d, const float *x, int ldx, const float *w, const f
     int e = dg::plane_refs(d, DG_OP_FWD, planes, r, pr);
     if (e != DG_OK) return e;
     return dg::run_engine(d, DG_OP_FWD, x, ldx, w, d->transpose ? 0 : d->Cout, y, ldy, bias, beta, act, alpha, ws,
-                          ws_bytes, (hipStream_t)stream, nullptr, 0, DG_ACT_NONE, 0.f, pr);
+                          ws_bytes, (hipStream_t)stream, nullptr, 0, DG_ACT_NONE, 0.f, pr,
+                          planes ? (unsigned short *)planes->out : nullptr);
 }
 
 int dg_conv_fwd(dg_conv_t d, const float *x, int ldx, const float *w, const float *bias, float *y, int ldy,
@@ -1414,7 +1427,7 @@ int dg_conv_bwd_data_pl(dg_conv_t d, const float *dy, int lddy, const float *w, 
     if (e != DG_OK) return e;
     return dg::run_engine(d, DG_OP_BWD_DATA, dy, lddy, w, d->transpose ? d->g.Co : 0, dx, lddx, nullptr, beta,
                           DG_ACT_NONE, 0.f, ws, ws_bytes, (hipStream_t)stream, z, z ? ldz : 0,
-                          z ? act : DG_ACT_NONE, alpha, pr);
+                          z ? act : DG_ACT_NONE, alpha, pr, planes ? (unsigned short *)planes->out : nullptr);
 }
 
 int dg_conv_bwd_data(dg_conv_t d, const float *dy, int lddy, const float *w, float *dx, int lddx, float beta,

@@ -11,24 +11,6 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
-// (lo_src -> bits 15:0, hi_src -> bits 31:16), round-to-nearest-even
-__device__ __forceinline__ unsigned cvt_pk_bf16(float lo_src, float hi_src) {
-    unsigned r;
-    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo_src), "v"(hi_src));
-    return r;
-}
-
-// exact three-way split of the pair (x0, x1) into packed bf16 planes
-__device__ __forceinline__ void split3(float x0, float x1, unsigned &h, unsigned &m, unsigned &l) {
-    h = cvt_pk_bf16(x0, x1);
-    const float r0 = x0 - __uint_as_float(h << 16);
-    const float r1 = x1 - __uint_as_float(h & 0xffff0000u);
-    m = cvt_pk_bf16(r0, r1);
-    const float s0 = r0 - __uint_as_float(m << 16);
-    const float s1 = r1 - __uint_as_float(m & 0xffff0000u);
-    l = cvt_pk_bf16(s0, s1);
-}
-
 // LDS plane images (bf16), read by v_mfma_f32_16x16x32_bf16 fragments whose
 // 32-wide K is two 16-wide plane pieces side by side (see the kernel):
 //   KC image [rows][16 k], 32-byte rows: lane l of a read takes row l&15 and

@@ -24,6 +24,7 @@ turns it into a fixed forward + backward schedule for one input shape:
 Nothing here computes on the host: PyTorch only allocates device memory.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -354,6 +355,33 @@ class GraphPlan:
                 for p, p0 in zip(ps, self.cplanes[0].values()):
                     p.dy = p0.dy   # one dy scratch per plan
             self.cplanes.append({n.idx: p for n, p in zip(conv_nodes, ps)})
+        # producer-written planes on conv -> conv chains (VGG19): a conv whose
+        # activation output feeds exactly one conv (premask) writes that
+        # consumer's x planes in its forward epilogue, and the consumer's
+        # input-gradient epilogue writes the producer's dy planes -- no split
+        # pass for either tensor.  Every fed tensor has a buffer of its own.
+        self.fed_x, self.fed_dy = set(), set()
+        for n in (conv_nodes if not os.environ.get("DG_NO_FEED") else []):
+            t = n.out
+            if t.id not in self.premask or cons[t.id][0].kind != "conv":
+                continue
+            c = cons[t.id][0]
+            dn, dc = self.desc[n.idx], self.desc[c.idx]
+            if dn.Cout % 16:
+                continue
+            if dc.plane_mask[ops.OP_FWD] & ops.TENSOR_X:
+                for k in range(slots):
+                    pc = self.cplanes[k][c.idx]
+                    if pc.x is None:
+                        pc.x = ops.PlaneBuf(dc.plane_bytes(ops.TENSOR_X), device)
+                    self.cplanes[k][n.idx].fwd_out = pc.x
+                self.fed_x.add(c.idx)
+            if train and (dn.plane_mask[ops.OP_BWD_DATA] | dn.plane_mask[ops.OP_BWD_FILTER]) & ops.TENSOR_DY:
+                for k in range(slots):
+                    pn = self.cplanes[k][n.idx]
+                    pn.dy = ops.PlaneBuf(dn.plane_bytes(ops.TENSOR_DY), device)
+                    self.cplanes[k][c.idx].bwd_out = pn.dy
+                self.fed_dy.add(n.idx)
         # ---- workspace ----
         ws = [0]
         for n in nodes[1:]:
@@ -425,7 +453,8 @@ class GraphPlan:
                 d = self.desc[n.idx]
                 bias = A.param(f"{n.name}/bias") if n.attrs["bias"] else None
                 P = self.cplanes[slot][n.idx]
-                P.invalidate(ops.TENSOR_X | ops.TENSOR_W)
+                # (a fed input's planes were written by its producer in this pass)
+                P.invalidate(ops.TENSOR_W | (0 if n.idx in self.fed_x else ops.TENSOR_X))
                 d.fwd(xin, A.param(f"{n.name}/kernel"), y, bias=bias, act=n.attrs["act"],
                       alpha=n.attrs["alpha"], ws=ws, planes=P)
             elif k == "bn":
@@ -510,7 +539,8 @@ class GraphPlan:
                 else:
                     dy = dz   # (already multiplied by act'(z) by the consumer when premasked)
                 P = self.cplanes[slot][n.idx]
-                P.invalidate(ops.TENSOR_DY)
+                if n.idx not in self.fed_dy:  # (else written by the consumer's bwd_data just now)
+                    P.invalidate(ops.TENSOR_DY)
                 if pg:
                     db = A.grad_of(f"{n.name}/bias") if n.attrs["bias"] else None
                     d.bwd_filter(s[t_in.id], dy, A.grad_of(f"{n.name}/kernel"), dbias=db, beta=param_beta, ws=ws,

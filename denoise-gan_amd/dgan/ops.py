@@ -100,7 +100,8 @@ TENSOR_X, TENSOR_DY, TENSOR_W = 1, 2, 4
 
 
 class _PlanesC(ctypes.Structure):
-    _fields_ = [("x", ctypes.c_void_p), ("dy", ctypes.c_void_p), ("w", ctypes.c_void_p), ("ready", ctypes.c_int)]
+    _fields_ = [("x", ctypes.c_void_p), ("dy", ctypes.c_void_p), ("w", ctypes.c_void_p), ("out", ctypes.c_void_p),
+                ("ready", ctypes.c_int)]
 
 
 class PlaneBuf:
@@ -128,12 +129,15 @@ class ConvPlanes:
     x / dy / w: PlaneBuf or None.  A conv wrapper called with planes marks
     a buffer ready after its op split that tensor into it; callers
     `invalidate` the tensors that change -- a new forward input or weights,
-    a new output gradient."""
+    a new output gradient.  out: the consumer's PlaneBuf for this layer's
+    output (fwd) or input gradient (bwd_data); the op writes it beside the
+    fp32 tensor and marks it ready (`fwd_out` / `bwd_out`)."""
 
-    __slots__ = ("x", "dy", "w")
+    __slots__ = ("x", "dy", "w", "fwd_out", "bwd_out")
 
-    def __init__(self, x=None, dy=None, w=None):
+    def __init__(self, x=None, dy=None, w=None, fwd_out=None, bwd_out=None):
         self.x, self.dy, self.w = x, dy, w
+        self.fwd_out, self.bwd_out = fwd_out, bwd_out
 
     @classmethod
     def for_desc(cls, d, x=False, dy=False, w=False, device=None):
@@ -163,9 +167,9 @@ class ConvPlanes:
             if b is not None and (bits & t):
                 b.ready = True
 
-    def _c(self):
+    def _c(self, out=None):
         ptr = lambda b: None if b is None else b.buf.data_ptr()
-        return _PlanesC(ptr(self.x), ptr(self.dy), ptr(self.w), self.ready)
+        return _PlanesC(ptr(self.x), ptr(self.dy), ptr(self.w), ptr(out), self.ready)
 
     def _have(self):
         return sum(t for t, b in self._bufs() if b is not None)
@@ -260,9 +264,12 @@ class ConvDesc:
 
     def _pl(self, op, planes):
         """(struct pointer, bits this op fills) for a ConvPlanes (None -> no planes)."""
-        if planes is None or not self.plane_mask[op]:
+        if planes is None:
             return None, 0
-        st = planes._c()
+        out = planes.fwd_out if op == OP_FWD else (planes.bwd_out if op == OP_BWD_DATA else None)
+        if not self.plane_mask[op] and out is None:
+            return None, 0
+        st = planes._c(out)
         return ctypes.byref(st), self.plane_mask[op] & planes._have()
 
     def __del__(self):
@@ -314,6 +321,8 @@ class ConvDesc:
         _prof_end(ev, self, "fwd")
         if fills:
             planes._filled(fills)
+        if planes is not None and planes.fwd_out is not None:
+            planes.fwd_out.ready = True
         return y
 
     def bwd_data(self, dy, w, dx, beta=0.0, ws=None, planes=None):
@@ -334,6 +343,8 @@ class ConvDesc:
         _prof_end(ev, self, "bwd_data")
         if fills:
             planes._filled(fills)
+        if planes is not None and planes.bwd_out is not None:
+            planes.bwd_out.ready = True
         return dx
 
     def bwd_filter(self, x, dy, dw, dbias=None, beta=0.0, ws=None, planes=None):

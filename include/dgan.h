@@ -110,6 +110,9 @@ int dg_conv_bwd_filter(dg_conv_t d, const float *x, int ldx, const float *dy, in
 enum { DG_TENSOR_X = 1, DG_TENSOR_DY = 2, DG_TENSOR_W = 4 };
 typedef struct dg_conv_planes {
     void *x, *dy, *w;  /* plane buffers (NULL: split into the workspace) */
+    void *out;         /* if not NULL: the op also writes the planes of its output
+                          (fwd: y, bwd_data: dx; channels % 16 == 0) -- the
+                          consumer's x / dy planes, with no split pass */
     int ready;         /* DG_TENSOR_* bits whose buffer already holds the split */
 } dg_conv_planes_t;
 int dg_conv_planes_size(dg_conv_t d, int tensor, size_t *bytes);

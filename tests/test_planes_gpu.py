@@ -100,3 +100,57 @@ def test_planes_ignored_by_fp32_and_narrow_plans():
     torch.cuda.synchronize()
     assert torch.equal(y0, y1)
     assert P.ready == 0
+
+
+@gpu
+@pytest.mark.parametrize("halo", [True, False])
+def test_output_planes_feed_the_next_conv(halo, monkeypatch):
+    """dg_conv_planes_t.out: a conv writes the planes of its output (fwd) or
+    input gradient (bwd_data) for the next conv, which then reads them
+    instead of splitting -- results bit-identical to splitting (VGG19 chains,
+    GraphPlan fed_x / fed_dy).  Covers the halo kernel (3x3 s1) and the
+    generic kernel + split-K reduce (4x4 s2)."""
+    monkeypatch.setenv("DG_FORCE_X6CFG", "0")  # bf16x6 plans at these small sizes
+    if halo:
+        d1 = ops.ConvDesc(4, 32, 32, 64, 64, 3, 1, "same", math="bf16x6")
+        d2 = ops.ConvDesc(4, 32, 32, 64, 128, 3, 1, "same", math="bf16x6")
+    else:
+        d1 = ops.ConvDesc(8, 32, 32, 64, 128, 4, 2, "same", math="bf16x6")
+        d2 = ops.ConvDesc(8, 16, 16, 128, 256, 4, 2, "same", math="bf16x6")
+    assert d2.plane_mask[ops.OP_FWD] & ops.TENSOR_X and d1.plane_mask[ops.OP_BWD_DATA] & ops.TENSOR_DY
+    x = _rand((d1.N, d1.H, d1.W, d1.Cin), 11)
+    w1 = _rand(d1.weight_shape, 12) * 0.05
+    w2 = _rand(d2.weight_shape, 13) * 0.05
+    dz = _rand(d2.out_shape, 14)
+    ws = ops.Workspace()
+    # reference: every op splits its own operands
+    y0 = torch.empty(d1.out_shape, device="cuda")
+    z0 = torch.empty(d2.out_shape, device="cuda")
+    dy0 = torch.empty_like(y0)
+    dx0 = torch.empty_like(x)
+    d1.fwd(x, w1, y0, act="relu", ws=ws)
+    d2.fwd(y0, w2, z0, ws=ws)
+    d2.bwd_data_masked(dz, w2, dy0, y0, "relu", ws=ws)
+    d1.bwd_data(dy0, w1, dx0, ws=ws)
+    # fed: d1.fwd writes d2's x planes, d2.bwd_data writes d1's dy planes
+    p2x = ops.PlaneBuf(d2.plane_bytes(ops.TENSOR_X))
+    p1dy = ops.PlaneBuf(d1.plane_bytes(ops.TENSOR_DY))
+    y1 = torch.empty_like(y0)
+    z1 = torch.full_like(z0, float("nan"))
+    dy1 = torch.empty_like(dy0)
+    dx1 = torch.full_like(dx0, float("nan"))
+    d1.fwd(x, w1, y1, act="relu", ws=ws, planes=ops.ConvPlanes(fwd_out=p2x))
+    assert p2x.ready
+    keep = y1.clone()
+    y1.fill_(float("nan"))     # d2 must read the planes, not the fp32 tensor
+    d2.fwd(y1, w2, z1, ws=ws, planes=ops.ConvPlanes(x=p2x))
+    y1.copy_(keep)
+    d2.bwd_data_masked(dz, w2, dy1, y1, "relu", ws=ws, planes=ops.ConvPlanes(bwd_out=p1dy))
+    assert p1dy.ready
+    keep = dy1.clone()
+    dy1.fill_(float("nan"))
+    d1.bwd_data(dy1, w1, dx1, ws=ws, planes=ops.ConvPlanes(dy=p1dy))
+    torch.cuda.synchronize()
+    assert torch.equal(z0, z1)
+    assert torch.equal(dy0, keep)
+    assert torch.equal(dx0, dx1)
