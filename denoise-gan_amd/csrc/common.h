@@ -48,6 +48,48 @@ __host__ __device__ __forceinline__ bool dropout_keep(uint32_t seed, uint32_t st
     return u >= rate;
 }
 
+// ---- bf16x6 plane layout (k_split3): per pixel row, per 16-channel group,
+// hi[16] mid[16] lo[16] -- the producers that write a consumer's planes
+// directly use these (conv epilogues, max pool)
+// (lo_src -> bits 15:0, hi_src -> bits 31:16), round-to-nearest-even
+__device__ __forceinline__ unsigned cvt_pk_bf16(float lo_src, float hi_src) {
+    unsigned r;
+    asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo_src), "v"(hi_src));
+    return r;
+}
+
+// exact three-way split of the pair (x0, x1) into packed bf16 planes
+__device__ __forceinline__ void split3(float x0, float x1, unsigned &h, unsigned &m, unsigned &l) {
+    h = cvt_pk_bf16(x0, x1);
+    const float r0 = x0 - __uint_as_float(h << 16);
+    const float r1 = x1 - __uint_as_float(h & 0xffff0000u);
+    m = cvt_pk_bf16(r0, r1);
+    const float s0 = r0 - __uint_as_float(m << 16);
+    const float s1 = r1 - __uint_as_float(m & 0xffff0000u);
+    l = cvt_pk_bf16(s0, s1);
+}
+
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+// planes of one output element / of 4 consecutive elements (col % 4 == 0)
+__device__ __forceinline__ void store_planes1(unsigned short *yp, int C, long pix, int col, float x) {
+    unsigned h, m, l;
+    split3(x, 0.f, h, m, l);
+    unsigned short *d = yp + pix * 3 * C + (col >> 4) * 48 + (col & 15);
+    d[0] = (unsigned short)h;
+    d[16] = (unsigned short)m;
+    d[32] = (unsigned short)l;
+}
+__device__ __forceinline__ void store_planes4(unsigned short *yp, int C, long pix, int col, f32x4 v) {
+    unsigned h0, m0, l0, h1, m1, l1;
+    split3(v[0], v[1], h0, m0, l0);
+    split3(v[2], v[3], h1, m1, l1);
+    unsigned short *d = yp + pix * 3 * C + (col >> 4) * 48 + (col & 15);
+    *reinterpret_cast<u32x2_t *>(d) = u32x2_t{h0, h1};
+    *reinterpret_cast<u32x2_t *>(d + 16) = u32x2_t{m0, m1};
+    *reinterpret_cast<u32x2_t *>(d + 32) = u32x2_t{l0, l1};
+}
+
+
 }  // namespace dg
 
 #define DG_ARG(cond, ...)                                  \

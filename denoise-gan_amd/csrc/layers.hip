@@ -218,8 +218,66 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd(int N, int H, int W, int C,
     }
 }
 
+// float4 over channels (C % 4 == 0, 16-byte rows): one thread per (window,
+// 4 channels).  yp / dxp: optional bf16x6 planes of the output / input
+// gradient (C % 16 == 0) for the conv that consumes it -- no split pass.
+__global__ void __launch_bounds__(256) k_maxpool_fwd4(int N, int H, int W, int C, const float *x, int ldx, float *y,
+                                                     int ldy, unsigned short *yp) {
+    const int Ho = H / 2, Wo = W / 2, C4 = C >> 2;
+    const int total = N * Ho * Wo * C4;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+        const int op = e / C4;
+        const int c = (e - op * C4) * 4;
+        const int wo = op % Wo, t = op / Wo, ho = t % Ho, n = t / Ho;
+        const long ip = ((long)n * H + 2 * ho) * W + 2 * wo;
+        const f32x4 a = *reinterpret_cast<const f32x4 *>(x + ip * ldx + c);
+        const f32x4 b = *reinterpret_cast<const f32x4 *>(x + (ip + 1) * ldx + c);
+        const f32x4 d = *reinterpret_cast<const f32x4 *>(x + (ip + W) * ldx + c);
+        const f32x4 f = *reinterpret_cast<const f32x4 *>(x + (ip + W + 1) * ldx + c);
+        f32x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = fmaxf(fmaxf(a[q], b[q]), fmaxf(d[q], f[q]));
+        *reinterpret_cast<f32x4 *>(y + (long)op * ldy + c) = o;
+        if (yp) store_planes4(yp, C, op, c, o);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_maxpool_bwd4(int N, int H, int W, int C, const float *x, int ldx,
+                                                     const float *dy, int lddy, float *dx, int lddx, float beta,
+                                                     int act, float alpha, unsigned short *dxp) {
+    const int Ho = H / 2, Wo = W / 2, C4 = C >> 2;
+    const int total = N * Ho * Wo * C4;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+        const int op = e / C4;
+        const int c = (e - op * C4) * 4;
+        const int wo = op % Wo, t = op / Wo, ho = t % Ho, n = t / Ho;
+        const long p0 = ((long)n * H + 2 * ho) * W + 2 * wo;
+        const long pp[4] = {p0, p0 + 1, p0 + W, p0 + W + 1};
+        f32x4 v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const f32x4 *>(x + pp[q] * ldx + c);
+        const f32x4 gy = *reinterpret_cast<const f32x4 *>(dy + (long)op * lddy + c);
+        int am[4] = {0, 0, 0, 0};  // first maximum per channel
+#pragma unroll
+        for (int q = 1; q < 4; ++q)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (v[q][k] > v[am[k]][k]) am[k] = q;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            f32x4 g;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) g[k] = am[k] == q ? gy[k] * act_grad_from_out(v[q][k], act, alpha) : 0.f;
+            f32x4 *o = reinterpret_cast<f32x4 *>(dx + pp[q] * lddx + c);
+            if (beta != 0.f) g += beta * *o;
+            *o = g;
+            if (dxp) store_planes4(dxp, C, pp[q], c, g);
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) k_maxpool_bwd_tail(int N, int H, int W, int C, float *dx, int lddx,
-                                                         float beta) {
+                                                         float beta, unsigned short *dxp) {
     const int H2 = H / 2 * 2, W2 = W / 2 * 2;
     const long total = (long)N * H * W * C;
     for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
@@ -230,6 +288,7 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd_tail(int N, int H, int W, i
         if (h < H2 && w < W2) continue;
         float *o = dx + ip * lddx + c;
         *o = beta != 0.f ? beta * *o : 0.f;
+        if (dxp) store_planes1(dxp, C, ip, c, *o);
     }
 }
 
@@ -652,31 +711,63 @@ int dg_act_fwd(int64_t npix, int C, const float *x, int ldx, int act, float alph
     return DG_OK;
 }
 
-int dg_maxpool2_fwd(int N, int H, int W, int C, const float *x, int ldx, float *y, int ldy, dg_stream_t stream) {
+static bool pool_vec4(int C, const void *a, int lda, const void *b, int ldb, const void *c, int ldc) {
+    return C % 4 == 0 && lda % 4 == 0 && ldb % 4 == 0 && ldc % 4 == 0 &&
+           ((((uintptr_t)a) | ((uintptr_t)b) | ((uintptr_t)c)) & 15) == 0;
+}
+
+int dg_maxpool2_fwd_pl(int N, int H, int W, int C, const float *x, int ldx, float *y, int ldy, void *y_planes,
+                       dg_stream_t stream) {
     DG_ARG(x && y, "NULL tensor");
     DG_ARG(N > 0 && H >= 2 && W >= 2 && C > 0 && ldx >= C && ldy >= C, "bad shape");
     const long total = (long)N * (H / 2) * (W / 2) * C;
-    hipLaunchKernelGGL(dg::k_maxpool_fwd, dim3(dg::lgrid(total)), dim3(256), 0, (hipStream_t)stream, N, H, W, C, x, ldx,
-                       y, ldy);
+    DG_ARG(total < (1L << 31), "tensor too large");
+    const bool v4 = pool_vec4(C, x, ldx, y, ldy, y, ldy);
+    DG_ARG(!y_planes || (v4 && C % 16 == 0 && (((uintptr_t)y_planes) & 15) == 0),
+           "output planes need C %% 16 == 0 and 16-byte aligned rows");
+    if (v4)
+        hipLaunchKernelGGL(dg::k_maxpool_fwd4, dim3(dg::lgrid(total / 4)), dim3(256), 0, (hipStream_t)stream, N, H, W,
+                           C, x, ldx, y, ldy, (unsigned short *)y_planes);
+    else
+        hipLaunchKernelGGL(dg::k_maxpool_fwd, dim3(dg::lgrid(total)), dim3(256), 0, (hipStream_t)stream, N, H, W, C, x,
+                           ldx, y, ldy);
     DG_LAUNCHED("maxpool_fwd");
+    return DG_OK;
+}
+
+int dg_maxpool2_fwd(int N, int H, int W, int C, const float *x, int ldx, float *y, int ldy, dg_stream_t stream) {
+    return dg_maxpool2_fwd_pl(N, H, W, C, x, ldx, y, ldy, nullptr, stream);
+}
+
+int dg_maxpool2_bwd_pl(int N, int H, int W, int C, const float *x, int ldx, const float *dy, int lddy, float *dx,
+                       int lddx, float beta, int act, float alpha, void *dx_planes, dg_stream_t stream) {
+    DG_ARG(x && dy && dx, "NULL tensor");
+    DG_ARG(N > 0 && H >= 2 && W >= 2 && C > 0 && ldx >= C && lddy >= C && lddx >= C, "bad shape");
+    DG_ARG(act >= DG_ACT_NONE && act <= DG_ACT_SIGMOID, "unknown activation %d", act);
+    const long total = (long)N * (H / 2) * (W / 2) * C;
+    DG_ARG((long)N * H * W * C < (1L << 31), "tensor too large");
+    const bool v4 = pool_vec4(C, x, ldx, dy, lddy, dx, lddx);
+    DG_ARG(!dx_planes || (v4 && C % 16 == 0 && (((uintptr_t)dx_planes) & 15) == 0),
+           "gradient planes need C %% 16 == 0 and 16-byte aligned rows");
+    unsigned short *dxp = (unsigned short *)dx_planes;
+    if (v4)
+        hipLaunchKernelGGL(dg::k_maxpool_bwd4, dim3(dg::lgrid(total / 4)), dim3(256), 0, (hipStream_t)stream, N, H, W,
+                           C, x, ldx, dy, lddy, dx, lddx, beta, act, alpha, dxp);
+    else
+        hipLaunchKernelGGL(dg::k_maxpool_bwd, dim3(dg::lgrid(total)), dim3(256), 0, (hipStream_t)stream, N, H, W, C, x,
+                           ldx, dy, lddy, dx, lddx, beta, act, alpha);
+    DG_LAUNCHED("maxpool_bwd");
+    if ((H & 1) || (W & 1)) {
+        hipLaunchKernelGGL(dg::k_maxpool_bwd_tail, dim3(dg::lgrid((long)N * H * W * C)), dim3(256), 0,
+                           (hipStream_t)stream, N, H, W, C, dx, lddx, beta, dxp);
+        DG_LAUNCHED("maxpool_bwd_tail");
+    }
     return DG_OK;
 }
 
 int dg_maxpool2_bwd(int N, int H, int W, int C, const float *x, int ldx, const float *dy, int lddy, float *dx,
                     int lddx, float beta, int act, float alpha, dg_stream_t stream) {
-    DG_ARG(x && dy && dx, "NULL tensor");
-    DG_ARG(N > 0 && H >= 2 && W >= 2 && C > 0 && ldx >= C && lddy >= C && lddx >= C, "bad shape");
-    DG_ARG(act >= DG_ACT_NONE && act <= DG_ACT_SIGMOID, "unknown activation %d", act);
-    const long total = (long)N * (H / 2) * (W / 2) * C;
-    hipLaunchKernelGGL(dg::k_maxpool_bwd, dim3(dg::lgrid(total)), dim3(256), 0, (hipStream_t)stream, N, H, W, C, x, ldx,
-                       dy, lddy, dx, lddx, beta, act, alpha);
-    DG_LAUNCHED("maxpool_bwd");
-    if ((H & 1) || (W & 1)) {
-        hipLaunchKernelGGL(dg::k_maxpool_bwd_tail, dim3(dg::lgrid((long)N * H * W * C)), dim3(256), 0,
-                           (hipStream_t)stream, N, H, W, C, dx, lddx, beta);
-        DG_LAUNCHED("maxpool_bwd_tail");
-    }
-    return DG_OK;
+    return dg_maxpool2_bwd_pl(N, H, W, C, x, ldx, dy, lddy, dx, lddx, beta, act, alpha, nullptr, stream);
 }
 
 int dg_upsample2_relu_fwd(int N, int H, int W, int C, const float *x, int ldx, float *z, int ldz,

@@ -361,7 +361,36 @@ class GraphPlan:
         # input-gradient epilogue writes the producer's dy planes -- no split
         # pass for either tensor.  Every fed tensor has a buffer of its own.
         self.fed_x, self.fed_dy = set(), set()
-        for n in (conv_nodes if not os.environ.get("DG_NO_FEED") else []):
+        self.pool_out = [dict() for _ in range(slots)]    # maxpool node -> consumer conv's x planes
+        self.pool_gout = [dict() for _ in range(slots)]   # maxpool node -> producer conv's dy planes
+        feed = not os.environ.get("DG_NO_FEED")
+        for m in (nodes[1:] if feed else []):
+            # max pool between two convs: its output is the next conv's input,
+            # its input gradient the previous conv's dy (premask: act' folded in)
+            if m.kind != "maxpool" or m.out.C % 16:
+                continue
+            cs = cons[m.out.id]
+            if len(cs) == 1 and cs[0].kind == "conv" and m.out.id not in self.slice_of:
+                c = cs[0]
+                dc = self.desc[c.idx]
+                if dc.plane_mask[ops.OP_FWD] & ops.TENSOR_X:
+                    for k in range(slots):
+                        pc = self.cplanes[k][c.idx]
+                        if pc.x is None:
+                            pc.x = ops.PlaneBuf(dc.plane_bytes(ops.TENSOR_X), device)
+                        self.pool_out[k][m.idx] = pc.x
+                    self.fed_x.add(c.idx)
+            t_in = m.ins[0]
+            n = t_in.node
+            if train and n.kind == "conv" and t_in.id in self.premask:
+                dn = self.desc[n.idx]
+                if (dn.plane_mask[ops.OP_BWD_DATA] | dn.plane_mask[ops.OP_BWD_FILTER]) & ops.TENSOR_DY:
+                    for k in range(slots):
+                        pn = self.cplanes[k][n.idx]
+                        pn.dy = ops.PlaneBuf(dn.plane_bytes(ops.TENSOR_DY), device)
+                        self.pool_gout[k][m.idx] = pn.dy
+                    self.fed_dy.add(n.idx)
+        for n in (conv_nodes if feed else []):
             t = n.out
             if t.id not in self.premask or cons[t.id][0].kind != "conv":
                 continue
@@ -479,7 +508,7 @@ class GraphPlan:
                         ops.strided_copy(s[t.id], y[..., off:off + t.C])
                     off += t.C
             elif k == "maxpool":
-                ops.maxpool2_fwd(xin, y)
+                ops.maxpool2_fwd(xin, y, planes_out=self.pool_out[slot].get(n.idx))
             elif k == "upsample":
                 ops.upsample2_relu_fwd(xin, y)
             elif k == "dwconv":
@@ -580,7 +609,7 @@ class GraphPlan:
                 if need(t_in):
                     pa = t_in.node.attrs if t_in.id in self.premask else {"act": "none", "alpha": 0.0}
                     ops.maxpool2_bwd(s[t_in.id], dz, gr[t_in.id], beta=beta_of(n, t_in), act=pa["act"],
-                                     alpha=pa["alpha"])
+                                     alpha=pa["alpha"], planes_out=self.pool_gout[slot].get(n.idx))
             elif k == "upsample":
                 if need(t_in):
                     ops.upsample2_relu_bwd(s[t_in.id], dz, gr[t_in.id], beta=beta_of(n, t_in))

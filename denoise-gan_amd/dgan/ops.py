@@ -567,17 +567,24 @@ def act_fwd(x, z, act, alpha=0.3):
     return z
 
 
-def maxpool2_fwd(x, y):
+def maxpool2_fwd(x, y, planes_out=None):
+    """planes_out: PlaneBuf of the consuming conv's input planes, written beside y."""
     N, H, W, C = _nhwc(x)
-    call("dg_maxpool2_fwd", N, H, W, C, _p(x), pix_ld(x, C), _p(y), pix_ld(y, C), _stream())
+    call("dg_maxpool2_fwd_pl", N, H, W, C, _p(x), pix_ld(x, C), _p(y), pix_ld(y, C),
+         None if planes_out is None else _p(planes_out.buf), _stream())
+    if planes_out is not None:
+        planes_out.ready = True
     return y
 
 
-def maxpool2_bwd(x, dy, dx, beta=0.0, act="none", alpha=0.3):
-    """dx = routed dy * act'(x) + beta*dx (act: the activation whose output x is)."""
+def maxpool2_bwd(x, dy, dx, beta=0.0, act="none", alpha=0.3, planes_out=None):
+    """dx = routed dy * act'(x) + beta*dx (act: the activation whose output x is);
+    planes_out: PlaneBuf of the producing conv's dy planes, written beside dx."""
     N, H, W, C = _nhwc(x)
-    call("dg_maxpool2_bwd", N, H, W, C, _p(x), pix_ld(x, C), _p(dy), pix_ld(dy, C), _p(dx), pix_ld(dx, C),
-         float(beta), act_id(act), float(alpha), _stream())
+    call("dg_maxpool2_bwd_pl", N, H, W, C, _p(x), pix_ld(x, C), _p(dy), pix_ld(dy, C), _p(dx), pix_ld(dx, C),
+         float(beta), act_id(act), float(alpha), None if planes_out is None else _p(planes_out.buf), _stream())
+    if planes_out is not None:
+        planes_out.ready = True
     return dx
 
 

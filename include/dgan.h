@@ -242,6 +242,12 @@ int dg_maxpool2_fwd(int N, int H, int W, int C, const float *x, int ldx, float *
  * gradient of the activation that produced the pool input (DG_ACT_NONE: plain MaxPoolGrad) */
 int dg_maxpool2_bwd(int N, int H, int W, int C, const float *x, int ldx, const float *dy, int lddy,
                     float *dx, int lddx, float beta, int act, float alpha, dg_stream_t stream);
+/* the same, also writing the bf16x6 planes (dg_conv_planes_t layout, C % 16 == 0) of y / dx for
+ * the conv that reads them (VGG19: pool -> conv input, pool gradient -> the previous conv's dy) */
+int dg_maxpool2_fwd_pl(int N, int H, int W, int C, const float *x, int ldx, float *y, int ldy, void *y_planes,
+                       dg_stream_t stream);
+int dg_maxpool2_bwd_pl(int N, int H, int W, int C, const float *x, int ldx, const float *dy, int lddy,
+                       float *dx, int lddx, float beta, int act, float alpha, void *dx_planes, dg_stream_t stream);
 /* UpSampling2D(2, 'nearest') + relu (autoencoder.py:117-131): [N,H,W,C] -> [N,2H,2W,C] */
 int dg_upsample2_relu_fwd(int N, int H, int W, int C, const float *x, int ldx, float *z, int ldz,
                           dg_stream_t stream);
