@@ -587,6 +587,117 @@ k_narrow_dgrad(const GemmArgs p, int w_in_lds) {
     }
 }
 
+// DGRAD with a few input channels (Ci = CI <= 8, Co 32 or 64): VGG19
+// block1_conv1's input gradient (3x3 s1, Ci 3) and D.down1's (4x4 s2, Ci 6).  One thread per output
+// pixel of one phase, a block = an 8 x 32 tile of the phase grid; per
+// 32-channel chunk the block stages the dy halo its taps read
+// ((8+TH-1) x (32+TW-1) pixels, 16-byte loads, pixel stride 36 floats so the
+// per-lane ds_read_b128 are conflict-free) and the chunk's weights of the
+// phase's TH x TW taps (read as LDS broadcasts), then runs fp32 FMA chains.
+// dy is read from HBM once (the GEMM recast writes and re-reads a
+// pixels x (taps*Ci) matrix instead).
+constexpr int DIR_PH = 8, DIR_PW = 32, DIR_CC = 32, DIR_CS = DIR_CC + 4;
+
+template <int CI, int TH, int TW>
+__global__ void __launch_bounds__(256)
+k_direct_dgrad(const GemmArgs p, int tiles_x, int tiles_y) {
+    constexpr int HH = DIR_PH + TH - 1, HW = DIR_PW + TW - 1;
+    __shared__ __attribute__((aligned(16))) float hal[HH * HW * DIR_CS];
+    __shared__ __attribute__((aligned(16))) float wl[TH * TW * CI * DIR_CC];
+    const ConvGeom &g = p.g;
+    // the phases of one tile are adjacent blocks, so they share the tile's dy
+    // rows through L2 (phase-major order would re-read dy from HBM per phase)
+    const int nph = g.sh * g.sw;
+    const PhaseInfo ph = phase_info(g, blockIdx.x % nph, g.N);
+    int t = blockIdx.x / nph;
+    const int tx = t % tiles_x;
+    t /= tiles_x;
+    const int ty = t % tiles_y;
+    const int n = t / tiles_y;
+    const int hh0 = ty * DIR_PH, ww0 = tx * DIR_PW;
+    if (hh0 >= ph.Hp || ww0 >= ph.Wp) return;  // block-uniform: this phase's grid is smaller
+    // phase pixel (hh, ww) = output pixel (hh*sh + ph, ww*sw + pw); tap a of
+    // the phase is filter row i0h + a*sh and reads dy row hh + oh - a
+    const int oh = (ph.ph + g.pt - ph.i0h) / g.sh, ow = (ph.pw + g.pl - ph.i0w) / g.sw;
+    const int ho0 = hh0 + oh - (TH - 1), wo0 = ww0 + ow - (TW - 1);
+    const int lr = threadIdx.x / DIR_PW, lc = threadIdx.x % DIR_PW;
+    float acc[CI];
+#pragma unroll
+    for (int ci = 0; ci < CI; ++ci) acc[ci] = 0.f;
+    for (int c0 = 0; c0 < g.Co; c0 += DIR_CC) {
+        __syncthreads();  // every thread is done with the previous chunk
+        for (int e = threadIdx.x; e < HH * HW * (DIR_CC / 4); e += 256) {
+            const int q = e % (DIR_CC / 4), px = e / (DIR_CC / 4);
+            const int r = px / HW, c = px - r * HW;
+            const int ho = ho0 + r, wo = wo0 + c;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if ((unsigned)ho < (unsigned)g.Ho && (unsigned)wo < (unsigned)g.Wo)
+                v = *reinterpret_cast<const f32x4 *>(p.A + ((long)(n * g.Ho + ho) * g.Wo + wo) * p.lda + c0 + 4 * q);
+            *reinterpret_cast<f32x4 *>(&hal[px * DIR_CS + 4 * q]) = v;
+        }
+        for (int e = threadIdx.x; e < TH * TW * CI * DIR_CC; e += 256) {
+            const int cc = e % DIR_CC, k = e / DIR_CC;
+            const int ci = k % CI, tap = k / CI;
+            const int i = ph.i0h + (tap / TW) * g.sh, j = ph.i0w + (tap % TW) * g.sw;
+            wl[e] = (i < g.kh && j < g.kw) ? p.B[((long)(i * g.kw + j) * g.Ci + ci) * g.Co + c0 + cc] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int a = 0; a < TH; ++a)
+#pragma unroll
+            for (int b = 0; b < TW; ++b) {
+                const float *hp = &hal[((lr + TH - 1 - a) * HW + (lc + TW - 1 - b)) * DIR_CS];
+                const float *wp = &wl[(a * TW + b) * CI * DIR_CC];
+#pragma unroll
+                for (int q = 0; q < DIR_CC / 4; ++q) {
+                    const f32x4 d = *reinterpret_cast<const f32x4 *>(hp + 4 * q);
+#pragma unroll
+                    for (int ci = 0; ci < CI; ++ci) {
+                        const f32x4 w = *reinterpret_cast<const f32x4 *>(wp + ci * DIR_CC + 4 * q);
+                        float v = acc[ci];
+                        v = fmaf(d[0], w[0], v);
+                        v = fmaf(d[1], w[1], v);
+                        v = fmaf(d[2], w[2], v);
+                        v = fmaf(d[3], w[3], v);
+                        acc[ci] = v;
+                    }
+                }
+            }
+    }
+    const int hh = hh0 + lr, ww = ww0 + lc;
+    if (hh >= ph.Hp || ww >= ph.Wp) return;
+    const long pix = (long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw;
+    const long off = pix * p.ldc;
+#pragma unroll
+    for (int ci = 0; ci < CI; ++ci) {
+        float v = acc[ci];
+        if (p.bias) v += p.bias[ci];
+        v = epi_mask(p, pix, ci, act_fwd(v, p.act, p.alpha));
+        if (p.beta != 0.f) v += p.beta * p.C[off + ci];
+        p.C[off + ci] = v;
+    }
+}
+
+// direct DGRAD kernels instantiated: (Ci, taps per phase) of the layers above
+// (measured per layer in the training step: VGG block1_conv1 dgrad 0.210 ->
+// 0.172 ms, D.down1 dgrad 0.208 -> 0.127 ms; G.last forward with Co 128 ran
+// 0.239 -> 0.38 ms, so Co > 64 stays on the GEMM recast)
+static bool direct_dgrad_ok(const ConvGeom &g) {
+    if (g.Co % DIR_CC || g.Co > 64) return false;
+    const bool t33 = g.Th == 3 && g.Tw == 3, t22 = g.Th == 2 && g.Tw == 2;
+    return (g.Ci == 3 && (t33 || t22)) || (g.Ci == 6 && t22);
+}
+
+static void launch_direct_dgrad(const GemmArgs &a, hipStream_t s) {
+    const ConvGeom &g = a.g;
+    const int Hp = (g.H + g.sh - 1) / g.sh, Wp = (g.W + g.sw - 1) / g.sw;
+    const int tx = (Wp + DIR_PW - 1) / DIR_PW, ty = (Hp + DIR_PH - 1) / DIR_PH;
+    const dim3 grid((unsigned)(g.N * tx * ty * g.sh * g.sw));
+    if (g.Ci == 3 && g.Th == 3) hipLaunchKernelGGL((k_direct_dgrad<3, 3, 3>), grid, dim3(256), 0, s, a, tx, ty);
+    else if (g.Ci == 3) hipLaunchKernelGGL((k_direct_dgrad<3, 2, 2>), grid, dim3(256), 0, s, a, tx, ty);
+    else hipLaunchKernelGGL((k_direct_dgrad<6, 2, 2>), grid, dim3(256), 0, s, a, tx, ty);
+}
+
 // WGRAD with Co <= 4: partial[split][k=(tap,ci)][co]; thread per ci, loop over pixels.
 __global__ void __launch_bounds__(256)
 k_narrow_wgrad(const GemmArgs p) {
@@ -756,6 +867,7 @@ constexpr int kNumX6Cfgs = sizeof(kX6Cfgs) / sizeof(kX6Cfgs[0]);
 
 struct OpPlan {
     int narrow;      // 1 => VALU narrow kernel
+    int direct;      // narrow DGRAD on k_direct_dgrad (dy halo staged in LDS)
     int x6;          // 1 => bf16x6 split-precision kernel (kX6Cfgs), else fp32 MFMA (kCfgs)
     int cfg;         // tile config index
     int vec;
@@ -979,6 +1091,10 @@ static void plan_recast(dg_conv_desc_s *d, int op) {
         rc.slab_off = al256(rc.v_off + (size_t)P * ntap * 4);
     } else if (mode == MODE_DGRAD) {
         const int nv = ntap * g.Ci;
+        if (direct_dgrad_ok(g) && !getenv("DG_NO_DIRECT")) {
+            d->plan[op].direct = 1;
+            return;
+        }
         if (g.Co % 32 || nv < 8) return;
         const int nvp = (nv + 15) & ~15;  // zero-padded columns (e.g. VGG block1_conv1: 3x3x3 = 27 -> 32)
         long P = (long)g.N * g.Ho * g.Wo;
@@ -1141,6 +1257,9 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
         if (mode == MODE_FWD) {
             hipLaunchKernelGGL(k_narrow_fwd, dim3(dg_cdiv(pl.M, 4)), dim3(256), 0, s, a);
             DG_LAUNCHED("narrow_fwd");
+        } else if (mode == MODE_DGRAD && pl.direct && a.lda % 4 == 0 && ((uintptr_t)a.A & 15) == 0) {
+            launch_direct_dgrad(a, s);
+            DG_LAUNCHED("direct_dgrad");
         } else if (mode == MODE_DGRAD) {
             size_t wbytes = (size_t)d->g.kh * d->g.kw * d->g.Ci * d->g.Co * sizeof(float);
             int in_lds = wbytes <= 64 * 1024;

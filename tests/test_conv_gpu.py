@@ -36,6 +36,13 @@ CASES = [
     ("k3s2", 2, 12, 12, 32, 64, 3, 2, "same", False, True),
     ("k1s1", 2, 6, 6, 64, 3, 1, 1, "same", False, True),
     ("odd", 3, 9, 7, 8, 32, 4, 2, "same", False, False),
+    # input gradients with Cin 3 / 6 on the direct narrow-DGRAD kernel (ragged
+    # 8x32 phase tiles, two 32-channel chunks, k3 s2 phases with fewer taps);
+    # G.last.odd (Co 160 in the conv view) stays on the GEMM recast
+    ("V.b1c1", 2, 37, 45, 3, 64, 3, 1, "same", False, True),
+    ("D.down1.odd", 2, 27, 70, 6, 64, 4, 2, "same", False, False),
+    ("k3s2.c3", 2, 17, 19, 3, 64, 3, 2, "same", False, False),
+    ("G.last.odd", 2, 13, 21, 160, 3, 4, 2, "same", True, True),
 ]
 
 
