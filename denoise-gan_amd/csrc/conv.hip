@@ -937,6 +937,15 @@ static double choose_tiles(OpPlan &pl, const TileCfg *cfgs, int ncfg, double pea
     static const double occ_eff[] = {0.0, 0.62, 0.80, 0.88, 0.92};
     int forced = -1;
     if (const char *f = getenv(force_env)) forced = atoi(f);
+    // fp32 GEMMs with a short K over many rows (the Cin 3/6 layers and the
+    // G.last recast: K 27..128, M >= 64K): per-layer sweep on MI355X (bs32)
+    // has the 128x64 BK-16 three-blocks-per-CU tile fastest on every one
+    // (D.down1 fwd 0.159 -> 0.117 ms, G.last bwd_data 0.188 -> 0.166, G.last
+    // recast 0.241 -> 0.219); the MFMA-time model misses their prologue /
+    // epilogue weight
+    if (forced < 0 && cfgs == kCfgs && pl.K <= 256 && pl.N <= 128 && (long)pl.M * pl.nphase >= 65536 &&
+        !getenv("DG_PLAN_NO_SHORTK"))
+        forced = 6;
     int best = -1; double best_t = 1e30; long best_splits = 1;
     for (int c = 0; c < ncfg; ++c) {
         const TileCfg &t = cfgs[c];
