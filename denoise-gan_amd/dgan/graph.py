@@ -232,6 +232,7 @@ class GraphPlan:
                  alias=None):
         self.g = graph
         self.arena, self.bn = arena, bn_state
+        self._wver = None  # arena.version at the last forward (frozen networks)
         self.device = device
         self.N = N
         self.train = train
@@ -472,6 +473,13 @@ class GraphPlan:
         A = self.arena
         s = self.slots[slot]
         s[g.input.id] = x
+        # weight planes: re-split every forward, except for a frozen network
+        # (VGG19 content loss) whose weights did not change since the last one
+        wbit = ops.TENSOR_W
+        if getattr(A, "frozen", False):
+            if self._wver == A.version:
+                wbit = 0
+            self._wver = A.version
         if out is not None:
             s[g.output.id] = out
         for n in g.nodes[1:]:
@@ -483,7 +491,7 @@ class GraphPlan:
                 bias = A.param(f"{n.name}/bias") if n.attrs["bias"] else None
                 P = self.cplanes[slot][n.idx]
                 # (a fed input's planes were written by its producer in this pass)
-                P.invalidate(ops.TENSOR_W | (0 if n.idx in self.fed_x else ops.TENSOR_X))
+                P.invalidate(wbit | (0 if n.idx in self.fed_x else ops.TENSOR_X))
                 d.fwd(xin, A.param(f"{n.name}/kernel"), y, bias=bias, act=n.attrs["act"],
                       alpha=n.attrs["alpha"], ws=ws, planes=P)
             elif k == "bn":
@@ -650,6 +658,9 @@ class GraphNetwork:
         self.bn = BNState(dict(graph.bn_layers), self.device)
         self.arena.load(init_graph_variables(graph, seed))
         self.trainable = trainable
+        # a frozen network's weights change only through arena.load (version
+        # bump): its bf16x6 weight planes stay valid across forwards
+        self.arena.frozen = not trainable
         self._plans = {}
 
     @property

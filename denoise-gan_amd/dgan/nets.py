@@ -140,6 +140,7 @@ class Arena:
     def load(self, values):
         for n, a in values.items():
             self.param(n).copy_(torch.as_tensor(np.ascontiguousarray(a), dtype=torch.float32))
+        self.version = getattr(self, "version", 0) + 1  # host-side weight writes (frozen nets' plane reuse)
 
     def export(self, buf=None):
         return {n: self._v(self.data if buf is None else buf, n).detach().cpu().numpy().copy()
