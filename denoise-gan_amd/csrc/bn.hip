@@ -328,8 +328,10 @@ template <int V>
 __global__ void __launch_bounds__(256)
 k_bn_bwd_apply(const float *__restrict__ dz, int lddz, const float *__restrict__ z, int ldz,
                const float *__restrict__ y, int ldy, long M, int C, int act, float alpha, float dscale,
-               const float *__restrict__ coef, float *__restrict__ dy, int lddy) {
+               const float *__restrict__ coef, float *__restrict__ dy, int lddy, unsigned short *__restrict__ dyp) {
     // coef = [A | B | D | mean] per channel:  dy = A * dbn + B * (y - mean) + D
+    // dyp (V = 4, C % 16 == 0): dy's bf16x6 planes too, in the packed layout
+    // the consuming conv reads (no split pass before its backward GEMMs)
     const int CV = C / V;
     const long total = M * CV;
     for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
@@ -347,6 +349,9 @@ k_bn_bwd_apply(const float *__restrict__ dz, int lddz, const float *__restrict__
         for (int q = 0; q < V; ++q)
             o[q] = A[q] * (dv[q] * act_grad_from_out(zv[q], act, alpha) * dscale) + B[q] * (yv[q] - Mu[q]) + D[q];
         storev<V>(dy + r * lddy + c, o);
+        if constexpr (V == 4) {
+            if (dyp) store_planes4(dyp, C, r, c, f32x4{o[0], o[1], o[2], o[3]});
+        }
     }
 }
 
@@ -440,6 +445,14 @@ int dg_bn_bwd(int M, int C, const float *dz, int lddz, const float *z, int ldz, 
               const float *gamma, const float *save_mean, const float *save_invstd, int act, float alpha,
               float drop_rate, float *dy, int lddy, float *dgamma, float *dbeta, float beta, void *ws,
               size_t ws_bytes, dg_stream_t stream) {
+    return dg_bn_bwd_pl(M, C, dz, lddz, z, ldz, y, ldy, gamma, save_mean, save_invstd, act, alpha, drop_rate, dy,
+                        lddy, nullptr, dgamma, dbeta, beta, ws, ws_bytes, stream);
+}
+
+int dg_bn_bwd_pl(int M, int C, const float *dz, int lddz, const float *z, int ldz, const float *y, int ldy,
+                 const float *gamma, const float *save_mean, const float *save_invstd, int act, float alpha,
+                 float drop_rate, float *dy, int lddy, void *dy_planes, float *dgamma, float *dbeta, float beta,
+                 void *ws, size_t ws_bytes, dg_stream_t stream) {
     DG_ARG(dz && z && y && save_mean && save_invstd && dy && ws, "NULL tensor");
     DG_ARG(M > 0 && C > 0 && lddz >= C && ldz >= C && ldy >= C && lddy >= C, "bad shape");
     DG_ARG(ws_bytes >= dg::bn_ws_floats(M, C) * sizeof(float), "workspace too small");
@@ -466,12 +479,16 @@ int dg_bn_bwd(int M, int C, const float *dz, int lddz, const float *z, int ldz, 
     hipLaunchKernelGGL(dg::k_bn_bwd_final, dim3(dg_cdiv(C, dg::FIN_C)), dim3(256), 0, s, p1, p2, bp.R, C, (long)M, gamma,
                        save_mean, save_invstd, dgamma, dbeta, beta, coef);
     DG_LAUNCHED("bn_bwd_final");
-    if (dg::vec4_ok(C, {{dz, lddz}, {z, ldz}, {y, ldy}, {dy, lddy}}))
+    const bool av4 = dg::vec4_ok(C, {{dz, lddz}, {z, ldz}, {y, ldy}, {dy, lddy}});
+    unsigned short *dyp = (unsigned short *)dy_planes;
+    DG_ARG(!dyp || (av4 && C % 16 == 0 && (((uintptr_t)dyp) & 15) == 0),
+           "dy planes need C %% 16 == 0, float4-aligned tensors and a 16-byte aligned plane buffer");
+    if (av4)
         hipLaunchKernelGGL(dg::k_bn_bwd_apply<4>, dim3(dg::ew_grid((long)M * C / 4)), dim3(256), 0, s, dz, lddz, z,
-                           ldz, y, ldy, (long)M, C, act, alpha, dscale, coef, dy, lddy);
+                           ldz, y, ldy, (long)M, C, act, alpha, dscale, coef, dy, lddy, dyp);
     else
         hipLaunchKernelGGL(dg::k_bn_bwd_apply<1>, dim3(dg::ew_grid((long)M * C)), dim3(256), 0, s, dz, lddz, z, ldz,
-                           y, ldy, (long)M, C, act, alpha, dscale, coef, dy, lddy);
+                           y, ldy, (long)M, C, act, alpha, dscale, coef, dy, lddy, dyp);
     DG_LAUNCHED("bn_bwd_apply");
     return DG_OK;
 }

@@ -37,6 +37,8 @@ _SIGS = {
     "dg_bn_fwd_infer": (c_int, [c_int, c_int, _P, c_int, _P, _P, _P, _P, c_float, _P, c_int, c_int, c_float, _P]),
     "dg_bn_bwd": (c_int, [c_int, c_int, _P, c_int, _P, c_int, _P, c_int, _P, _P, _P, c_int, c_float, c_float, _P,
                           c_int, _P, _P, c_float, _P, c_size_t, _P]),
+    "dg_bn_bwd_pl": (c_int, [c_int, c_int, _P, c_int, _P, c_int, _P, c_int, _P, _P, _P, c_int, c_float, c_float, _P,
+                             c_int, _P, _P, _P, c_float, _P, c_size_t, _P]),
     "dg_act_bwd": (c_int, [c_int, c_int, _P, c_int, _P, c_int, c_int, c_float, _P, c_int, _P]),
     "dg_p2p_loss_workspace_size": (c_int, [c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_size_t)]),
     "dg_p2p_loss": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, _P, _P, c_int,

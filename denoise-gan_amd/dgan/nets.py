@@ -17,6 +17,7 @@ Memory layout (HBM, all fp32 NHWC):
     whose fake half is written directly by the generator's last layer.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -28,6 +29,15 @@ ALPHA = 0.3       # Keras LeakyReLU default (pix2pix.py:121, :213)
 BN_EPS = 1e-3     # Keras BatchNormalization defaults (pix2pix.py:119)
 BN_MOMENTUM = 0.99
 DROP_RATE = 0.5   # pix2pix.py:138
+FEED_DY = not os.environ.get("DG_NO_FEED_DY")  # BN backward writes the conv's dy planes
+
+
+def plane_rows(buf, t, row0):
+    """The bytes of PlaneBuf `buf` holding rows [row0, row0 + rows of t) of a
+    [rows, C] tensor's bf16x6 planes (6 bytes per element)."""
+    C = t.shape[-1]
+    rows = t[..., 0].numel()
+    return buf.buf[row0 * 6 * C:(row0 + rows) * 6 * C]
 
 
 # ---------------------------------------------------------------------------
@@ -339,14 +349,22 @@ class GeneratorPlan:
                 ops.bn_fwd_infer(yh, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.bn.mean[name],
                                  self.bn.var[name], zh, act=act, alpha=ALPHA, eps=BN_EPS)
 
-    def _bn_bwd(self, s, name, dz, z, y, dy, act, beta, ws, drop_rate=0.0):
-        """BN backward per half; the gamma/beta gradients of the halves accumulate."""
+    def _bn_bwd(self, s, name, dz, z, y, dy, act, beta, ws, drop_rate=0.0, P=None):
+        """BN backward per half; the gamma/beta gradients of the halves accumulate.
+        P: the consuming conv's ConvPlanes -- when it keeps dy planes, the BN
+        backward writes them beside dy (no split pass before the conv's
+        backward GEMMs) and marks them ready."""
         A = self.arena
+        feed = P is not None and P.dy is not None
         for hv in range(self.halves):
+            dyh = self._half(dy, hv)
             ops.bn_bwd(self._half(dz, hv), self._half(z, hv), self._half(y, hv), A.param(f"{name}/gamma"),
-                       s["mean"][name][hv], s["inv"][name][hv], self._half(dy, hv), A.grad_of(f"{name}/gamma"),
+                       s["mean"][name][hv], s["inv"][name][hv], dyh, A.grad_of(f"{name}/gamma"),
                        A.grad_of(f"{name}/beta"), act=act, alpha=ALPHA, drop_rate=drop_rate,
-                       beta=beta if hv == 0 else 1.0, ws=ws)
+                       beta=beta if hv == 0 else 1.0, ws=ws,
+                       dy_planes=plane_rows(P.dy, dyh, hv * dyh[..., 0].numel()) if feed else None)
+        if feed:
+            P._filled(ops.TENSOR_DY)
 
     # backward ---------------------------------------------------------------
     def backward(self, dout, slot=0, beta=0.0, ws=None, drop_rate=DROP_RATE, on_grads_ready=None):
@@ -369,11 +387,11 @@ class GeneratorPlan:
             name, ci, co, drop = self.ups[u]
             d = self.udesc[u]
             dy = self._dy(d, co)
+            P = self._bwd_planes(8 + u)
             self._bn_bwd(s, name, self.dcat[u][..., :co], s["cat"][u][..., :co], s["yu"][u], dy, "relu", beta, ws,
-                         drop_rate=drop_rate if drop else 0.0)
+                         drop_rate=drop_rate if drop else 0.0, P=P if FEED_DY else None)
             hin = s["z8"] if u == 0 else s["cat"][u - 1]
             dhin = self.dz8 if u == 0 else self.dcat[u - 1]
-            P = self._bwd_planes(8 + u)
             d.bwd_filter(hin, dy, A.grad_of(f"{name}/kernel"), beta=beta, ws=ws, planes=P)
             d.bwd_data(dy, A.param(f"{name}/kernel"), dhin, ws=ws, planes=P)
             if on_grads_ready:
@@ -384,12 +402,12 @@ class GeneratorPlan:
             dz = self.dz_view(l)
             z = self.z_view(s, l)
             dy = self._dy(d, co)
+            P = self._bwd_planes(l)
             if bn:
-                self._bn_bwd(s, name, dz, z, s["yd"][l], dy, "lrelu", beta, ws)
+                self._bn_bwd(s, name, dz, z, s["yd"][l], dy, "lrelu", beta, ws, P=P if FEED_DY else None)
             else:
                 ops.act_bwd(dz, z, dy, "lrelu", ALPHA)
             hin = s["x"] if l == 0 else self.z_view(s, l - 1)
-            P = self._bwd_planes(l)
             d.bwd_filter(hin, dy, A.grad_of(f"{name}/kernel"), beta=beta, ws=ws, planes=P)
             if l > 0:
                 # accumulate into the skip-gradient already sitting in the concat grad buffer
@@ -546,13 +564,18 @@ class DiscriminatorPlan:
             else:
                 dy = self._dy(d)
                 if bn:
+                    feed = FEED_DY and P is not None and P.dy is not None
                     for k, hv in enumerate(hs):
                         rows = slice(k * self.N, (k + 1) * self.N)
                         ops.bn_bwd(dh[rows], self._half(self.z[i], hv), self._half(self.y[i], hv),
                                    A.param(f"{name}/gamma"), self.mean[name][hv], self.inv[name][hv], dy[rows],
                                    A.grad_of(f"{name}/gamma") if param_grads else None,
                                    A.grad_of(f"{name}/beta") if param_grads else None, act="lrelu", alpha=ALPHA,
-                                   beta=beta if k == 0 else 1.0, ws=ws)
+                                   beta=beta if k == 0 else 1.0, ws=ws,
+                                   dy_planes=plane_rows(P.dy, dy[rows], k * dy[rows][..., 0].numel()) if feed
+                                   else None)
+                    if feed:
+                        P._filled(ops.TENSOR_DY)
                 else:
                     ops.act_bwd(dh, sub(self.z[i]), dy, "lrelu", ALPHA)
                 if param_grads:

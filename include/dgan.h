@@ -156,6 +156,16 @@ int dg_bn_bwd(int M, int C, const float *dz, int lddz, const float *z, int ldz,
               int act, float alpha, float drop_rate,
               float *dy, int lddy, float *dgamma, float *dbeta, float beta,
               void *ws, size_t ws_bytes, dg_stream_t stream);
+/* dg_bn_bwd that also writes dy's bf16x6 operand planes (dg_conv_planes_t.dy layout:
+ * row r, channel c of plane p at r*3C + (c/16)*48 + 16p + c%16; C % 16 == 0, 16-byte
+ * aligned) beside dy, so the consuming conv's bwd_data / bwd_filter skip their split
+ * pass (pass those planes as ready).  dy_planes NULL == dg_bn_bwd. */
+int dg_bn_bwd_pl(int M, int C, const float *dz, int lddz, const float *z, int ldz,
+                 const float *y, int ldy, const float *gamma,
+                 const float *save_mean, const float *save_invstd,
+                 int act, float alpha, float drop_rate,
+                 float *dy, int lddy, void *dy_planes, float *dgamma, float *dbeta, float beta,
+                 void *ws, size_t ws_bytes, dg_stream_t stream);
 /* dy = dz * act'(z)  for blocks without BN (pix2pix.py:118-121 with apply_batchnorm=False) */
 int dg_act_bwd(int M, int C, const float *dz, int lddz, const float *z, int ldz,
                int act, float alpha, float *dy, int lddy, dg_stream_t stream);
