@@ -196,7 +196,8 @@ template <int V>
 __global__ void __launch_bounds__(256)
 k_bn_apply(const float *__restrict__ y, int ld, long M, int C, const float *__restrict__ scale,
            const float *__restrict__ shift, float *__restrict__ z, int ldz, int act, float alpha, float drop_rate,
-           uint32_t seed, const int32_t *step_dev) {
+           uint32_t seed, const int32_t *step_dev, unsigned short *zp0, int zp0C, int zp0col,
+           unsigned short *zp1, int zp1C, int zp1col) {
     const uint32_t step = step_dev ? (uint32_t)*step_dev : 0u;
     const float keep_scale = drop_rate > 0.f ? 1.f / (1.f - drop_rate) : 1.f;
     const int CV = C / V;
@@ -216,6 +217,12 @@ k_bn_apply(const float *__restrict__ y, int ld, long M, int C, const float *__re
             o[q] = act_fwd(t, act, alpha);
         }
         storev<V>(z + r * ldz + c, o);
+        // (V = 4) bf16x6 planes of z for up to two consuming convs, at channel
+        // column col of their [rows][3 C] packed x planes (a concat's slice)
+        if constexpr (V == 4) {
+            if (zp0) store_planes4(zp0, zp0C, r, zp0col + c, f32x4{o[0], o[1], o[2], o[3]});
+            if (zp1) store_planes4(zp1, zp1C, r, zp1col + c, f32x4{o[0], o[1], o[2], o[3]});
+        }
     }
 }
 
@@ -397,6 +404,16 @@ int dg_bn_fwd_train(int M, int C, const float *y, int ldy, const float *gamma, c
                     float *save_invstd, float *moving_mean, float *moving_var, float momentum, float eps, float *z,
                     int ldz, int act, float alpha, float drop_rate, uint32_t drop_seed, const int32_t *step_dev,
                     void *ws, size_t ws_bytes, dg_stream_t stream) {
+    return dg_bn_fwd_train_pl(M, C, y, ldy, gamma, beta, save_mean, save_invstd, moving_mean, moving_var, momentum,
+                              eps, z, ldz, act, alpha, drop_rate, drop_seed, step_dev, nullptr, 0, 0, nullptr, 0, 0,
+                              ws, ws_bytes, stream);
+}
+
+int dg_bn_fwd_train_pl(int M, int C, const float *y, int ldy, const float *gamma, const float *beta,
+                       float *save_mean, float *save_invstd, float *moving_mean, float *moving_var, float momentum,
+                       float eps, float *z, int ldz, int act, float alpha, float drop_rate, uint32_t drop_seed,
+                       const int32_t *step_dev, void *zp0, int zp0C, int zp0col, void *zp1, int zp1C, int zp1col,
+                       void *ws, size_t ws_bytes, dg_stream_t stream) {
     DG_ARG(y && z && ws, "NULL tensor");
     DG_ARG(M > 0 && C > 0 && ldy >= C && ldz >= C, "bad shape");
     DG_ARG(ws_bytes >= dg::bn_ws_floats(M, C) * sizeof(float), "workspace too small");
@@ -420,12 +437,21 @@ int dg_bn_fwd_train(int M, int C, const float *y, int ldy, const float *gamma, c
     hipLaunchKernelGGL(dg::k_bn_stats_final, dim3(dg_cdiv(C, dg::FIN_C)), dim3(256), 0, s, pn, pmean, pm2, bp.R, C, gamma,
                        beta, save_mean, save_invstd, moving_mean, moving_var, momentum, eps, scale, shift);
     DG_LAUNCHED("bn_stats_final");
-    if (dg::vec4_ok(C, {{y, ldy}, {z, ldz}}))
+    const bool av4 = dg::vec4_ok(C, {{y, ldy}, {z, ldz}});
+    unsigned short *p0 = (unsigned short *)zp0, *p1 = (unsigned short *)zp1;
+    auto pl_ok = [&](const unsigned short *p, int pc, int col) {
+        return !p || (av4 && pc % 16 == 0 && col % 16 == 0 && C % 16 == 0 && col + C <= pc && (((uintptr_t)p) & 15) == 0);
+    };
+    DG_ARG(pl_ok(p0, zp0C, zp0col) && pl_ok(p1, zp1C, zp1col),
+           "z planes need float4-aligned tensors, C and the column %% 16 == 0, col + C <= planes C, 16-byte alignment");
+    if (av4)
         hipLaunchKernelGGL(dg::k_bn_apply<4>, dim3(dg::ew_grid((long)M * C / 4)), dim3(256), 0, s, y, ldy, (long)M, C,
-                           scale, shift, z, ldz, act, alpha, drop_rate, drop_seed, step_dev);
+                           scale, shift, z, ldz, act, alpha, drop_rate, drop_seed, step_dev, p0, zp0C, zp0col, p1,
+                           zp1C, zp1col);
     else
         hipLaunchKernelGGL(dg::k_bn_apply<1>, dim3(dg::ew_grid((long)M * C)), dim3(256), 0, s, y, ldy, (long)M, C,
-                           scale, shift, z, ldz, act, alpha, drop_rate, drop_seed, step_dev);
+                           scale, shift, z, ldz, act, alpha, drop_rate, drop_seed, step_dev, p0, zp0C, zp0col, p1,
+                           zp1C, zp1col);
     DG_LAUNCHED("bn_apply");
     return DG_OK;
 }

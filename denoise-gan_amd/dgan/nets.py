@@ -30,6 +30,13 @@ BN_EPS = 1e-3     # Keras BatchNormalization defaults (pix2pix.py:119)
 BN_MOMENTUM = 0.99
 DROP_RATE = 0.5   # pix2pix.py:138
 FEED_DY = not os.environ.get("DG_NO_FEED_DY")  # BN backward writes the conv's dy planes
+FEED_X = not os.environ.get("DG_NO_FEED_X")    # BN forward writes the next convs' x planes
+
+
+def xrows(buf, row0, rows, C):
+    """The bytes of PlaneBuf `buf` holding rows [row0, row0 + rows) of a
+    [rows, C]-channel tensor's bf16x6 planes."""
+    return buf.buf[row0 * 6 * C:(row0 + rows) * 6 * C]
 
 
 def plane_rows(buf, t, row0):
@@ -300,6 +307,11 @@ class GeneratorPlan:
         s["x"], s["out"] = x, out
         A = self.arena
         P = self._fwd_planes()
+        feed = FEED_X and training
+
+        def xplanes(k):  # plane index k's kept x planes (None: its ops split x themselves)
+            return P[k].x if feed and P[k] is not None else None
+
         h = x
         for l, (name, ci, co, bn) in enumerate(self.downs):
             d = self.ddesc[l]
@@ -309,7 +321,16 @@ class GeneratorPlan:
             else:
                 y = s["yd"][l]
                 d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws, planes=P[l])
-                self._bn_fwd(s, name, y, z, "lrelu", training, ws)
+                # z feeds the next down conv (plane index l+1; down8's z8 feeds
+                # up1, index 8) and, as the skip half of cat[6-l], the up conv
+                # reading that concat (index 15-l, its columns after up 6-l's)
+                nxt = l + 1
+                outs = [(nxt, co, 0)] if xplanes(nxt) is not None else []
+                if 1 <= l <= 6 and xplanes(15 - l) is not None:
+                    outs.append((15 - l, self.ups[7 - l][1], self.ups[6 - l][2]))
+                self._bn_fwd(s, name, y, z, "lrelu", training, ws, outs=outs)
+                if xplanes(nxt) is not None:
+                    P[nxt]._filled(ops.TENSOR_X)
             h = z
         for u, (name, ci, co, drop) in enumerate(self.ups):
             d = self.udesc[u]
@@ -317,8 +338,17 @@ class GeneratorPlan:
             d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws, planes=P[8 + u])
             z = s["cat"][u][..., :co]
             rate = drop_rate if (drop and training) else 0.0
+            # z is the first half of cat[u], read by plane index 9+u (up u+1, or
+            # last); its skip half came from down 6-u's BN above (down1 is a
+            # conv: cat[6]'s planes are split by its consumer as before)
+            k = 9 + u
+            outs = []
+            if u <= 5 and xplanes(k) is not None:
+                outs.append((k, self.ups[u + 1][1], 0))
             self._bn_fwd(s, name, y, z, "relu", training, ws, rate, lambda hv: dropout_seed(drop_seed, u, hv),
-                         step_dev)
+                         step_dev, outs=outs)
+            if outs:
+                P[k]._filled(ops.TENSOR_X)
             h = s["cat"][u]
         self.ldesc.fwd(h, A.param("last/kernel"), out, bias=A.param("last/bias"), act="tanh", ws=ws, planes=P[15])
         return out
@@ -336,15 +366,19 @@ class GeneratorPlan:
             p.invalidate(ops.TENSOR_DY)
         return p
 
-    def _bn_fwd(self, s, name, y, z, act, training, ws, drop_rate=0.0, seed_of=None, step_dev=None):
+    def _bn_fwd(self, s, name, y, z, act, training, ws, drop_rate=0.0, seed_of=None, step_dev=None, outs=()):
+        """outs: (plane index k, its x channel count, column) -- the BN output is
+        also written into plane k's kept x planes at that column (training)."""
         A = self.arena
         for hv in range(self.halves):
             yh, zh = self._half(y, hv), self._half(z, hv)
             if training:
+                r0 = hv * zh[..., 0].numel()
+                zp = [(xrows(self.planes[k].x, r0, zh[..., 0].numel(), pc), pc, col) for k, pc, col in outs]
                 ops.bn_fwd_train(yh, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), s["mean"][name][hv],
                                  s["inv"][name][hv], self.bn.mean[name], self.bn.var[name], zh, act=act, alpha=ALPHA,
                                  momentum=BN_MOMENTUM, eps=BN_EPS, drop_rate=drop_rate,
-                                 drop_seed=seed_of(hv) if seed_of else 0, step_dev=step_dev, ws=ws)
+                                 drop_seed=seed_of(hv) if seed_of else 0, step_dev=step_dev, ws=ws, z_planes=zp)
             else:
                 ops.bn_fwd_infer(yh, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.bn.mean[name],
                                  self.bn.var[name], zh, act=act, alpha=ALPHA, eps=BN_EPS)
@@ -522,15 +556,22 @@ class DiscriminatorPlan:
             else:
                 y = self.y[i]
                 d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws, planes=P)
+                # z feeds the next conv's kept x planes (training)
+                Pn = self.planes[i + 1]
+                xp = Pn.x if FEED_X and training and Pn is not None else None
                 for hv in range(self.halves):
                     yh, zh = self._half(y, hv), self._half(z, hv)
                     if training:
+                        rows = zh[..., 0].numel()
                         ops.bn_fwd_train(yh, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.mean[name][hv],
                                          self.inv[name][hv], self.bn.mean[name], self.bn.var[name], zh, act="lrelu",
-                                         alpha=ALPHA, momentum=BN_MOMENTUM, eps=BN_EPS, ws=ws)
+                                         alpha=ALPHA, momentum=BN_MOMENTUM, eps=BN_EPS, ws=ws,
+                                         z_planes=[(xrows(xp, hv * rows, rows, co), co, 0)] if xp is not None else ())
                     else:
                         ops.bn_fwd_infer(yh, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.bn.mean[name],
                                          self.bn.var[name], zh, act="lrelu", alpha=ALPHA, eps=BN_EPS)
+                if xp is not None:
+                    Pn._filled(ops.TENSOR_X)
             h = z
 
     def backward(self, dlogits, slot=0, param_grads=True, beta=0.0, input_grad=None, input_beta=0.0, ws=None,

@@ -418,15 +418,18 @@ def _rows(t):
 
 
 def bn_fwd_train(y, gamma, beta, save_mean, save_invstd, moving_mean, moving_var, z, act="none", alpha=0.3,
-                 momentum=0.99, eps=1e-3, drop_rate=0.0, drop_seed=0, step_dev=None, ws=None):
+                 momentum=0.99, eps=1e-3, drop_rate=0.0, drop_seed=0, step_dev=None, ws=None, z_planes=()):
+    """z_planes: up to two (uint8 device tensor, planes C, column) -- packed x
+    planes of consuming convs that also receive z (dg_bn_fwd_train_pl)."""
     C = y.shape[-1]
     M = _rows(y)
     ws = ws or default_workspace()
     buf, n = ws.get(bn_workspace_bytes(M, C))
-    call("dg_bn_fwd_train", M, C, _p(y), pix_ld(y, C), _p(gamma), _p(beta), _p(save_mean), _p(save_invstd),
+    zp = [(t.data_ptr(), int(pc), int(col)) for t, pc, col in z_planes] + [(None, 0, 0)] * (2 - len(z_planes))
+    call("dg_bn_fwd_train_pl", M, C, _p(y), pix_ld(y, C), _p(gamma), _p(beta), _p(save_mean), _p(save_invstd),
          _p(moving_mean), _p(moving_var), float(momentum), float(eps), _p(z), pix_ld(z, C), act_id(act),
-         float(alpha), float(drop_rate), ctypes.c_uint32(drop_seed & 0xFFFFFFFF), _p(step_dev), _p(buf), n,
-         _stream())
+         float(alpha), float(drop_rate), ctypes.c_uint32(drop_seed & 0xFFFFFFFF), _p(step_dev),
+         zp[0][0], zp[0][1], zp[0][2], zp[1][0], zp[1][1], zp[1][2], _p(buf), n, _stream())
     return z
 
 

@@ -145,6 +145,18 @@ int dg_bn_fwd_train(int M, int C, const float *y, int ldy, const float *gamma, c
                     float *z, int ldz, int act, float alpha,
                     float drop_rate, uint32_t drop_seed, const int32_t *step_dev,
                     void *ws, size_t ws_bytes, dg_stream_t stream);
+/* dg_bn_fwd_train that also writes z's bf16x6 operand planes for up to two consuming
+ * convs (zp0 / zp1, NULL = none): channel c of z lands at column col + c of a packed
+ * [rows][3 * planesC] plane buffer (dg_conv_planes_t.x layout; a concat consumer gets
+ * its slice), so those convs skip their x split pass (pass the planes as ready once
+ * every slice is written).  planesC, col and C multiples of 16, 16-byte aligned. */
+int dg_bn_fwd_train_pl(int M, int C, const float *y, int ldy, const float *gamma, const float *beta,
+                       float *save_mean, float *save_invstd,
+                       float *moving_mean, float *moving_var, float momentum, float eps,
+                       float *z, int ldz, int act, float alpha,
+                       float drop_rate, uint32_t drop_seed, const int32_t *step_dev,
+                       void *zp0, int zp0C, int zp0col, void *zp1, int zp1C, int zp1col,
+                       void *ws, size_t ws_bytes, dg_stream_t stream);
 int dg_bn_fwd_infer(int M, int C, const float *y, int ldy, const float *gamma, const float *beta,
                     const float *moving_mean, const float *moving_var, float eps,
                     float *z, int ldz, int act, float alpha, dg_stream_t stream);
