@@ -267,6 +267,9 @@ class GeneratorPlan:
         # bwd_filter, w: fwd -> bwd_data, dy: bwd_filter -> bwd_data)
         descs = self.ddesc + self.udesc + [self.ldesc]
         self.planes = ops.plan_planes(descs, device) if train else [None] * len(descs)
+        # down1 (conv + LeakyReLU, no BN) writes down2's x planes in its epilogue
+        if train and FEED_X and self.planes[1].x is not None:
+            self.planes[0].fwd_out = self.planes[1].x
         self.ws_bytes = max([d.max_ws() for d in self.ddesc + self.udesc + [self.ldesc]] + [self._bn_ws_max()])
 
     @property
@@ -520,6 +523,9 @@ class DiscriminatorPlan:
         # shares the weight planes and splits its own dy
         if train:
             self.planes = ops.plan_planes(self.desc, device)
+            # D.down1 (conv + LeakyReLU, no BN) writes D.down2's x planes in its epilogue
+            if FEED_X and self.planes[1].x is not None:
+                self.planes[0].fwd_out = self.planes[1].x
             self.planes_half = (ops.plan_planes(self.desc_half, device, keep_x=False,
                                                 wbufs=[p.w for p in self.planes])
                                 if self.desc_half is not self.desc else self.planes)
