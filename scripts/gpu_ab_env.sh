@@ -7,7 +7,7 @@ tail -1 gpurun_out/test.log
 B="python bench.py --steps 30 --warmup 8 --no-cpu-baseline"
 for r in 1 2; do
   for v in base "$1"; do
-    if [ "$v" = base ]; then e=""; else e="$v=1"; fi
+    if [ "$v" = base ]; then e=""; else e="$v=${AB_VAL:-1}"; fi
     env $e timeout -k 10 300 $B > gpurun_out/abe_${v}_$r.json 2> gpurun_out/abe_${v}_$r.err || exit 1
     echo "$v $r $(python -c "import json;d=json.loads(open('gpurun_out/abe_${v}_$r.json').read().strip().splitlines()[-1]);print(d['value'],d['core']['value'],d['roofline']['conv_launch_ms_per_step'])")"
   done
