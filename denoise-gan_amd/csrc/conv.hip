@@ -624,16 +624,35 @@ k_direct_dgrad(const GemmArgs p, int tiles_x, int tiles_y) {
     float acc[CI];
 #pragma unroll
     for (int ci = 0; ci < CI; ++ci) acc[ci] = 0.f;
+    // dy halo of a chunk: NL 16-byte loads per thread, all issued before any
+    // is stored; the next chunk's are issued before this chunk's FMAs
+    constexpr int NE = HH * HW * (DIR_CC / 4), NL = (NE + 255) / 256;
+    f32x4 hv[NL];
+    auto load_halo = [&](int c0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+            const int e = threadIdx.x + 256 * k;
+            hv[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (e < NE) {
+                const int q = e % (DIR_CC / 4), px = e / (DIR_CC / 4);
+                const int r = px / HW, c = px - r * HW;
+                const int ho = ho0 + r, wo = wo0 + c;
+                if ((unsigned)ho < (unsigned)g.Ho && (unsigned)wo < (unsigned)g.Wo)
+                    hv[k] = *reinterpret_cast<const f32x4 *>(p.A + ((long)(n * g.Ho + ho) * g.Wo + wo) * p.lda + c0 +
+                                                             4 * q);
+            }
+        }
+    };
+    load_halo(0);
     for (int c0 = 0; c0 < g.Co; c0 += DIR_CC) {
         __syncthreads();  // every thread is done with the previous chunk
-        for (int e = threadIdx.x; e < HH * HW * (DIR_CC / 4); e += 256) {
-            const int q = e % (DIR_CC / 4), px = e / (DIR_CC / 4);
-            const int r = px / HW, c = px - r * HW;
-            const int ho = ho0 + r, wo = wo0 + c;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if ((unsigned)ho < (unsigned)g.Ho && (unsigned)wo < (unsigned)g.Wo)
-                v = *reinterpret_cast<const f32x4 *>(p.A + ((long)(n * g.Ho + ho) * g.Wo + wo) * p.lda + c0 + 4 * q);
-            *reinterpret_cast<f32x4 *>(&hal[px * DIR_CS + 4 * q]) = v;
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+            const int e = threadIdx.x + 256 * k;
+            if (e < NE) {
+                const int q = e % (DIR_CC / 4), px = e / (DIR_CC / 4);
+                *reinterpret_cast<f32x4 *>(&hal[px * DIR_CS + 4 * q]) = hv[k];
+            }
         }
         for (int e = threadIdx.x; e < TH * TW * CI * DIR_CC; e += 256) {
             const int cc = e % DIR_CC, k = e / DIR_CC;
@@ -642,6 +661,7 @@ k_direct_dgrad(const GemmArgs p, int tiles_x, int tiles_y) {
             wl[e] = (i < g.kh && j < g.kw) ? p.B[((long)(i * g.kw + j) * g.Ci + ci) * g.Co + c0 + cc] : 0.f;
         }
         __syncthreads();
+        if (c0 + DIR_CC < g.Co) load_halo(c0 + DIR_CC);
 #pragma unroll
         for (int a = 0; a < TH; ++a)
 #pragma unroll
@@ -680,8 +700,9 @@ k_direct_dgrad(const GemmArgs p, int tiles_x, int tiles_y) {
 
 // direct DGRAD kernels instantiated: (Ci, taps per phase) of the layers above
 // (measured per layer in the training step: VGG block1_conv1 dgrad 0.210 ->
-// 0.172 ms, D.down1 dgrad 0.208 -> 0.127 ms; G.last forward with Co 128 ran
-// 0.239 -> 0.38 ms, so Co > 64 stays on the GEMM recast)
+// 0.172 ms (0.132 with the batched, prefetched halo loads), D.down1 dgrad
+// 0.208 -> 0.122 ms; G.last forward with Co 128 ran 0.239 -> 0.38 ms, so
+// Co > 64 stays on the GEMM recast)
 static bool direct_dgrad_ok(const ConvGeom &g) {
     if (g.Co % DIR_CC || g.Co > 64) return false;
     const bool t33 = g.Th == 3 && g.Tw == 3, t22 = g.Th == 2 && g.Tw == 2;
