@@ -820,17 +820,39 @@ k_recast_col2im(const GemmArgs p, const float *__restrict__ V, int nv) {
         const int h = (int)((pix / g.W) % g.H);
         const int n = (int)(pix / ((long)g.W * g.H));
         float v = 0.f;
-        for (int i = 0; i < g.kh; ++i) {
-            int th = h + g.pt - i;
-            if (th < 0 || th % g.sh) continue;
-            int ho = th / g.sh;
-            if (ho >= g.Ho) continue;
-            for (int j = 0; j < g.kw; ++j) {
-                int tw = w + g.pl - j;
-                if (tw < 0 || tw % g.sw) continue;
-                int wo = tw / g.sw;
-                if (wo >= g.Wo) continue;
-                v += V[((long)(n * g.Ho + ho) * g.Wo + wo) * nv + (i * g.kw + j) * g.Ci + ci];
+        if (g.Th <= 4 && g.Tw <= 4) {
+            // the taps hitting (h, w) are i = i0 + a*sh, j = j0 + b*sw: all their
+            // loads issue before the sum, which adds them in the same (i, j)
+            // order as the loop below (absent taps add +0: the same bits)
+            const int i0 = (h + g.pt) % g.sh, j0 = (w + g.pl) % g.sw;
+            float t[4][4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const int i = i0 + a * g.sh, j = j0 + b * g.sw;
+                    const int ho = (h + g.pt - i) / g.sh, wo = (w + g.pl - j) / g.sw;
+                    const bool ok = a < g.Th && b < g.Tw && i < g.kh && j < g.kw && h + g.pt - i >= 0 &&
+                                    w + g.pl - j >= 0 && ho < g.Ho && wo < g.Wo;
+                    t[a][b] = ok ? V[((long)(n * g.Ho + ho) * g.Wo + wo) * nv + (i * g.kw + j) * g.Ci + ci] : 0.f;
+                }
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) v += t[a][b];
+        } else {
+            for (int i = 0; i < g.kh; ++i) {
+                int th = h + g.pt - i;
+                if (th < 0 || th % g.sh) continue;
+                int ho = th / g.sh;
+                if (ho >= g.Ho) continue;
+                for (int j = 0; j < g.kw; ++j) {
+                    int tw = w + g.pl - j;
+                    if (tw < 0 || tw % g.sw) continue;
+                    int wo = tw / g.sw;
+                    if (wo >= g.Wo) continue;
+                    v += V[((long)(n * g.Ho + ho) * g.Wo + wo) * nv + (i * g.kw + j) * g.Ci + ci];
+                }
             }
         }
         if (p.bias) v += p.bias[ci];
