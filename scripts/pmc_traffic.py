@@ -11,7 +11,7 @@ import csv
 import sys
 from collections import defaultdict
 
-CONV = ("k_conv_gemm", "k_split3", "k_splitk_reduce", "k_narrow", "k_recast", "k_transpose", "k_colsum")
+CONV = ("k_conv_gemm", "k_split3", "k_splitk_reduce", "k_narrow", "k_direct", "k_recast", "k_transpose", "k_colsum")
 
 
 def load(path, counter):
