@@ -42,6 +42,8 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from .decisions import of as _dec
+
 BN_EPS = 1e-3
 VGG_MEAN_BGR = (103.939, 116.779, 123.68)
 
@@ -136,17 +138,18 @@ def lrelu(x, a):
 # --------------------------------------------------------------------------
 # networks
 # --------------------------------------------------------------------------
-def srgan_generator(P, x, stats, scale=4, n_blocks=16, training=True):
-    """srgan.py:129-188."""
+def srgan_generator(P, x, stats, scale=4, n_blocks=16, training=True, dec=None):
+    """srgan.py:129-188.  dec: oracle.decisions.Decisions (activation sites by layer name)."""
+    dec = _dec(dec)
     n = conv(x, P["conv2d/kernel"])
     n = bn(n, P["batch_normalization/gamma"], P["batch_normalization/beta"], "batch_normalization", stats,
            training=training)
-    n = prelu(n, P["p_re_lu/alpha"])
+    n = dec.prelu("p_re_lu", n, P["p_re_lu/alpha"])
     temp = n
     for i in range(n_blocks):
         nn_ = conv(n, P[f"block_{i}_conv1/kernel"])
-        nn_ = F.relu(bn(nn_, P[f"block_{i}_bn1/gamma"], P[f"block_{i}_bn1/beta"], f"block_{i}_bn1", stats,
-                        training=training))
+        nn_ = dec.relu(f"block_{i}_bn1", bn(nn_, P[f"block_{i}_bn1/gamma"], P[f"block_{i}_bn1/beta"],
+                                            f"block_{i}_bn1", stats, training=training))
         nn_ = conv(nn_, P[f"block_{i}_conv2/kernel"])
         nn_ = bn(nn_, P[f"block_{i}_bn2/gamma"], P[f"block_{i}_bn2/beta"], f"block_{i}_bn2", stats,
                  training=training)
@@ -157,12 +160,13 @@ def srgan_generator(P, x, stats, scale=4, n_blocks=16, training=True):
     n = n + temp
     for i in range(scale // 2):
         n = conv(n, P[f"deconv_{i}_conv/kernel"], P[f"deconv_{i}_conv/bias"])
-        n = prelu(depth_to_space(n, 2), P[f"deconv_{i}_p_re_lu/alpha"])
+        n = dec.prelu(f"deconv_{i}_p_re_lu", depth_to_space(n, 2), P[f"deconv_{i}_p_re_lu/alpha"])
     return torch.tanh(conv(n, P["conv2d_out/kernel"], P["conv2d_out/bias"]))
 
 
-def sr_discriminator(P, x, stats, df=32, training=True):
+def sr_discriminator(P, x, stats, df=32, training=True, dec=None):
     """srgan.py:232-272 (logits)."""
+    dec = _dec(dec)
     spec = [(df, 1, False), (df, 2, True), (df, 1, True), (df, 2, True),
             (df * 2, 1, True), (df * 2, 2, True), (df * 2, 1, True), (df * 2, 2, True)]
     h = x
@@ -171,16 +175,19 @@ def sr_discriminator(P, x, stats, df=32, training=True):
         if use_bn:
             h = bn(h, P[f"d{i + 1}_bn/gamma"], P[f"d{i + 1}_bn/beta"], f"d{i + 1}_bn", stats, momentum=0.8,
                    training=training)
-        h = lrelu(h, 0.2)
+        h = dec.lrelu(f"d{i + 1}_bn" if use_bn else f"d{i + 1}_conv", h, 0.2)
     return conv(h, P["logits/kernel"], P["logits/bias"])
 
 
-def fsrgan_generator(P, x, stats, gf=32, n_blocks=6, training=True):
+def fsrgan_generator(P, x, stats, gf=32, n_blocks=6, training=True, dec=None):
     """fsrgan.py:99-214."""
+    dec = _dec(dec)
+
     def B(h, name, momentum=0.99):
         return bn(h, P[f"{name}/gamma"], P[f"{name}/beta"], name, stats, momentum=momentum, training=training)
 
-    c1 = prelu(B(conv(x, P["conv2d/kernel"], P["conv2d/bias"]), "batch_normalization"), P["p_re_lu/alpha"])
+    c1 = dec.prelu("p_re_lu", B(conv(x, P["conv2d/kernel"], P["conv2d/bias"]), "batch_normalization"),
+                   P["p_re_lu/alpha"])
     r = c1
     for bid in range(n_blocks):
         inp = r
@@ -188,11 +195,11 @@ def fsrgan_generator(P, x, stats, gf=32, n_blocks=6, training=True):
         if bid:
             pre = f"block_{bid}_"
             h = conv(h, P[pre + "expand/kernel"], P[pre + "expand/bias"])
-            h = F.relu(B(h, pre + "expand_BN", 0.999))
+            h = dec.relu(pre + "expand_BN", B(h, pre + "expand_BN", 0.999))
         else:
             pre = "expanded_conv_"
         h = dwconv3(h, P[pre + "depthwise/depthwise_kernel"], P[pre + "depthwise/bias"])
-        h = F.relu(B(h, pre + "depthwise_BN", 0.999))
+        h = dec.relu(pre + "depthwise_BN", B(h, pre + "depthwise_BN", 0.999))
         h = conv(h, P[pre + "project/kernel"], P[pre + "project/bias"])
         h = B(h, pre + "project_BN", 0.999)
         r = inp + h if inp.shape[-1] == h.shape[-1] else h
@@ -200,42 +207,46 @@ def fsrgan_generator(P, x, stats, gf=32, n_blocks=6, training=True):
     u = c2
     for i in range(2):
         u = conv(u, P[f"deconv_{i}_conv/kernel"], P[f"deconv_{i}_conv/bias"])
-        u = prelu(depth_to_space(u, 2), P[f"deconv_{i}_p_re_lu/alpha"])
+        u = dec.prelu(f"deconv_{i}_p_re_lu", depth_to_space(u, 2), P[f"deconv_{i}_p_re_lu/alpha"])
     return torch.tanh(conv(u, P["conv2d_out/kernel"], P["conv2d_out/bias"]))
 
 
-def autoencoder_generator(P, x):
+def autoencoder_generator(P, x, dec=None):
     """autoencoder.py:89-185."""
-    def c(h, name, act=F.relu):
-        return act(conv(h, P[f"{name}/kernel"], P[f"{name}/bias"]))
+    dec = _dec(dec)
+
+    def c(h, name, relu=True):
+        y = conv(h, P[f"{name}/kernel"], P[f"{name}/bias"])
+        return dec.relu(name, y) if relu else torch.tanh(y)
 
     h = c(c(x, "conv1"), "conv1b")
-    pool1 = maxpool2(h)
-    pool2 = maxpool2(c(pool1, "conv2"))
-    pool3 = maxpool2(c(pool2, "conv3"))
-    pool4 = maxpool2(c(pool3, "conv4"))
-    pool5 = maxpool2(c(pool4, "conv5"))
+    pool1 = dec.maxpool2("pool1", h)
+    pool2 = dec.maxpool2("pool2", c(pool1, "conv2"))
+    pool3 = dec.maxpool2("pool3", c(pool2, "conv3"))
+    pool4 = dec.maxpool2("pool4", c(pool3, "conv4"))
+    pool5 = dec.maxpool2("pool5", c(pool4, "conv5"))
     h = pool5
-    for lvl, skip in zip((6, 7, 8, 9), (pool4, pool3, pool2, pool1)):
-        h = torch.cat([F.relu(upsample2(h)), skip], dim=3)
+    for k, (lvl, skip) in enumerate(zip((6, 7, 8, 9), (pool4, pool3, pool2, pool1))):
+        h = torch.cat([dec.relu(f"unpool{4 - k}", upsample2(h)), skip], dim=3)
         h = c(c(h, f"conv{lvl}"), f"conv{lvl}b")
-    h = torch.cat([F.relu(upsample2(h)), x], dim=3)
+    h = torch.cat([dec.relu("unpool0", upsample2(h)), x], dim=3)
     h = c(c(h, "conv10"), "conv10b")
-    return c(h, "conv11", torch.tanh)
+    return c(h, "conv11", relu=False)
 
 
 VGG19_BLOCKS = [(64, 2), (128, 2), (256, 4), (512, 4), (512, 4)]
 
 
-def vgg19(P, x):
+def vgg19(P, x, dec=None):
     """VGG19 to block5_conv4 (post-ReLU); x already preprocessed."""
+    dec = _dec(dec)
     h = x
     for b, (_, n) in enumerate(VGG19_BLOCKS):
         for i in range(n):
             name = f"block{b + 1}_conv{i + 1}"
-            h = F.relu(conv(h, P[f"{name}/kernel"], P[f"{name}/bias"]))
+            h = dec.relu(name, conv(h, P[f"{name}/kernel"], P[f"{name}/bias"]))
         if b < 4:
-            h = maxpool2(h)
+            h = dec.maxpool2(f"block{b + 1}_pool", h)
     return h
 
 
@@ -246,10 +257,10 @@ def vgg_preprocess(img):
     return x - torch.tensor(VGG_MEAN_BGR, dtype=x.dtype)
 
 
-def content_loss(PV, hr, sr):
+def content_loss(PV, hr, sr, dec_sr=None, dec_hr=None):
     """srgan.py:69-76."""
-    fs = vgg19(PV, vgg_preprocess(sr)) / 12.75
-    fh = vgg19(PV, vgg_preprocess(hr)) / 12.75
+    fs = vgg19(PV, vgg_preprocess(sr), dec_sr) / 12.75
+    fh = vgg19(PV, vgg_preprocess(hr), dec_hr) / 12.75
     return ((fh - fs) ** 2).mean()
 
 
@@ -298,29 +309,33 @@ class SRState:
         self.vD = {k: np.zeros_like(v) for k, v in self.PD.items()}
         self.iterations = 0
 
-    def generator(self, P, x, training=True):
+    def generator(self, P, x, training=True, dec=None):
         if self.kind == "srgan":
-            return srgan_generator(P, x, self.Gs, self.scale, self.n_blocks, training=training)
+            return srgan_generator(P, x, self.Gs, self.scale, self.n_blocks, training=training, dec=dec)
         if self.kind == "fsrgan":
-            return fsrgan_generator(P, x, self.Gs, training=training)
-        return autoencoder_generator(P, x)
+            return fsrgan_generator(P, x, self.Gs, training=training, dec=dec)
+        return autoencoder_generator(P, x, dec=dec)
 
 
-def train_step(st, x, y, apply=True):
+def train_step(st, x, y, apply=True, dec=None):
     """One step of train_srgan.py:61-118 / train_fsrgan.py:61-120 /
     train_autoencoder.py:66-112 (all three share the gen-loss composition
     content + adv + 0*mse + mae; FSRGAN halves the disc loss).
     Returns dict(losses=(gen_total, adv, mae, mse, content, disc, var),
-    gen, gG, gD)."""
+    gen, gG, gD).  dec: {"G", "Dr", "Df", "Vsr", "Vhr": oracle.decisions.Decisions}
+    (any subset) -- the activation decisions of G(x), D(y), D(G(x)) and VGG19
+    on G(x) and on y (mask-conditioned parity)."""
+    dec = dec or {}
     PG = {k: torch.tensor(v, requires_grad=True) for k, v in st.PG.items()}
     PD = {k: torch.tensor(v, requires_grad=True) for k, v in st.PD.items()}
     PV = None if st.PV is None else {k: torch.tensor(v) for k, v in st.PV.items()}
     xt = torch.tensor(np.asarray(x, np.float64))
     yt = torch.tensor(np.asarray(y, np.float64))
-    gen = st.generator(PG, xt)
-    zr = sr_discriminator(PD, yt, st.Ds)
-    zf = sr_discriminator(PD, gen, st.Ds)
-    cont = content_loss(PV, yt, gen) if PV is not None else torch.zeros((), dtype=torch.float64)
+    gen = st.generator(PG, xt, dec=dec.get("G"))
+    zr = sr_discriminator(PD, yt, st.Ds, dec=dec.get("Dr"))
+    zf = sr_discriminator(PD, gen, st.Ds, dec=dec.get("Df"))
+    cont = (content_loss(PV, yt, gen, dec.get("Vsr"), dec.get("Vhr")) if PV is not None
+            else torch.zeros((), dtype=torch.float64))
     adv = 1e-3 * bce_logits(zf, 1.0)
     mse = ((yt - gen) ** 2).mean()
     mae = (yt - gen).abs().mean()

@@ -17,6 +17,7 @@ import torch
 import torch.nn.functional as F
 
 from . import p2p_oracle as O
+from .decisions import of as _dec
 
 
 def _pad_same(x, k, s):
@@ -47,11 +48,9 @@ def _bn(y, gamma, beta, eps=O.BN_EPS):
     return (y - mu) / torch.sqrt(var + eps) * gamma.view(1, -1, 1, 1) + beta.view(1, -1, 1, 1)
 
 
-def _lrelu(v):
-    return torch.where(v > 0, v, O.ALPHA * v)
-
-
-def generator(P, x, width, drop_rate=0.5, drop_seed=0, step=0, pass_idx=0):
+def generator(P, x, width, drop_rate=0.5, drop_seed=0, step=0, pass_idx=0, dec=None):
+    """dec: oracle.decisions.Decisions on NHWC masks, sites named like the layers."""
+    dec = _dec(dec)
     downs, ups, last = O.g_layer_specs(width)
     h = x
     skips = []
@@ -59,7 +58,7 @@ def generator(P, x, width, drop_rate=0.5, drop_seed=0, step=0, pass_idx=0):
         y = _conv(h, P[f"{name}/kernel"], 2, "same")
         if bn:
             y = _bn(y, P[f"{name}/gamma"], P[f"{name}/beta"])
-        h = _lrelu(y)
+        h = _nchw(dec.lrelu(name, _nhwc(y), O.ALPHA))
         skips.append(h)
     skips = list(reversed(skips[:-1]))
     for u, (name, ci, co, drop) in enumerate(ups):
@@ -71,11 +70,12 @@ def generator(P, x, width, drop_rate=0.5, drop_seed=0, step=0, pass_idx=0):
             m = O.dropout_mask(seed, step, y.numel(), drop_rate).reshape(n, hh, ww, c)
             m = torch.from_numpy(m).permute(0, 3, 1, 2).to(y.dtype)
             y = y * m / (1.0 - drop_rate)
-        h = torch.cat([F.relu(y), skips[u]], dim=1)
+        h = torch.cat([_nchw(dec.relu(name, _nhwc(y))), skips[u]], dim=1)
     return torch.tanh(_convT(h, P["last/kernel"], 2) + P["last/bias"].view(1, -1, 1, 1))
 
 
-def discriminator(P, inp, tar, width):
+def discriminator(P, inp, tar, width, dec=None):
+    dec = _dec(dec)
     h = torch.cat([inp, tar], dim=1)
     for name, ci, co, bn in O.d_layer_specs(width):
         if name.startswith("down"):
@@ -86,42 +86,55 @@ def discriminator(P, inp, tar, width):
             return y + P["last/bias"].view(1, -1, 1, 1)
         if bn:
             y = _bn(y, P[f"{name}/gamma"], P[f"{name}/beta"])
-        h = _lrelu(y)
+        h = _nchw(dec.lrelu(name, _nhwc(y), O.ALPHA))
+
+
+def _nhwc(t):
+    return t.permute(0, 2, 3, 1)
+
+
+def _nchw(t):
+    return t.permute(0, 3, 1, 2)
 
 
 def _bce(z, y):
     return (torch.clamp(z, min=0) - z * y + torch.log1p(torch.exp(-z.abs()))).mean()
 
 
-def _content(PV, yt, gen):
+def _content(PV, yt, gen, dec_sr=None, dec_hr=None):
     """VGG19 content loss (pix2pix.py:45-51) on NCHW tensors, via oracle/sr_oracle.py's restatement."""
     from . import sr_oracle as S
-    return S.content_loss(PV, yt.permute(0, 2, 3, 1), gen.permute(0, 2, 3, 1))
+    return S.content_loss(PV, yt.permute(0, 2, 3, 1), gen.permute(0, 2, 3, 1), dec_sr, dec_hr)
 
 
 def step_grads(Gnp, Dnp, x, y, width=1, drop_rate=0.5, drop_seed=0, step=0, identity=True, weights=None,
-               dtype=torch.float64, PV=None):
+               dtype=torch.float64, PV=None, dec=None):
     """One train_step's losses and gradients (no optimizer) -> (tuple8, gG, gD) as numpy float64.
-    PV: VGG19 weights for the content term (None: the term is 0)."""
+    PV: VGG19 weights for the content term (None: the term is 0).
+    dec: {"Gx", "Gy", "Dr", "Df", "Vsr", "Vhr": oracle.decisions.Decisions} (any subset):
+    the activation decisions of G(x), G(y), D(real), D(fake) and VGG19 on G(x) / y."""
+    dec = dec or {}
     w = dict(O.LOSS_WEIGHTS) if weights is None else weights
     G = {k: torch.tensor(v, dtype=dtype, requires_grad=True) for k, v in Gnp.items()}
     D = {k: torch.tensor(v, dtype=dtype, requires_grad=True) for k, v in Dnp.items()}
     xt = torch.tensor(x, dtype=dtype).permute(0, 3, 1, 2)
     yt = torch.tensor(y, dtype=dtype).permute(0, 3, 1, 2)
-    gen = generator(G, xt, width, drop_rate, drop_seed, step, 0)
-    zr = discriminator(D, xt, yt, width)
-    zf = discriminator(D, xt, gen, width)
+    gen = generator(G, xt, width, drop_rate, drop_seed, step, 0, dec=dec.get("Gx"))
+    zr = discriminator(D, xt, yt, width, dec=dec.get("Dr"))
+    zf = discriminator(D, xt, gen, width, dec=dec.get("Df"))
     d = yt - gen
     gan = w["gan"] * _bce(zf, 1.0)
     tv = w["tv"] * ((d[:, :, 1:] - d[:, :, :-1]).abs().sum() + (d[:, :, :, 1:] - d[:, :, :, :-1]).abs().sum()) / d.shape[0]
     l1 = w["l1"] * d.abs().mean()
     l2 = w["l2"] * (d * d).mean()
     if identity:
-        idl = w["identity"] * (generator(G, yt, width, drop_rate, drop_seed, step, 1) - yt).abs().mean()
+        idl = w["identity"] * (generator(G, yt, width, drop_rate, drop_seed, step, 1, dec=dec.get("Gy"))
+                               - yt).abs().mean()
     else:
         idl = torch.zeros((), dtype=dtype)
     if PV is not None:
-        cont = w["content"] * _content({k: torch.tensor(v, dtype=dtype) for k, v in PV.items()}, yt, gen)
+        cont = w["content"] * _content({k: torch.tensor(v, dtype=dtype) for k, v in PV.items()}, yt, gen,
+                                       dec.get("Vsr"), dec.get("Vhr"))
     else:
         cont = torch.zeros((), dtype=dtype)
     total = gan + l2 + cont + tv + l1 + idl

@@ -1,0 +1,94 @@
+"""Read the HIP path's activation decisions back from its activation buffers
+(test helper for mask-conditioned parity, see oracle/decisions.py).
+
+Every decision is recovered from what the HIP kernels themselves stored:
+  * ReLU / LeakyReLU (conv epilogue, BN apply, nearest-upsample + ReLU):
+    the post-activation value z is > 0 exactly where the kernel took the
+    positive branch (z = x for x > 0, 0 or alpha*x <= 0 otherwise);
+  * PReLU: the sign of its stored input (alpha may have either sign);
+  * 2x2 max pool: the first maximum of each window of the stored fp32 input,
+    the element the backward kernel routes the gradient to.
+Masks are returned on the host as numpy arrays keyed by the layer name the
+oracle uses for the same site.
+"""
+import numpy as np
+import torch
+
+RELU_ACTS = ("relu", "lrelu", "leaky_relu")
+
+
+def _pos(t):
+    return (t.detach() > 0).cpu().numpy()
+
+
+def pool_argmax(x):
+    """First-maximum index (row-major 2x2 window) of every pool window of NHWC x."""
+    N, H, W, C = x.shape
+    x = x.detach()[:, :H // 2 * 2, :W // 2 * 2].float()
+    win = x.reshape(N, H // 2, 2, W // 2, 2, C).permute(0, 1, 3, 5, 2, 4).reshape(N, H // 2, W // 2, C, 4)
+    return win.cpu().argmax(dim=-1).numpy()
+
+
+def _depth_to_space(m, b):
+    N, H, W, CB = m.shape
+    C = CB // (b * b)
+    return m.reshape(N, H, W, b, b, C).transpose(0, 1, 3, 2, 4, 5).reshape(N, H * b, W * b, C)
+
+
+def graph_decisions(plan, slot=0, rows=None):
+    """{layer name: mask / argmax} of one dgan.graph.GraphPlan slot; rows: a
+    slice of the batch (e.g. one half of a batched forward)."""
+    g = plan.g
+    s = plan.slots[slot]
+    sel = (lambda t: t) if rows is None else (lambda t: t[rows])
+    out = {}
+    for n in g.nodes[1:]:
+        k = n.kind
+        if k in ("conv", "bn", "act") and n.attrs.get("act") in RELU_ACTS:
+            out[n.name] = _pos(sel(s[n.out.id]))
+        elif k == "upsample":
+            out[n.name] = _pos(sel(s[n.out.id]))
+        elif k == "prelu":
+            m = _pos(sel(s[n.ins[0].id]))
+            b = n.attrs["block"]
+            out[n.name] = _depth_to_space(m, b) if b > 1 else m
+        elif k == "maxpool":
+            out[n.name] = pool_argmax(sel(s[n.ins[0].id]))
+    return out
+
+
+def generator_decisions(plan, half=0):
+    """pix2pix GeneratorPlan (dgan.nets): LeakyReLU of down1-8, ReLU of up1-7, one half."""
+    s = plan.s
+    rows = slice(half * plan.N, (half + 1) * plan.N)
+    out = {}
+    for l, (name, _, _, _) in enumerate(plan.downs):
+        out[name] = _pos(plan.z_view(s, l)[rows])
+    for u, (name, _, co, _) in enumerate(plan.ups):
+        out[name] = _pos(s["cat"][u][..., :co][rows])
+    return out
+
+
+def discriminator_decisions(plan, half=0):
+    """pix2pix DiscriminatorPlan: LeakyReLU of down1-3 and conv, one half (0 real, 1 fake)."""
+    rows = slice(half * plan.N, (half + 1) * plan.N)
+    return {name: _pos(z[rows]) for (name, _, _, _), z in zip(plan.specs, plan.z)}
+
+
+def to_oracle(masks):
+    """oracle.decisions.Decisions over exported masks."""
+    from oracle.decisions import Decisions
+    return Decisions({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in masks.items()})
+
+
+def audit_ok(decs, tie_tol, what=""):
+    """Every overridden decision is a near-tie: |fp64 pre-activation| (or the gap
+    to the window maximum) below tie_tol of the layer's scale.  Returns the
+    total number of overridden elements."""
+    tot = 0
+    for label, d in decs.items():
+        n, worst, where = d.worst()
+        tot += n
+        assert worst <= tie_tol, (f"{what} {label}: decision at {where} differs from the oracle's on a value "
+                                  f"{worst:.2e} of the layer scale from the tie (> {tie_tol:.0e})")
+    return tot

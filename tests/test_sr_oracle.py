@@ -157,3 +157,32 @@ def test_graph_plan_beta_schedule_on_cpu_shapes():
     ae = zoo.autoencoder_generator()
     kinds = [n.kind for n in ae.nodes]
     assert kinds.count("concat") == 5 and kinds.count("maxpool") == 5 and kinds.count("upsample") == 5
+
+
+def test_decisions_plain_and_forced():
+    """oracle/decisions.py: forcing the oracle's own decisions changes nothing; forcing a flipped
+    decision on a clear (non-tie) value is reported by the audit."""
+    import torch
+    from oracle.decisions import Decisions
+    rng = np.random.default_rng(4)
+    x = torch.tensor(rng.standard_normal((2, 4, 6, 5)), requires_grad=True)
+    a = torch.tensor([0.2] * 5)
+    plain = Decisions()
+    own = {"r": (x > 0).detach().numpy(), "p": torch.tensor(rng.standard_normal((2, 4, 6, 5))).numpy()}
+    win = x.detach().reshape(2, 2, 2, 3, 2, 5).permute(0, 1, 3, 5, 2, 4).reshape(2, 2, 3, 5, 4)
+    own["p"] = win.argmax(-1).numpy()
+    forced = Decisions(own | {"l": own["r"], "q": own["r"]})
+    for d in (plain, forced):
+        y = d.relu("r", x).sum() + d.lrelu("l", x, 0.3).sum() + d.prelu("q", x, a).sum() + d.maxpool2("p", x).sum()
+        g = torch.autograd.grad(y, x)[0]
+        if d is plain:
+            y0, g0 = y.detach(), g
+    assert torch.equal(y.detach(), y0) and torch.equal(g, g0)
+    assert forced.worst()[0] == 0
+    flip = own["r"].copy()
+    i = np.unravel_index(np.argmax(np.abs(x.detach().numpy())), flip.shape)
+    flip[i] = ~flip[i]
+    d = Decisions({"r": flip})
+    d.relu("r", x)
+    n, worst, where = d.worst()
+    assert n == 1 and worst == 1.0 and where == "r"

@@ -163,9 +163,11 @@ def test_generator_inference_uses_moving_stats():
 def test_step_parity_with_vgg_content():
     """The reference-equivalent step incl. the VGG19 content loss (pix2pix.py:45-51, :87; seeded
     stand-in VGG weights, channel width /8 to keep the fp64 CPU oracle fast) vs the torch fp64
-    autograd restatement (oracle/torch_p2p.py + oracle/sr_oracle.py's VGG19).  Losses to 1e-5;
-    gradients: relative L2 per variable < 2e-2 (the VGG input gradient is piecewise smooth; see
-    tests/test_sr_gpu.py::_grads_close_l2) and max-abs < 1e-4 where the content-free part dominates."""
+    autograd restatement (oracle/torch_p2p.py + oracle/sr_oracle.py's VGG19), mask-conditioned:
+    the oracle takes the HIP path's ReLU / LeakyReLU / max-pool decisions (G(x), G(y), D real,
+    D fake, VGG19 on G(x) and on y; oracle/decisions.py), each override audited to be a near-tie.
+    Losses to 1e-5, |dPSNR| < 0.01 dB, every G and D gradient to max-abs 1e-4."""
+    from gpu_decisions import audit_ok, discriminator_decisions, generator_decisions, graph_decisions, to_oracle
     from oracle import torch_p2p as T
     from pix2pix import Pix2Pix
     width, seed = 16, 5
@@ -174,18 +176,22 @@ def test_step_parity_with_vgg_content():
     D = m.discriminator.arena.export()
     PV = m.vgg.arena.export()
     x, y = O.synthetic_pair(2, 256, seed=21)
-    vals, gG, gD, gen_ref = T.step_grads(G, D, x, y, width=width, drop_rate=0.0, PV=PV)
     tr = m.trainer(x.shape)
     loss = tr.step(torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda(), apply=False)
     torch.cuda.synchronize()
+    N = x.shape[0]
+    dec = {"Gx": generator_decisions(tr.G, 0), "Gy": generator_decisions(tr.G, 1),
+           "Dr": discriminator_decisions(tr.D, 0), "Df": discriminator_decisions(tr.D, 1),
+           "Vsr": graph_decisions(tr.content.fplan, 0, rows=slice(0, N)),
+           "Vhr": graph_decisions(tr.content.fplan, 0, rows=slice(N, 2 * N))}
+    dec = {k: to_oracle(v) for k, v in dec.items()}
+    vals, gG, gD, gen_ref = T.step_grads(G, D, x, y, width=width, drop_rate=0.0, PV=PV, dec=dec)
+    n_over = audit_ok(dec, 1e-5, "pix2pix+vgg")
     got = loss.cpu().double().numpy()
     assert got[4] > 0.0
     assert np.allclose(got, np.array(vals), rtol=1e-5, atol=1e-7), (got, vals)
     gen = tr.gen_output.cpu().numpy()
     assert abs(psnr(gen, y) - psnr(gen_ref, y)) < 0.01
-    for arena, ref in ((m.generator.arena, gG), (m.discriminator.arena, gD)):
-        for name, g_ref in ref.items():
-            g = arena.grad_of(name).detach().double().cpu().numpy()
-            den = np.linalg.norm(g_ref)
-            if den > 1e-12:
-                assert np.linalg.norm(g - g_ref) / den < 2e-2, name
+    wg = _compare_grads(m.generator.arena, gG, "G")
+    wd = _compare_grads(m.discriminator.arena, gD, "D")
+    print(f"pix2pix+VGG parity: worst G {wg}, worst D {wd}, overridden decisions {n_over}")
