@@ -36,7 +36,8 @@ TF/Keras semantics (each checked by a known-answer test):
 Dropout: Keras' RNG stream cannot be reproduced; both this oracle and the
 HIP path use the counter-based hash `dropout_keep` below (bit-identical).
 The VGG19 content loss needs ImageNet weights that are unavailable offline;
-its weight is an input (default: value 0).
+train_step takes the VGG19 weights to use (PV; None = the term is 0) and
+evaluates the term through oracle/sr_oracle.py's VGG19 restatement.
 """
 import numpy as np
 
@@ -528,7 +529,21 @@ class P2PState:
         self.w = dict(LOSS_WEIGHTS) if loss_weights is None else dict(loss_weights)
 
 
-def train_step(st, x, y, return_grads=False, apply=True):
+def content_value_and_grad(PV, gen, tgt):
+    """VGG19 content loss MSE(vgg(pre(tgt))/12.75, vgg(pre(gen))/12.75) (pix2pix.py:45-51) and its
+    gradient w.r.t. gen, float64, through oracle/sr_oracle.py's VGG19 restatement (torch autograd)."""
+    import torch
+    from . import sr_oracle as S
+    PVt = {k: torch.tensor(np.asarray(v, np.float64)) for k, v in PV.items()}
+    g = torch.tensor(np.asarray(gen, np.float64), requires_grad=True)
+    c = S.content_loss(PVt, torch.tensor(np.asarray(tgt, np.float64)), g)
+    dg = torch.autograd.grad(c, g)[0]
+    return float(c.detach()), dg.numpy()
+
+
+def train_step(st, x, y, return_grads=False, apply=True, PV=None):
+    """One train_step (train_pix2pix.py:33-71).  PV: VGG19 weights of the content term
+    (pix2pix.py:87; None = term 0)."""
     step = st.iterations
     gen, cg = generator_forward(st.G, x, st.width, True, st.Gs, st.drop_rate, st.drop_seed, step, 0)
     ident, ci = (None, None)
@@ -536,12 +551,15 @@ def train_step(st, x, y, return_grads=False, apply=True):
         ident, ci = generator_forward(st.G, y, st.width, True, st.Gs, st.drop_rate, st.drop_seed, step, 1)
     zr, cdr = discriminator_forward(st.D, x, y, st.width, True, st.Ds)
     zf, cdf = discriminator_forward(st.D, x, gen, st.width, True, st.Ds)
-    vals, lg = losses_and_grads(gen, y, ident, zr, zf, st.w)
+    content, dcont = (0.0, None) if PV is None else content_value_and_grad(PV, gen, y)
+    vals, lg = losses_and_grads(gen, y, ident, zr, zf, st.w, content=content)
     gDr, _ = discriminator_backward(st.D, cdr, lg["dzr_d"])
     gDf, _ = discriminator_backward(st.D, cdf, lg["dzf_d"])
     gD = {k: gDr[k] + gDf[k] for k in gDr}
     _, dinp = discriminator_backward(st.D, cdf, lg["dzf_g"], need_input_grad=True, need_param_grad=False)
     dgen = lg["dgen"] + dinp[..., 3:]
+    if dcont is not None:
+        dgen = dgen + st.w["content"] * dcont
     gG = generator_backward(st.G, cg, dgen, st.width, st.drop_rate)
     if st.identity:
         gGi = generator_backward(st.G, ci, lg["dident"], st.width, st.drop_rate)

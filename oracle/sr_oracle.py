@@ -349,7 +349,7 @@ def train_step(st, x, y, apply=True, dec=None):
     gD = torch.autograd.grad(disc, list(PD.values()))
     gG = {k: g.numpy() for k, g in zip(PG, gG)}
     gD = {k: g.numpy() for k, g in zip(PD, gD)}
-    out = dict(losses=tuple(float(v) for v in (gen_loss, adv, mae, mse, cont, disc, var)),
+    out = dict(losses=tuple(float(v.detach()) for v in (gen_loss, adv, mae, mse, cont, disc, var)),
                gen=gen.detach().numpy(), dgen=dgen.numpy(), gG=gG, gD=gD)
     if apply:
         t = st.iterations + 1

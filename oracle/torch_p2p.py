@@ -183,6 +183,6 @@ def make_fp32_step(Gnp, Dnp, width=1, lr=2e-4, b1=0.5, b2=0.999, eps=1e-7, PV=No
         opt_state["t"] += 1
         adam(list(G.values()), gG)
         adam(list(D.values()), gD)
-        return float(total), float(disc)
+        return float(total.detach()), float(disc.detach())
 
     return step
