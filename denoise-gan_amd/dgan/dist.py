@@ -5,8 +5,15 @@ BASELINE.json's north star adds batch data parallelism: each rank runs the
 full step on its own 16 images, then the fp32 gradient arenas are summed
 with RCCL (torch.distributed backend "nccl" on ROCm) over xGMI and Adam
 applies them scaled by 1/world (ops.adam grad_scale) on every rank, so the
-replicas stay bit-identical without any parameter broadcast.  BN statistics
-stay per replica (local batch), as tf.distribute would do.
+replicas stay bit-identical without any parameter broadcast.
+
+BatchNorm: the training step normalises with each replica's local batch
+statistics (SyncBatchNorm is not used, as in tf.distribute's default), and
+each replica updates its own moving averages from them.  Keras keeps those
+moving variables ON_READ with MEAN aggregation, i.e. a read under
+tf.distribute returns the cross-replica mean; `sync_bn_stats` performs that
+read-time averaging (all-reduce mean of every moving mean / variance) and
+the drivers call it before a checkpoint save or an inference read.
 
 Overlap: D's gradients are final after the two D backwards and go out at
 once (they travel while G's backward runs); G's arena is laid out in
@@ -19,8 +26,15 @@ import torch
 import torch.distributed as dist
 
 
+BUCKET_BYTES = 25 << 20   # ~25 MB buckets -> 9 G buckets + D for pix2pix
+
+
 class GradSync:
-    def __init__(self, g_arena, d_arena, bucket_bytes=64 << 20, group=None):
+    """Bucketed gradient all-reduce of one G and one D arena.  Works for any
+    network whose backward reports finished layers by name (pix2pix plans,
+    dgan.graph plans): a layer is the variable-name prefix before '/'."""
+
+    def __init__(self, g_arena, d_arena, bucket_bytes=BUCKET_BYTES, group=None):
         self.g, self.d = g_arena, d_arena
         self.group = group
         self.world = dist.get_world_size(group)
@@ -65,7 +79,22 @@ def broadcast_parameters(model, src=0, group=None):
             dist.broadcast(t, src, group=group)
 
 
-def setup_data_parallel(model, bucket_bytes=64 << 20):
+def sync_bn_stats(model, group=None):
+    """Cross-replica mean of every BN moving mean / variance (Keras ON_READ MEAN
+    aggregation); identical on every rank afterwards."""
+    world = dist.get_world_size(group)
+    for net in (model.generator, model.discriminator):
+        for t in net.non_trainable_variables:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+            t.mul_(1.0 / world)
+
+
+def setup_data_parallel(model, bucket_bytes=BUCKET_BYTES):
+    """Attach the gradient exchange to a model container (Pix2Pix or an SR-family
+    model) and broadcast rank 0's weights.  Trainers built before this call are
+    dropped so every step built afterwards all-reduces."""
     model.grad_sync = GradSync(model.generator.arena, model.discriminator.arena, bucket_bytes)
+    if hasattr(model, "_trainers"):
+        model._trainers.clear()
     broadcast_parameters(model)
     return model.grad_sync

@@ -74,6 +74,7 @@ class SRFamily(object):
         self.coef = COEF[self.coef_key]
         self._trainers = {}
         self._content = {}
+        self._ws = None
         self.grad_sync = None
 
     # --- to override -----------------------------------------------------
@@ -94,9 +95,10 @@ class SRFamily(object):
         if key not in self._content:
             self._content[key] = ContentLoss(self.vgg, N, H, W, self.device, train=False)
         c = self._content[key]
-        ws = ops.Workspace(self.device)
-        ws.get(c.ws_bytes)
-        return c.forward(sr, hr, ws=ws)[0].clone()
+        if self._ws is None:
+            self._ws = ops.Workspace(self.device)
+        self._ws.get(c.ws_bytes)
+        return c.forward(sr, hr, ws=self._ws)[0].clone()
 
     def _sched(self, opt):
         s = opt.learning_rate

@@ -23,6 +23,9 @@ class AdamConfig:
     def __init__(self, lr=2e-4, beta_1=0.5, beta_2=0.999, epsilon=1e-7):
         self.lr, self.beta_1, self.beta_2, self.epsilon = lr, beta_1, beta_2, epsilon
 
+    def current_lr(self):
+        return float(self.lr)
+
 
 class Pix2PixTrainer:
     """One fused pix2pix step for x, y [N,H,W,3].
@@ -127,8 +130,10 @@ class Pix2PixTrainer:
         # ---- apply_gradients (train_pix2pix.py:68-69) ----------------------
         if apply:
             scale = sync.grad_scale if sync else 1.0
+            # the optimizers' hyper-parameters are read at every step (a changed or callable
+            # learning_rate takes effect; a captured HIP graph keeps the values of its capture)
             for A, o in ((self.gA, self.g_opt), (self.dA, self.d_opt)):
-                ops.adam(A.data, A.grad, A.m, A.v, o.lr, o.beta_1, o.beta_2, o.epsilon, A.iterations,
+                ops.adam(A.data, A.grad, A.m, A.v, o.current_lr(), o.beta_1, o.beta_2, o.epsilon, A.iterations,
                          grad_scale=scale)
                 ops.counter_add(A.iterations, 1)
         return self.loss

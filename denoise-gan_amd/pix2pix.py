@@ -92,6 +92,7 @@ class Pix2Pix(object):
         self.vgg = VGGNetwork(weights=getattr(args, "vgg_weights", None), seed=self.seed + 7,
                               width=int(getattr(args, "vgg_width", 1)), device=self.device) if self.use_content else None
         self._content = {}
+        self._ws = None
         self.generator, self.discriminator = self.build_gan()
         self.gen_optimizer.bind(self.generator.arena)
         self.disc_optimizer.bind(self.discriminator.arena)
@@ -108,9 +109,14 @@ class Pix2Pix(object):
         if (N, H, W) not in self._content:
             self._content[(N, H, W)] = ContentLoss(self.vgg, N, H, W, self.device, train=False)
         c = self._content[(N, H, W)]
-        ws = ops.Workspace(self.device)
-        ws.get(c.ws_bytes)
-        return c.forward(gen, tgt, ws=ws)[0].clone()
+        return c.forward(gen, tgt, ws=self._workspace(c.ws_bytes))[0].clone()
+
+    def _workspace(self, nbytes):
+        """One workspace for the eager Keras-surface calls (grown on demand, never per call)."""
+        if self._ws is None:
+            self._ws = ops.Workspace(self.device)
+        self._ws.get(nbytes)
+        return self._ws
 
     def build_vgg(self):
         return self.vgg
@@ -149,12 +155,6 @@ class Pix2Pix(object):
             self._trainers[key] = Pix2PixTrainer(
                 self.generator.arena, self.generator.bn, self.discriminator.arena, self.discriminator.bn, N, H, W,
                 self.device, width=self.width, identity=self.identity, loss_weights=self.loss_weights,
-                drop_rate=self.dropout_rate, drop_seed=self.dropout_seed, g_opt=_opt_cfg(self.gen_optimizer),
-                d_opt=_opt_cfg(self.disc_optimizer), grad_sync=self.grad_sync, vgg=self.vgg)
+                drop_rate=self.dropout_rate, drop_seed=self.dropout_seed, g_opt=self.gen_optimizer,
+                d_opt=self.disc_optimizer, grad_sync=self.grad_sync, vgg=self.vgg)
         return self._trainers[key]
-
-
-def _opt_cfg(opt):
-    from dgan.trainer import AdamConfig
-    lr = opt.learning_rate(0) if callable(opt.learning_rate) else opt.learning_rate
-    return AdamConfig(float(lr), opt.beta_1, opt.beta_2, opt.epsilon)

@@ -5,21 +5,17 @@
 forwards, VGG content loss, losses, both gradients, Adam with
 ExponentialDecay on G then D) as one launch sequence on libdgan
 (dgan.sr_trainer.SRTrainer).  `train` / `main` follow the reference's loop
-with the synthetic DataLoader stand-in, JSONL summaries and .npz weights.
+with the shared driver loop (dgan.driver), JSONL summaries and .npz weights.
 """
-import glob
 import os
 from argparse import ArgumentParser
-from datetime import datetime
-from time import time
 
 import numpy as np
 import torch
 
 from dataloader import DataLoader
 from autoencoder import Autoencoder
-from dgan import summary as tf_summary
-from dgan.checkpoint import Checkpoint, CheckpointManager
+from dgan import driver
 from dgan.models import to_device
 
 LOSS_NAMES = ("disc_loss", "adv_loss", "content_loss", "mse_loss", "mae_loss")
@@ -54,35 +50,19 @@ def get_path(path):
     return os.path.realpath(os.path.expanduser(os.path.expandvars(path)))
 
 
+def save_final(model, timestamp):
+    name = model.model_name
+    model.generator.save(os.path.join(model.model_dir, f"{name}.npz"))
+    model.discriminator.save(os.path.join(model.model_dir, f"discriminator_{name}.npz"))
+    model.generator.save(os.path.join(model.model_dir, "backups", f"{name}_{timestamp}.npz"))
+
+
 def main(args):
-    os.makedirs(os.path.join(args.model_dir, "checkpoints"), exist_ok=True)
-    os.makedirs(os.path.join(args.model_dir, "backups"), exist_ok=True)
-    os.makedirs(args.logdir, exist_ok=True)
+    """The reference's main (dgan.driver.run: restore, epochs, checkpoints, exports)."""
     ds = DataLoader(args).dataset()
-    traindirs = glob.glob(os.path.join(args.logdir, "train_*"))
-    train_num = max([int(x.split("_")[-1]) for x in traindirs]) + 1 if traindirs else 1
-    writer = tf_summary.create_file_writer(os.path.join(args.logdir, f"train_{train_num}"))
     model = Autoencoder(args)
-    ckpt = Checkpoint(gen_optimizer=model.gen_optimizer, disc_optimizer=model.disc_optimizer,
-                      generator=model.generator, discriminator=model.discriminator)
-    manager = CheckpointManager(ckpt, os.path.join(args.model_dir, "checkpoints"), max_to_keep=3)
-    if args.retrain and manager.latest_checkpoint:
-        ckpt.restore(manager.latest_checkpoint).expect_partial()
-    timestamp = datetime.now().strftime("%Y-%m-%d_%H-%M-%S")
-    for epoch in range(args.epochs):
-        t0 = time()
-        train(model, ds, args, writer)
-        torch.cuda.synchronize()
-        if args.ckpt and epoch % 5 == 0:
-            manager.save()
-        model.epochs += 1
-        print(f"====== Finished epoch: {epoch + 1}, iterations: {model.iterations}, "
-              f"train time: {time() - t0:0.2f} ======")
-    if args.save_model:
-        model.generator.save(os.path.join(args.model_dir, f"{args.model_name}.npz"))
-        model.discriminator.save(os.path.join(args.model_dir, f"discriminator_{args.model_name}.npz"))
-        model.generator.save(os.path.join(args.model_dir, "backups", f"{args.model_name}_{timestamp}.npz"))
-    return model
+    model.model_dir, model.model_name = args.model_dir, args.model_name
+    return driver.run(args, model, ds, train, save_final)
 
 
 params = dict(
@@ -101,7 +81,8 @@ params = dict(
     fp16=0,
     scale=1,
     jpeg_quality=50,
-    steps_per_epoch=8,
+    synthetic=0,
+    steps_per_epoch=8,   # synthetic pairs only; image_dir runs use images // batch_size
     seed=0,
 )
 

@@ -4,24 +4,23 @@
 (train_pix2pix.py:33-71); it runs the whole step (G/D forwards, losses, both
 gradients, Adam G then D) as one fused launch sequence on libdgan.  `train`
 and `main` follow :73-107 and :112-195 (TensorBoard -> dgan.summary JSONL,
-tf.train.Checkpoint -> dgan.checkpoint, .h5 -> .npz).  The published driver
-crashes before training (`policy` undefined at :231 when fp16=0, and
-DataLoader needs args.scale / args.jpeg_quality absent from `params`,
-SURVEY.md §3A); this one supplies scale=1 and jpeg_quality=50.
+tf.train.Checkpoint -> dgan.checkpoint, .h5 -> .npz; the shared loop is
+dgan.driver.run).  The published driver crashes before training (`policy`
+undefined at :231 when fp16=0, and DataLoader needs args.scale /
+args.jpeg_quality absent from `params`); this one supplies
+scale=1 and jpeg_quality=50.  Steps per epoch = images // batch_size
+(DataLoader, drop_remainder); --synthetic 1 trains on seeded synthetic
+pairs instead of image_dir.
 """
-import glob
 import os
 from argparse import ArgumentParser
-from datetime import datetime
-from time import time
 
 import numpy as np
 import torch
 
 from dataloader import DataLoader
 from pix2pix import Pix2Pix
-from dgan import summary as tf_summary
-from dgan.checkpoint import Checkpoint, CheckpointManager
+from dgan import driver
 from dgan.models import to_device
 
 
@@ -59,47 +58,22 @@ def get_path(path):
     return os.path.realpath(os.path.expanduser(os.path.expandvars(path)))
 
 
+def save_final(model, timestamp):
+    """Final exports (train_pix2pix.py:189-195; .h5 -> .npz + .json)."""
+    model.generator.save(os.path.join(model.model_dir, "pix2pix.npz"))
+    model.discriminator.save(os.path.join(model.model_dir, "discriminator_p2p.npz"))
+    model.generator.save(os.path.join(model.model_dir, "backups", f"pix2pix_{timestamp}.npz"))
+    model.discriminator.save(os.path.join(model.model_dir, "backups", f"discriminator_p2p_{timestamp}.npz"))
+
+
 def main(args):
-    os.makedirs(os.path.join(args.model_dir, "checkpoints"), exist_ok=True)
-    os.makedirs(os.path.join(args.model_dir, "backups"), exist_ok=True)
-    os.makedirs(args.logdir, exist_ok=True)
-    steps_per_epoch = int(getattr(args, "steps_per_epoch", 0) or 8)
-    print(f"Steps per epoch: {steps_per_epoch}")
-    if args.save_iter > steps_per_epoch:
-        args.save_iter = steps_per_epoch
+    """train_pix2pix.py:112-195 (dgan.driver.run: restore, epochs, checkpoints, exports)."""
     ds = DataLoader(args).dataset()
-    logdir = get_path(args.logdir)
-    traindirs = glob.glob(os.path.join(logdir, "train_*"))
-    train_num = max([int(x.split("_")[-1]) for x in traindirs]) + 1 if traindirs else 1
-    writer = tf_summary.create_file_writer(os.path.join(logdir, f"train_{train_num}"))
-
+    if args.save_iter > len(ds):
+        args.save_iter = max(1, len(ds))
     model = Pix2Pix(args)
-    checkpoint_dir = os.path.join(args.model_dir, "checkpoints")
-    checkpoint = Checkpoint(gen_optimizer=model.gen_optimizer, disc_optimizer=model.disc_optimizer,
-                            generator=model.generator, discriminator=model.discriminator)
-    ckpt_manager = CheckpointManager(checkpoint, checkpoint_dir, max_to_keep=3)
-    if bool(args.retrain):
-        checkpoint.restore(ckpt_manager.latest_checkpoint).expect_partial()
-
-    timestamp = datetime.now().strftime("%Y-%m-%d_%H-%M-%S")
-    for epoch in range(args.epochs):
-        train_begin = time()
-        train(model, ds, args, writer)
-        torch.cuda.synchronize()
-        train_end = time()
-        if args.ckpt and epoch % 5 == 0:
-            ckpt_manager.save()
-        end = time()
-        model.epochs += 1
-        print(f"====== Finished epoch: {epoch + 1}, iterations: {model.iterations}, "
-              f"train time: {train_end - train_begin:0.2f}, total time: {end - train_begin:0.2f} ======")
-    if args.save_model:
-        ckpt_manager.save()
-        model.generator.save(os.path.join(args.model_dir, "pix2pix.npz"))
-        model.discriminator.save(os.path.join(args.model_dir, "discriminator_p2p.npz"))
-        model.generator.save(os.path.join(args.model_dir, "backups", f"pix2pix_{timestamp}.npz"))
-        model.discriminator.save(os.path.join(args.model_dir, "backups", f"discriminator_p2p_{timestamp}.npz"))
-    return model
+    model.model_dir = args.model_dir
+    return driver.run(args, model, ds, train, save_final)
 
 
 params = dict(
@@ -117,7 +91,8 @@ params = dict(
     fp16=0,
     scale=1,
     jpeg_quality=50,
-    steps_per_epoch=8,
+    synthetic=0,
+    steps_per_epoch=8,   # synthetic pairs only; image_dir runs use images // batch_size
     seed=0,
 )
 

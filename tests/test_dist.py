@@ -81,3 +81,58 @@ def test_gradsync_two_ranks(bucket_kb):
     # the small bucket size must have produced several in-flight buckets
     if bucket_kb == 256:
         assert len(res[0][4]) >= 3
+
+
+def _sr_worker(rank, world, port, kind, bucket_bytes, q):
+    """GradSync over a dgan.graph network arena, driven by the layer names the
+    graph executor's backward reports (GraphPlan.backward -> on_grads_ready)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from dgan import zoo
+        from dgan.dist import GradSync
+        from dgan.nets import Arena
+        g = zoo.srgan_generator(scale=4) if kind == "srgan" else zoo.fsrgan_generator()
+        d = zoo.sr_discriminator(df=32)
+        gA = Arena(g.var_list(), torch.device("cpu"), g.layout_order())
+        dA = Arena(d.var_list(), torch.device("cpu"), d.layout_order())
+        gA.grad.copy_(torch.arange(gA.numel, dtype=torch.float32) * 1e-3 + rank)
+        dA.grad.copy_(torch.arange(dA.numel, dtype=torch.float32) * 1e-3 - rank)
+        sync = GradSync(gA, dA, bucket_bytes=bucket_bytes)
+        sync.start("D")
+        issued = []
+        for n in reversed(g.nodes[1:]):          # GraphPlan.backward's reporting order
+            if n.kind in ("conv", "bn", "prelu", "dwconv"):
+                before = sync.issued
+                sync.ready_G(n.name)
+                if sync.issued != before:
+                    issued.append((before, sync.issued))
+        sync.finish()
+        q.put((rank, gA.grad.numpy().copy(), dA.grad.numpy().copy(), issued, gA.numel))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["srgan", "fsrgan"])
+def test_gradsync_sr_graph_two_ranks(kind):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sr_worker, args=(r, world, port, kind, 64 << 10, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n = res[0][4]
+    for rank, g, d, issued, _ in res:
+        assert np.allclose(g, np.arange(n, dtype=np.float32) * 2e-3 + 1.0, rtol=1e-6)
+        assert np.allclose(d, np.arange(d.size, dtype=np.float32) * 2e-3 - 1.0, rtol=1e-6, atol=1e-6)
+        pos = 0
+        for a, b in issued:
+            assert a == pos and b > a
+            pos = b
+        assert len(issued) >= 3   # buckets went out during the backward, not all at finish()
