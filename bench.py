@@ -1,35 +1,49 @@
 #!/usr/bin/env python3
-"""Throughput of the pix2pix training step on MI355X (BASELINE.json metric:
+"""Throughput of the GAN training steps on MI355X (BASELINE.json metric:
 training images/sec, pix2pix 256x256 bs16 per GPU, 1/2/4/8 GPUs).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--model pix2pix|srgan|fsrgan|autoencoder]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-One step = the reference's train_step (train_pix2pix.py:33-71) on 16 synthetic
-256x256 noisy/clean pairs per GPU already resident in HBM: G(x), the identity
-pass G(y), D real + fake, L1/L2/TV/GAN/identity losses, both gradients, the
-data-parallel gradient all-reduce (N>1) and Keras-Adam on G and D, plus the
-VGG19 content loss (pix2pix.py:45-51: VGG19-to-block5_conv4 forward on G(x)
-and on y, backward into G(x)) with seeded stand-in weights (ImageNet weights
-are a download; same FLOPs and shapes).  `--no-content` drops the VGG term;
-at N=1 the same run also reports that content-free step as `core`.  fp32 tensors
-throughout; the conv GEMMs use the library's default conv math, bf16x6
-(fp32 operands split exactly into three bf16 pieces, the six significant
-piece products accumulated in fp32 -- fp32-accurate); set
-DG_CONV_MATH=fp32 for the exact-fp32 MFMA path.
+Workloads (one "step" = the reference's train_step on one synthetic batch
+already resident in HBM, per GPU):
+  pix2pix      (default, the headline) train_pix2pix.py:33-71 at 256x256, 16
+               noisy/clean pairs: G(x), the identity pass G(y), D real +
+               fake, L1/L2/TV/GAN/identity losses, the VGG19 content loss
+               (pix2pix.py:45-51; seeded stand-in weights, ImageNet weights
+               are a download; same FLOPs and shapes), both gradients, the
+               data-parallel all-reduce (N>1), Keras-Adam on G and D.
+               `--no-content` drops the VGG term; at N=1 that content-free
+               step is also reported as `core` (the north star's
+               "L1 + adversarial" step).                     BASELINE configs[1]
+  srgan        train_srgan.py:61-118, 4x SR 24 -> 96, 16 residual blocks,
+               bs32, VGG19 content loss                     BASELINE configs[2]
+  fsrgan       train_fsrgan.py:61-120, 128 -> 512, bs8 per GPU
+                                                            BASELINE configs[4]
+  autoencoder  train_autoencoder.py:66-112, 64x64 grayscale (replicated to
+               3 channels), bs4                             BASELINE configs[0]
+fp32 tensors throughout; the conv GEMMs use the library's default conv
+math, bf16x6 (fp32 operands split exactly into three bf16 pieces, the six
+significant piece products accumulated in fp32 -- fp32-accurate, see
+DESIGN.md); DG_CONV_MATH=fp32 selects the exact-fp32 MFMA path.
 
 Prints ONE JSON line (rank 0).  Extra fields:
   roofline      conv engine (the dominant kernels): algorithmic conv FLOPs of
                 one step / summed conv launch time measured with HIP events on
                 the launching stream, vs the peak of the conv math in use
-                (bf16x6: bf16 dense peak / 6 = 419.4 TF/s; fp32: 157.3 TF/s)
-  cpu_baseline  the CPU restatement of the same graph (oracle/torch_p2p.py,
-                torch fp32 autograd) timed on this box's host cores, rank 0,
-                N=1 only, bounded sample
+                (bf16x6: bf16 dense peak / 6 = 419.4 TF/s; fp32: 157.3 TF/s);
+                `traffic` = HBM bytes per step of those launches from the
+                committed rocprofv3 PMC profile named in `traffic_source`
+                (scripts/gpu_pmc_bench.sh re-measures it; --pmc-leg runs the
+                two PMC passes as child processes and reports them live)
+  cpu_baseline  the CPU restatement of the same step (oracle/, torch fp32
+                autograd) timed on this box's host cores, rank 0, N=1 only,
+                bounded sample of the same workload
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -46,15 +60,33 @@ BF16_MFMA_PEAK = 2516.6e12  # gfx950 dense bf16 MFMA: 1024 FLOP/clk/SIMD x 1024 
 # fp32-equivalent ceiling is the bf16 peak / 6
 X6_PEAK = BF16_MFMA_PEAK / 6.0
 
+WORKLOADS = {
+    "pix2pix": dict(metric="training images/sec, pix2pix 256x256 bs16/GPU", batch=16, size=256, scale=1,
+                    model="pix2pix U-Net G (54.4M) + PatchGAN D (2.77M)", traffic="pmc_traffic.json"),
+    "srgan": dict(metric="training images/sec, SRGAN 4x 24->96 bs32/GPU", batch=32, size=96, scale=4,
+                  model="SRGAN G (16 residual blocks) + SR D", traffic="pmc_traffic_srgan.json"),
+    "fsrgan": dict(metric="training images/sec, FastSRGAN 4x 128->512 bs8/GPU", batch=8, size=512, scale=4,
+                   model="FastSRGAN G (6 inverted-residual blocks) + SR D", traffic="pmc_traffic_fsrgan.json"),
+    "autoencoder": dict(metric="training images/sec, autoencoder 64x64 grayscale bs4/GPU", batch=4, size=64,
+                        scale=1, model="conv autoencoder G + sigmoid D", traffic="pmc_traffic_autoencoder.json",
+                        gray=True),
+}
+
 
 class Args:
     def __init__(self, **kw):
         self.__dict__.update(kw)
 
 
-def synthetic_batch(n, size, seed):
+def synthetic_batch(wl, n, seed):
     from dataloader import synthetic_pair
-    return synthetic_pair(n, size, seed)
+    x, y = synthetic_pair(n, wl["size"], seed)
+    if wl.get("gray"):
+        x = np.repeat(x.mean(-1, keepdims=True), 3, -1).astype(np.float32)
+        y = np.repeat(y.mean(-1, keepdims=True), 3, -1).astype(np.float32)
+    if wl["scale"] > 1:
+        x = np.ascontiguousarray(x[:, ::wl["scale"], ::wl["scale"]])
+    return x, y
 
 
 def main():
@@ -62,18 +94,22 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=16, help="images per GPU")
-    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--model", default="pix2pix", choices=sorted(WORKLOADS))
+    ap.add_argument("--batch", type=int, default=None, help="images per GPU (default: the workload's)")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of a captured HIP graph")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-steps", type=int, default=3, help="CPU baseline: timed steps at the full batch")
     ap.add_argument("--no-identity", action="store_true")
     ap.add_argument("--no-content", action="store_true", help="drop the VGG19 content term")
     ap.add_argument("--no-core", action="store_true", help="skip the content-free secondary measurement")
     ap.add_argument("--profile-only", action="store_true", help="skip roofline/cpu legs (for rocprofv3 runs)")
+    ap.add_argument("--pmc-leg", action="store_true",
+                    help="measure roofline.traffic now: two rocprofv3 --pmc child runs (FETCH_SIZE, WRITE_SIZE)")
     ap.add_argument("--dist", action="store_true",
                     help="data-parallel path (process group + gradient all-reduce) even at world size 1")
     args = ap.parse_args()
+    wl = WORKLOADS[args.model]
+    batch = args.batch or wl["batch"]
     # the one JSON line goes to the original stdout; everything else written to
     # fd 1 (RCCL's version banner, library logs) is sent to stderr
     json_out = os.fdopen(os.dup(1), "w")
@@ -103,18 +139,26 @@ def main():
 
     import dgan
     dgan.build()  # no-op when the in-tree library is current
-    from pix2pix import Pix2Pix
     from dgan import ops
 
     def build(content):
-        m = Pix2Pix(Args(crop_size=args.size, retrain=0, width=1, seed=1234, dropout_seed=rank,
-                         identity_loss=0 if args.no_identity else 1, content_loss=int(content)))
+        if args.model == "pix2pix":
+            from pix2pix import Pix2Pix
+            m = Pix2Pix(Args(crop_size=wl["size"], retrain=0, width=1, seed=1234, dropout_seed=rank,
+                             identity_loss=0 if args.no_identity else 1, content_loss=int(content)))
+        else:
+            from autoencoder import Autoencoder
+            from fsrgan import FastSRGAN
+            from srgan import SRGAN
+            cls = {"srgan": SRGAN, "fsrgan": FastSRGAN, "autoencoder": Autoencoder}[args.model]
+            m = cls(Args(crop_size=wl["size"], scale=wl["scale"], lr=1e-3, fp16=0, retrain=0, seed=1234,
+                         content_loss=int(content)))
         if distributed:
             from dgan.dist import setup_data_parallel
             setup_data_parallel(m)
         return m
 
-    x_np, y_np = synthetic_batch(args.batch, args.size, seed=1000 + rank)
+    x_np, y_np = synthetic_batch(wl, batch, seed=1000 + rank)
     x = torch.from_numpy(x_np).to(dev)
     y = torch.from_numpy(y_np).to(dev)
     # N=1: the step is captured once into a HIP graph and replayed (eager
@@ -123,9 +167,12 @@ def main():
     # on multi-rank RCCL graph capture (a world-size-1 RCCL group does capture)
     use_graph = not args.no_graph and world == 1
 
+    def trainer_of(model):
+        return model.trainer(x.shape) if args.model == "pix2pix" else model.trainer(x.shape, y.shape)
+
     def measure(content):
         model = build(content)
-        trainer = model.trainer(x.shape)
+        trainer = trainer_of(model)
         for _ in range(max(1, args.warmup // 2)):
             trainer.step(x, y)
         torch.cuda.synchronize()
@@ -175,10 +222,10 @@ def main():
     content = not args.no_content
     model, trainer, graph, elapsed = measure(content)
     hip_graph = graph is not None
-    conv_math = "bf16x6" if trainer.G.ldesc.math == ops.MATH_BF16X6 else "fp32"
+    conv_math = "bf16x6" if ops.default_conv_math() == ops.MATH_BF16X6 else "fp32"
     losses = trainer.loss.cpu().numpy()
     ms_per_step = elapsed / args.steps * 1e3
-    images = world * args.batch * args.steps
+    images = world * batch * args.steps
     value = images / elapsed
 
     # ---- roofline of the conv engine (HIP events, eager pass) ---------------
@@ -195,16 +242,13 @@ def main():
         step_flops = conv_flops
         achieved = conv_flops / (conv_ms * 1e-3)
         peak = X6_PEAK if conv_math == "bf16x6" else FP32_MFMA_PEAK
-        traffic = None
-        tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
-        if os.path.exists(tpath) and content:
-            with open(tpath) as f:
-                traffic = round(json.load(f)["conv_engine_bytes_per_step"], 0)
+        traffic, source = traffic_of(args, wl, content, batch, rank, world)
         roofline = {"bound": "mfma", "achieved": round(achieved / 1e12, 2), "peak": round(peak / 1e12, 1),
                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
-                    "traffic_unit": "HBM bytes per step over the conv-engine launches (rocprofv3 PMC, "
-                                    "profiles/pmc_traffic.json; algorithmic operand bytes per step: "
-                                    f"{round(conv_alg_bytes / 1e9, 2)} GB)",
+                    "traffic_unit": "HBM bytes per step over the conv-engine launches (rocprofv3 PMC "
+                                    "FETCH_SIZE x2 + WRITE_SIZE); algorithmic fp32 operand bytes per step: "
+                                    f"{round(conv_alg_bytes / 1e9, 2)} GB",
+                    "traffic_source": source,
                     "kernel": "dg conv engine (k_conv_gemm_x6 / k_conv_gemm + split passes + narrow + split-K "
                               "reduce), all conv launches of one step",
                     "peak_basis": ("bf16 dense MFMA peak / 6 (six bf16 piece products per fp32 product)"
@@ -217,7 +261,9 @@ def main():
                 print(json.dumps({**r, "tflops": r["flops"] / (r["ms"] * 1e-3) / 1e12}), file=sys.stderr)
 
     core = None
-    if content and world == 1 and not args.no_core and not args.profile_only:
+    if args.model == "pix2pix" and content and world == 1 and not args.no_core and not args.profile_only:
+        del model, trainer, graph
+        torch.cuda.empty_cache()
         _, _, _, el_core = measure(False)
         core = {"value": round(images / el_core, 2), "ms_per_step": round(el_core / args.steps * 1e3, 3),
                 "workload": "the same step without the VGG19 content term (pix2pix.py:87 weight 0)"}
@@ -225,12 +271,20 @@ def main():
     # ---- CPU baseline: torch fp32 restatement, rank 0, N=1 only -------------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_only:
-        cpu = cpu_baseline(args.size, args.cpu_seconds, identity=not args.no_identity,
-                           vgg=model.vgg.arena.export() if model.vgg is not None else None)
+        cpu = cpu_baseline(args, wl, batch, content)
 
     if rank == 0:
+        if args.model == "pix2pix":
+            workload = ("pix2pix train_step (train_pix2pix.py:33-71): G(x)+G(y) identity pass, D real+fake, "
+                        "GAN/L1/L2/TV/identity losses, D and G gradients, Keras Adam G and D; "
+                        + ("VGG19 content loss (seeded stand-in weights: ImageNet weights are a download)"
+                           if content else "VGG content term 0"))
+        else:
+            workload = (f"{args.model} train_step (train_{args.model}.py): G, D real+fake, VGG19 content loss "
+                        f"(seeded stand-in weights), GAN/MAE/MSE/TV losses, both gradients, Adam with "
+                        f"ExponentialDecay (D lr x5)")
         out = {
-            "metric": "training images/sec, pix2pix 256x256 bs16/GPU",
+            "metric": wl["metric"],
             "value": round(value, 2),
             "unit": "images/s",
             "n_gpus": world,
@@ -242,16 +296,13 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32",
             "conv_math": conv_math,
-            "data": "synthetic (seeded noisy/clean 256x256 pairs resident in HBM; random-init weights)",
-            "config": {"workload": "pix2pix train_step (train_pix2pix.py:33-71): G(x)+G(y) identity pass, D real+fake, "
-                                   "GAN/L1/L2/TV/identity losses, D and G gradients, Keras Adam G and D; "
-                                   + ("VGG19 content loss (seeded stand-in weights: ImageNet weights are a download)"
-                                      if content else "VGG content term 0"),
-                       "model": "pix2pix U-Net G (54.4M) + PatchGAN D (2.77M)",
-                       "global_batch": world * args.batch, "batch_per_gpu": args.batch, "image_size": args.size,
+            "data": f"synthetic (seeded noisy/clean {wl['size']}x{wl['size']} pairs resident in HBM; "
+                    "random-init weights)",
+            "config": {"workload": workload, "model": wl["model"], "global_batch": world * batch,
+                       "batch_per_gpu": batch, "image_size": wl["size"], "scale": wl["scale"],
                        "parallelism": f"dp{world}", "hip_graph": hip_graph,
-                       "identity_pass": not args.no_identity,
-                       "conv_gflop_per_image": round(step_flops / args.batch / 1e9, 2) if step_flops else None},
+                       "identity_pass": not args.no_identity if args.model == "pix2pix" else None,
+                       "conv_gflop_per_image": round(step_flops / batch / 1e9, 2) if step_flops else None},
             "losses": [round(float(v), 6) for v in losses],
             "core": core,
             "roofline": roofline,
@@ -262,30 +313,92 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(size, seconds, identity=True, vgg=None):
-    """The oracle's torch-fp32 restatement of the same step on the host cores."""
-    from oracle import torch_p2p as T
-    from oracle import p2p_oracle as O
+def traffic_of(args, wl, content, batch, rank, world):
+    """(HBM bytes per step of the conv engine, where the number came from)."""
+    if args.pmc_leg and rank == 0 and world == 1:
+        try:
+            return pmc_leg(args, batch)
+        except Exception as e:  # report and fall back to the committed profile
+            print(f"[bench] PMC leg failed ({e}); using the committed profile", file=sys.stderr)
+    path = os.path.join(REPO, "profiles", wl["traffic"])
+    if not content or batch != wl["batch"] or not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        t = json.load(f)
+    return (round(t["conv_engine_bytes_per_step"], 0),
+            f"profiles/{wl['traffic']}: {t.get('profile', '?')} (commit {t.get('commit', '?')}), "
+            f"{t.get('method', '')}")
+
+
+def pmc_leg(args, batch):
+    """Two rocprofv3 --pmc passes (FETCH_SIZE, then WRITE_SIZE: they do not fit one
+    pass) over a short --profile-only run of this same workload, as child processes."""
+    import tempfile
+    sys.path.insert(0, os.path.join(REPO, "scripts"))
+    from pmc_traffic import summarise
+    steps = 3
+    out = tempfile.mkdtemp(prefix="dg_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    child = [sys.executable, os.path.join(REPO, "bench.py"), "--profile-only", "--no-graph", "--steps", str(steps),
+             "--warmup", "2", "--model", args.model, "--batch", str(batch)]
+    csvs = []
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(out, ctr)
+        subprocess.run(["timeout", "-s", "KILL", "300", "rocprofv3", "--pmc", ctr, "-d", d, "-o", "pmc",
+                        "--output-format", "csv", "--"] + child, check=True, stdout=subprocess.DEVNULL,
+                       stderr=subprocess.DEVNULL)
+        found = [os.path.join(r, f) for r, _, fs in os.walk(d) for f in fs if f.endswith("counter_collection.csv")]
+        if not found:
+            raise RuntimeError(f"no counter_collection.csv for {ctr}")
+        csvs.append(found[0])
+    # the child runs warmup + timed steps + nothing else: count every launch, divide by the step count
+    t = summarise(csvs[0], csvs[1], steps + 2)
+    return round(t["conv_engine_bytes_per_step"], 0), f"live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child runs ({t['method']})"
+
+
+def cpu_baseline(args, wl, batch, content):
+    """The oracle's torch-fp32 restatement of the same step on the host cores, at the full batch."""
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
     torch.set_num_threads(threads)
-    bs = 2
-    G = O.init_variables(O.g_variables(1), 1234)
-    D = O.init_variables(O.d_variables(1), 1235)
-    step = T.make_fp32_step(G, D, PV=vgg)
-    x, y = O.synthetic_pair(bs, size, seed=7)
+    if args.model == "pix2pix":
+        from oracle import p2p_oracle as O
+        from oracle import torch_p2p as T
+        from dgan.graph import init_graph_variables
+        from dgan.zoo import vgg19_features
+        G = O.init_variables(O.g_variables(1), 1234)
+        D = O.init_variables(O.d_variables(1), 1235)
+        PV = init_graph_variables(vgg19_features(1), 1241) if content else None
+        step = T.make_fp32_step(G, D, PV=PV)
+        what = (f"torch fp32 CPU autograd restatement (oracle/torch_p2p.py) incl. identity pass, "
+                f"{'VGG19 content loss, ' if content else ''}Keras-Adam")
+    else:
+        from oracle import sr_oracle as S
+        from dgan import zoo
+        from dgan.graph import init_graph_variables
+        g = {"srgan": lambda: zoo.srgan_generator(scale=wl["scale"]), "fsrgan": zoo.fsrgan_generator,
+             "autoencoder": zoo.autoencoder_generator}[args.model]()
+        st = S.SRState(args.model, init_graph_variables(g, 1234), init_graph_variables(zoo.sr_discriminator(), 1235),
+                       init_graph_variables(vgg19_features_(), 1241) if content else None, scale=wl["scale"],
+                       dtype=np.float32)
+
+        def step(x, y):
+            S.train_step(st, x, y, apply=True)
+        what = f"torch fp32 CPU autograd restatement (oracle/sr_oracle.py) incl. VGG19 content loss, Adam"
+    x, y = synthetic_batch(wl, batch, seed=7)
     step(x, y)  # warm-up
-    n = 0
     t0 = time.perf_counter()
-    while True:
+    n = 0
+    while n < args.cpu_steps or (time.perf_counter() - t0 < 10.0 and n < 200):   # >= cpu_steps and ~10 s
         step(x, y)
         n += 1
-        if time.perf_counter() - t0 > seconds or n >= 20:
-            break
     el = time.perf_counter() - t0
-    return {"value": round(n * bs / el, 3), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} steps x {bs} images at {size}x{size}, torch fp32 CPU autograd restatement "
-                      f"(oracle/torch_p2p.py) incl. identity pass, {'VGG19 content loss, ' if vgg else ''}"
-                      f"Keras-Adam; {el:.1f}s"}
+    return {"value": round(n * batch / el, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} steps x {batch} images (the full per-GPU batch) at {wl['size']}x{wl['size']}, "
+                      f"{what}; {el:.1f}s"}
+
+
+def vgg19_features_():
+    from dgan.zoo import vgg19_features
+    return vgg19_features(1)
 
 
 if __name__ == "__main__":

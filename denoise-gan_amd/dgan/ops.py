@@ -84,6 +84,11 @@ class Workspace:
 _default_ws = {}
 
 
+def default_conv_math():
+    """The conv arithmetic new descriptors get (DG_CONV_MATH, default bf16x6)."""
+    return ConvDesc(1, 8, 8, 16, 16, 3, 1, "same").math
+
+
 def default_workspace():
     dev = torch.cuda.current_device()
     if dev not in _default_ws:

@@ -296,11 +296,13 @@ def adam_update(p, g, m, v, t, lr, b1=0.9, b2=0.999, eps=1e-7):
 class SRState:
     """Oracle-side copy of one SR model: weights (float64), BN stats, Adam slots."""
 
-    def __init__(self, kind, PG, PD, PV=None, scale=4, lr=1e-3, n_blocks=16):
+    def __init__(self, kind, PG, PD, PV=None, scale=4, lr=1e-3, n_blocks=16, dtype=np.float64):
+        """dtype float32: the fp32 CPU restatement timed by bench.py's cpu_baseline leg."""
         self.kind = kind
-        self.PG = {k: np.asarray(v, np.float64) for k, v in PG.items()}
-        self.PD = {k: np.asarray(v, np.float64) for k, v in PD.items()}
-        self.PV = None if PV is None else {k: np.asarray(v, np.float64) for k, v in PV.items()}
+        self.dtype = dtype
+        self.PG = {k: np.asarray(v, dtype) for k, v in PG.items()}
+        self.PD = {k: np.asarray(v, dtype) for k, v in PD.items()}
+        self.PV = None if PV is None else {k: np.asarray(v, dtype) for k, v in PV.items()}
         self.scale, self.lr, self.n_blocks = scale, lr, n_blocks
         self.Gs, self.Ds = BNStats(), BNStats()
         self.mG = {k: np.zeros_like(v) for k, v in self.PG.items()}
@@ -329,13 +331,13 @@ def train_step(st, x, y, apply=True, dec=None):
     PG = {k: torch.tensor(v, requires_grad=True) for k, v in st.PG.items()}
     PD = {k: torch.tensor(v, requires_grad=True) for k, v in st.PD.items()}
     PV = None if st.PV is None else {k: torch.tensor(v) for k, v in st.PV.items()}
-    xt = torch.tensor(np.asarray(x, np.float64))
-    yt = torch.tensor(np.asarray(y, np.float64))
+    xt = torch.tensor(np.asarray(x, st.dtype))
+    yt = torch.tensor(np.asarray(y, st.dtype))
     gen = st.generator(PG, xt, dec=dec.get("G"))
     zr = sr_discriminator(PD, yt, st.Ds, dec=dec.get("Dr"))
     zf = sr_discriminator(PD, gen, st.Ds, dec=dec.get("Df"))
     cont = (content_loss(PV, yt, gen, dec.get("Vsr"), dec.get("Vhr")) if PV is not None
-            else torch.zeros((), dtype=torch.float64))
+            else torch.zeros((), dtype=xt.dtype))
     adv = 1e-3 * bce_logits(zf, 1.0)
     mse = ((yt - gen) ** 2).mean()
     mae = (yt - gen).abs().mean()

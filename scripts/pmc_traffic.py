@@ -5,7 +5,7 @@ doubled: on gfx950 it reports half the bytes of 16-B-per-lane streaming
 reads (MI355X_MICROARCH.md, HBM section), the access width of the conv
 engine's operand loads (buffer_load ... lds dwordx4) and split passes.
 
-usage: pmc_traffic.py FETCH_CSV WRITE_CSV STEPS [OUT_JSON]"""
+usage: pmc_traffic.py FETCH_CSV WRITE_CSV STEPS [OUT_JSON [PROFILE_LABEL [COMMIT]]]"""
 import json
 import csv
 import sys
@@ -27,7 +27,21 @@ def load(path, counter):
     return per, n
 
 
-def main(fetch_csv, write_csv, steps, out_json=None):
+METHOD = ("rocprofv3 --pmc FETCH_SIZE (x2, gfx950 16B/lane correction) and --pmc WRITE_SIZE in separate "
+          "passes over bench.py --profile-only --no-graph; kernels " + ", ".join(CONV))
+
+
+def summarise(fetch_csv, write_csv, steps):
+    """Per-step conv-engine HBM bytes of two PMC passes over `steps` training steps."""
+    fe, _ = load(fetch_csv, "FETCH_SIZE")
+    wr, _ = load(write_csv, "WRITE_SIZE")
+    tot_f = sum(v for k, v in fe.items() if any(c in k for c in CONV)) * 2.0
+    tot_w = sum(v for k, v in wr.items() if any(c in k for c in CONV))
+    return {"conv_engine_bytes_per_step": (tot_f + tot_w) / steps, "read_bytes_per_step": tot_f / steps,
+            "write_bytes_per_step": tot_w / steps, "steps": steps, "method": METHOD}
+
+
+def main(fetch_csv, write_csv, steps, out_json=None, profile=None, commit=None):
     steps = int(steps)
     fe, _ = load(fetch_csv, "FETCH_SIZE")
     wr, _ = load(write_csv, "WRITE_SIZE")
@@ -43,13 +57,12 @@ def main(fetch_csv, write_csv, steps, out_json=None):
     for k, (f, w) in sorted(rows.items(), key=lambda kv: -(kv[1][0] + kv[1][1]))[:25]:
         print(f"  {k:60s} read {f / 1e9:8.3f} GB  write {w / 1e9:8.3f} GB")
     if out_json:
+        t = summarise(fetch_csv, write_csv, steps)
+        t["profile"] = profile
+        t["commit"] = commit
         with open(out_json, "w") as f:
-            json.dump({"conv_engine_bytes_per_step": (tot_f + tot_w) / steps, "read_bytes_per_step": tot_f / steps,
-                       "write_bytes_per_step": tot_w / steps, "steps": steps,
-                       "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 16B/lane correction) and --pmc WRITE_SIZE "
-                                 "in separate passes over bench.py --profile-only --no-graph; kernels "
-                                 + ", ".join(CONV)}, f, indent=1)
+            json.dump(t, f, indent=1)
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:7])
