@@ -34,10 +34,20 @@ static BnPlan bn_plan(long M, int C) {
     return p;
 }
 
-// ws layout (floats): [3*R*C partials] [4*C scale/shift or bwd coefs]
-static size_t bn_ws_floats(long M, int C) {
+// ws layout (floats) for S row segments of M rows each (independent
+// statistics per segment: e.g. the G(x) and G(y) halves of one batched
+// generator pass, pix2pix.py:44 / :90):
+//   [3*S*R*C partials] [4*S*C scale/shift or bwd coefs]
+static size_t bn_ws_floats(long M, int C, int S = 1) {
     BnPlan p = bn_plan(M, C);
-    return (size_t)3 * p.R * C + (size_t)4 * C + 64;
+    return (size_t)3 * S * p.R * C + (size_t)4 * S * C + 64;
+}
+
+// segment of global row r (S is 1 or 2 in practice: a loop, no 64-bit divide)
+__device__ __forceinline__ int seg_of(long &r, long M) {
+    int s = 0;
+    while (r >= M) { r -= M; ++s; }
+    return s;
 }
 
 // block geometry of the partial passes: CPB channel slots (V channels each) x RL row lanes
@@ -76,7 +86,7 @@ __device__ __forceinline__ void storev(float *p, const float (&v)[V]) {
     }
 }
 
-// per (chunk, channel): n, mean, M2
+// per (segment, chunk, channel): n, mean, M2; grid (channel groups, chunks, segments)
 template <int V>
 __global__ void __launch_bounds__(256)
 k_bn_stats_partial(const float *__restrict__ y, int ld, long M, int C, long rows, int cpb, float *__restrict__ pn,
@@ -84,6 +94,8 @@ k_bn_stats_partial(const float *__restrict__ y, int ld, long M, int C, long rows
     __shared__ float s1s[256 * V], s2s[256 * V];
     const int slot = threadIdx.x % cpb, rl = threadIdx.x / cpb, RL = 256 / cpb;
     const int c0 = (blockIdx.x * cpb + slot) * V;
+    y += (long)blockIdx.z * M * ld;
+    const long pbase = (long)blockIdx.z * gridDim.y;
     const long r0 = (long)blockIdx.y * rows;
     const long r1 = min(M, r0 + rows);
     float s1[V], s2[V], K[V];
@@ -131,7 +143,7 @@ k_bn_stats_partial(const float *__restrict__ y, int ld, long M, int C, long rows
     const float n = (float)(r1 - r0);
 #pragma unroll
     for (int q = 0; q < V; ++q) {
-        const long o = (long)blockIdx.y * C + c0 + q;
+        const long o = (pbase + blockIdx.y) * C + c0 + q;
         pn[o] = n;
         pmean[o] = K[q] + s1[q] / n;
         pm2[o] = fmaxf(s2[q] - s1[q] * s1[q] / n, 0.f);
@@ -152,68 +164,87 @@ __device__ __forceinline__ float lane_sum32(float v, float *sh, int cl, int ln) 
     return s;
 }
 
+// segments in order: segment s's statistics normalise its rows, and the moving
+// averages take the segments' updates one after the other (the reference's
+// separate BN calls, e.g. G(x) then G(y))
 __global__ void __launch_bounds__(256)
-k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, int C, const float *gamma,
+k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, int C, int S, const float *gamma,
                  const float *beta, float *save_mean, float *save_invstd, float *mm, float *mv, float momentum,
                  float eps, float *scale, float *shift) {
     __shared__ float sh[256];
     const int cl = threadIdx.x % FIN_C, ln = threadIdx.x / FIN_C;
     const int c = blockIdx.x * FIN_C + cl;
-    float sn = 0.f, sm = 0.f;
-    if (c < C)
-        for (int r = ln; r < R; r += FIN_L) {
-            const float n = pn[(long)r * C + c];
-            sn += n;
-            sm += n * pmean[(long)r * C + c];
-        }
-    const float n = lane_sum32(sn, sh, cl, ln);
-    const float msum = lane_sum32(sm, sh, cl, ln);
-    const float mu = n > 0.f ? msum / n : 0.f;
-    float q = 0.f;
-    if (c < C)
-        for (int r = ln; r < R; r += FIN_L) {
-            const float d = pmean[(long)r * C + c] - mu;
-            q += pm2[(long)r * C + c] + pn[(long)r * C + c] * d * d;
-        }
-    const float m2 = lane_sum32(q, sh, cl, ln);
-    if (ln != 0 || c >= C) return;
-    const float var = n > 0.f ? m2 / n : 0.f;
-    const float inv = 1.f / sqrtf(var + eps);
-    if (save_mean) save_mean[c] = mu;
-    if (save_invstd) save_invstd[c] = inv;
-    const float g = gamma ? gamma[c] : 1.f;
-    const float b = beta ? beta[c] : 0.f;
-    scale[c] = g * inv;
-    shift[c] = b - mu * g * inv;
-    if (mm) mm[c] -= (mm[c] - mu) * (1.f - momentum);
-    if (mv) {
+    float mmc = 0.f, mvc = 0.f;
+    if (ln == 0 && c < C) {
+        if (mm) mmc = mm[c];
+        if (mv) mvc = mv[c];
+    }
+    for (int sg = 0; sg < S; ++sg) {
+        const long o = (long)sg * R * C;
+        float sn = 0.f, sm = 0.f;
+        if (c < C)
+            for (int r = ln; r < R; r += FIN_L) {
+                const float n = pn[o + (long)r * C + c];
+                sn += n;
+                sm += n * pmean[o + (long)r * C + c];
+            }
+        const float n = lane_sum32(sn, sh, cl, ln);
+        const float msum = lane_sum32(sm, sh, cl, ln);
+        const float mu = n > 0.f ? msum / n : 0.f;
+        float q = 0.f;
+        if (c < C)
+            for (int r = ln; r < R; r += FIN_L) {
+                const float d = pmean[o + (long)r * C + c] - mu;
+                q += pm2[o + (long)r * C + c] + pn[o + (long)r * C + c] * d * d;
+            }
+        const float m2 = lane_sum32(q, sh, cl, ln);
+        if (ln != 0 || c >= C) continue;
+        const float var = n > 0.f ? m2 / n : 0.f;
+        const float inv = 1.f / sqrtf(var + eps);
+        const int sc = sg * C + c;
+        if (save_mean) save_mean[sc] = mu;
+        if (save_invstd) save_invstd[sc] = inv;
+        const float g = gamma ? gamma[c] : 1.f;
+        const float b = beta ? beta[c] : 0.f;
+        scale[sc] = g * inv;
+        shift[sc] = b - mu * g * inv;
+        mmc -= (mmc - mu) * (1.f - momentum);
         const float unb = n > 1.f ? m2 / (n - 1.f) : m2;
-        mv[c] -= (mv[c] - unb) * (1.f - momentum);
+        mvc -= (mvc - unb) * (1.f - momentum);
+    }
+    if (ln == 0 && c < C) {
+        if (mm) mm[c] = mmc;
+        if (mv) mv[c] = mvc;
     }
 }
 
+// S segments of M rows: segment s uses its own scale / shift ([S][C]) and
+// dropout seed (seed + s * seed_stride; the mask index restarts per segment)
 template <int V>
 __global__ void __launch_bounds__(256)
-k_bn_apply(const float *__restrict__ y, int ld, long M, int C, const float *__restrict__ scale,
+k_bn_apply(const float *__restrict__ y, int ld, long M, int S, int C, const float *__restrict__ scale,
            const float *__restrict__ shift, float *__restrict__ z, int ldz, int act, float alpha, float drop_rate,
-           uint32_t seed, const int32_t *step_dev, unsigned short *zp0, int zp0C, int zp0col,
+           uint32_t seed, uint32_t seed_stride, const int32_t *step_dev, unsigned short *zp0, int zp0C, int zp0col,
            unsigned short *zp1, int zp1C, int zp1col) {
     const uint32_t step = step_dev ? (uint32_t)*step_dev : 0u;
     const float keep_scale = drop_rate > 0.f ? 1.f / (1.f - drop_rate) : 1.f;
     const int CV = C / V;
-    const long total = M * CV;
+    const long total = (long)S * M * CV;
     for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
         const long r = e / CV;
         const int c = (int)(e - r * CV) * V;
+        long rr = r;
+        const int sg = seg_of(rr, M);
         float v[V], o[V], sc[V], sh[V];
         loadv<V>(y + r * ld + c, v);
-        loadv<V>(scale + c, sc);
-        loadv<V>(shift + c, sh);
+        loadv<V>(scale + sg * C + c, sc);
+        loadv<V>(shift + sg * C + c, sh);
+        const uint32_t sd = seed + (uint32_t)sg * seed_stride;
 #pragma unroll
         for (int q = 0; q < V; ++q) {
             float t = v[q] * sc[q] + sh[q];
             if (drop_rate > 0.f)
-                t = dropout_keep(seed, step, (uint32_t)(r * C + c + q), drop_rate) ? t * keep_scale : 0.f;
+                t = dropout_keep(sd, step, (uint32_t)(rr * C + c + q), drop_rate) ? t * keep_scale : 0.f;
             o[q] = act_fwd(t, act, alpha);
         }
         storev<V>(z + r * ldz + c, o);
@@ -251,6 +282,12 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
     __shared__ float a1s[256 * V], a2s[256 * V];
     const int slot = threadIdx.x % cpb, rl = threadIdx.x / cpb, RL = 256 / cpb;
     const int c0 = (blockIdx.x * cpb + slot) * V;
+    {   // segment blockIdx.z: its rows and its saved statistics
+        const long ro = (long)blockIdx.z * M;
+        dz += ro * lddz; z += ro * ldz; y += ro * ldy;
+        mean += (long)blockIdx.z * C; invstd += (long)blockIdx.z * C;
+    }
+    const long pbase = (long)blockIdx.z * gridDim.y;
     const long r0 = (long)blockIdx.y * rows;
     const long r1 = min(M, r0 + rows);
     float a1[V], a2[V], mu[V], inv[V];
@@ -301,57 +338,70 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
     }
 #pragma unroll
     for (int q = 0; q < V; ++q) {
-        const long o = (long)blockIdx.y * C + c0 + q;
+        const long o = (pbase + blockIdx.y) * C + c0 + q;
         p1[o] = a1[q];
         p2[o] = a2[q];
     }
 }
 
+// per segment s: coef[s] = [A | B | D | mean] ([S][4][C]); dgamma / dbeta = the
+// sum over the segments (the reference's calls share the BN variables)
 __global__ void __launch_bounds__(256)
-k_bn_bwd_final(const float *p1, const float *p2, int R, int C, long M, const float *gamma, const float *mean,
+k_bn_bwd_final(const float *p1, const float *p2, int R, int C, int S, long M, const float *gamma, const float *mean,
                const float *invstd, float *dgamma, float *dbeta, float beta, float *coef) {
     __shared__ float sh[256];
     const int cl = threadIdx.x % FIN_C, ln = threadIdx.x / FIN_C;
     const int c = blockIdx.x * FIN_C + cl;
-    float a1 = 0.f, a2 = 0.f;
-    if (c < C)
-        for (int r = ln; r < R; r += FIN_L) { a1 += p1[(long)r * C + c]; a2 += p2[(long)r * C + c]; }
-    a1 = lane_sum32(a1, sh, cl, ln);
-    a2 = lane_sum32(a2, sh, cl, ln);
+    float t1 = 0.f, t2 = 0.f;
+    for (int sg = 0; sg < S; ++sg) {
+        const long o = (long)sg * R * C;
+        float a1 = 0.f, a2 = 0.f;
+        if (c < C)
+            for (int r = ln; r < R; r += FIN_L) { a1 += p1[o + (long)r * C + c]; a2 += p2[o + (long)r * C + c]; }
+        a1 = lane_sum32(a1, sh, cl, ln);
+        a2 = lane_sum32(a2, sh, cl, ln);
+        if (ln != 0 || c >= C) continue;
+        t1 += a1;
+        t2 += a2;
+        // dy = k1 (dbn - m1 - xhat m2), xhat = (y - mean) invstd  ==>  dy = A dbn + B (y - mean) + D
+        const int sc = sg * C + c;
+        const float g = gamma ? gamma[c] : 1.f;
+        const float k1 = g * invstd[sc];
+        const float m1 = a1 / (float)M, m2 = a2 / (float)M;
+        float *cf = coef + (long)sg * 4 * C;
+        cf[c] = k1;
+        cf[C + c] = -k1 * m2 * invstd[sc];
+        cf[2 * C + c] = -k1 * m1;
+        cf[3 * C + c] = mean[sc];
+    }
     if (ln != 0 || c >= C) return;
-    if (dbeta) dbeta[c] = a1 + (beta != 0.f ? beta * dbeta[c] : 0.f);
-    if (dgamma) dgamma[c] = a2 + (beta != 0.f ? beta * dgamma[c] : 0.f);
-    // dy = k1 (dbn - m1 - xhat m2), xhat = (y - mean) invstd  ==>  dy = A dbn + B (y - mean) + D
-    const float g = gamma ? gamma[c] : 1.f;
-    const float k1 = g * invstd[c];
-    const float m1 = a1 / (float)M, m2 = a2 / (float)M;
-    coef[c] = k1;
-    coef[C + c] = -k1 * m2 * invstd[c];
-    coef[2 * C + c] = -k1 * m1;
-    coef[3 * C + c] = mean[c];
+    if (dbeta) dbeta[c] = t1 + (beta != 0.f ? beta * dbeta[c] : 0.f);
+    if (dgamma) dgamma[c] = t2 + (beta != 0.f ? beta * dgamma[c] : 0.f);
 }
 
 template <int V>
 __global__ void __launch_bounds__(256)
 k_bn_bwd_apply(const float *__restrict__ dz, int lddz, const float *__restrict__ z, int ldz,
-               const float *__restrict__ y, int ldy, long M, int C, int act, float alpha, float dscale,
+               const float *__restrict__ y, int ldy, long M, int S, int C, int act, float alpha, float dscale,
                const float *__restrict__ coef, float *__restrict__ dy, int lddy, unsigned short *__restrict__ dyp) {
-    // coef = [A | B | D | mean] per channel:  dy = A * dbn + B * (y - mean) + D
+    // coef[s] = [A | B | D | mean] per channel:  dy = A * dbn + B * (y - mean) + D
     // dyp (V = 4, C % 16 == 0): dy's bf16x6 planes too, in the packed layout
     // the consuming conv reads (no split pass before its backward GEMMs)
     const int CV = C / V;
-    const long total = M * CV;
+    const long total = (long)S * M * CV;
     for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
         const long r = e / CV;
         const int c = (int)(e - r * CV) * V;
+        long rr = r;
+        const float *cf = coef + (long)seg_of(rr, M) * 4 * C;
         float dv[V], zv[V], yv[V], A[V], B[V], D[V], Mu[V], o[V];
         loadv<V>(dz + r * lddz + c, dv);
         loadv<V>(z + r * ldz + c, zv);
         loadv<V>(y + r * ldy + c, yv);
-        loadv<V>(coef + c, A);
-        loadv<V>(coef + C + c, B);
-        loadv<V>(coef + 2 * C + c, D);
-        loadv<V>(coef + 3 * C + c, Mu);
+        loadv<V>(cf + c, A);
+        loadv<V>(cf + C + c, B);
+        loadv<V>(cf + 2 * C + c, D);
+        loadv<V>(cf + 3 * C + c, Mu);
 #pragma unroll
         for (int q = 0; q < V; ++q)
             o[q] = A[q] * (dv[q] * act_grad_from_out(zv[q], act, alpha) * dscale) + B[q] * (yv[q] - Mu[q]) + D[q];
@@ -394,9 +444,11 @@ static bool vec4_ok(int C, std::initializer_list<std::pair<const void *, int>> t
 
 extern "C" {
 
-int dg_bn_workspace_size(int M, int C, size_t *bytes) {
-    DG_ARG(bytes && M >= 0 && C > 0, "bad arguments");
-    *bytes = dg::bn_ws_floats(M, C) * sizeof(float);
+int dg_bn_workspace_size(int M, int C, size_t *bytes) { return dg_bn_workspace_size_seg(1, M, C, bytes); }
+
+int dg_bn_workspace_size_seg(int S, int M, int C, size_t *bytes) {
+    DG_ARG(bytes && S >= 1 && M >= 0 && C > 0, "bad arguments");
+    *bytes = dg::bn_ws_floats(M, C, S) * sizeof(float);
     return DG_OK;
 }
 
@@ -404,9 +456,9 @@ int dg_bn_fwd_train(int M, int C, const float *y, int ldy, const float *gamma, c
                     float *save_invstd, float *moving_mean, float *moving_var, float momentum, float eps, float *z,
                     int ldz, int act, float alpha, float drop_rate, uint32_t drop_seed, const int32_t *step_dev,
                     void *ws, size_t ws_bytes, dg_stream_t stream) {
-    return dg_bn_fwd_train_pl(M, C, y, ldy, gamma, beta, save_mean, save_invstd, moving_mean, moving_var, momentum,
-                              eps, z, ldz, act, alpha, drop_rate, drop_seed, step_dev, nullptr, 0, 0, nullptr, 0, 0,
-                              ws, ws_bytes, stream);
+    return dg_bn_fwd_train_seg(1, M, C, y, ldy, gamma, beta, save_mean, save_invstd, moving_mean, moving_var,
+                               momentum, eps, z, ldz, act, alpha, drop_rate, drop_seed, 0u, step_dev, nullptr, 0, 0,
+                               nullptr, 0, 0, ws, ws_bytes, stream);
 }
 
 int dg_bn_fwd_train_pl(int M, int C, const float *y, int ldy, const float *gamma, const float *beta,
@@ -414,28 +466,39 @@ int dg_bn_fwd_train_pl(int M, int C, const float *y, int ldy, const float *gamma
                        float eps, float *z, int ldz, int act, float alpha, float drop_rate, uint32_t drop_seed,
                        const int32_t *step_dev, void *zp0, int zp0C, int zp0col, void *zp1, int zp1C, int zp1col,
                        void *ws, size_t ws_bytes, dg_stream_t stream) {
+    return dg_bn_fwd_train_seg(1, M, C, y, ldy, gamma, beta, save_mean, save_invstd, moving_mean, moving_var,
+                               momentum, eps, z, ldz, act, alpha, drop_rate, drop_seed, 0u, step_dev, zp0, zp0C,
+                               zp0col, zp1, zp1C, zp1col, ws, ws_bytes, stream);
+}
+
+int dg_bn_fwd_train_seg(int S, int M, int C, const float *y, int ldy, const float *gamma, const float *beta,
+                        float *save_mean, float *save_invstd, float *moving_mean, float *moving_var, float momentum,
+                        float eps, float *z, int ldz, int act, float alpha, float drop_rate, uint32_t drop_seed,
+                        uint32_t drop_seed_stride, const int32_t *step_dev, void *zp0, int zp0C, int zp0col,
+                        void *zp1, int zp1C, int zp1col, void *ws, size_t ws_bytes, dg_stream_t stream) {
     DG_ARG(y && z && ws, "NULL tensor");
-    DG_ARG(M > 0 && C > 0 && ldy >= C && ldz >= C, "bad shape");
-    DG_ARG(ws_bytes >= dg::bn_ws_floats(M, C) * sizeof(float), "workspace too small");
+    DG_ARG(S >= 1 && S <= 8 && M > 0 && C > 0 && ldy >= C && ldz >= C, "bad shape");
+    DG_ARG(ws_bytes >= dg::bn_ws_floats(M, C, S) * sizeof(float), "workspace too small");
     DG_ARG(drop_rate >= 0.f && drop_rate < 1.f, "bad dropout rate");
     hipStream_t s = (hipStream_t)stream;
     dg::BnPlan bp = dg::bn_plan(M, C);
     float *w = (float *)ws;
-    float *pn = w, *pmean = w + (size_t)bp.R * C, *pm2 = w + (size_t)2 * bp.R * C;
-    float *scale = w + (size_t)3 * bp.R * C, *shift = scale + C;
+    const size_t RC = (size_t)S * bp.R * C;
+    float *pn = w, *pmean = w + RC, *pm2 = w + 2 * RC;
+    float *scale = w + 3 * RC, *shift = scale + (size_t)S * C;
     const bool v4y = dg::vec4_ok(C, {{y, ldy}});
     if (v4y) {
         dg::PartGeom pg = dg::part_geom(C, 4);
-        hipLaunchKernelGGL(dg::k_bn_stats_partial<4>, dim3(pg.cg, bp.R), dim3(256), 0, s, y, ldy, (long)M, C, bp.rows,
-                           pg.cpb, pn, pmean, pm2);
+        hipLaunchKernelGGL(dg::k_bn_stats_partial<4>, dim3(pg.cg, bp.R, S), dim3(256), 0, s, y, ldy, (long)M, C,
+                           bp.rows, pg.cpb, pn, pmean, pm2);
     } else {
         dg::PartGeom pg = dg::part_geom(C, 1);
-        hipLaunchKernelGGL(dg::k_bn_stats_partial<1>, dim3(pg.cg, bp.R), dim3(256), 0, s, y, ldy, (long)M, C, bp.rows,
-                           pg.cpb, pn, pmean, pm2);
+        hipLaunchKernelGGL(dg::k_bn_stats_partial<1>, dim3(pg.cg, bp.R, S), dim3(256), 0, s, y, ldy, (long)M, C,
+                           bp.rows, pg.cpb, pn, pmean, pm2);
     }
     DG_LAUNCHED("bn_stats_partial");
-    hipLaunchKernelGGL(dg::k_bn_stats_final, dim3(dg_cdiv(C, dg::FIN_C)), dim3(256), 0, s, pn, pmean, pm2, bp.R, C, gamma,
-                       beta, save_mean, save_invstd, moving_mean, moving_var, momentum, eps, scale, shift);
+    hipLaunchKernelGGL(dg::k_bn_stats_final, dim3(dg_cdiv(C, dg::FIN_C)), dim3(256), 0, s, pn, pmean, pm2, bp.R, C, S,
+                       gamma, beta, save_mean, save_invstd, moving_mean, moving_var, momentum, eps, scale, shift);
     DG_LAUNCHED("bn_stats_final");
     const bool av4 = dg::vec4_ok(C, {{y, ldy}, {z, ldz}});
     unsigned short *p0 = (unsigned short *)zp0, *p1 = (unsigned short *)zp1;
@@ -444,14 +507,15 @@ int dg_bn_fwd_train_pl(int M, int C, const float *y, int ldy, const float *gamma
     };
     DG_ARG(pl_ok(p0, zp0C, zp0col) && pl_ok(p1, zp1C, zp1col),
            "z planes need float4-aligned tensors, C and the column %% 16 == 0, col + C <= planes C, 16-byte alignment");
+    const long MT = (long)S * M;
     if (av4)
-        hipLaunchKernelGGL(dg::k_bn_apply<4>, dim3(dg::ew_grid((long)M * C / 4)), dim3(256), 0, s, y, ldy, (long)M, C,
-                           scale, shift, z, ldz, act, alpha, drop_rate, drop_seed, step_dev, p0, zp0C, zp0col, p1,
-                           zp1C, zp1col);
+        hipLaunchKernelGGL(dg::k_bn_apply<4>, dim3(dg::ew_grid(MT * C / 4)), dim3(256), 0, s, y, ldy, (long)M, S, C,
+                           scale, shift, z, ldz, act, alpha, drop_rate, drop_seed, drop_seed_stride, step_dev, p0,
+                           zp0C, zp0col, p1, zp1C, zp1col);
     else
-        hipLaunchKernelGGL(dg::k_bn_apply<1>, dim3(dg::ew_grid((long)M * C)), dim3(256), 0, s, y, ldy, (long)M, C,
-                           scale, shift, z, ldz, act, alpha, drop_rate, drop_seed, step_dev, p0, zp0C, zp0col, p1,
-                           zp1C, zp1col);
+        hipLaunchKernelGGL(dg::k_bn_apply<1>, dim3(dg::ew_grid(MT * C)), dim3(256), 0, s, y, ldy, (long)M, S, C, scale,
+                           shift, z, ldz, act, alpha, drop_rate, drop_seed, drop_seed_stride, step_dev, p0, zp0C,
+                           zp0col, p1, zp1C, zp1col);
     DG_LAUNCHED("bn_apply");
     return DG_OK;
 }
@@ -471,17 +535,25 @@ int dg_bn_bwd(int M, int C, const float *dz, int lddz, const float *z, int ldz, 
               const float *gamma, const float *save_mean, const float *save_invstd, int act, float alpha,
               float drop_rate, float *dy, int lddy, float *dgamma, float *dbeta, float beta, void *ws,
               size_t ws_bytes, dg_stream_t stream) {
-    return dg_bn_bwd_pl(M, C, dz, lddz, z, ldz, y, ldy, gamma, save_mean, save_invstd, act, alpha, drop_rate, dy,
-                        lddy, nullptr, dgamma, dbeta, beta, ws, ws_bytes, stream);
+    return dg_bn_bwd_seg(1, M, C, dz, lddz, z, ldz, y, ldy, gamma, save_mean, save_invstd, act, alpha, drop_rate, dy,
+                         lddy, nullptr, dgamma, dbeta, beta, ws, ws_bytes, stream);
 }
 
 int dg_bn_bwd_pl(int M, int C, const float *dz, int lddz, const float *z, int ldz, const float *y, int ldy,
                  const float *gamma, const float *save_mean, const float *save_invstd, int act, float alpha,
                  float drop_rate, float *dy, int lddy, void *dy_planes, float *dgamma, float *dbeta, float beta,
                  void *ws, size_t ws_bytes, dg_stream_t stream) {
+    return dg_bn_bwd_seg(1, M, C, dz, lddz, z, ldz, y, ldy, gamma, save_mean, save_invstd, act, alpha, drop_rate, dy,
+                         lddy, dy_planes, dgamma, dbeta, beta, ws, ws_bytes, stream);
+}
+
+int dg_bn_bwd_seg(int S, int M, int C, const float *dz, int lddz, const float *z, int ldz, const float *y, int ldy,
+                  const float *gamma, const float *save_mean, const float *save_invstd, int act, float alpha,
+                  float drop_rate, float *dy, int lddy, void *dy_planes, float *dgamma, float *dbeta, float beta,
+                  void *ws, size_t ws_bytes, dg_stream_t stream) {
     DG_ARG(dz && z && y && save_mean && save_invstd && dy && ws, "NULL tensor");
-    DG_ARG(M > 0 && C > 0 && lddz >= C && ldz >= C && ldy >= C && lddy >= C, "bad shape");
-    DG_ARG(ws_bytes >= dg::bn_ws_floats(M, C) * sizeof(float), "workspace too small");
+    DG_ARG(S >= 1 && S <= 8 && M > 0 && C > 0 && lddz >= C && ldz >= C && ldy >= C && lddy >= C, "bad shape");
+    DG_ARG(ws_bytes >= dg::bn_ws_floats(M, C, S) * sizeof(float), "workspace too small");
     if (drop_rate > 0.f && act != DG_ACT_RELU) {
         dg::set_error("dropout backward needs a ReLU after it (mask recovered from the output)");
         return DG_ERR_UNSUPPORTED;
@@ -490,31 +562,33 @@ int dg_bn_bwd_pl(int M, int C, const float *dz, int lddz, const float *z, int ld
     const float dscale = drop_rate > 0.f ? 1.f / (1.f - drop_rate) : 1.f;
     dg::BnPlan bp = dg::bn_plan(M, C);
     float *w = (float *)ws;
-    float *p1 = w, *p2 = w + (size_t)bp.R * C, *coef = w + (size_t)3 * bp.R * C;
+    const size_t RC = (size_t)S * bp.R * C;
+    float *p1 = w, *p2 = w + RC, *coef = w + 3 * RC;
     const bool v4 = dg::vec4_ok(C, {{dz, lddz}, {z, ldz}, {y, ldy}, {save_mean, 4}, {save_invstd, 4}});
     if (v4) {
         dg::PartGeom pg = dg::part_geom(C, 4);
-        hipLaunchKernelGGL(dg::k_bn_bwd_partial<4>, dim3(pg.cg, bp.R), dim3(256), 0, s, dz, lddz, z, ldz, y, ldy,
+        hipLaunchKernelGGL(dg::k_bn_bwd_partial<4>, dim3(pg.cg, bp.R, S), dim3(256), 0, s, dz, lddz, z, ldz, y, ldy,
                            (long)M, C, bp.rows, pg.cpb, save_mean, save_invstd, act, alpha, dscale, p1, p2);
     } else {
         dg::PartGeom pg = dg::part_geom(C, 1);
-        hipLaunchKernelGGL(dg::k_bn_bwd_partial<1>, dim3(pg.cg, bp.R), dim3(256), 0, s, dz, lddz, z, ldz, y, ldy,
+        hipLaunchKernelGGL(dg::k_bn_bwd_partial<1>, dim3(pg.cg, bp.R, S), dim3(256), 0, s, dz, lddz, z, ldz, y, ldy,
                            (long)M, C, bp.rows, pg.cpb, save_mean, save_invstd, act, alpha, dscale, p1, p2);
     }
     DG_LAUNCHED("bn_bwd_partial");
-    hipLaunchKernelGGL(dg::k_bn_bwd_final, dim3(dg_cdiv(C, dg::FIN_C)), dim3(256), 0, s, p1, p2, bp.R, C, (long)M, gamma,
-                       save_mean, save_invstd, dgamma, dbeta, beta, coef);
+    hipLaunchKernelGGL(dg::k_bn_bwd_final, dim3(dg_cdiv(C, dg::FIN_C)), dim3(256), 0, s, p1, p2, bp.R, C, S, (long)M,
+                       gamma, save_mean, save_invstd, dgamma, dbeta, beta, coef);
     DG_LAUNCHED("bn_bwd_final");
     const bool av4 = dg::vec4_ok(C, {{dz, lddz}, {z, ldz}, {y, ldy}, {dy, lddy}});
     unsigned short *dyp = (unsigned short *)dy_planes;
     DG_ARG(!dyp || (av4 && C % 16 == 0 && (((uintptr_t)dyp) & 15) == 0),
            "dy planes need C %% 16 == 0, float4-aligned tensors and a 16-byte aligned plane buffer");
+    const long MT = (long)S * M;
     if (av4)
-        hipLaunchKernelGGL(dg::k_bn_bwd_apply<4>, dim3(dg::ew_grid((long)M * C / 4)), dim3(256), 0, s, dz, lddz, z,
-                           ldz, y, ldy, (long)M, C, act, alpha, dscale, coef, dy, lddy, dyp);
+        hipLaunchKernelGGL(dg::k_bn_bwd_apply<4>, dim3(dg::ew_grid(MT * C / 4)), dim3(256), 0, s, dz, lddz, z, ldz, y,
+                           ldy, (long)M, S, C, act, alpha, dscale, coef, dy, lddy, dyp);
     else
-        hipLaunchKernelGGL(dg::k_bn_bwd_apply<1>, dim3(dg::ew_grid((long)M * C)), dim3(256), 0, s, dz, lddz, z, ldz,
-                           y, ldy, (long)M, C, act, alpha, dscale, coef, dy, lddy, dyp);
+        hipLaunchKernelGGL(dg::k_bn_bwd_apply<1>, dim3(dg::ew_grid(MT * C)), dim3(256), 0, s, dz, lddz, z, ldz, y,
+                           ldy, (long)M, S, C, act, alpha, dscale, coef, dy, lddy, dyp);
     DG_LAUNCHED("bn_bwd_apply");
     return DG_OK;
 }

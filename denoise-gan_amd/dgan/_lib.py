@@ -37,6 +37,12 @@ _SIGS = {
     "dg_bn_fwd_train_pl": (c_int, [c_int, c_int, _P, c_int, _P, _P, _P, _P, _P, _P, c_float, c_float, _P, c_int,
                                    c_int, c_float, c_float, c_uint32, _P, _P, c_int, c_int, _P, c_int, c_int, _P,
                                    c_size_t, _P]),
+    "dg_bn_workspace_size_seg": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_size_t)]),
+    "dg_bn_fwd_train_seg": (c_int, [c_int, c_int, c_int, _P, c_int, _P, _P, _P, _P, _P, _P, c_float, c_float, _P,
+                                    c_int, c_int, c_float, c_float, c_uint32, c_uint32, _P, _P, c_int, c_int, _P,
+                                    c_int, c_int, _P, c_size_t, _P]),
+    "dg_bn_bwd_seg": (c_int, [c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, _P, _P, _P, c_int, c_float,
+                              c_float, _P, c_int, _P, _P, _P, c_float, _P, c_size_t, _P]),
     "dg_bn_fwd_infer": (c_int, [c_int, c_int, _P, c_int, _P, _P, _P, _P, c_float, _P, c_int, c_int, c_float, _P]),
     "dg_bn_bwd": (c_int, [c_int, c_int, _P, c_int, _P, c_int, _P, c_int, _P, _P, _P, c_int, c_float, c_float, _P,
                           c_int, _P, _P, c_float, _P, c_size_t, _P]),

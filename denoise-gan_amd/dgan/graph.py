@@ -248,6 +248,7 @@ class GraphPlan:
             _, h, w, c = x
             if n.kind == "conv":
                 d = ops.ConvDesc(N, h, w, c, n.out.C, n.attrs["k"], n.attrs["s"], n.attrs["padding"])
+                d.label = f"{graph.name}.{n.name}"
                 self.desc[n.idx] = d
                 shp[n.out.id] = d.out_shape
             elif n.kind == "prelu":

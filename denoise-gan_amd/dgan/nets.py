@@ -236,6 +236,8 @@ class GeneratorPlan:
             self.udesc.append(d)
             h, w = d.Ho, d.Wo
         self.ldesc = ConvDesc(NT, h, w, self.last[1], self.last[2], 4, 2, "same", transpose=True)
+        for d, (name, *_) in zip(self.ddesc + self.udesc + [self.ldesc], self.downs + self.ups + [self.last]):
+            d.label = f"G.{name}"
         self.out_shape = self.ldesc.out_shape
         # activations
         s = {}
@@ -251,9 +253,9 @@ class GeneratorPlan:
         s["mean"] = {}
         s["inv"] = {}
         for name, _, co, bn in self.downs + [(n, a, b, True) for n, a, b, _ in self.ups]:
-            if bn:
-                s["mean"][name] = [_empty((co,), device) for _ in range(halves)]
-                s["inv"][name] = [_empty((co,), device) for _ in range(halves)]
+            if bn:  # [half, channel]: one segmented BN call covers the halves
+                s["mean"][name] = _empty((halves, co), device)
+                s["inv"][name] = _empty((halves, co), device)
         s["x"] = None
         s["out"] = None
         self.s = s
@@ -279,7 +281,7 @@ class GeneratorPlan:
     def _bn_ws_max(self):
         m = 0
         for d in self.ddesc + self.udesc:
-            m = max(m, ops.bn_workspace_bytes(self.N * d.Ho * d.Wo, d.Cout))
+            m = max(m, ops.bn_workspace_bytes(self.N * d.Ho * d.Wo, d.Cout, self.halves))
         return m
 
     def _half(self, t, h):
@@ -371,20 +373,24 @@ class GeneratorPlan:
 
     def _bn_fwd(self, s, name, y, z, act, training, ws, drop_rate=0.0, seed_of=None, step_dev=None, outs=()):
         """outs: (plane index k, its x channel count, column) -- the BN output is
-        also written into plane k's kept x planes at that column (training)."""
+        also written into plane k's kept x planes at that column (training).
+        Training: one segmented call, each half normalised by its own statistics
+        and the moving averages updated half 0 then half 1 (the reference's
+        two generator calls); dropout seeds follow dropout_seed(base, layer, half)."""
         A = self.arena
+        if training:
+            rows = z[..., 0].numel()
+            zp = [(xrows(self.planes[k].x, 0, rows, pc), pc, col) for k, pc, col in outs]
+            seed0 = seed_of(0) if seed_of else 0
+            stride = ((seed_of(1) - seed0) & 0xFFFFFFFF) if (seed_of and self.halves > 1) else 0
+            ops.bn_fwd_train(y, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), s["mean"][name], s["inv"][name],
+                             self.bn.mean[name], self.bn.var[name], z, act=act, alpha=ALPHA, momentum=BN_MOMENTUM,
+                             eps=BN_EPS, drop_rate=drop_rate, drop_seed=seed0, step_dev=step_dev, ws=ws, z_planes=zp,
+                             segments=self.halves, drop_seed_stride=stride)
+            return
         for hv in range(self.halves):
-            yh, zh = self._half(y, hv), self._half(z, hv)
-            if training:
-                r0 = hv * zh[..., 0].numel()
-                zp = [(xrows(self.planes[k].x, r0, zh[..., 0].numel(), pc), pc, col) for k, pc, col in outs]
-                ops.bn_fwd_train(yh, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), s["mean"][name][hv],
-                                 s["inv"][name][hv], self.bn.mean[name], self.bn.var[name], zh, act=act, alpha=ALPHA,
-                                 momentum=BN_MOMENTUM, eps=BN_EPS, drop_rate=drop_rate,
-                                 drop_seed=seed_of(hv) if seed_of else 0, step_dev=step_dev, ws=ws, z_planes=zp)
-            else:
-                ops.bn_fwd_infer(yh, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.bn.mean[name],
-                                 self.bn.var[name], zh, act=act, alpha=ALPHA, eps=BN_EPS)
+            ops.bn_fwd_infer(self._half(y, hv), A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.bn.mean[name],
+                             self.bn.var[name], self._half(z, hv), act=act, alpha=ALPHA, eps=BN_EPS)
 
     def _bn_bwd(self, s, name, dz, z, y, dy, act, beta, ws, drop_rate=0.0, P=None):
         """BN backward per half; the gamma/beta gradients of the halves accumulate.
@@ -393,13 +399,9 @@ class GeneratorPlan:
         backward GEMMs) and marks them ready."""
         A = self.arena
         feed = P is not None and P.dy is not None
-        for hv in range(self.halves):
-            dyh = self._half(dy, hv)
-            ops.bn_bwd(self._half(dz, hv), self._half(z, hv), self._half(y, hv), A.param(f"{name}/gamma"),
-                       s["mean"][name][hv], s["inv"][name][hv], dyh, A.grad_of(f"{name}/gamma"),
-                       A.grad_of(f"{name}/beta"), act=act, alpha=ALPHA, drop_rate=drop_rate,
-                       beta=beta if hv == 0 else 1.0, ws=ws,
-                       dy_planes=plane_rows(P.dy, dyh, hv * dyh[..., 0].numel()) if feed else None)
+        ops.bn_bwd(dz, z, y, A.param(f"{name}/gamma"), s["mean"][name], s["inv"][name], dy, A.grad_of(f"{name}/gamma"),
+                   A.grad_of(f"{name}/beta"), act=act, alpha=ALPHA, drop_rate=drop_rate, beta=beta, ws=ws,
+                   dy_planes=plane_rows(P.dy, dy, 0) if feed else None, segments=self.halves)
         if feed:
             P._filled(ops.TENSOR_DY)
 
@@ -502,6 +504,7 @@ class DiscriminatorPlan:
                     d = ConvDesc(n, h, w, ci, co, 4, 2, "same")
                 else:  # ZeroPadding2D() + Conv2D(k4, s1, 'valid') == explicit pad 1
                     d = ConvDesc(n, h, w, ci, co, 4, 1, (1, 1, 1, 1))
+                d.label = f"D.{name}"
                 out.append(d)
                 h, w = d.Ho, d.Wo
             return out
@@ -513,8 +516,8 @@ class DiscriminatorPlan:
         self.y = [(_empty(d.out_shape, device) if sp[3] else None) for d, sp in zip(self.desc, self.specs)]
         self.z = [_empty(d.out_shape, device) for d in self.desc[:-1]]
         self.logits = _empty(self.out_shape, device)
-        self.mean = {sp[0]: [_empty((sp[2],), device) for _ in range(halves)] for sp in self.specs if sp[3]}
-        self.inv = {sp[0]: [_empty((sp[2],), device) for _ in range(halves)] for sp in self.specs if sp[3]}
+        self.mean = {sp[0]: _empty((halves, sp[2]), device) for sp in self.specs if sp[3]}   # [half, channel]
+        self.inv = {sp[0]: _empty((halves, sp[2]), device) for sp in self.specs if sp[3]}
         if train:
             self.dz = [_empty(d.out_shape, device) for d in self.desc[:-1]]
             maxdy = max(d.N * d.Ho * d.Wo * d.Cout for d in self.desc)
@@ -532,7 +535,7 @@ class DiscriminatorPlan:
         else:
             self.planes = self.planes_half = [None] * len(self.desc)
         self.ws_bytes = max([d.max_ws() for d in self.desc + self.desc_half] +
-                            [ops.bn_workspace_bytes(N * d.Ho * d.Wo, d.Cout) for d in self.desc])
+                            [ops.bn_workspace_bytes(N * d.Ho * d.Wo, d.Cout, halves) for d in self.desc])
 
     @property
     def slots(self):
@@ -565,17 +568,18 @@ class DiscriminatorPlan:
                 # z feeds the next conv's kept x planes (training)
                 Pn = self.planes[i + 1]
                 xp = Pn.x if FEED_X and training and Pn is not None else None
-                for hv in range(self.halves):
-                    yh, zh = self._half(y, hv), self._half(z, hv)
-                    if training:
-                        rows = zh[..., 0].numel()
-                        ops.bn_fwd_train(yh, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.mean[name][hv],
-                                         self.inv[name][hv], self.bn.mean[name], self.bn.var[name], zh, act="lrelu",
-                                         alpha=ALPHA, momentum=BN_MOMENTUM, eps=BN_EPS, ws=ws,
-                                         z_planes=[(xrows(xp, hv * rows, rows, co), co, 0)] if xp is not None else ())
-                    else:
-                        ops.bn_fwd_infer(yh, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.bn.mean[name],
-                                         self.bn.var[name], zh, act="lrelu", alpha=ALPHA, eps=BN_EPS)
+                if training:   # one segmented call: real and fake normalised separately, moving stats in order
+                    rows = z[..., 0].numel()
+                    ops.bn_fwd_train(y, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.mean[name],
+                                     self.inv[name], self.bn.mean[name], self.bn.var[name], z, act="lrelu",
+                                     alpha=ALPHA, momentum=BN_MOMENTUM, eps=BN_EPS, ws=ws,
+                                     z_planes=[(xrows(xp, 0, rows, co), co, 0)] if xp is not None else (),
+                                     segments=self.halves)
+                else:
+                    for hv in range(self.halves):
+                        ops.bn_fwd_infer(self._half(y, hv), A.param(f"{name}/gamma"), A.param(f"{name}/beta"),
+                                         self.bn.mean[name], self.bn.var[name], self._half(z, hv), act="lrelu",
+                                         alpha=ALPHA, eps=BN_EPS)
                 if xp is not None:
                     Pn._filled(ops.TENSOR_X)
             h = z
@@ -612,15 +616,14 @@ class DiscriminatorPlan:
                 dy = self._dy(d)
                 if bn:
                     feed = FEED_DY and P is not None and P.dy is not None
-                    for k, hv in enumerate(hs):
-                        rows = slice(k * self.N, (k + 1) * self.N)
-                        ops.bn_bwd(dh[rows], self._half(self.z[i], hv), self._half(self.y[i], hv),
-                                   A.param(f"{name}/gamma"), self.mean[name][hv], self.inv[name][hv], dy[rows],
-                                   A.grad_of(f"{name}/gamma") if param_grads else None,
-                                   A.grad_of(f"{name}/beta") if param_grads else None, act="lrelu", alpha=ALPHA,
-                                   beta=beta if k == 0 else 1.0, ws=ws,
-                                   dy_planes=plane_rows(P.dy, dy[rows], k * dy[rows][..., 0].numel()) if feed
-                                   else None)
+                    # all halves in one segmented call, or the one half's statistics
+                    mean = self.mean[name] if half is None else self.mean[name][half]
+                    inv = self.inv[name] if half is None else self.inv[name][half]
+                    ops.bn_bwd(dh, sub(self.z[i]), sub(self.y[i]), A.param(f"{name}/gamma"), mean, inv, dy,
+                               A.grad_of(f"{name}/gamma") if param_grads else None,
+                               A.grad_of(f"{name}/beta") if param_grads else None, act="lrelu", alpha=ALPHA,
+                               beta=beta, ws=ws, dy_planes=plane_rows(P.dy, dy, 0) if feed else None,
+                               segments=len(hs))
                     if feed:
                         P._filled(ops.TENSOR_DY)
                 else:

@@ -391,7 +391,8 @@ class ConvProfile:
         """-> list of dicts (op, shape, flops, ms); call after synchronising."""
         out = []
         for e0, e1, d, op in self.records:
-            out.append(dict(op=op, transpose=d.transpose, shape=(d.N, d.H, d.W, d.Cin, d.Cout, d.kh, d.sh),
+            out.append(dict(op=op, label=getattr(d, "label", None), transpose=d.transpose,
+                            shape=(d.N, d.H, d.W, d.Cin, d.Cout, d.kh, d.sh),
                             flops=d.flops, bytes=d.op_bytes(op), ms=e0.elapsed_time(e1)))
         return out
 
@@ -412,9 +413,9 @@ def _prof_end(e0, desc, op):
     _PROF.records.append((e0, e1, desc, op))
 
 
-def bn_workspace_bytes(M, C):
+def bn_workspace_bytes(M, C, segments=1):
     n = ctypes.c_size_t()
-    call("dg_bn_workspace_size", M, C, ctypes.byref(n))
+    call("dg_bn_workspace_size_seg", segments, M, C, ctypes.byref(n))
     return n.value
 
 
@@ -423,17 +424,24 @@ def _rows(t):
 
 
 def bn_fwd_train(y, gamma, beta, save_mean, save_invstd, moving_mean, moving_var, z, act="none", alpha=0.3,
-                 momentum=0.99, eps=1e-3, drop_rate=0.0, drop_seed=0, step_dev=None, ws=None, z_planes=()):
+                 momentum=0.99, eps=1e-3, drop_rate=0.0, drop_seed=0, step_dev=None, ws=None, z_planes=(),
+                 segments=1, drop_seed_stride=0):
     """z_planes: up to two (uint8 device tensor, planes C, column) -- packed x
-    planes of consuming convs that also receive z (dg_bn_fwd_train_pl)."""
+    planes of consuming convs that also receive z.  segments: the rows are that
+    many consecutive independent BN calls (dg_bn_fwd_train_seg; save_mean /
+    save_invstd [segments, C], dropout seed drop_seed + s * drop_seed_stride)."""
     C = y.shape[-1]
     M = _rows(y)
+    if M % segments:
+        raise DGError(f"{M} rows do not split into {segments} segments")
+    M //= segments
     ws = ws or default_workspace()
-    buf, n = ws.get(bn_workspace_bytes(M, C))
+    buf, n = ws.get(bn_workspace_bytes(M, C, segments))
     zp = [(t.data_ptr(), int(pc), int(col)) for t, pc, col in z_planes] + [(None, 0, 0)] * (2 - len(z_planes))
-    call("dg_bn_fwd_train_pl", M, C, _p(y), pix_ld(y, C), _p(gamma), _p(beta), _p(save_mean), _p(save_invstd),
-         _p(moving_mean), _p(moving_var), float(momentum), float(eps), _p(z), pix_ld(z, C), act_id(act),
-         float(alpha), float(drop_rate), ctypes.c_uint32(drop_seed & 0xFFFFFFFF), _p(step_dev),
+    call("dg_bn_fwd_train_seg", segments, M, C, _p(y), pix_ld(y, C), _p(gamma), _p(beta), _p(save_mean),
+         _p(save_invstd), _p(moving_mean), _p(moving_var), float(momentum), float(eps), _p(z), pix_ld(z, C),
+         act_id(act), float(alpha), float(drop_rate), ctypes.c_uint32(drop_seed & 0xFFFFFFFF),
+         ctypes.c_uint32(drop_seed_stride & 0xFFFFFFFF), _p(step_dev),
          zp[0][0], zp[0][1], zp[0][2], zp[1][0], zp[1][1], zp[1][2], _p(buf), n, _stream())
     return z
 
@@ -446,14 +454,18 @@ def bn_fwd_infer(y, gamma, beta, moving_mean, moving_var, z, act="none", alpha=0
 
 
 def bn_bwd(dz, z, y, gamma, save_mean, save_invstd, dy, dgamma, dbeta, act="none", alpha=0.3, drop_rate=0.0,
-           beta=0.0, ws=None, dy_planes=None):
+           beta=0.0, ws=None, dy_planes=None, segments=1):
     """dy_planes: a uint8 device tensor (e.g. a slice of a ConvPlanes' dy
-    PlaneBuf) that also receives dy's bf16x6 planes (dg_bn_bwd_pl)."""
+    PlaneBuf) that also receives dy's bf16x6 planes.  segments: see bn_fwd_train
+    (dg_bn_bwd_seg; dgamma / dbeta summed over the segments)."""
     C = y.shape[-1]
     M = _rows(y)
+    if M % segments:
+        raise DGError(f"{M} rows do not split into {segments} segments")
+    M //= segments
     ws = ws or default_workspace()
-    buf, n = ws.get(bn_workspace_bytes(M, C))
-    call("dg_bn_bwd_pl", M, C, _p(dz), pix_ld(dz, C), _p(z), pix_ld(z, C), _p(y), pix_ld(y, C), _p(gamma),
+    buf, n = ws.get(bn_workspace_bytes(M, C, segments))
+    call("dg_bn_bwd_seg", segments, M, C, _p(dz), pix_ld(dz, C), _p(z), pix_ld(z, C), _p(y), pix_ld(y, C), _p(gamma),
          _p(save_mean), _p(save_invstd), act_id(act), float(alpha), float(drop_rate), _p(dy), pix_ld(dy, C),
          None if dy_planes is None else dy_planes.data_ptr(),
          _p(dgamma), _p(dbeta), float(beta), _p(buf), n, _stream())

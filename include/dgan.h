@@ -178,6 +178,28 @@ int dg_bn_bwd_pl(int M, int C, const float *dz, int lddz, const float *z, int ld
                  int act, float alpha, float drop_rate,
                  float *dy, int lddy, void *dy_planes, float *dgamma, float *dbeta, float beta,
                  void *ws, size_t ws_bytes, dg_stream_t stream);
+/* Segmented forms: S independent BN calls over S consecutive row segments of M rows
+ * each, in ONE launch set -- the reference's separate calls of one layer that the
+ * step batches into one pass (G(x) / G(target), pix2pix.py:44 / :90; D(real) /
+ * D(fake), train_pix2pix.py:47-48).  Segment s normalises with its own statistics
+ * (save_mean / save_invstd are [S][C]); the moving averages take the segments'
+ * updates in order; dropout on segment s uses seed drop_seed + s * drop_seed_stride
+ * with the element index restarting per segment; backward: per-segment coefficients,
+ * dgamma / dbeta summed over the segments.  S == 1 is the plain call. */
+int dg_bn_workspace_size_seg(int S, int M, int C, size_t *bytes);
+int dg_bn_fwd_train_seg(int S, int M, int C, const float *y, int ldy, const float *gamma, const float *beta,
+                        float *save_mean, float *save_invstd,
+                        float *moving_mean, float *moving_var, float momentum, float eps,
+                        float *z, int ldz, int act, float alpha,
+                        float drop_rate, uint32_t drop_seed, uint32_t drop_seed_stride, const int32_t *step_dev,
+                        void *zp0, int zp0C, int zp0col, void *zp1, int zp1C, int zp1col,
+                        void *ws, size_t ws_bytes, dg_stream_t stream);
+int dg_bn_bwd_seg(int S, int M, int C, const float *dz, int lddz, const float *z, int ldz,
+                  const float *y, int ldy, const float *gamma,
+                  const float *save_mean, const float *save_invstd,
+                  int act, float alpha, float drop_rate,
+                  float *dy, int lddy, void *dy_planes, float *dgamma, float *dbeta, float beta,
+                  void *ws, size_t ws_bytes, dg_stream_t stream);
 /* dy = dz * act'(z)  for blocks without BN (pix2pix.py:118-121 with apply_batchnorm=False) */
 int dg_act_bwd(int M, int C, const float *dz, int lddz, const float *z, int ldz,
                int act, float alpha, float *dy, int lddy, dg_stream_t stream);

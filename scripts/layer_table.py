@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Per-layer conv table of one pix2pix bs16 training step (HIP events per conv
+call, dgan.ops.ConvProfile), grouped by layer geometry and op, as a markdown
+table: GFLOP, ms, TF/s (fp32-equivalent) and the fraction of the bf16x6
+basis (bf16 dense peak / 6 = 419.4 TF/s).
+
+    python scripts/layer_table.py [--content 0|1] [--steps 3] > profiles/...md
+"""
+import argparse
+import os
+import sys
+from collections import defaultdict
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "denoise-gan_amd"), REPO]
+
+import torch  # noqa: E402
+
+BASIS = 2516.6e12 / 6
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--content", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16)
+    a = ap.parse_args()
+    from bench import Args, WORKLOADS, synthetic_batch
+    from dgan import ops
+    from pix2pix import Pix2Pix
+    m = Pix2Pix(Args(crop_size=256, retrain=0, width=1, seed=1234, dropout_seed=0, identity_loss=1,
+                     content_loss=a.content))
+    x, y = (torch.from_numpy(t).cuda() for t in synthetic_batch(WORKLOADS["pix2pix"], a.batch, 1000))
+    tr = m.trainer(x.shape)
+    for _ in range(3):
+        tr.step(x, y)
+    torch.cuda.synchronize()
+    agg = defaultdict(lambda: [0, 0.0, 0.0])
+    for _ in range(a.steps):
+        with ops.ConvProfile() as prof:
+            tr.step(x, y)
+        torch.cuda.synchronize()
+        for r in prof.summary():
+            N, H, W, Ci, Co, k, s = r["shape"]
+            net, layer = (r["label"] or "?.?").split(".", 1)
+            key = (net, layer + (" (T)" if r["transpose"] else ""), r["op"], N, H, W, Ci, Co, k, s)
+            agg[key][0] += 1
+            agg[key][1] += r["flops"]
+            agg[key][2] += r["ms"]
+    rows = sorted(agg.items(), key=lambda kv: -kv[1][2])
+    tot = defaultdict(lambda: [0.0, 0.0])
+    print(f"| net | layer | op | N | H x W | Cin -> Cout | k/s | calls/step | GFLOP/step | ms/step | TF/s | frac |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|")
+    for (net, kind, op, N, H, W, Ci, Co, k, s), (n, fl, ms) in rows:
+        fl /= a.steps; ms /= a.steps
+        tot[net][0] += fl; tot[net][1] += ms
+        tf = fl / (ms * 1e-3) / 1e12
+        print(f"| {net} | {kind} | {op} | {N} | {H}x{W} | {Ci}->{Co} | {k}/{s} | {n // a.steps} | {fl / 1e9:.1f} | "
+              f"{ms:.3f} | {tf:.1f} | {tf * 1e12 / BASIS:.3f} |")
+    print()
+    for net, (fl, ms) in sorted(tot.items()):
+        tf = fl / (ms * 1e-3) / 1e12
+        print(f"- {net}: {fl / 1e9:.1f} GFLOP in {ms:.3f} ms/step = {tf:.1f} TF/s = {tf * 1e12 / BASIS:.3f} of the basis")
+    fl = sum(v[0] for v in tot.values()); ms = sum(v[1] for v in tot.values())
+    print(f"- all convs: {fl / 1e9:.1f} GFLOP in {ms:.3f} ms/step = {fl / (ms * 1e-3) / 1e12:.1f} TF/s = "
+          f"{fl / (ms * 1e-3) / BASIS:.3f} of the basis")
+
+
+if __name__ == "__main__":
+    main()
