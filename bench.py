@@ -64,7 +64,8 @@ WORKLOADS = {
     "pix2pix": dict(metric="training images/sec, pix2pix 256x256 bs16/GPU", batch=16, size=256, scale=1,
                     model="pix2pix U-Net G (54.4M) + PatchGAN D (2.77M)", traffic="pmc_traffic.json"),
     "srgan": dict(metric="training images/sec, SRGAN 4x 24->96 bs32/GPU", batch=32, size=96, scale=4,
-                  model="SRGAN G (16 residual blocks) + SR D", traffic="pmc_traffic_srgan.json"),
+                  model="SRGAN G (16 residual blocks) + SR D", traffic="pmc_traffic_srgan.json",
+                  fp16=1),   # train_srgan.py:275 defaults to the mixed_float16 policy
     "fsrgan": dict(metric="training images/sec, FastSRGAN 4x 128->512 bs8/GPU", batch=8, size=512, scale=4,
                    model="FastSRGAN G (6 inverted-residual blocks) + SR D", traffic="pmc_traffic_fsrgan.json"),
     "autoencoder": dict(metric="training images/sec, autoencoder 64x64 grayscale bs4/GPU", batch=4, size=64,
@@ -105,11 +106,15 @@ def main():
     ap.add_argument("--profile-only", action="store_true", help="skip roofline/cpu legs (for rocprofv3 runs)")
     ap.add_argument("--pmc-leg", action="store_true",
                     help="measure roofline.traffic now: two rocprofv3 --pmc child runs (FETCH_SIZE, WRITE_SIZE)")
+    ap.add_argument("--fp16", type=int, default=None,
+                    help="SR family: mixed_float16 (fp16 conv GEMMs + dynamic loss scale); default: the "
+                         "reference driver's (train_srgan.py fp16=1, the others 0)")
     ap.add_argument("--dist", action="store_true",
                     help="data-parallel path (process group + gradient all-reduce) even at world size 1")
     args = ap.parse_args()
     wl = WORKLOADS[args.model]
     batch = args.batch or wl["batch"]
+    fp16 = bool(wl.get("fp16", 0) if args.fp16 is None else args.fp16) and args.model != "pix2pix"
     # the one JSON line goes to the original stdout; everything else written to
     # fd 1 (RCCL's version banner, library logs) is sent to stderr
     json_out = os.fdopen(os.dup(1), "w")
@@ -151,7 +156,7 @@ def main():
             from fsrgan import FastSRGAN
             from srgan import SRGAN
             cls = {"srgan": SRGAN, "fsrgan": FastSRGAN, "autoencoder": Autoencoder}[args.model]
-            m = cls(Args(crop_size=wl["size"], scale=wl["scale"], lr=1e-3, fp16=0, retrain=0, seed=1234,
+            m = cls(Args(crop_size=wl["size"], scale=wl["scale"], lr=1e-3, fp16=int(fp16), retrain=0, seed=1234,
                          content_loss=int(content)))
         if distributed:
             from dgan.dist import setup_data_parallel
@@ -222,7 +227,7 @@ def main():
     content = not args.no_content
     model, trainer, graph, elapsed = measure(content)
     hip_graph = graph is not None
-    conv_math = "bf16x6" if ops.default_conv_math() == ops.MATH_BF16X6 else "fp32"
+    conv_math = "fp16" if fp16 else ("bf16x6" if ops.default_conv_math() == ops.MATH_BF16X6 else "fp32")
     losses = trainer.loss.cpu().numpy()
     ms_per_step = elapsed / args.steps * 1e3
     images = world * batch * args.steps
@@ -241,8 +246,8 @@ def main():
         conv_ms = sum(r["ms"] for r in recs)
         step_flops = conv_flops
         achieved = conv_flops / (conv_ms * 1e-3)
-        peak = X6_PEAK if conv_math == "bf16x6" else FP32_MFMA_PEAK
-        traffic, source = traffic_of(args, wl, content, batch, rank, world)
+        peak = {"bf16x6": X6_PEAK, "fp16": BF16_MFMA_PEAK}.get(conv_math, FP32_MFMA_PEAK)
+        traffic, source = traffic_of(args, wl, content, batch, rank, world) if not fp16 else (None, None)
         roofline = {"bound": "mfma", "achieved": round(achieved / 1e12, 2), "peak": round(peak / 1e12, 1),
                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
                     "traffic_unit": "HBM bytes per step over the conv-engine launches (rocprofv3 PMC "
@@ -251,8 +256,9 @@ def main():
                     "traffic_source": source,
                     "kernel": "dg conv engine (k_conv_gemm_x6 / k_conv_gemm + split passes + narrow + split-K "
                               "reduce), all conv launches of one step",
-                    "peak_basis": ("bf16 dense MFMA peak / 6 (six bf16 piece products per fp32 product)"
-                                   if conv_math == "bf16x6" else "fp32 dense MFMA peak"),
+                    "peak_basis": {"bf16x6": "bf16 dense MFMA peak / 6 (six bf16 piece products per fp32 product)",
+                                   "fp16": "fp16 dense MFMA peak (mixed_float16: eligible GEMMs fp16, the rest "
+                                           "fp32-accurate)"}.get(conv_math, "fp32 dense MFMA peak"),
                     "frac_of_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK, 4),
                     "conv_launch_ms_per_step": round(conv_ms, 3), "conv_gflop_per_step": round(conv_flops / 1e9, 1),
                     "step_frac": round(conv_flops / (ms_per_step * 1e-3) / peak, 4)}
@@ -282,7 +288,9 @@ def main():
         else:
             workload = (f"{args.model} train_step (train_{args.model}.py): G, D real+fake, VGG19 content loss "
                         f"(seeded stand-in weights), GAN/MAE/MSE/TV losses, both gradients, Adam with "
-                        f"ExponentialDecay (D lr x5)")
+                        f"ExponentialDecay (D lr x5)"
+                        + ("; mixed_float16: fp16 conv GEMMs, dynamic loss scale (LossScaleOptimizer)"
+                           if fp16 else ""))
         out = {
             "metric": wl["metric"],
             "value": round(value, 2),
@@ -294,7 +302,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "fp16 GEMM operands, fp32 accumulation (mixed_float16)" if fp16 else "fp32",
             "conv_math": conv_math,
             "data": f"synthetic (seeded noisy/clean {wl['size']}x{wl['size']} pairs resident in HBM; "
                     "random-init weights)",

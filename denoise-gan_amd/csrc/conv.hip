@@ -907,11 +907,17 @@ static const TileCfg kX6Cfgs[] = {
     {64, 64, 2, 2, 16, 3, 4, 1.40},   {256, 128, 4, 2, 16, 2, 1, 1.00}, {128, 256, 2, 4, 16, 2, 1, 0.90},
 };
 constexpr int kNumX6Cfgs = sizeof(kX6Cfgs) / sizeof(kX6Cfgs[0]);
+// fp16 kernel configs (conv_x6.hip launch_gemm_f16: the same tiles, K-tile 32)
+static const TileCfg kF16Cfgs[] = {
+    {128, 128, 2, 2, 32, 2, 2, 1.00}, {128, 64, 2, 2, 32, 2, 2, 1.15}, {64, 128, 2, 2, 32, 2, 2, 1.15},
+    {64, 64, 2, 2, 32, 3, 4, 1.40},   {256, 128, 4, 2, 32, 2, 1, 1.00}, {128, 256, 2, 4, 32, 2, 1, 0.90},
+};
+constexpr int kNumF16Cfgs = sizeof(kF16Cfgs) / sizeof(kF16Cfgs[0]);
 
 struct OpPlan {
     int narrow;      // 1 => VALU narrow kernel
     int direct;      // narrow DGRAD on k_direct_dgrad (dy halo staged in LDS)
-    int x6;          // 1 => bf16x6 split-precision kernel (kX6Cfgs), else fp32 MFMA (kCfgs)
+    int x6;          // 1 => bf16x6 split-precision kernel (kX6Cfgs), 2 => fp16 (kF16Cfgs), else fp32 MFMA (kCfgs)
     int cfg;         // tile config index
     int vec;
     int splits, kchunk;
@@ -1080,8 +1086,22 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
             pl.x6_ra = ra; pl.x6_ca = (int)ca; pl.x6_rb = rb; pl.x6_cb = (int)cb;
         }
     }
+    if (math == DG_MATH_FP16) {
+        // the reference's mixed_float16 policy: one fp16 plane per operand, K-tiles of 32
+        int ok = 0;
+        if (mode == MODE_FWD) ok = g.Ci % 32 == 0 && g.Co % 16 == 0;
+        else if (mode == MODE_DGRAD) ok = g.Co % 32 == 0;
+        else ok = g.Ci % 16 == 0 && g.Co % 16 == 0;
+        ok = ok && 2.0 * ra * ca < 2.0e9 && 2.0 * rb * cb < 2.0e9 && g.kh * g.kw <= 32;
+        if (ok) {
+            pl.x6 = 0;
+            choose_tiles(pl, kF16Cfgs, kNumF16Cfgs, 2516.6e12, "DG_FORCE_F16CFG", nullptr);
+            pl.x6 = 2;
+            pl.x6_ra = ra; pl.x6_ca = (int)ca; pl.x6_rb = rb; pl.x6_cb = (int)cb;
+        }
+    }
     if (!pl.x6) choose_tiles(pl, kCfgs, kNumCfgs, 157.3e12, "DG_FORCE_CFG", nullptr);
-    if (pl.x6 && (mode == MODE_FWD || mode == MODE_DGRAD) && g.kh == 3 && g.kw == 3 && g.sh == 1 && g.sw == 1 &&
+    if (pl.x6 == 1 && (mode == MODE_FWD || mode == MODE_DGRAD) && g.kh == 3 && g.kw == 3 && g.sh == 1 && g.sw == 1 &&
         pl.K % 144 == 0 && !getenv("DG_NO_HALO")) {
         // each input pixel staged once per 16-channel chunk instead of once per tap
         const int Hout = mode == MODE_FWD ? g.Ho : g.H, Wout = mode == MODE_FWD ? g.Wo : g.W;
@@ -1105,15 +1125,16 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     pl.slab_bytes = pl.splits > 1 ? (size_t)pl.nphase * pl.splits * pl.M * pl.N * sizeof(float) : 0;
     pl.ws_bytes = pl.slab_bytes;
     if (pl.x6) {
-        // workspace: [split-K slabs][A planes][B planes]
+        // workspace: [split-K slabs][A planes][B planes] (6 B per element bf16x6, 2 B fp16)
+        const size_t eb = pl.x6 == 2 ? 2 : 6;
         pl.x6_a_off = (pl.ws_bytes + 255) & ~(size_t)255;
-        pl.x6_b_off = (pl.x6_a_off + (size_t)6 * ra * ca + 255) & ~(size_t)255;
-        pl.ws_bytes = pl.x6_b_off + (size_t)6 * rb * cb;
+        pl.x6_b_off = (pl.x6_a_off + eb * ra * ca + 255) & ~(size_t)255;
+        pl.ws_bytes = pl.x6_b_off + eb * rb * cb;
     }
     pl.gemm_bytes = pl.ws_bytes;
     if (getenv("DG_PLAN_DEBUG"))
         fprintf(stderr, "[dg plan] mode %d M=%d N=%d K=%d -> %s cfg %d splits %d\n", mode, pl.M, pl.N, pl.K,
-                pl.halo ? "x6h" : (pl.x6 ? "x6" : "fp32"), pl.cfg, pl.splits);
+                pl.halo ? "x6h" : (pl.x6 == 2 ? "f16" : (pl.x6 ? "x6" : "fp32")), pl.cfg, pl.splits);
     return pl;
 }
 
@@ -1194,6 +1215,7 @@ static void plan_all(dg_conv_desc_s *d) {
 static int default_math() {
     const char *m = getenv("DG_CONV_MATH");
     if (m && (!strcmp(m, "fp32") || !strcmp(m, "0"))) return DG_MATH_FP32;
+    if (m && (!strcmp(m, "fp16") || !strcmp(m, "2"))) return DG_MATH_FP16;
     (void)m;
     return DG_MATH_BF16X6;
 }
@@ -1354,6 +1376,26 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
         a.a_bytes = (unsigned)ab;
         a.b_bytes = (unsigned)bb;
     }
+    if (pl.x6 == 2) {
+        // fp16: round both operands into one fp16 plane each in the workspace
+        char *ws = (char *)a.slab;
+        DG_ARG(ws != nullptr, "workspace pointer is NULL");
+        void *pa = ws + pl.x6_a_off, *pb = ws + pl.x6_b_off;
+        const int ldbw = (mode == MODE_DGRAD) ? a.g.Co : ldb;
+        launch_split_f16(A, lda, pl.x6_ra, pl.x6_ca, pa, s);
+        DG_LAUNCHED("split_f16_a");
+        launch_split_f16(B, ldbw, pl.x6_rb, pl.x6_cb, pb, s);
+        DG_LAUNCHED("split_f16_b");
+        a.A = (const float *)pa; a.lda = pl.x6_ca; a.a_bytes = (unsigned)(2 * pl.x6_ra * pl.x6_ca);
+        a.B = (const float *)pb; a.ldb = pl.x6_cb; a.b_bytes = (unsigned)(2 * pl.x6_rb * pl.x6_cb);
+        fastdiv_magic((unsigned)a.g.Wo, a.mg_wo, a.sh_wo);
+        fastdiv_magic((unsigned)a.g.Ho, a.mg_ho, a.sh_ho);
+        DG_ARG(a.yp == nullptr, "fp16 conv math writes no bf16x6 output planes");
+        dim3 grid(pl.mtiles * pl.ntiles, pl.nphase * pl.splits);
+        launch_gemm_f16(mode, pl.cfg, grid, a, s);
+        DG_LAUNCHED("conv_gemm_f16");
+        return finish_splitk(mode, pl, a, s);
+    }
     if (pl.x6) {
         // split both operands into bf16 hi/mid/lo planes in the workspace, then
         // point the GEMM at plane 0 of each (dense rows of x6_ca / x6_cb)
@@ -1454,7 +1496,7 @@ static size_t tensor_plane_bytes(const dg_conv_desc_s *d, int t) {
 // tensors op reads as bf16x6 planes (0 for fp32 / narrow / recast plans)
 static int op_plane_mask(const dg_conv_desc_s *d, int op) {
     const OpPlan &pl = d->plan[op];
-    if (!pl.x6 || pl.narrow || d->rc[op].on || pl.M == 0 || pl.N == 0) return 0;
+    if (pl.x6 != 1 || pl.narrow || d->rc[op].on || pl.M == 0 || pl.N == 0) return 0;
     int ta, tb;
     op_tensors(d, op, ta, tb);
     return ta | tb;
@@ -1524,7 +1566,7 @@ int dg_conv_desc_create(dg_conv_t *out, int N, int H, int W, int Cin, int Cout, 
 
 int dg_conv_set_math(dg_conv_t d, int math) {
     DG_ARG(d != nullptr, "descriptor is NULL");
-    DG_ARG(math == DG_MATH_FP32 || math == DG_MATH_BF16X6, "unknown conv math mode %d", math);
+    DG_ARG(math == DG_MATH_FP32 || math == DG_MATH_BF16X6 || math == DG_MATH_FP16, "unknown conv math mode %d", math);
     d->math = math;
     dg::plan_all(d);
     return DG_OK;

@@ -239,5 +239,8 @@ void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t
 void launch_gemm_x6h(int mode, int bn, dim3 grid, const GemmArgs &a, int tiles_x, int tiles_y, hipStream_t s);
 // fp32 [rows][ld] (first C columns, C % 8 == 0) -> bf16 hi/mid/lo planes [rows][C]
 void launch_split3(const float *src, int ld, long rows, int C, unsigned short *dst, hipStream_t s);
+// the fp16 conv math (DG_MATH_FP16): one fp16 plane [rows][C] and its GEMM (kF16Cfgs)
+void launch_split_f16(const float *src, int ld, long rows, int C, void *dst, hipStream_t s);
+void launch_gemm_f16(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s);
 
 }  // namespace dg

@@ -66,14 +66,53 @@ k_split3(const float *__restrict__ src, int ld, long rows, int C, unsigned short
     }
 }
 
-// The GEMM.  A and B of GemmArgs point at the operands' packed bf16 planes
-// (k_split3 output); lda / ldb are their column counts C (rows are 3C
-// elements), a_bytes / b_bytes their extents.
-template <int MODE, int BM, int BN, int WGM, int WGN, int MINW, int NBUF = 3>
+// Split pass of the fp16 conv math (DG_MATH_FP16, the reference's
+// mixed_float16 policy): fp32 [rows][ld] -> fp16 [rows][C] (round to nearest
+// even; beyond the fp16 range the value becomes inf, which the dynamic loss
+// scale detects downstream).
+__global__ void __launch_bounds__(256)
+k_split_f16(const float *__restrict__ src, int ld, long rows, int C, _Float16 *__restrict__ dst) {
+    const int C8 = C >> 3;
+    const long total = rows * C8;
+    const bool vec = ((ld & 3) == 0) && ((((uintptr_t)src) & 15) == 0);
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long r = e / C8;
+        const int c = (int)(e - r * C8) * 8;
+        const float *sp = src + r * ld + c;
+        f32x4 v0, v1;
+        if (vec) {
+            v0 = *reinterpret_cast<const f32x4 *>(sp);
+            v1 = *reinterpret_cast<const f32x4 *>(sp + 4);
+        } else {
+            v0 = f32x4{sp[0], sp[1], sp[2], sp[3]};
+            v1 = f32x4{sp[4], sp[5], sp[6], sp[7]};
+        }
+        f16x8 h;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { h[q] = (_Float16)v0[q]; h[4 + q] = (_Float16)v1[q]; }
+        *reinterpret_cast<f16x8 *>(dst + r * C + c) = h;
+    }
+}
+
+// The GEMM.  A and B of GemmArgs point at the operands' packed planes; lda /
+// ldb are their column counts C, a_bytes / b_bytes their extents.
+//   NI = 3 (DG_MATH_BF16X6): k_split3 planes, rows of 3C bf16, a K-tile is 16
+//     channels whose three plane images feed three MFMAs (six piece products);
+//   NI = 2 (DG_MATH_FP16): one fp16 plane, rows of C, a K-tile is 32 channels
+//     (pixels for WGRAD) staged as two 16-wide images of one MFMA.
+// An operand row's K-chunk group holds 16 * NI elements in both layouts, so
+// the KC images (k contiguous in memory) address identically; RC images
+// (k-rows = GEMM rows of memory) take image i as plane i (NI = 3) or as the
+// k-rows 16 i .. 16 i + 15 of the tile (NI = 2).
+template <int MODE, int BM, int BN, int WGM, int WGN, int MINW, int NBUF = 3, int NI = 3>
 __global__ void __launch_bounds__(64 * WGM * WGN, MINW)
 k_conv_gemm_x6(const GemmArgs p) {
     static_assert(NBUF == 3 || NBUF == 4, "3 or 4 LDS buffers (2 or 3 K-tiles in flight)");
-    constexpr int BK = 16;
+    static_assert(NI == 3 || NI == 2, "bf16x6 (3 plane images) or fp16 (2 chunk images)");
+    constexpr bool X6 = NI == 3;
+    constexpr int BK = X6 ? 16 : 32;   // k per K-tile
+    constexpr int GS = 16 * NI;        // elements of one K-chunk group in an operand row
+    constexpr int RM = X6 ? 3 : 1;     // operand row = RM * C elements
     constexpr bool A_KC = (MODE != MODE_WGRAD);
     constexpr bool B_KC = (MODE == MODE_DGRAD);
     constexpr int NT = 64 * WGM * WGN;  // threads
@@ -83,7 +122,8 @@ k_conv_gemm_x6(const GemmArgs p) {
     // groups, so the 8 lanes of a ds_write_b128 group (chunks of 2 rows x 3
     // planes) land on distinct banks
     constexpr int APL = BM * 32 + 96, BPL = BN * 32 + 96;
-    constexpr int BUF = 3 * (APL + BPL);            // bytes per buffer
+    constexpr int BUF = NI * (APL + BPL);           // bytes per buffer
+    constexpr int NW_ = WGM * WGN;
     static_assert(WGM * WGN == 4 || WGM * WGN == 8, "4 or 8 waves");
     static_assert(TM >= 1 && TN >= 1 && WTM % 16 == 0 && WTN % 16 == 0, "wave tile of 16x16 tiles");
     static_assert(BM % 32 == 0 && BN % 32 == 0 && BM <= 256 && BN <= 256, "tile");
@@ -92,7 +132,9 @@ k_conv_gemm_x6(const GemmArgs p) {
     // three every DMA and every fragment read names its buffer statically, so
     // the compiler's LDS-DMA alias tracking does not drain the in-flight DMAs
     // of the other buffers before each read
-    __shared__ __attribute__((aligned(16))) char smem0[BUF];
+    constexpr int STAGE = 16 * (WTN + 4);  // epilogue staging floats per wave (in smem0)
+    constexpr int BUF0 = BUF > NW_ * STAGE * 4 ? BUF : NW_ * STAGE * 4;
+    __shared__ __attribute__((aligned(16))) char smem0[BUF0];
     __shared__ __attribute__((aligned(16))) char smem1[BUF];
     __shared__ __attribute__((aligned(16))) char smem2[BUF];
     __shared__ __attribute__((aligned(16))) char smem3[NBUF == 4 ? BUF : 16];
@@ -131,7 +173,7 @@ k_conv_gemm_x6(const GemmArgs p) {
     // belongs at its position.  Operand with X rows (KC) / X columns (RC) has
     // 3*X/32 such 1-KB slots per K-tile, dealt round-robin over the waves.
     constexpr int NW = WGM * WGN;
-    constexpr int A_SL = 3 * BM / 32, B_SL = 3 * BN / 32;          // slots per tile
+    constexpr int A_SL = NI * BM / 32, B_SL = NI * BN / 32;        // slots per tile
     constexpr int A_NJ = (A_SL + NW - 1) / NW, B_NJ = (B_SL + NW - 1) / NW;
     struct Slot { int plane, r, c; bool live; };  // KC: row r, half c; RC: k-row r, column c
     auto slot_of = [&](int d, bool kc, int X) __attribute__((always_inline)) {
@@ -200,7 +242,7 @@ k_conv_gemm_x6(const GemmArgs p) {
             if (mc < p.M) {
                 arow_n[j] = 0;  // column valid
                 int tap = mc / g.Ci; int ci = mc - tap * g.Ci; wg_i[j] = tap / g.kw; wg_j[j] = tap - wg_i[j] * g.kw;
-                wg_ci[j] = (ci >> 4) * 48 + 16 * asl[j].plane + (ci & 8);  // packed column offset
+                wg_ci[j] = X6 ? (ci >> 4) * 48 + 16 * asl[j].plane + (ci & 8) : ci;  // packed column offset
             }
         }
     }
@@ -226,7 +268,7 @@ k_conv_gemm_x6(const GemmArgs p) {
             abase[j] = 0; amask[j] = 0;
             if (arow_n[j] < 0) continue;
             if constexpr (MODE == MODE_FWD) {
-                abase[j] = (((arow_n[j] * g.H + arow_h[j]) * g.W + arow_w[j]) * (3 * p.lda) + 16 * asl[j].plane +
+                abase[j] = (((arow_n[j] * g.H + arow_h[j]) * g.W + arow_w[j]) * (RM * p.lda) + 16 * asl[j].plane +
                             8 * asl[j].c) * 2;
                 for (int a = 0; a < TA; ++a)
                     for (int b = 0; b < TB; ++b) {
@@ -234,7 +276,7 @@ k_conv_gemm_x6(const GemmArgs p) {
                         if ((unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W) amask[j] |= 1 << (a * TB + b);
                     }
             } else {
-                abase[j] = (((arow_n[j] * g.Ho + arow_h[j]) * g.Wo + arow_w[j]) * (3 * p.lda) + 16 * asl[j].plane +
+                abase[j] = (((arow_n[j] * g.Ho + arow_h[j]) * g.Wo + arow_w[j]) * (RM * p.lda) + 16 * asl[j].plane +
                             8 * asl[j].c) * 2;
                 for (int a = 0; a < TA; ++a)
                     for (int b = 0; b < TB; ++b) {
@@ -250,11 +292,12 @@ k_conv_gemm_x6(const GemmArgs p) {
             if constexpr (MODE == MODE_FWD) {  // RC weights: k-row r, columns c..c+7
                 const int col = n0 + bsl[j].c;
                 bok[j] = col < p.N;
-                bbase[j] = (bsl[j].r * (3 * p.ldb) + (col >> 4) * 48 + 16 * bsl[j].plane + (col & 8)) * 2;
+                bbase[j] = X6 ? (bsl[j].r * (3 * p.ldb) + (col >> 4) * 48 + 16 * bsl[j].plane + (col & 8)) * 2
+                              : ((bsl[j].r + 16 * bsl[j].plane) * p.ldb + col) * 2;
             } else {                           // KC weights: row ci
                 const int ci = n0 + bsl[j].r;
                 bok[j] = ci < p.N;
-                bbase[j] = (ci * (3 * p.ldb) + 16 * bsl[j].plane + 8 * bsl[j].c) * 2;
+                bbase[j] = (ci * (RM * p.ldb) + 16 * bsl[j].plane + 8 * bsl[j].c) * 2;
             }
         }
     }
@@ -277,19 +320,19 @@ k_conv_gemm_x6(const GemmArgs p) {
     // issue the DMA of the K-tile at k0 (the walker's tile) into LDS buffer sm
     auto issue_tile = [&](int k0, char *sm) __attribute__((always_inline)) {
         char *As = sm;
-        char *Bs = As + 3 * APL;
+        char *Bs = As + NI * APL;
         // wave-uniform parts of this K-tile's offsets (tap (wk_a, wk_b) of chunk wk_chunk)
         int a_delta = 0, b_delta = 0, tap_bit = 0;
         bool b_tap_ok = true;
         if constexpr (MODE == MODE_FWD) {
-            a_delta = ((wk_a * g.W + wk_b) * (3 * p.lda) + wk_chunk * 48) * 2;
-            b_delta = (((wk_a * g.kw + wk_b) * g.Ci + wk_chunk * BK) * (3 * p.ldb)) * 2;
+            a_delta = ((wk_a * g.W + wk_b) * (RM * p.lda) + wk_chunk * GS) * 2;
+            b_delta = (((wk_a * g.kw + wk_b) * g.Ci + wk_chunk * BK) * (RM * p.ldb)) * 2;
             tap_bit = wk_a * TB + wk_b;
         } else if constexpr (MODE == MODE_DGRAD) {
-            a_delta = (wk_chunk * 48 - (wk_a * g.Wo + wk_b) * (3 * p.lda)) * 2;
+            a_delta = (wk_chunk * GS - (wk_a * g.Wo + wk_b) * (RM * p.lda)) * 2;
             const int i = ph.i0h + wk_a * g.sh, jj = ph.i0w + wk_b * g.sw;
             b_tap_ok = i < g.kh && jj < g.kw;
-            b_delta = ((b_tap_ok ? (i * g.kw + jj) * g.Ci * (3 * p.ldb) : 0) + wk_chunk * 48) * 2;
+            b_delta = ((b_tap_ok ? (i * g.kw + jj) * g.Ci * (RM * p.ldb) : 0) + wk_chunk * GS) * 2;
             tap_bit = wk_a * TB + wk_b;
         }
         (void)a_delta; (void)b_delta; (void)tap_bit; (void)b_tap_ok;
@@ -303,12 +346,12 @@ k_conv_gemm_x6(const GemmArgs p) {
                 ok = (amask[j] >> tap_bit) & 1;
                 off = (unsigned)(abase[j] + a_delta);
             } else {
-                const unsigned pix = (unsigned)(k0 + asl[j].r);
+                const unsigned pix = (unsigned)(k0 + asl[j].r + (X6 ? 0 : 16 * asl[j].plane));
                 const unsigned t = fdiv(pix, p.mg_wo, p.sh_wo); const int wo = (int)(pix - t * g.Wo);
                 const unsigned n = fdiv(t, p.mg_ho, p.sh_ho); const int ho = (int)(t - n * g.Ho);
                 const int hi = ho * g.sh - g.pt + wg_i[j], wi = wo * g.sw - g.pl + wg_j[j];
                 ok = arow_n[j] >= 0 && (int)pix < kend && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
-                off = ((unsigned)(((int)n * g.H + hi) * g.W + wi) * (3 * p.lda) + wg_ci[j]) * 2u;
+                off = ((unsigned)(((int)n * g.H + hi) * g.W + wi) * (RM * p.lda) + wg_ci[j]) * 2u;
             }
             dma(rA, dst, ok ? off : DG_OOB);
         }
@@ -326,9 +369,10 @@ k_conv_gemm_x6(const GemmArgs p) {
                 off = (unsigned)(bbase[j] + b_delta);
             } else {  // WGRAD: dy rows (pixels) contiguous along co
                 const int col = n0 + bsl[j].c;
-                const int pix = k0 + bsl[j].r;
+                const int pix = k0 + bsl[j].r + (X6 ? 0 : 16 * bsl[j].plane);
                 ok = col < p.N && pix < kend;
-                off = ((unsigned)pix * (3 * p.ldb) + (col >> 4) * 48 + 16 * bsl[j].plane + (col & 8)) * 2u;
+                off = X6 ? ((unsigned)pix * (3 * p.ldb) + (col >> 4) * 48 + 16 * bsl[j].plane + (col & 8)) * 2u
+                         : ((unsigned)pix * p.ldb + col) * 2u;
             }
             dma(rB, dst, ok ? off : DG_OOB);
         }
@@ -352,32 +396,29 @@ k_conv_gemm_x6(const GemmArgs p) {
     // [lo;hi].  Per 16x16 tile three MFMAs then sum all six piece products:
     //   [hi|mid].[hi;mid] = hi.hi + mid.mid,  [hi|mid].[mid;hi] = hi.mid + mid.hi,
     //   [hi|lo].[lo;hi]   = hi.lo + lo.hi.
+    // fp16 (NI = 2): A [k0..15 | k16..31], B [k0..15; k16..31], one
+    // v_mfma_f32_16x16x32_f16 per 16x16 tile.
+    auto frag = [&](const char *p0, const char *p1, int rc0, bool kc, bool is_a) __attribute__((always_inline)) {
+        if (kc) return x6_kc_frag(p0, p1, rc0, lane);
+        return is_a ? x6_rc_frag<BM>(p0, p1, rc0, lane) : x6_rc_frag<BN>(p0, p1, rc0, lane);
+    };
     auto read_frags = [&](const char *sm, bf16x8 (&ahm)[TM], bf16x8 (&ahl)[TM], bf16x8 (&b1)[TN],
                           bf16x8 (&b2)[TN], bf16x8 (&b3)[TN]) __attribute__((always_inline)) {
-        const char *A0 = sm, *A1 = sm + APL, *A2 = sm + 2 * APL;
-        const char *B0 = sm + 3 * APL, *B1 = B0 + BPL, *B2 = B0 + 2 * BPL;
+        const char *A0 = sm, *A1 = sm + APL, *A2 = sm + (NI - 1) * APL;
+        const char *B0 = sm + NI * APL, *B1 = B0 + BPL, *B2 = B0 + (NI - 1) * BPL;
 #pragma unroll
         for (int a = 0; a < TM; ++a) {
             const int r0 = wm * WTM + a * 16;
-            if constexpr (A_KC) {
-                ahm[a] = x6_kc_frag(A0, A1, r0, lane);
-                ahl[a] = x6_kc_frag(A0, A2, r0, lane);
-            } else {
-                ahm[a] = x6_rc_frag<BM>(A0, A1, r0, lane);
-                ahl[a] = x6_rc_frag<BM>(A0, A2, r0, lane);
-            }
+            ahm[a] = frag(A0, A1, r0, A_KC, true);
+            if constexpr (X6) ahl[a] = frag(A0, A2, r0, A_KC, true);
         }
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
             const int c0 = wn * WTN + b * 16;
-            if constexpr (B_KC) {
-                b1[b] = x6_kc_frag(B0, B1, c0, lane);
-                b2[b] = x6_kc_frag(B1, B0, c0, lane);
-                b3[b] = x6_kc_frag(B2, B0, c0, lane);
-            } else {
-                b1[b] = x6_rc_frag<BN>(B0, B1, c0, lane);
-                b2[b] = x6_rc_frag<BN>(B1, B0, c0, lane);
-                b3[b] = x6_rc_frag<BN>(B2, B0, c0, lane);
+            b1[b] = frag(B0, B1, c0, B_KC, false);
+            if constexpr (X6) {
+                b2[b] = frag(B1, B0, c0, B_KC, false);
+                b3[b] = frag(B2, B0, c0, B_KC, false);
             }
         }
     };
@@ -390,24 +431,39 @@ k_conv_gemm_x6(const GemmArgs p) {
     // fetch harmless data into idle buffers.
     constexpr int AHEAD = NBUF - 1;
     auto ktile = [&](int kt, const char *cur, char *nxt) __attribute__((always_inline)) {
-        bf16x8 ahm[TM], ahl[TM], b1[TN], b2[TN], b3[TN];
-        read_frags(cur, ahm, ahl, b1, b2, b3);
+        bf16x8 ahm[TM], ahl[X6 ? TM : 1], b1[TN], b2[X6 ? TN : 1], b3[X6 ? TN : 1];
+        if constexpr (X6) {
+            read_frags(cur, ahm, ahl, b1, b2, b3);
+        } else {
+            bf16x8 dA[TM], dB[TN];
+            read_frags(cur, ahm, dA, b1, dB, dB);
+        }
         issue_tile(kbeg + (kt + AHEAD) * BK, nxt);
+        if constexpr (X6) {
 #pragma unroll
-        for (int a = 0; a < TM; ++a)
+            for (int a = 0; a < TM; ++a)
 #pragma unroll
-            for (int b = 0; b < TN; ++b)
-                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahm[a], b1[b], acc[a][b], 0, 0, 0);
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahm[a], b1[b], acc[a][b], 0, 0, 0);
 #pragma unroll
-        for (int a = 0; a < TM; ++a)
+            for (int a = 0; a < TM; ++a)
 #pragma unroll
-            for (int b = 0; b < TN; ++b)
-                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahm[a], b2[b], acc[a][b], 0, 0, 0);
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahm[a], b2[b], acc[a][b], 0, 0, 0);
 #pragma unroll
-        for (int a = 0; a < TM; ++a)
+            for (int a = 0; a < TM; ++a)
 #pragma unroll
-            for (int b = 0; b < TN; ++b)
-                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahl[a], b3[b], acc[a][b], 0, 0, 0);
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahl[a], b3[b], acc[a][b], 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, ahm[a]),
+                                                                       __builtin_bit_cast(f16x8, b1[b]), acc[a][b],
+                                                                       0, 0, 0);
+        }
         wait_dma_c<(AHEAD - 1) * NMINE>();
         barrier();
     };
@@ -444,8 +500,7 @@ k_conv_gemm_x6(const GemmArgs p) {
     // before smem0 becomes the epilogue's staging area
     wait_dma_c<0>();
     barrier();
-    constexpr int STAGE = 16 * (WTN + 4);  // floats per wave
-    static_assert(NW * STAGE * 4 <= BUF, "epilogue staging fits in one LDS buffer");
+    static_assert(NW * STAGE * 4 <= BUF0, "epilogue staging fits in LDS buffer 0");
     // GEMM row -> output pixel (DGRAD: the phase's sub-grid; unit stride and
     // FWD / WGRAD rows are pixels / filter rows); slab rows are GEMM rows
     const bool ident = MODE != MODE_DGRAD || (g.sh == 1 && g.sw == 1);
@@ -471,14 +526,22 @@ void launch_split3(const float *src, int ld, long rows, int C, unsigned short *d
     hipLaunchKernelGGL(k_split3, dim3(blocks), dim3(256), 0, s, src, ld, rows, C, dst);
 }
 
-// tile configs of the bf16x6 kernel (index = kX6Cfgs in conv.hip)
-void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s) {
+void launch_split_f16(const float *src, int ld, long rows, int C, void *dst, hipStream_t s) {
+    const long total = rows * (C / 8);
+    if (total == 0) return;
+    const unsigned blocks = (unsigned)std::min<long>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_split_f16, dim3(blocks), dim3(256), 0, s, src, ld, rows, C, (_Float16 *)dst);
+}
+
+// tile configs of the bf16x6 (ni 3) and fp16 (ni 2) kernels (index = kX6Cfgs / kF16Cfgs in conv.hip)
+template <int NI>
+static void launch_gemm_planes(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s) {
 #define DG_X6(C, BM_, BN_, WM_, WN_, MW_, NB_)                                                                  \
     case C: {                                                                                                   \
         const dim3 blk(64 * WM_ * WN_);                                                                         \
-        if (mode == MODE_FWD) hipLaunchKernelGGL((k_conv_gemm_x6<MODE_FWD, BM_, BN_, WM_, WN_, MW_, NB_>), grid, blk, 0, s, a); \
-        else if (mode == MODE_DGRAD) hipLaunchKernelGGL((k_conv_gemm_x6<MODE_DGRAD, BM_, BN_, WM_, WN_, MW_, NB_>), grid, blk, 0, s, a); \
-        else hipLaunchKernelGGL((k_conv_gemm_x6<MODE_WGRAD, BM_, BN_, WM_, WN_, MW_, NB_>), grid, blk, 0, s, a); \
+        if (mode == MODE_FWD) hipLaunchKernelGGL((k_conv_gemm_x6<MODE_FWD, BM_, BN_, WM_, WN_, MW_, NB_, NI>), grid, blk, 0, s, a); \
+        else if (mode == MODE_DGRAD) hipLaunchKernelGGL((k_conv_gemm_x6<MODE_DGRAD, BM_, BN_, WM_, WN_, MW_, NB_, NI>), grid, blk, 0, s, a); \
+        else hipLaunchKernelGGL((k_conv_gemm_x6<MODE_WGRAD, BM_, BN_, WM_, WN_, MW_, NB_, NI>), grid, blk, 0, s, a); \
         break;                                                                                                  \
     }
     switch (cfg) {
@@ -490,6 +553,14 @@ void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t
         DG_X6(5, 128, 256, 2, 4, 2, 3)
     }
 #undef DG_X6
+}
+
+void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s) {
+    launch_gemm_planes<3>(mode, cfg, grid, a, s);
+}
+
+void launch_gemm_f16(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s) {
+    launch_gemm_planes<2>(mode, cfg, grid, a, s);
 }
 
 }  // namespace dg

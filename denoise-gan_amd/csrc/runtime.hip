@@ -22,7 +22,11 @@ void set_error(const char *fmt, ...) {
 __global__ void __launch_bounds__(256)
 k_adam(float *__restrict__ p, const float *__restrict__ g, float *__restrict__ m, float *__restrict__ v, long n,
        float lr, float b1, float b2, float eps, float gscale, const int32_t *iter, long decay_steps,
-       float decay_rate, int staircase) {
+       float decay_rate, int staircase, const float *ls) {
+    if (ls) {   // dynamic loss scale: skip the step on non-finite gradients, else unscale
+        if (ls[2] == 0.f) return;
+        gscale /= ls[0];
+    }
     const int it = iter ? *iter : 0;
     if (decay_steps > 0) {  // ExponentialDecay evaluated at optimizer.iterations (before the increment)
         float e = (float)it / (float)decay_steps;
@@ -57,7 +61,44 @@ k_adam(float *__restrict__ p, const float *__restrict__ g, float *__restrict__ m
     }
 }
 
-__global__ void k_counter_add(int32_t *c, int32_t inc) { *c += inc; }
+__global__ void k_counter_add(int32_t *c, int32_t inc, const float *ls) {
+    if (!ls || ls[2] != 0.f) *c += inc;
+}
+
+// ---- dynamic loss scale (tf.keras mixed_precision LossScaleOptimizer, loss_scale='dynamic',
+// srgan.py:64-67): state ls = {scale, good steps, finite flag, 0} on the device ----
+__global__ void __launch_bounds__(256) k_scale_by(float *x, long n, const float *ls) {
+    const float sc = ls[0];
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x) x[e] *= sc;
+}
+
+// every thread that sees a non-finite gradient stores 0 to the flag (same value: race-free)
+__global__ void __launch_bounds__(256) k_check_finite(const float *g, long n, float *ls) {
+    bool bad = false;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (long)gridDim.x * blockDim.x)
+        bad |= !isfinite(g[e]);
+    if (bad) ls[2] = 0.f;
+}
+
+// DynamicLossScale.update: finite -> good steps + 1, doubling the scale after `period`
+// of them; non-finite -> halve (not below 1) and restart the count.  Re-arms the flag.
+__global__ void k_loss_scale_update(float *ls, int period, float mult) {
+    float sc = ls[0], good = ls[1];
+    if (ls[2] != 0.f) {
+        good += 1.f;
+        if (good >= (float)period) {
+            const float nx = sc * mult;
+            if (isfinite(nx)) sc = nx;
+            good = 0.f;
+        }
+    } else {
+        sc = fmaxf(sc / mult, 1.f);
+        good = 0.f;
+    }
+    ls[0] = sc;
+    ls[1] = good;
+    ls[2] = 1.f;
+}
 
 __global__ void __launch_bounds__(256)
 k_channel_concat(long npix, const float *a, int lda, int ca, const float *b, int ldb, int cb, float *out, int ldo) {
@@ -101,7 +142,7 @@ int dg_adam(float *p, const float *g, float *m, float *v, int64_t n, float lr, f
     if (n == 0) return DG_OK;
     unsigned grid = (unsigned)std::max<long>(1, std::min<long>(dg_cdiv(n / 4 + 1, 256), 4096));
     hipLaunchKernelGGL(dg::k_adam, dim3(grid), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (long)n, lr, beta1,
-                       beta2, eps, grad_scale, iter_dev, 0L, 1.f, 0);
+                       beta2, eps, grad_scale, iter_dev, 0L, 1.f, 0, (const float *)nullptr);
     DG_LAUNCHED("adam");
     return DG_OK;
 }
@@ -115,14 +156,63 @@ int dg_adam_sched(float *p, const float *g, float *m, float *v, int64_t n, float
     if (n == 0) return DG_OK;
     unsigned grid = (unsigned)std::max<long>(1, std::min<long>(dg_cdiv(n / 4 + 1, 256), 4096));
     hipLaunchKernelGGL(dg::k_adam, dim3(grid), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (long)n, lr, beta1,
-                       beta2, eps, grad_scale, iter_dev, (long)decay_steps, decay_rate, staircase);
+                       beta2, eps, grad_scale, iter_dev, (long)decay_steps, decay_rate, staircase,
+                       (const float *)nullptr);
     DG_LAUNCHED("adam_sched");
+    return DG_OK;
+}
+
+int dg_adam_ls(float *p, const float *g, float *m, float *v, int64_t n, float lr, int64_t decay_steps,
+               float decay_rate, int staircase, float beta1, float beta2, float eps, float grad_scale,
+               const int32_t *iter_dev, const float *loss_scale, dg_stream_t stream) {
+    DG_ARG(p && g && m && v && loss_scale, "NULL tensor");
+    DG_ARG(n >= 0, "negative size");
+    DG_ARG((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0, "adam buffers must be 16B aligned");
+    if (n == 0) return DG_OK;
+    unsigned grid = (unsigned)std::max<long>(1, std::min<long>(dg_cdiv(n / 4 + 1, 256), 4096));
+    hipLaunchKernelGGL(dg::k_adam, dim3(grid), dim3(256), 0, (hipStream_t)stream, p, g, m, v, (long)n, lr, beta1,
+                       beta2, eps, grad_scale, iter_dev, (long)decay_steps, decay_rate, staircase, loss_scale);
+    DG_LAUNCHED("adam_ls");
+    return DG_OK;
+}
+
+int dg_counter_add_ls(int32_t *counter_dev, int32_t inc, const float *loss_scale, dg_stream_t stream) {
+    DG_ARG(counter_dev, "NULL counter");
+    hipLaunchKernelGGL(dg::k_counter_add, dim3(1), dim3(1), 0, (hipStream_t)stream, counter_dev, inc, loss_scale);
+    DG_LAUNCHED("counter_add_ls");
+    return DG_OK;
+}
+
+int dg_scale_by(int64_t n, float *x, const float *loss_scale, dg_stream_t stream) {
+    DG_ARG((x || n == 0) && loss_scale, "NULL tensor");
+    if (n == 0) return DG_OK;
+    hipLaunchKernelGGL(dg::k_scale_by, dim3(dg::grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, (long)n,
+                       loss_scale);
+    DG_LAUNCHED("scale_by");
+    return DG_OK;
+}
+
+int dg_check_finite(int64_t n, const float *g, float *loss_scale, dg_stream_t stream) {
+    DG_ARG((g || n == 0) && loss_scale, "NULL tensor");
+    if (n == 0) return DG_OK;
+    hipLaunchKernelGGL(dg::k_check_finite, dim3(std::min<unsigned>(dg::grid_for(n), 2048)), dim3(256), 0,
+                       (hipStream_t)stream, g, (long)n, loss_scale);
+    DG_LAUNCHED("check_finite");
+    return DG_OK;
+}
+
+int dg_loss_scale_update(float *loss_scale, int period, float multiplier, dg_stream_t stream) {
+    DG_ARG(loss_scale && period > 0 && multiplier > 1.f, "bad arguments");
+    hipLaunchKernelGGL(dg::k_loss_scale_update, dim3(1), dim3(1), 0, (hipStream_t)stream, loss_scale, period,
+                       multiplier);
+    DG_LAUNCHED("loss_scale_update");
     return DG_OK;
 }
 
 int dg_counter_add(int32_t *counter_dev, int32_t inc, dg_stream_t stream) {
     DG_ARG(counter_dev, "NULL counter");
-    hipLaunchKernelGGL(dg::k_counter_add, dim3(1), dim3(1), 0, (hipStream_t)stream, counter_dev, inc);
+    hipLaunchKernelGGL(dg::k_counter_add, dim3(1), dim3(1), 0, (hipStream_t)stream, counter_dev, inc,
+                       (const float *)nullptr);
     DG_LAUNCHED("counter_add");
     return DG_OK;
 }

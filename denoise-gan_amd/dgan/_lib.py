@@ -54,6 +54,12 @@ _SIGS = {
                             ctypes.POINTER(c_float), _P, _P, _P, c_int, _P, c_int, _P, _P, _P, _P, c_size_t, _P]),
     "dg_adam": (c_int, [_P, _P, _P, _P, c_int64, c_float, c_float, c_float, c_float, c_float, _P, _P]),
     "dg_counter_add": (c_int, [_P, ctypes.c_int32, _P]),
+    "dg_scale_by": (c_int, [c_int64, _P, _P, _P]),
+    "dg_check_finite": (c_int, [c_int64, _P, _P, _P]),
+    "dg_adam_ls": (c_int, [_P, _P, _P, _P, c_int64, c_float, c_int64, c_float, c_int, c_float, c_float, c_float,
+                           c_float, _P, _P, _P]),
+    "dg_counter_add_ls": (c_int, [_P, ctypes.c_int32, _P, _P]),
+    "dg_loss_scale_update": (c_int, [_P, c_int, c_float, _P]),
     "dg_channel_concat": (c_int, [c_int64, _P, c_int, c_int, _P, c_int, c_int, _P, c_int, _P]),
     "dg_fill": (c_int, [_P, c_int64, c_float, _P]),
     "dg_strided_copy": (c_int, [c_int64, c_int, _P, c_int, _P, c_int, _P]),

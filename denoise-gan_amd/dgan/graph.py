@@ -229,7 +229,7 @@ class GraphPlan:
     backward over one half of a batched forward."""
 
     def __init__(self, graph, N, H, W, arena, bn_state, device, slots=1, train=True, param_grads=True,
-                 alias=None):
+                 alias=None, math=None):
         self.g = graph
         self.arena, self.bn = arena, bn_state
         self._wver = None  # arena.version at the last forward (frozen networks)
@@ -247,7 +247,7 @@ class GraphPlan:
             x = shp[n.ins[0].id]
             _, h, w, c = x
             if n.kind == "conv":
-                d = ops.ConvDesc(N, h, w, c, n.out.C, n.attrs["k"], n.attrs["s"], n.attrs["padding"])
+                d = ops.ConvDesc(N, h, w, c, n.out.C, n.attrs["k"], n.attrs["s"], n.attrs["padding"], math=math)
                 d.label = f"{graph.name}.{n.name}"
                 self.desc[n.idx] = d
                 shp[n.out.id] = d.out_shape
@@ -662,6 +662,9 @@ class GraphNetwork:
         # a frozen network's weights change only through arena.load (version
         # bump): its bf16x6 weight planes stay valid across forwards
         self.arena.frozen = not trainable
+        # conv arithmetic of this network's plans (None: the library default,
+        # "fp16": the reference's mixed_float16 policy, include/dgan.h DG_MATH_FP16)
+        self.conv_math = None
         self._plans = {}
 
     @property
@@ -692,10 +695,10 @@ class GraphNetwork:
         print_fn(f"Trainable params: {self.arena.count if self.trainable else 0:,d}")
 
     def plan(self, N, H, W, slots=1, train=False, param_grads=True, alias=None):
-        key = (N, H, W, slots, train, param_grads, id(alias) if alias is not None else None)
+        key = (N, H, W, slots, train, param_grads, id(alias) if alias is not None else None, self.conv_math)
         if key not in self._plans:
             self._plans[key] = GraphPlan(self.graph, N, H, W, self.arena, self.bn, self.device, slots=slots,
-                                         train=train, param_grads=param_grads, alias=alias)
+                                         train=train, param_grads=param_grads, alias=alias, math=self.conv_math)
         return self._plans[key]
 
     def __call__(self, x, training=False):

@@ -97,8 +97,8 @@ def default_workspace():
 
 
 # conv GEMM arithmetic (include/dgan.h DG_MATH_*)
-MATH_FP32, MATH_BF16X6 = 0, 1
-MATH_MODES = {"fp32": MATH_FP32, "bf16x6": MATH_BF16X6}
+MATH_FP32, MATH_BF16X6, MATH_FP16 = 0, 1, 2
+MATH_MODES = {"fp32": MATH_FP32, "bf16x6": MATH_BF16X6, "fp16": MATH_FP16}
 
 # layer tensors of dg_conv_planes_t (include/dgan.h DG_TENSOR_*)
 TENSOR_X, TENSOR_DY, TENSOR_W = 1, 2, 4
@@ -506,6 +506,32 @@ def p2p_loss(gen, tgt, logit_real, logit_fake, out, ident=None, weights=LOSS_WEI
 def adam(p, g, m, v, lr, beta1, beta2, eps, iter_dev, grad_scale=1.0):
     call("dg_adam", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), float(beta1), float(beta2), float(eps),
          float(grad_scale), _p(iter_dev), _stream())
+
+
+def scale_by(t, loss_scale):
+    """t *= loss_scale[0] (contiguous device tensor; the dynamic loss scale's seed scaling)."""
+    if not t.is_contiguous():
+        raise DGError("scale_by needs a contiguous tensor")
+    call("dg_scale_by", t.numel(), _p(t), _p(loss_scale), _stream())
+
+
+def check_finite(g, loss_scale):
+    call("dg_check_finite", g.numel(), _p(g), _p(loss_scale), _stream())
+
+
+def adam_ls(p, g, m, v, lr, decay_steps, decay_rate, staircase, beta1, beta2, eps, iter_dev, loss_scale,
+            grad_scale=1.0):
+    call("dg_adam_ls", _p(p), _p(g), _p(m), _p(v), p.numel(), float(lr), int(decay_steps), float(decay_rate),
+         int(bool(staircase)), float(beta1), float(beta2), float(eps), float(grad_scale), _p(iter_dev),
+         _p(loss_scale), _stream())
+
+
+def counter_add_ls(c, loss_scale, inc=1):
+    call("dg_counter_add_ls", _p(c), int(inc), _p(loss_scale), _stream())
+
+
+def loss_scale_update(loss_scale, period=2000, multiplier=2.0):
+    call("dg_loss_scale_update", _p(loss_scale), int(period), float(multiplier), _stream())
 
 
 def counter_add(c, inc=1):

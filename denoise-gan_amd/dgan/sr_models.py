@@ -13,10 +13,13 @@ Reference surface kept:
   .content_loss(hr, sr)              VGG feature MSE / 12.75^2
   .disc_patch / .gf / .df / .n_residual_blocks where the reference defines them
 
-mixed_float16 (args.fp16, srgan.py:63-66): the HIP path computes every
-product fp32-accurately (include/dgan.h DG_MATH_*), i.e. at or above the
-precision of the reference's fp16 policy; the loss-scale API is kept and
-is exact (scale 1).
+mixed_float16 (args.fp16, srgan.py:63-66, train_srgan.py:312-318): every
+eligible conv GEMM of G, D and VGG19 rounds its operands to fp16 and runs
+one fp16 MFMA per product (include/dgan.h DG_MATH_FP16; activations,
+accumulation and the layer math stay fp32), and both optimizers carry a
+dynamic loss scale (2^15, halve and skip on inf/nan, double after 2000
+finite steps) on the device.  Without args.fp16 the conv GEMMs are
+fp32-accurate (bf16x6) and the loss scale is 1.
 """
 import torch
 
@@ -30,15 +33,22 @@ ExponentialDecay = ScheduleConfig
 
 
 class _LossScaleAdam(Adam):
-    """Adam + the mixed_precision.LossScaleOptimizer surface used by train_srgan.py:98-109."""
+    """Adam + the mixed_precision.LossScaleOptimizer surface used by train_srgan.py:98-109.
+    With args.fp16 the scale is the trainer's device state (dynamic, 2^15 initial);
+    otherwise it is 1 (fp32-accurate conv math needs none)."""
 
-    loss_scale = 1.0
+    _ls = None   # device loss-scale state (dgan.sr_trainer.new_loss_scale), fp16 only
+
+    @property
+    def loss_scale(self):
+        return float(self._ls[0].item()) if self._ls is not None else 1.0
 
     def get_scaled_loss(self, loss):
         return loss * self.loss_scale
 
     def get_unscaled_gradients(self, grads):
-        return [None if g is None else g / self.loss_scale for g in grads]
+        s = self.loss_scale
+        return [None if g is None else g / s for g in grads]
 
 
 class SRFamily(object):
@@ -69,6 +79,14 @@ class SRFamily(object):
         self.vgg = VGGNetwork(weights=vw, seed=self.seed + 7, width=int(getattr(args, "vgg_width", 1)),
                               device=self.device) if self.use_content else None
         self.generator, self.discriminator = self.build_networks(args)
+        self.loss_scales = None
+        if self.fp16:
+            from .sr_trainer import new_loss_scale
+            for net in (self.generator, self.discriminator, self.vgg):
+                if net is not None:
+                    net.conv_math = "fp16"
+            self.loss_scales = (new_loss_scale(self.device), new_loss_scale(self.device))
+            self.gen_optimizer._ls, self.disc_optimizer._ls = self.loss_scales
         self.gen_optimizer.bind(self.generator.arena)
         self.disc_optimizer.bind(self.discriminator.arena)
         self.coef = COEF[self.coef_key]
@@ -117,7 +135,8 @@ class SRFamily(object):
         if key not in self._trainers:
             self._trainers[key] = SRTrainer(self.generator, self.discriminator, self.vgg, N, (h, w), (H, W),
                                             self.device, self.coef, self._sched(self.gen_optimizer),
-                                            self._sched(self.disc_optimizer), grad_sync=self.grad_sync)
+                                            self._sched(self.disc_optimizer), grad_sync=self.grad_sync,
+                                            loss_scales=self.loss_scales)
         return self._trainers[key]
 
 

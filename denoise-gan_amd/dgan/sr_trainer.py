@@ -37,7 +37,19 @@ class ScheduleConfig:
         return self.lr * self.decay_rate ** e
 
 
-def apply_adam(arena, cfg, grad_scale=1.0):
+def apply_adam(arena, cfg, grad_scale=1.0, loss_scale=None):
+    """loss_scale: the optimizer's device loss-scale state (fp16): the update is unscaled
+    by it, or skipped with the iteration count when its gradients were not finite."""
+    if loss_scale is not None:
+        if isinstance(cfg, ScheduleConfig):
+            ops.adam_ls(arena.data, arena.grad, arena.m, arena.v, cfg.lr, cfg.decay_steps, cfg.decay_rate,
+                        cfg.staircase, cfg.beta_1, cfg.beta_2, cfg.epsilon, arena.iterations, loss_scale,
+                        grad_scale=grad_scale)
+        else:
+            ops.adam_ls(arena.data, arena.grad, arena.m, arena.v, cfg.lr, 0, 1.0, False, cfg.beta_1, cfg.beta_2,
+                        cfg.epsilon, arena.iterations, loss_scale, grad_scale=grad_scale)
+        ops.counter_add_ls(arena.iterations, loss_scale)
+        return
     if isinstance(cfg, ScheduleConfig):
         ops.adam_sched(arena.data, arena.grad, arena.m, arena.v, cfg.lr, cfg.decay_steps, cfg.decay_rate,
                        cfg.staircase, cfg.beta_1, cfg.beta_2, cfg.epsilon, arena.iterations, grad_scale=grad_scale)
@@ -110,10 +122,27 @@ COEF = {
 }
 
 
-class SRTrainer:
-    """Static plan of one SR-family training step for x [N,h,w,3] -> y [N,H,W,3]."""
+LOSS_SCALE_INIT = 2.0 ** 15     # tf.keras DynamicLossScale defaults (srgan.py:64-67)
+LOSS_SCALE_PERIOD = 2000
+LOSS_SCALE_MULT = 2.0
 
-    def __init__(self, G, D, vgg, N, in_hw, out_hw, device, coef, g_opt, d_opt, grad_sync=None):
+
+def new_loss_scale(device):
+    """Device state of one dynamic loss scale: {scale, good steps, finite flag, 0}."""
+    return torch.tensor([LOSS_SCALE_INIT, 0.0, 1.0, 0.0], dtype=torch.float32, device=device)
+
+
+class SRTrainer:
+    """Static plan of one SR-family training step for x [N,h,w,3] -> y [N,H,W,3].
+
+    loss_scales: (G, D) device loss-scale states for the fp16 conv math (the
+    reference's mixed_float16 policy with LossScaleOptimizer, train_srgan.py:
+    98-109): the loss-gradient seeds are multiplied by the scale, so every fp16
+    GEMM operand of the backward carries scaled gradients; the gradients are
+    checked for inf / nan after the (all-reduced) backward and Adam unscales
+    them or skips the step, then the scale is updated (Keras' dynamic rule)."""
+
+    def __init__(self, G, D, vgg, N, in_hw, out_hw, device, coef, g_opt, d_opt, grad_sync=None, loss_scales=None):
         self.G, self.D, self.vgg = G, D, vgg
         self.N = N
         h, w = in_hw
@@ -121,6 +150,7 @@ class SRTrainer:
         self.coef = tuple(coef)
         self.g_opt, self.d_opt = g_opt, d_opt
         self.grad_sync = grad_sync
+        self.ls_g, self.ls_d = loss_scales if loss_scales is not None else (None, None)
         self.Gp = G.plan(N, h, w, slots=1, train=True)
         if tuple(self.Gp.out_shape) != (N, H, W, 3):
             raise ValueError(f"generator output {self.Gp.out_shape} != target {(N, H, W, 3)}")
@@ -158,6 +188,12 @@ class SRTrainer:
         # ---- losses and their gradients (train_srgan.py:84-96) -------------
         ops.gan_loss(gen, y, zr, zf, self.loss, self.coef, content=content, dgen=self.dgen, dlogit_real_d=self.dzr,
                      dlogit_fake_d=self.dzf_d, dlogit_fake_g=self.dzf_g, ws=ws)
+        if self.ls_g is not None:
+            # get_scaled_loss (train_srgan.py:98-100): the gradient seeds of each loss times its scale
+            for t in (self.dzr, self.dzf_d):
+                ops.scale_by(t, self.ls_d)
+            for t in (self.dgen, self.dzf_g) + ((self.content.dfeat,) if self.content is not None else ()):
+                ops.scale_by(t, self.ls_g)
         sync = self.grad_sync
         # ---- disc gradients (train_srgan.py:105-106) ------------------------
         Dp.backward(self.dzr, slot=0, param_beta=0.0, ws=ws)
@@ -172,9 +208,16 @@ class SRTrainer:
                     on_grads_ready=(sync.ready_G if sync else None))
         if sync:
             sync.finish()
+        if self.ls_g is not None:
+            # LossScaleOptimizer.apply_gradients: are the (all-reduced) gradients finite?
+            ops.check_finite(self.G.arena.grad, self.ls_g)
+            ops.check_finite(self.D.arena.grad, self.ls_d)
         # ---- apply_gradients (train_srgan.py:113-114) -----------------------
         if apply:
             scale = sync.grad_scale if sync else 1.0
-            apply_adam(self.G.arena, self.g_opt, scale)
-            apply_adam(self.D.arena, self.d_opt, scale)
+            apply_adam(self.G.arena, self.g_opt, scale, self.ls_g)
+            apply_adam(self.D.arena, self.d_opt, scale, self.ls_d)
+            if self.ls_g is not None:
+                ops.loss_scale_update(self.ls_g, LOSS_SCALE_PERIOD, LOSS_SCALE_MULT)
+                ops.loss_scale_update(self.ls_d, LOSS_SCALE_PERIOD, LOSS_SCALE_MULT)
         return self.loss

@@ -70,9 +70,18 @@ int dg_conv_workspace_size(dg_conv_t d, int op, size_t *bytes);
  *                    six piece products >= 2^-18 |ab| summed in the fp32 MFMA
  *                    accumulator (dropped terms < 2^-26 |ab|, below fp32
  *                    rounding) on the bf16 matrix cores, 2.7x the f32 MFMA rate.
- * New descriptors take $DG_CONV_MATH ("fp32" | "bf16x6"; default bf16x6).
+ *   DG_MATH_FP16   : the reference's mixed_float16 policy (srgan.py:63-66,
+ *                    train_srgan.py:312-318): both GEMM operands rounded to
+ *                    fp16 (RNE), one v_mfma_f32_16x16x32_f16 per product,
+ *                    fp32 accumulation and fp32 outputs; 6x the bf16x6 MFMA
+ *                    rate.  Gradient operands need the caller's loss scale
+ *                    (dg_loss_scale_*) to stay inside the fp16 range.
+ *                    Eligible GEMMs: FWD Cin % 32 == 0, DGRAD Cout % 32 == 0,
+ *                    WGRAD Cin, Cout % 16 == 0 (others keep fp32); no
+ *                    caller-held planes (dg_conv_op_planes reports none).
+ * New descriptors take $DG_CONV_MATH ("fp32" | "bf16x6" | "fp16"; default bf16x6).
  * Changing the mode re-plans the descriptor: query workspace sizes after it. */
-enum { DG_MATH_FP32 = 0, DG_MATH_BF16X6 = 1 };
+enum { DG_MATH_FP32 = 0, DG_MATH_BF16X6 = 1, DG_MATH_FP16 = 2 };
 int dg_conv_set_math(dg_conv_t d, int math);
 int dg_conv_get_math(dg_conv_t d, int *math);
 
@@ -235,6 +244,23 @@ int dg_adam(float *p, const float *g, float *m, float *v, int64_t n,
             float lr, float beta1, float beta2, float eps, float grad_scale,
             const int32_t *iter_dev, dg_stream_t stream);
 int dg_counter_add(int32_t *counter_dev, int32_t inc, dg_stream_t stream);
+/* Dynamic loss scaling of the fp16 conv math (tf.keras mixed_precision
+ * LossScaleOptimizer(loss_scale='dynamic'), srgan.py:64-67, used by
+ * train_srgan.py:98-109): device state ls[4] = {scale, good steps, finite flag, 0},
+ * initial {2^15, 0, 1, 0}.  Per step: dg_scale_by multiplies the loss-gradient
+ * seeds by the scale, dg_check_finite clears the flag when a gradient is inf/nan,
+ * dg_adam_ls unscales (grad_scale / scale) or skips the whole update when the flag
+ * is clear (Keras skips apply_gradients), dg_counter_add_ls advances the optimizer's
+ * iterations only on an applied step, and dg_loss_scale_update applies Keras'
+ * rule (finite: after `period` (2000) good steps scale *= multiplier (2); not
+ * finite: scale /= multiplier, at least 1) and re-arms the flag. */
+int dg_scale_by(int64_t n, float *x, const float *loss_scale, dg_stream_t stream);
+int dg_check_finite(int64_t n, const float *g, float *loss_scale, dg_stream_t stream);
+int dg_adam_ls(float *p, const float *g, float *m, float *v, int64_t n, float lr, int64_t decay_steps,
+               float decay_rate, int staircase, float beta1, float beta2, float eps, float grad_scale,
+               const int32_t *iter_dev, const float *loss_scale, dg_stream_t stream);
+int dg_counter_add_ls(int32_t *counter_dev, int32_t inc, const float *loss_scale, dg_stream_t stream);
+int dg_loss_scale_update(float *loss_scale, int period, float multiplier, dg_stream_t stream);
 /* Adam under keras.optimizers.schedules.ExponentialDecay (srgan.py:34-46,
  * fsrgan.py:30-43, autoencoder.py:26-37): the learning rate of the update
  * with iterations = *iter_dev is lr * decay_rate^(it / decay_steps) (floor

@@ -35,6 +35,9 @@ TF semantics (beyond those of p2p_oracle):
   S5 vgg19.preprocess_input (caffe): RGB->BGR, minus (103.939, 116.779, 123.68)
   S6 Keras BinaryCrossentropy() on a Sigmoid output in graph mode = BCE with the logits
   S7 ExponentialDecay staircase: lr * rate^floor(iterations / steps), iterations before the update
+  S8 mixed_float16 (fp16=1): GEMM operands rounded to fp16 as the HIP path's DG_MATH_FP16 does them
+     (FP16 below), gradients through the GEMMs at the optimizer's loss scale; LossScaleOptimizer
+     'dynamic' (2^15, x2 after 2000 finite steps, /2 and skip on inf/nan)
 """
 import math
 
@@ -57,15 +60,62 @@ def tf_same_pads(size, k, s):
     return total // 2, total - total // 2
 
 
-def conv(x, w, b=None, s=1):
-    """Conv2D 'same': x NHWC, w HWIO."""
+def _conv_plain(x, w, s):
     k = w.shape[0]
     xt = x.permute(0, 3, 1, 2)
     pt, pb = tf_same_pads(xt.shape[2], k, s)
     pl, pr = tf_same_pads(xt.shape[3], k, s)
     xt = F.pad(xt, (pl, pr, pt, pb))
-    y = F.conv2d(xt, w.permute(3, 2, 0, 1), bias=b, stride=s)
-    return y.permute(0, 2, 3, 1)
+    return F.conv2d(xt, w.permute(3, 2, 0, 1), stride=s).permute(0, 2, 3, 1)
+
+
+# ---- mixed_float16 emulation (S8): the HIP path's DG_MATH_FP16 rounds both
+# operands of each eligible conv GEMM to fp16 and accumulates exactly enough
+# (fp32); the backward GEMMs see the loss-scaled gradient, rounded to fp16.
+# FP16 = None: plain fp64 convs; else {"scale": current loss scale}.
+FP16 = None
+
+
+def _q16(t):
+    return t.to(torch.float16).to(t.dtype)
+
+
+def fp16_ops(ci, co):
+    """Which GEMMs of a conv run in fp16 on the HIP path (include/dgan.h DG_MATH_FP16):
+    (fwd, input grad, weight grad)."""
+    return (ci % 32 == 0 and co % 16 == 0, ci >= 8 and co % 32 == 0, ci % 16 == 0 and co % 16 == 0)
+
+
+class _F16Conv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, s):
+        q = fp16_ops(w.shape[2], w.shape[3])
+        ctx.save_for_backward(x, w)
+        ctx.s, ctx.q = s, q
+        return _conv_plain(_q16(x), _q16(w), s) if q[0] else _conv_plain(x, w, s)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        sc = FP16["scale"]
+        dyq = _q16(dy * sc) / sc
+        dx = dw = None
+        with torch.enable_grad():
+            if ctx.needs_input_grad[0]:
+                xx = x.detach().requires_grad_()
+                y = _conv_plain(xx, _q16(w) if ctx.q[1] else w, ctx.s)
+                dx = torch.autograd.grad(y, xx, dyq if ctx.q[1] else dy)[0]
+            if ctx.needs_input_grad[1]:
+                ww = w.detach().requires_grad_()
+                y = _conv_plain(_q16(x) if ctx.q[2] else x, ww, ctx.s)
+                dw = torch.autograd.grad(y, ww, dyq if ctx.q[2] else dy)[0]
+        return dx, dw, None
+
+
+def conv(x, w, b=None, s=1):
+    """Conv2D 'same': x NHWC, w HWIO (fp16-operand GEMMs while FP16 is set)."""
+    y = _F16Conv.apply(x, w, s) if FP16 is not None else _conv_plain(x, w, s)
+    return y if b is None else y + b
 
 
 def dwconv3(x, k, b=None):
@@ -296,9 +346,12 @@ def adam_update(p, g, m, v, t, lr, b1=0.9, b2=0.999, eps=1e-7):
 class SRState:
     """Oracle-side copy of one SR model: weights (float64), BN stats, Adam slots."""
 
-    def __init__(self, kind, PG, PD, PV=None, scale=4, lr=1e-3, n_blocks=16, dtype=np.float64):
-        """dtype float32: the fp32 CPU restatement timed by bench.py's cpu_baseline leg."""
+    def __init__(self, kind, PG, PD, PV=None, scale=4, lr=1e-3, n_blocks=16, dtype=np.float64, fp16=False):
+        """dtype float32: the fp32 CPU restatement timed by bench.py's cpu_baseline leg.
+        fp16: the mixed_float16 emulation (S8) with a dynamic loss scale per optimizer."""
         self.kind = kind
+        self.fp16 = fp16
+        self.ls = {"G": [2.0 ** 15, 0], "D": [2.0 ** 15, 0]}   # [scale, good steps]
         self.dtype = dtype
         self.PG = {k: np.asarray(v, dtype) for k, v in PG.items()}
         self.PD = {k: np.asarray(v, dtype) for k, v in PD.items()}
@@ -327,7 +380,17 @@ def train_step(st, x, y, apply=True, dec=None):
     gen, gG, gD).  dec: {"G", "Dr", "Df", "Vsr", "Vhr": oracle.decisions.Decisions}
     (any subset) -- the activation decisions of G(x), D(y), D(G(x)) and VGG19
     on G(x) and on y (mask-conditioned parity)."""
+    global FP16
     dec = dec or {}
+    FP16 = {"scale": st.ls["G"][0]} if st.fp16 else None
+    try:
+        return _train_step(st, x, y, apply, dec)
+    finally:
+        FP16 = None
+
+
+def _train_step(st, x, y, apply, dec):
+    global FP16
     PG = {k: torch.tensor(v, requires_grad=True) for k, v in st.PG.items()}
     PD = {k: torch.tensor(v, requires_grad=True) for k, v in st.PD.items()}
     PV = None if st.PV is None else {k: torch.tensor(v) for k, v in st.PV.items()}
@@ -347,19 +410,35 @@ def train_step(st, x, y, apply=True, dec=None):
     if st.kind == "fsrgan":
         disc = 0.5 * disc
     dgen = torch.autograd.grad(gen_loss, gen, retain_graph=True)[0]
-    gG = torch.autograd.grad(gen_loss, list(PG.values()), retain_graph=True)
+    gG = torch.autograd.grad(gen_loss, list(PG.values()), retain_graph=True)   # at G's loss scale
+    if st.fp16:
+        FP16 = {"scale": st.ls["D"][0]}
     gD = torch.autograd.grad(disc, list(PD.values()))
     gG = {k: g.numpy() for k, g in zip(PG, gG)}
     gD = {k: g.numpy() for k, g in zip(PD, gD)}
+    finite = {"G": all(np.isfinite(g).all() for g in gG.values()),
+              "D": all(np.isfinite(g).all() for g in gD.values())}
     out = dict(losses=tuple(float(v.detach()) for v in (gen_loss, adv, mae, mse, cont, disc, var)),
                gen=gen.detach().numpy(), dgen=dgen.numpy(), gG=gG, gD=gD)
     if apply:
         t = st.iterations + 1
         lrg = exp_decay(st.lr, st.iterations)
         lrd = exp_decay(st.lr * 5, st.iterations)
-        for k in st.PG:
-            st.PG[k], st.mG[k], st.vG[k] = adam_update(st.PG[k], gG[k], st.mG[k], st.vG[k], t, lrg)
-        for k in st.PD:
-            st.PD[k], st.mD[k], st.vD[k] = adam_update(st.PD[k], gD[k], st.mD[k], st.vD[k], t, lrd)
+        if not st.fp16 or finite["G"]:
+            for k in st.PG:
+                st.PG[k], st.mG[k], st.vG[k] = adam_update(st.PG[k], gG[k], st.mG[k], st.vG[k], t, lrg)
+        if not st.fp16 or finite["D"]:
+            for k in st.PD:
+                st.PD[k], st.mD[k], st.vD[k] = adam_update(st.PD[k], gD[k], st.mD[k], st.vD[k], t, lrd)
         st.iterations += 1
+        if st.fp16:   # DynamicLossScale.update (after the apply decision)
+            for n in ("G", "D"):
+                sc, good = st.ls[n]
+                if finite[n]:
+                    good += 1
+                    if good >= 2000:
+                        sc, good = sc * 2, 0
+                else:
+                    sc, good = max(sc / 2, 1.0), 0
+                st.ls[n] = [sc, good]
     return out

@@ -1,0 +1,189 @@
+"""The mixed_float16 path of the SR family (args.fp16, srgan.py:63-66,
+train_srgan.py:98-109, :312-318) on the HIP path: DG_MATH_FP16 conv GEMMs
+(operands rounded to fp16, one fp16 MFMA per product, fp32 accumulation) and
+the dynamic loss scale of both optimizers.
+
+  * conv GEMMs vs torch fp64 on the same fp16-rounded operands: only the
+    accumulation order differs (tolerance 2e-5 of the output scale);
+  * the SRGAN / FastSRGAN training step vs oracle/sr_oracle.py's mixed_float16
+    emulation (S8: the same operand rounding, gradients at the loss scale):
+    losses to 1e-3 relative, G(x) max-abs 2e-3, each gradient within 2x the
+    emulation's own distance from the fp64 step (relative L2; see _run);
+  * against the plain fp64 oracle: |dPSNR| < 0.05 dB, losses to 1e-2;
+  * loss scale: an overflowing scale skips the step (weights, Adam slots and
+    the iteration count unchanged) and halves; finite steps keep it and count.
+"""
+import math
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import sr_oracle as S
+
+gpu = pytest.mark.gpu
+DEV = "cuda"
+
+F16_CONVS = [
+    # (name, N, H, W, Cin, Cout, k, s)
+    ("srgan.res", 2, 12, 12, 64, 64, 3, 1),
+    ("d.s2", 2, 24, 24, 32, 32, 3, 2),
+    ("fsrgan.expand", 2, 16, 16, 32, 192, 1, 1),
+    ("fsrgan.project", 2, 16, 16, 192, 32, 1, 1),
+    ("vgg.b3", 2, 12, 12, 256, 256, 3, 1),
+    ("odd.7x5", 3, 7, 5, 64, 96, 3, 1),
+]
+
+
+@gpu
+@pytest.mark.parametrize("case", F16_CONVS, ids=[c[0] for c in F16_CONVS])
+def test_fp16_conv_matches_rounded_operands(case):
+    from torch_ref import conv2d_ref
+    from dgan.ops import ConvDesc
+    name, N, H, W, Ci, Co, k, s = case
+    torch.manual_seed(zlib.crc32(name.encode()))
+    d = ConvDesc(N, H, W, Ci, Co, k, s, "same", math="fp16")
+    assert d.math == 2
+    x = torch.randn(N, H, W, Ci)
+    w = torch.randn(*d.weight_shape) * 0.05
+    dy = torch.randn(N, d.Ho, d.Wo, Co)
+    q = lambda t: t.half().double()
+    xr, wr = q(x).requires_grad_(), q(w).requires_grad_()
+    yr = conv2d_ref(xr, wr, s, d.pads, None)
+    yr.backward(q(dy))
+    y = torch.zeros(N, d.Ho, d.Wo, Co, device=DEV)
+    d.fwd(x.to(DEV), w.to(DEV), y)
+    dx = torch.zeros(N, H, W, Ci, device=DEV)
+    d.bwd_data(dy.to(DEV), w.to(DEV), dx)
+    dw = torch.zeros_like(w, device=DEV)
+    d.bwd_filter(x.to(DEV), dy.to(DEV), dw)
+    torch.cuda.synchronize()
+    for got, ref, what in ((y, yr, "fwd"), (dx, xr.grad, "bwd_data"), (dw, wr.grad, "bwd_filter")):
+        g, r = got.double().cpu(), ref.detach()
+        err = float((g - r).abs().max())
+        assert err <= 2e-5 * float(r.abs().max()), f"{name} {what}: {err:.3e} vs scale {float(r.abs().max()):.3e}"
+
+
+class Args:
+    def __init__(self, **kw):
+        self.crop_size = 32
+        self.scale = 4
+        self.fp16 = 1
+        self.lr = 1e-3
+        self.retrain = 0
+        self.seed = 21
+        self.__dict__.update(kw)
+
+
+def psnr(img, ref):
+    a = (np.asarray(img, np.float64) + 1) / 2
+    b = (np.asarray(ref, np.float64) + 1) / 2
+    return 10 * math.log10(1.0 / np.mean((a - b) ** 2))
+
+
+def _synthetic(N, H, scale, seed):
+    from dataloader import synthetic_pair
+    x, y = synthetic_pair(N, H, seed=seed)
+    return np.ascontiguousarray(x[:, ::scale, ::scale]), y
+
+
+LS = 2.0 ** 8
+
+
+def _run(model_cls, kind, N, H, **kw):
+    m = model_cls(Args(crop_size=H, **kw))
+    assert m.fp16 and m.generator.conv_math == "fp16"
+    PG, PD = m.generator.arena.export(), m.discriminator.arena.export()
+    PV = m.vgg.arena.export() if m.vgg is not None else None
+    x, y = _synthetic(N, H, 4, seed=61)
+    tr = m.trainer(x.shape, y.shape)
+    # Keras' initial 2^15 overflows fp16 in these randomly initialised discriminators' backward
+    # (Keras would halve it over the first steps, as test_dynamic_loss_scale_skips_and_halves
+    # checks); compare at a scale that keeps every fp16 operand finite
+    for t in m.loss_scales:
+        t[0] = LS
+    loss = tr.step(torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV), apply=False)
+    torch.cuda.synchronize()
+    got = loss.cpu().double().numpy()
+    gen = tr.gen_output.detach().cpu().numpy()
+    # the arenas hold the loss-scaled gradients (Adam unscales them); the scales the step
+    # used are 2^15, untouched by apply=False
+    sg, sd = (float(t[0]) for t in m.loss_scales)
+    assert sg == sd == LS and float(m.loss_scales[0][2]) == 1.0 and float(m.loss_scales[1][2]) == 1.0
+    gG = {n: m.generator.arena.grad_of(n).cpu().double().numpy() / sg for n, _ in m.generator.arena.var_list}
+    gD = {n: m.discriminator.arena.grad_of(n).cpu().double().numpy() / sd for n, _ in m.discriminator.arena.var_list}
+    st = S.SRState(kind, PG, PD, PV, scale=4, lr=1e-3, fp16=True)
+    st.ls = {"G": [LS, 0], "D": [LS, 0]}
+    emu = S.train_step(st, x, y, apply=False)
+    ref = S.train_step(S.SRState(kind, PG, PD, PV, scale=4, lr=1e-3), x, y, apply=False)
+    assert np.allclose(got, emu["losses"], rtol=1e-3, atol=1e-6), (got, emu["losses"])
+    assert np.abs(gen - emu["gen"]).max() < 2e-3
+    # Gradients: fp16 operand rounding is itself a perturbation of ~2^-12 per operand, which the
+    # BN backward's mean subtractions amplify into the early layers (measured: the fp16 emulation
+    # differs from the fp64 oracle by 14% of scale on G conv2d/kernel), and fp32 (GPU) vs fp64
+    # (oracle) values round to different fp16 neighbours at rounding ties.  So each variable's
+    # GPU gradient must be as close to the emulation as the emulation is to the fp64 step
+    # (relative L2 within 2x that noise, or within 2e-2) -- a wrong GEMM is orders larger.
+    worst = 0.0
+    for grads, refg, fp64, label in ((gG, emu["gG"], ref["gG"], "G"), (gD, emu["gD"], ref["gD"], "D")):
+        for n, g_ref in refg.items():
+            den = float(np.linalg.norm(g_ref))
+            if den < 1e-12:
+                continue
+            err = float(np.linalg.norm(grads[n] - g_ref)) / den
+            noise = float(np.linalg.norm(g_ref - fp64[n])) / den
+            worst = max(worst, err / max(noise, 1e-2))
+            assert err <= max(2.0 * noise, 2e-2), f"{label} {n}: rel-L2 {err:.3e}, fp16 noise {noise:.3e}"
+    # mixed precision vs the fp64 step
+    assert abs(psnr(gen, y) - psnr(ref["gen"], y)) < 0.05
+    assert np.allclose(got, ref["losses"], rtol=1e-2, atol=1e-5), (got, ref["losses"])
+    print(f"{kind} fp16: worst grad error / max(fp16 noise, 1e-2) {worst:.2f}; dPSNR vs fp64 "
+          f"{abs(psnr(gen, y) - psnr(ref['gen'], y)):.2e} dB")
+    return m
+
+
+@gpu
+def test_srgan_fp16_step_matches_mixed_float16_oracle():
+    from srgan import SRGAN
+    _run(SRGAN, "srgan", N=2, H=32)
+
+
+@gpu
+def test_fsrgan_fp16_step_matches_mixed_float16_oracle():
+    from fsrgan import FastSRGAN
+    _run(FastSRGAN, "fsrgan", N=2, H=64)
+
+
+@gpu
+def test_dynamic_loss_scale_skips_and_halves():
+    """LossScaleOptimizer(loss_scale='dynamic') semantics on the device: a scale whose
+    scaled gradients overflow fp16 gives inf/nan gradients -> the step is skipped (no
+    weight, slot or iteration change) and the scale halves; a finite step updates and
+    counts a good step."""
+    from srgan import SRGAN
+    m = SRGAN(Args(crop_size=32, vgg_width=8))
+    x, y = _synthetic(2, 32, 4, seed=3)
+    tr = m.trainer(x.shape, y.shape)
+    xd, yd = torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV)
+    lsg, lsd = m.loss_scales
+    lsd[0] = LS
+    lsg[0] = 3.0e38          # scaled seeds overflow fp16 in the first backward GEMM
+    before = m.generator.arena.data.clone()
+    bm = m.generator.arena.m.clone()
+    tr.step(xd, yd)
+    torch.cuda.synchronize()
+    assert torch.equal(m.generator.arena.data, before) and torch.equal(m.generator.arena.m, bm)
+    assert int(m.generator.arena.iterations.item()) == 0
+    assert float(lsg[0]) == float(np.float32(3.0e38)) / 2 and float(lsg[1]) == 0.0 and float(lsg[2]) == 1.0
+    assert int(m.discriminator.arena.iterations.item()) == 1      # D's own scale was fine
+    assert float(lsd[0]) == LS and float(lsd[1]) == 1.0
+    lsg[0] = LS
+    lsg[1] = 1999.0           # the next finite step completes an increment period
+    tr.step(xd, yd)
+    torch.cuda.synchronize()
+    assert int(m.generator.arena.iterations.item()) == 1
+    assert not torch.equal(m.generator.arena.data, before)
+    assert float(lsg[0]) == 2 * LS and float(lsg[1]) == 0.0
+    assert m.gen_optimizer.loss_scale == 2 * LS
+    assert np.isfinite(m.generator.arena.data.cpu().numpy()).all()
