@@ -934,6 +934,8 @@ struct OpPlan {
     // halo-tiled bf16x6 kernel (stride-1 3x3 FWD / DGRAD, conv_x6h.hip):
     // cfg = its BN, tiles of 8 x 16 output pixels
     int halo, htx, hty;
+    // small-Cin 4x4 stride-2 kernels (conv_small.hip); WGRAD: conv-view output rows per block
+    int small, small_rows;
 };
 
 // A narrow op (GEMM N <= 8) recast as a 1x1-geometry MFMA GEMM plus a gather:
@@ -1057,6 +1059,22 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
             pl.ws_bytes = pl.slab_bytes;
         }
         pl.gemm_bytes = pl.ws_bytes;
+        return pl;
+    }
+    if (small_conv_ok(g, mode, 0) && !getenv("DG_NO_SMALL")) {
+        // 3 / 6 input channels, 4x4 stride 2 (G.down1, D.down1, G.last's gradients): exact fp32
+        // on the 32x32x2 MFMA whatever the math mode (neither low-precision path takes Cin 3 / 6)
+        pl.small = 1;
+        pl.splits = 1; pl.kchunk = pl.K; pl.mtiles = pl.ntiles = 1;
+        if (mode == MODE_WGRAD) {
+            pl.small_rows = small_wgrad_rows_per_block(g);
+            const int rows = g.N * g.Ho;
+            pl.splits = (rows + pl.small_rows - 1) / pl.small_rows;
+        }
+        pl.slab_bytes = pl.splits > 1 ? (size_t)pl.splits * pl.M * pl.N * sizeof(float) : 0;
+        pl.ws_bytes = pl.gemm_bytes = pl.slab_bytes;
+        if (getenv("DG_PLAN_DEBUG"))
+            fprintf(stderr, "[dg plan] mode %d M=%d N=%d K=%d -> small splits %d\n", mode, pl.M, pl.N, pl.K, pl.splits);
         return pl;
     }
     // Tile + split-K choice: the cheaper of the fp32 kernel and (math mode
@@ -1350,6 +1368,15 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
             DG_LAUNCHED("narrow_wgrad_reduce");
         }
         return DG_OK;
+    }
+    if (pl.small) {
+        const ConvGeom &g = d->g;
+        const long xin = (long)g.N * g.H * g.W, xout = (long)g.N * g.Ho * g.Wo;
+        DG_ARG((xin - 1) * lda + g.Ci < (1L << 31) && xout * ldb < (1L << 31) && xout * ldc < (1L << 31),
+               "operand larger than 2^31 elements");
+        launch_small_conv(mode, a, pl.small_rows, s);
+        DG_LAUNCHED(mode == MODE_WGRAD ? "small_wgrad" : "small_fwd");
+        return finish_splitk(mode, pl, a, s);
     }
     return run_gemm(mode, pl, a, s, pr);
 }

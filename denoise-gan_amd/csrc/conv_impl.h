@@ -242,5 +242,9 @@ void launch_split3(const float *src, int ld, long rows, int C, unsigned short *d
 // the fp16 conv math (DG_MATH_FP16): one fp16 plane [rows][C] and its GEMM (kF16Cfgs)
 void launch_split_f16(const float *src, int ld, long rows, int C, void *dst, hipStream_t s);
 void launch_gemm_f16(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s);
+// small-Cin 4x4 stride-2 FWD / WGRAD on fp32 MFMA (conv_small.hip)
+bool small_conv_ok(const ConvGeom &g, int mode, int lda);
+int small_wgrad_rows_per_block(const ConvGeom &g);
+void launch_small_conv(int mode, const GemmArgs &a, int rows_per_block, hipStream_t s);
 
 }  // namespace dg

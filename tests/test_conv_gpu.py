@@ -43,6 +43,13 @@ CASES = [
     ("D.down1.odd", 2, 27, 70, 6, 64, 4, 2, "same", False, False),
     ("k3s2.c3", 2, 17, 19, 3, 64, 3, 2, "same", False, False),
     ("G.last.odd", 2, 13, 21, 160, 3, 4, 2, "same", True, True),
+    # small-Cin 4x4 stride-2 kernels (conv_small.hip: Cin 3 / 6, Wo % 32 == 0): two row
+    # segments, two column tiles, several conv-view rows per WGRAD block, valid padding
+    ("small.wide", 3, 32, 128, 3, 64, 4, 2, "same", False, True),
+    ("small.co128", 1, 64, 64, 6, 128, 4, 2, "same", False, False),
+    ("small.rows", 3, 384, 64, 3, 64, 4, 2, "same", False, False),
+    ("small.valid", 2, 66, 66, 6, 64, 4, 2, "valid", False, True),
+    ("small.tlast", 1, 64, 64, 64, 3, 4, 2, "same", True, True),
 ]
 
 
