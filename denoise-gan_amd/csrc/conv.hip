@@ -1321,11 +1321,29 @@ static int run_recast(const dg_conv_desc_s *d, int op, const GemmArgs &a0, char 
     return run_gemm(MODE_WGRAD, rc.p1, a, s);
 }
 
+// outputs of the max pool fused into a forward epilogue (dg_conv_fwd_pool)
+struct PoolOut {
+    unsigned char *idx;
+    float *y;
+    int ldy;
+    unsigned short *planes;
+};
+
+// the forward plan of d can run MaxPool2D(2) in its epilogue: the halo-tiled
+// bf16x6 kernel with one split over whole 8 x 16 patches, and an activation
+// whose derivative is a function of the output's sign
+static bool pool_fusable(const dg_conv_desc_s *d, int act) {
+    const OpPlan &pl = d->plan[DG_OP_FWD];
+    return !d->transpose && pl.x6 == 1 && pl.halo && pl.splits == 1 && !d->rc[DG_OP_FWD].on && d->g.Ho % 8 == 0 &&
+           d->g.Wo % 16 == 0 && d->g.Co % 16 == 0 &&
+           (act == DG_ACT_NONE || act == DG_ACT_RELU || act == DG_ACT_LRELU);
+}
+
 static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, const float *B, int ldb,
                       float *C, int ldc, const float *bias, float beta, int act, float alpha,
                       void *ws, size_t ws_bytes, hipStream_t s, const float *mz = nullptr, int ldmz = 0,
                       int mact = DG_ACT_NONE, float malpha = 0.f, const PlaneRefs *pr = nullptr,
-                      unsigned short *yp = nullptr) {
+                      unsigned short *yp = nullptr, const PoolOut *po = nullptr) {
     const int mode = engine_mode(d, op);
     const OpPlan &pl = d->plan[op];
     const size_t need = d->rc[op].on ? d->rc[op].bytes : pl.gemm_bytes;
@@ -1333,6 +1351,17 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
     DG_ARG(need == 0 || ws != nullptr, "workspace pointer is NULL");
     GemmArgs a = make_args(d->g, pl, A, lda, B, ldb, C, ldc, bias, beta, act, alpha, ws);
     a.mz = mz; a.ldmz = ldmz; a.mact = mact; a.malpha = malpha;
+    if (po) {
+        DG_ARG(op == DG_OP_FWD && pool_fusable(d, act), "this forward plan cannot fuse the max pool");
+        DG_ARG(po->idx && (((uintptr_t)po->idx) & 3) == 0, "pool index buffer NULL or not 4-byte aligned");
+        DG_ARG(po->y || po->planes, "fused pool writes neither values nor planes");
+        DG_ARG(!po->y || (po->ldy % 4 == 0 && po->ldy >= d->g.Co && (((uintptr_t)po->y) & 15) == 0),
+               "pooled output needs ldy %% 4 == 0 and 16-byte alignment");
+        DG_ARG(!po->planes || (((uintptr_t)po->planes) & 15) == 0, "plane buffers must be 16-byte aligned");
+        DG_ARG(beta == 0.f, "the fused pool overwrites its output (beta must be 0)");
+        a.pidx = po->idx; a.pool_y = po->y; a.ldpy = po->ldy;
+        a.yp = po->planes; a.ypC = d->g.Co;
+    }
     if (pl.M == 0 || pl.N == 0) return DG_OK;
     if (yp) {
         // planes of the output beside it: the GEMM epilogues (fp32, bf16x6,
@@ -1649,6 +1678,31 @@ int dg_conv_fwd_pl(dg_conv_t d, const float *x, int ldx, const float *w, const f
     return dg::run_engine(d, DG_OP_FWD, x, ldx, w, d->transpose ? 0 : d->Cout, y, ldy, bias, beta, act, alpha, ws,
                           ws_bytes, (hipStream_t)stream, nullptr, 0, DG_ACT_NONE, 0.f, pr,
                           planes ? (unsigned short *)planes->out : nullptr);
+}
+
+int dg_conv_fwd_pool_ok(dg_conv_t d, int act, int *ok) {
+    DG_ARG(d && ok, "NULL argument");
+    *ok = dg::pool_fusable(d, act) ? 1 : 0;
+    return DG_OK;
+}
+
+int dg_conv_fwd_pool(dg_conv_t d, const float *x, int ldx, const float *w, const float *bias, int act, float alpha,
+                     float *pool_y, int ldpy, unsigned char *pool_idx, const dg_conv_planes_t *planes, void *ws,
+                     size_t ws_bytes, dg_stream_t stream) {
+    DG_ARG(d && x && w && pool_idx, "NULL tensor");
+    DG_ARG(ldx >= d->Cin, "pixel stride smaller than channels");
+    DG_ARG(act >= DG_ACT_NONE && act <= DG_ACT_SIGMOID, "unknown activation %d", act);
+    if (!dg::pool_fusable(d, act)) {
+        dg::set_error("forward plan cannot fuse the max pool (dg_conv_fwd_pool_ok)");
+        return DG_ERR_UNSUPPORTED;
+    }
+    dg::PlaneRefs r{};
+    const dg::PlaneRefs *pr;
+    int e = dg::plane_refs(d, DG_OP_FWD, planes, r, pr);
+    if (e != DG_OK) return e;
+    dg::PoolOut po{pool_idx, pool_y, ldpy, planes ? (unsigned short *)planes->out : nullptr};
+    return dg::run_engine(d, DG_OP_FWD, x, ldx, w, d->Cout, nullptr, d->Cout, bias, 0.f, act, alpha, ws, ws_bytes,
+                          (hipStream_t)stream, nullptr, 0, DG_ACT_NONE, 0.f, pr, nullptr, &po);
 }
 
 int dg_conv_fwd(dg_conv_t d, const float *x, int ldx, const float *w, const float *bias, float *y, int ldy,

@@ -36,6 +36,13 @@ struct GemmArgs {
     // optional bf16x6 planes of the final output (dg_conv_planes_t.out):
     // [pixel][3 * ypC] in the packed layout of k_split3, written beside C
     unsigned short *yp; int ypC;
+    // optional MaxPool2D(2) of the activated output, fused into the forward
+    // epilogue of the halo kernel (dg_conv_fwd_pool): the pooled output's
+    // planes go to yp (pooled pixel index), its fp32 values to pool_y (may be
+    // NULL), and per element one byte to pidx: bits 0-1 the window position
+    // of the first maximum (row-major), bit 2 set when the pooled value > 0.
+    // C (the full-size output) is not written.
+    unsigned char *pidx; float *pool_y; int ldpy;
 };
 
 __device__ __forceinline__ float epi_mask(const GemmArgs &p, long pix, int col, float v) {
@@ -236,6 +243,7 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
 // launcher of the bf16x6 kernels (conv_x6.hip); cfg indexes kX6Cfgs
 void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s);
 // the halo-tiled bf16x6 kernel (conv_x6h.hip) for stride-1 3x3 FWD / DGRAD; bn = 64 | 128
+// a.pidx != NULL selects the fused max-pool epilogue (FWD, one split, output Ho % 8 == 0, Wo % 16 == 0)
 void launch_gemm_x6h(int mode, int bn, dim3 grid, const GemmArgs &a, int tiles_x, int tiles_y, hipStream_t s);
 // fp32 [rows][ld] (first C columns, C % 8 == 0) -> bf16 hi/mid/lo planes [rows][C]
 void launch_split3(const float *src, int ld, long rows, int C, unsigned short *dst, hipStream_t s);

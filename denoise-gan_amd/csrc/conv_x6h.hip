@@ -39,10 +39,91 @@ constexpr int HX_HPL = 6 * 1024;                                   // bytes per 
 constexpr int HX_HDMA = 3 * HX_HPL / 1024;                         // 18 one-KiB DMAs per halo
 static_assert(HX_HPX * 32 <= HX_HPL, "halo plane image");
 
-template <int MODE, int BN>
+// Forward epilogue fused with the 2x2 max pool that follows the conv (VGG19
+// blockN_conv{2,4} -> blockN_pool, pix2pix.py:53-67 content features): a
+// wave's 64 GEMM rows are 4 patch rows of 16 pixels, so every pool window
+// (two patch rows a, a+1 of the same wave, two neighbouring pixels) lies in
+// one wave's tile.  Rows are staged through LDS as in conv_epilogue16; the
+// two pixels of a window row sit in lanes l and l ^ C4 (one swap), the
+// window's row pair in registers across the a-loop.  The first maximum in
+// row-major window order is kept (strict >: the pairwise and the sequential
+// scan pick the same element), as k_maxpool_bwd4 routes.  Per pooled
+// element: its bf16x6 planes (the next conv's x operand), optionally its
+// fp32 value, and one byte {argmax, value > 0} for the backward -- the
+// full-size activation is never written.
+template <int TM, int TN>
+__device__ __forceinline__ void conv_epilogue16_pool(const GemmArgs &p, f32x4 (&acc)[TM][TN], int prow0, int cbase,
+                                                     int ty, int tx, int nimg, int lane, float *stage) {
+    constexpr int WTN = 16 * TN;
+    constexpr int LD = WTN + 4;
+    constexpr int C4 = WTN / 4;
+    constexpr int RPP = 64 / C4;
+    constexpr int NP = 16 / RPP;
+    static_assert(TM % 2 == 0 && 64 % C4 == 0 && 16 % RPP == 0 && RPP % 2 == 0, "window rows / pixel pairs in one wave");
+    const ConvGeom &g = p.g;
+    const int c4 = lane % C4, rsub = lane / C4;
+    const int col = cbase + c4 * 4;
+    const bool lead = (rsub & 1) == 0;          // holds the even pixel of its pair
+    const bool colok = col < p.N;                // (N % 16 == 0: a float4 is all in or all out)
+    const int Ho2 = g.Ho >> 1, Wo2 = g.Wo >> 1;
+    f32x4 bias = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias && colok) bias = *reinterpret_cast<const f32x4 *>(p.bias + col);
+    f32x4 hv[NP];
+    unsigned hix[NP];
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) stage[(4 * (lane >> 4) + r) * LD + b * 16 + (lane & 15)] = acc[a][b][r];
+#pragma unroll
+        for (int pass = 0; pass < NP; ++pass) {
+            const int rl = pass * RPP + rsub;
+            f32x4 o = *reinterpret_cast<const f32x4 *>(stage + rl * LD + c4 * 4);
+            o += bias;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = act_fwd(o[q], p.act, p.alpha);
+            f32x4 po;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) po[q] = __shfl_xor(o[q], C4);
+            // window row: (this pixel, the next one) for the lead lane
+            f32x4 hvv;
+            unsigned hi = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bool t = po[q] > o[q];
+                hvv[q] = t ? po[q] : o[q];
+                hi |= (t ? 1u : 0u) << (8 * q);
+            }
+            if ((a & 1) == 0) {
+                hv[pass] = hvv;
+                hix[pass] = hi;
+                continue;
+            }
+            f32x4 fv;
+            unsigned fi = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bool t = hvv[q] > hv[pass][q];   // the lower row only when strictly greater
+                fv[q] = t ? hvv[q] : hv[pass][q];
+                const unsigned id = t ? (((hi >> (8 * q)) & 1u) + 2u) : ((hix[pass] >> (8 * q)) & 1u);
+                fi |= (id | (fv[q] > 0.f ? 4u : 0u)) << (8 * q);
+            }
+            if (!lead || !colok) continue;
+            const int ho2 = (ty * HX_PH + prow0 + a) >> 1, wo2 = (tx * HX_PW + rl) >> 1;
+            const long pp = ((long)nimg * Ho2 + ho2) * Wo2 + wo2;
+            *reinterpret_cast<unsigned *>(p.pidx + pp * p.N + col) = fi;
+            if (p.pool_y) *reinterpret_cast<f32x4 *>(p.pool_y + pp * p.ldpy + col) = fv;
+            if (p.yp) store_planes4(p.yp, p.ypC, pp, col, fv);
+        }
+    }
+}
+
+template <int MODE, int BN, bool POOL>
 __global__ void __launch_bounds__(256, 2)
 k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "forward or input gradient");
+    static_assert(!POOL || MODE == MODE_FWD, "the pool epilogue is a forward epilogue");
     constexpr int BK = 16, NW = 4;
     constexpr int WTM = 64, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
     constexpr bool B_KC = MODE == MODE_DGRAD;
@@ -257,19 +338,28 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         const long pix = ((long)nimg * Hout + ho) * Wout + wo;
         return RowPix{pix, pix};
     };
-    conv_epilogue16<MODE, TM, TN>(p, acc, wm * WTM, n0 + wn * WTN, rowmap, 0, split, lane,
-                                  reinterpret_cast<float *>(hal0) + wid * STAGE);
+    if constexpr (POOL)
+        conv_epilogue16_pool<TM, TN>(p, acc, wm * TM, n0 + wn * WTN, ty, tx, nimg, lane,
+                                     reinterpret_cast<float *>(hal0) + wid * STAGE);
+    else
+        conv_epilogue16<MODE, TM, TN>(p, acc, wm * WTM, n0 + wn * WTN, rowmap, 0, split, lane,
+                                      reinterpret_cast<float *>(hal0) + wid * STAGE);
 }
 
 void launch_gemm_x6h(int mode, int bn, dim3 grid, const GemmArgs &a, int tiles_x, int tiles_y, hipStream_t s) {
     const dim3 blk(256);
-    if (mode == MODE_FWD) {
-        if (bn == 128) hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_FWD, 128>), grid, blk, 0, s, a, tiles_x, tiles_y);
-        else hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_FWD, 64>), grid, blk, 0, s, a, tiles_x, tiles_y);
+#define DG_X6H(M_, B_, P_) hipLaunchKernelGGL((k_conv_gemm_x6h<M_, B_, P_>), grid, blk, 0, s, a, tiles_x, tiles_y)
+    if (mode == MODE_FWD && a.pidx) {
+        if (bn == 128) DG_X6H(MODE_FWD, 128, true);
+        else DG_X6H(MODE_FWD, 64, true);
+    } else if (mode == MODE_FWD) {
+        if (bn == 128) DG_X6H(MODE_FWD, 128, false);
+        else DG_X6H(MODE_FWD, 64, false);
     } else {
-        if (bn == 128) hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_DGRAD, 128>), grid, blk, 0, s, a, tiles_x, tiles_y);
-        else hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_DGRAD, 64>), grid, blk, 0, s, a, tiles_x, tiles_y);
+        if (bn == 128) DG_X6H(MODE_DGRAD, 128, false);
+        else DG_X6H(MODE_DGRAD, 64, false);
     }
+#undef DG_X6H
 }
 
 }  // namespace dg

@@ -276,6 +276,43 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd4(int N, int H, int W, int C
     }
 }
 
+// backward of a max pool fused into its conv's forward (dg_conv_fwd_pool): the
+// window position and the sign of the pooled value were stored as one byte per
+// element, so the full-size activation is not read.  The routed gradient is
+// dy * act'(pooled) at the first maximum, 0 at the other three positions.
+// dx (fp32) may be NULL when only its planes are consumed (a conv's backward
+// on bf16x6 planes).
+__global__ void __launch_bounds__(256) k_maxpool_bwd_idx4(int N, int H, int W, int C, const unsigned char *idx,
+                                                         const float *dy, int lddy, float *dx, int lddx, float beta,
+                                                         float neg, unsigned short *dxp) {
+    const int Ho = H / 2, Wo = W / 2, C4 = C >> 2;
+    const int total = N * Ho * Wo * C4;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+        const int op = e / C4;
+        const int c = (e - op * C4) * 4;
+        const int wo = op % Wo, t = op / Wo, ho = t % Ho, n = t / Ho;
+        const long p0 = ((long)n * H + 2 * ho) * W + 2 * wo;
+        const long pp[4] = {p0, p0 + 1, p0 + W, p0 + W + 1};
+        const unsigned b = *reinterpret_cast<const unsigned *>(idx + (long)op * C + c);
+        const f32x4 gy = *reinterpret_cast<const f32x4 *>(dy + (long)op * lddy + c);
+        f32x4 gg;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) gg[k] = gy[k] * (((b >> (8 * k)) & 4u) ? 1.f : neg);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            f32x4 g;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) g[k] = ((b >> (8 * k)) & 3u) == (unsigned)q ? gg[k] : 0.f;
+            if (dx) {
+                f32x4 *o = reinterpret_cast<f32x4 *>(dx + pp[q] * lddx + c);
+                if (beta != 0.f) g += beta * *o;
+                *o = g;
+            }
+            if (dxp) store_planes4(dxp, C, pp[q], c, g);
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) k_maxpool_bwd_tail(int N, int H, int W, int C, float *dx, int lddx,
                                                          float beta, unsigned short *dxp) {
     const int H2 = H / 2 * 2, W2 = W / 2 * 2;
@@ -768,6 +805,25 @@ int dg_maxpool2_bwd_pl(int N, int H, int W, int C, const float *x, int ldx, cons
 int dg_maxpool2_bwd(int N, int H, int W, int C, const float *x, int ldx, const float *dy, int lddy, float *dx,
                     int lddx, float beta, int act, float alpha, dg_stream_t stream) {
     return dg_maxpool2_bwd_pl(N, H, W, C, x, ldx, dy, lddy, dx, lddx, beta, act, alpha, nullptr, stream);
+}
+
+int dg_maxpool2_bwd_idx(int N, int H, int W, int C, const unsigned char *idx, const float *dy, int lddy,
+                        float *dx, int lddx, float beta, int act, float alpha, void *dx_planes, dg_stream_t stream) {
+    DG_ARG(idx && dy && (dx || dx_planes), "NULL tensor");
+    DG_ARG(N > 0 && H >= 2 && W >= 2 && H % 2 == 0 && W % 2 == 0 && C > 0 && C % 16 == 0, "bad shape");
+    DG_ARG(lddy >= C && lddy % 4 == 0 && (((uintptr_t)dy) & 15) == 0 && (((uintptr_t)idx) & 3) == 0,
+           "dy needs a float4-aligned layout, idx 4-byte alignment");
+    DG_ARG(!dx || (lddx >= C && lddx % 4 == 0 && (((uintptr_t)dx) & 15) == 0), "dx needs a float4-aligned layout");
+    DG_ARG(dx || beta == 0.f, "accumulation (beta != 0) needs the fp32 dx");
+    DG_ARG(!dx_planes || (((uintptr_t)dx_planes) & 15) == 0, "plane buffers must be 16-byte aligned");
+    DG_ARG(act == DG_ACT_NONE || act == DG_ACT_RELU || act == DG_ACT_LRELU, "activation %d not sign-determined", act);
+    DG_ARG((long)N * H * W * C < (1L << 31), "tensor too large");
+    const float neg = act == DG_ACT_RELU ? 0.f : (act == DG_ACT_LRELU ? alpha : 1.f);
+    const long total = (long)N * (H / 2) * (W / 2) * C;
+    hipLaunchKernelGGL(dg::k_maxpool_bwd_idx4, dim3(dg::lgrid(total / 4)), dim3(256), 0, (hipStream_t)stream, N, H, W,
+                       C, idx, dy, lddy, dx, lddx, beta, neg, (unsigned short *)dx_planes);
+    DG_LAUNCHED("maxpool_bwd_idx");
+    return DG_OK;
 }
 
 int dg_upsample2_relu_fwd(int N, int H, int W, int C, const float *x, int ldx, float *z, int ldz,

@@ -413,6 +413,34 @@ class GraphPlan:
                     pn.dy = ops.PlaneBuf(dn.plane_bytes(ops.TENSOR_DY), device)
                     self.cplanes[k][c.idx].bwd_out = pn.dy
                 self.fed_dy.add(n.idx)
+        # ---- max pools fused into their conv's forward epilogue ----
+        # a conv (ReLU / LeakyReLU / linear) whose output feeds only a 2x2 max
+        # pool, on a plan that can run the pool in its epilogue, writes the
+        # pooled values, their planes and a {argmax, sign} byte per pooled
+        # element instead of its full-size activation; the pool's backward
+        # routes from those bytes.  An aliasing plan follows its forward plan.
+        self.fused_pool = {}   # maxpool node idx -> producing conv node
+        self.pool_idx = [dict() for _ in range(slots)]
+        if alias is not None:
+            self.fused_pool = dict(alias.fused_pool)
+        elif not os.environ.get("DG_NO_FUSED_POOL"):
+            for m in nodes[1:]:
+                if m.kind != "maxpool":
+                    continue
+                t_in = m.ins[0]
+                n = t_in.node
+                if (n.kind != "conv" or len(cons[t_in.id]) != 1 or t_in.id in self.slice_of
+                        or t_in.id == graph.output.id or ops.act_id(n.attrs["act"]) not in (0, 1, 2)):
+                    continue
+                if self.desc[n.idx].pool_fusable(n.attrs["act"]):
+                    self.fused_pool[m.idx] = n
+        self.fused_conv = {n.idx: m for m, n in ((nodes[i], c) for i, c in self.fused_pool.items())}
+        for k in range(slots):
+            for midx in self.fused_pool:
+                if alias is not None and k == 0:
+                    self.pool_idx[k][midx] = alias.pool_idx[0][midx][:N]
+                else:
+                    self.pool_idx[k][midx] = torch.empty(shp[nodes[midx].out.id], dtype=torch.uint8, device=device)
         # ---- workspace ----
         ws = [0]
         for n in nodes[1:]:
@@ -493,8 +521,14 @@ class GraphPlan:
                 P = self.cplanes[slot][n.idx]
                 # (a fed input's planes were written by its producer in this pass)
                 P.invalidate(wbit | (0 if n.idx in self.fed_x else ops.TENSOR_X))
-                d.fwd(xin, A.param(f"{n.name}/kernel"), y, bias=bias, act=n.attrs["act"],
-                      alpha=n.attrs["alpha"], ws=ws, planes=P)
+                mp = self.fused_conv.get(n.idx)
+                if mp is not None:
+                    d.fwd_pool(xin, A.param(f"{n.name}/kernel"), self.pool_idx[slot][mp.idx], bias=bias,
+                               act=n.attrs["act"], alpha=n.attrs["alpha"], pool_y=s[mp.out.id], ws=ws, planes=P,
+                               pool_planes=self.pool_out[slot].get(mp.idx))
+                else:
+                    d.fwd(xin, A.param(f"{n.name}/kernel"), y, bias=bias, act=n.attrs["act"],
+                          alpha=n.attrs["alpha"], ws=ws, planes=P)
             elif k == "bn":
                 mean, inv = self.saved[slot][n.name]
                 if training:
@@ -517,7 +551,8 @@ class GraphPlan:
                         ops.strided_copy(s[t.id], y[..., off:off + t.C])
                     off += t.C
             elif k == "maxpool":
-                ops.maxpool2_fwd(xin, y, planes_out=self.pool_out[slot].get(n.idx))
+                if n.idx not in self.fused_pool:   # (else done by its conv's epilogue)
+                    ops.maxpool2_fwd(xin, y, planes_out=self.pool_out[slot].get(n.idx))
             elif k == "upsample":
                 ops.upsample2_relu_fwd(xin, y)
             elif k == "dwconv":
@@ -614,6 +649,18 @@ class GraphPlan:
                     if self.slice_of.get(t.id, (None,))[0] != n.out.id and need(t):
                         ops.accumulate(dz[..., off:off + t.C], gr[t.id], beta_of(n, t))
                     off += t.C
+            elif k == "maxpool" and n.idx in self.fused_pool:
+                if need(t_in):
+                    pa = t_in.node.attrs
+                    b = beta_of(n, t_in)
+                    gout = self.pool_gout[slot].get(n.idx)
+                    # the fp32 gradient is read only by a bias / filter gradient or an
+                    # accumulation; the conv's input gradient reads its dy planes
+                    keep = gout is None or pg or b != 0.0
+                    _, H, W, C = self.shape[t_in.id]
+                    ops.maxpool2_bwd_idx(self.pool_idx[slot][n.idx], dz, gr[t_in.id] if keep else None, C, H, W,
+                                         beta=b, act=pa["act"] if t_in.id in self.premask else "none",
+                                         alpha=pa["alpha"], planes_out=gout)
             elif k == "maxpool":
                 if need(t_in):
                     pa = t_in.node.attrs if t_in.id in self.premask else {"act": "none", "alpha": 0.0}

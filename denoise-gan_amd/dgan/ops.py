@@ -330,6 +330,39 @@ class ConvDesc:
             planes.fwd_out.ready = True
         return y
 
+    def pool_fusable(self, act):
+        """Whether fwd_pool can run MaxPool2D(2) in this layer's forward epilogue."""
+        ok = ctypes.c_int()
+        call("dg_conv_fwd_pool_ok", self._h, act_id(act), ctypes.byref(ok))
+        return bool(ok.value)
+
+    def fwd_pool(self, x, w, pool_idx, bias=None, act="none", alpha=0.3, pool_y=None, ws=None, planes=None,
+                 pool_planes=None):
+        """Conv forward + MaxPool2D(2) of its activated output in one epilogue
+        (dg_conv_fwd_pool): the pooled values go to pool_y (may be None) and
+        their bf16x6 planes to pool_planes (the next conv's x PlaneBuf);
+        pool_idx [N, Ho/2, Wo/2, Cout] uint8 receives {argmax, value > 0} for
+        maxpool2_bwd_idx.  The full-size activation is not written."""
+        ldx = pix_ld(x, self.Cin)
+        ldpy = pix_ld(pool_y, self.Cout) if pool_y is not None else 0
+        wp, wn = self._ws(OP_FWD, ws)
+        if planes is not None:
+            saved, planes.fwd_out = planes.fwd_out, pool_planes
+        pp, fills = self._pl(OP_FWD, planes)
+        if planes is None and pool_planes is not None:
+            pp, fills = ctypes.byref(_PlanesC(None, None, None, pool_planes.buf.data_ptr(), 0)), 0
+        ev = _prof_begin()
+        call("dg_conv_fwd_pool", self._h, _p(x), ldx, _p(w), _p(bias), act_id(act), float(alpha), _p(pool_y), ldpy,
+             _p(pool_idx), pp, wp, wn, _stream())
+        _prof_end(ev, self, "fwd")
+        if planes is not None:
+            planes.fwd_out = saved
+            if fills:
+                planes._filled(fills)
+        if pool_planes is not None:
+            pool_planes.ready = True
+        return pool_y
+
     def bwd_data(self, dy, w, dx, beta=0.0, ws=None, planes=None):
         return self._bwd_data(dy, w, dx, None, 0, 0.0, beta, ws, planes)
 
@@ -632,6 +665,18 @@ def maxpool2_bwd(x, dy, dx, beta=0.0, act="none", alpha=0.3, planes_out=None):
     N, H, W, C = _nhwc(x)
     call("dg_maxpool2_bwd_pl", N, H, W, C, _p(x), pix_ld(x, C), _p(dy), pix_ld(dy, C), _p(dx), pix_ld(dx, C),
          float(beta), act_id(act), float(alpha), None if planes_out is None else _p(planes_out.buf), _stream())
+    if planes_out is not None:
+        planes_out.ready = True
+    return dx
+
+
+def maxpool2_bwd_idx(idx, dy, dx, C, H, W, beta=0.0, act="none", alpha=0.3, planes_out=None):
+    """Backward of a pool fused by ConvDesc.fwd_pool: dx [N,H,W,C] (may be None
+    when planes_out, the producing conv's dy PlaneBuf, is all that is read)."""
+    N = dy.shape[0]
+    call("dg_maxpool2_bwd_idx", N, H, W, C, _p(idx), _p(dy), pix_ld(dy, C), _p(dx),
+         pix_ld(dx, C) if dx is not None else 0, float(beta), act_id(act), float(alpha),
+         None if planes_out is None else _p(planes_out.buf), _stream())
     if planes_out is not None:
         planes_out.ready = True
     return dx

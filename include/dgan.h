@@ -136,6 +136,21 @@ int dg_conv_bwd_data_pl(dg_conv_t d, const float *dy, int lddy, const float *w,
 int dg_conv_bwd_filter_pl(dg_conv_t d, const float *x, int ldx, const float *dy, int lddy,
                           float *dw, float *dbias, float beta,
                           const dg_conv_planes_t *planes, void *ws, size_t ws_bytes, dg_stream_t stream);
+/* Conv2D forward followed by MaxPool2D(2) on its activated output, fused into
+ * the forward epilogue (VGG19 blockN_conv{2,4} -> blockN_pool, keras
+ * applications VGG19 as built by pix2pix.py:53-67 / srgan.py:70-76; replaces
+ * the conv + pool pair of dg_conv_fwd_pl + dg_maxpool2_fwd_pl).  Writes the
+ * pooled output's bf16x6 planes (planes->out: the next conv's x planes) and/or
+ * its fp32 values (pool_y, [N, Ho/2, Wo/2, Cout], may be NULL), and pool_idx
+ * [N*Ho/2*Wo/2][Cout] bytes (bits 0-1: row-major window position of the first
+ * maximum, bit 2: pooled value > 0) for dg_maxpool2_bwd_idx.  The conv's own
+ * full-size output is not written.  DG_ERR_UNSUPPORTED unless
+ * dg_conv_fwd_pool_ok: halo-tiled bf16x6 forward plan with one split,
+ * Ho % 8 == 0, Wo % 16 == 0, act NONE / RELU / LRELU. */
+int dg_conv_fwd_pool_ok(dg_conv_t d, int act, int *ok);
+int dg_conv_fwd_pool(dg_conv_t d, const float *x, int ldx, const float *w, const float *bias, int act, float alpha,
+                     float *pool_y, int ldpy, unsigned char *pool_idx, const dg_conv_planes_t *planes,
+                     void *ws, size_t ws_bytes, dg_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * BatchNormalization, training semantics of Keras' fused kernel
@@ -318,6 +333,12 @@ int dg_maxpool2_fwd_pl(int N, int H, int W, int C, const float *x, int ldx, floa
                        dg_stream_t stream);
 int dg_maxpool2_bwd_pl(int N, int H, int W, int C, const float *x, int ldx, const float *dy, int lddy,
                        float *dx, int lddx, float beta, int act, float alpha, void *dx_planes, dg_stream_t stream);
+/* backward of a pool fused by dg_conv_fwd_pool, from its index bytes (the full-size
+ * activation is not read): dx = dy * act'(pooled) at the first maximum, 0 elsewhere;
+ * H, W even (the conv output), C % 16 == 0; dx may be NULL (beta 0) when only its
+ * bf16x6 planes (dx_planes) are consumed */
+int dg_maxpool2_bwd_idx(int N, int H, int W, int C, const unsigned char *idx, const float *dy, int lddy,
+                        float *dx, int lddx, float beta, int act, float alpha, void *dx_planes, dg_stream_t stream);
 /* UpSampling2D(2, 'nearest') + relu (autoencoder.py:117-131): [N,H,W,C] -> [N,2H,2W,C] */
 int dg_upsample2_relu_fwd(int N, int H, int W, int C, const float *x, int ldx, float *z, int ldz,
                           dg_stream_t stream);

@@ -28,8 +28,10 @@ import torch.nn.functional as F
 class Decisions:
     """forced: {layer name: bool mask (activation sites, the activation's
     output shape) or int argmax in 0..3 (max-pool sites, row-major 2x2 window
-    index, the pool's output shape)}, numpy or torch.  Sites without an
-    entry use the oracle's own decision."""
+    index, the pool's output shape)}, numpy or torch, or a (decisions, known)
+    pair of which only the `known` elements are forced (a conv whose max pool
+    ran in its epilogue exports its ReLU decision at the pooled element only).
+    Sites without an entry use the oracle's own decision."""
 
     def __init__(self, forced=None):
         self.forced = dict(forced or {})
@@ -39,9 +41,15 @@ class Decisions:
         f = self.forced.get(name)
         if f is None:
             return own
+        known = None
+        if isinstance(f, tuple):   # (decisions, where they are known): the oracle's own elsewhere
+            f, known = f
+            known = torch.as_tensor(known).to(own.device).reshape(own.shape)
         f = torch.as_tensor(f).to(own.device).reshape(own.shape)
         if f.dtype != own.dtype:
             f = f.to(own.dtype)
+        if known is not None:
+            f = torch.where(known, f, own)
         diff = f != own
         n = int(diff.sum())
         worst = float(tie[diff].max() / scale) if n else 0.0

@@ -35,6 +35,24 @@ def _depth_to_space(m, b):
     return m.reshape(N, H, W, b, b, C).transpose(0, 1, 3, 2, 4, 5).reshape(N, H * b, W * b, C)
 
 
+def fused_pool_decisions(idx):
+    """A pool fused into its conv's epilogue stores one byte per pooled element
+    (bits 0-1 the argmax, bit 2 the activation's sign there): -> (argmax [N,H/2,W/2,C],
+    (conv mask, known) at full size -- the conv's decision is known where the
+    pool routes the gradient)."""
+    b = idx.detach().cpu().numpy().astype(np.int64)
+    arg = b & 3
+    pos = (b & 4) != 0
+    N, H2, W2, C = b.shape
+    mask = np.zeros((N, H2, 2, W2, 2, C), dtype=bool)
+    known = np.zeros_like(mask)
+    for q in range(4):
+        sel = arg == q
+        known[:, :, q // 2, :, q % 2, :] = sel
+        mask[:, :, q // 2, :, q % 2, :] = sel & pos
+    return arg, (mask.reshape(N, 2 * H2, 2 * W2, C), known.reshape(N, 2 * H2, 2 * W2, C))
+
+
 def graph_decisions(plan, slot=0, rows=None):
     """{layer name: mask / argmax} of one dgan.graph.GraphPlan slot; rows: a
     slice of the batch (e.g. one half of a batched forward)."""
@@ -42,9 +60,18 @@ def graph_decisions(plan, slot=0, rows=None):
     s = plan.slots[slot]
     sel = (lambda t: t) if rows is None else (lambda t: t[rows])
     out = {}
+    fused_conv = getattr(plan, "fused_conv", {})
     for n in g.nodes[1:]:
         k = n.kind
-        if k in ("conv", "bn", "act") and n.attrs.get("act") in RELU_ACTS:
+        if k == "conv" and n.idx in fused_conv:
+            m = fused_conv[n.idx]
+            arg, cm = fused_pool_decisions(sel(plan.pool_idx[slot][m.idx]))
+            out[m.name] = arg
+            if n.attrs.get("act") in RELU_ACTS:
+                out[n.name] = cm
+        elif k == "maxpool" and n.idx in getattr(plan, "fused_pool", {}):
+            continue
+        elif k in ("conv", "bn", "act") and n.attrs.get("act") in RELU_ACTS:
             out[n.name] = _pos(sel(s[n.out.id]))
         elif k == "upsample":
             out[n.name] = _pos(sel(s[n.out.id]))
@@ -78,7 +105,8 @@ def discriminator_decisions(plan, half=0):
 def to_oracle(masks):
     """oracle.decisions.Decisions over exported masks."""
     from oracle.decisions import Decisions
-    return Decisions({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in masks.items()})
+    t = lambda v: torch.from_numpy(np.ascontiguousarray(v))
+    return Decisions({k: (t(v[0]), t(v[1])) if isinstance(v, tuple) else t(v) for k, v in masks.items()})
 
 
 def audit_ok(decs, tie_tol, what=""):
