@@ -440,9 +440,11 @@ k_splitk_reduce(const GemmArgs p, int V4) {
                 if (p.bias) x += p.bias[col + q];
                 o[q] = epi_mask(p, pix, col + q, act_fwd(x, p.act, p.alpha));
             }
-            f32x4 *dst = reinterpret_cast<f32x4 *>(p.C + off + col);
-            if (p.beta != 0.f) o += p.beta * (*dst);
-            *dst = o;
+            if (p.C) {
+                f32x4 *dst = reinterpret_cast<f32x4 *>(p.C + off + col);
+                if (p.beta != 0.f) o += p.beta * (*dst);
+                *dst = o;
+            }
             if (p.yp) store_planes4(p.yp, p.ypC, pix, col, o);
         }
         return;
@@ -463,8 +465,10 @@ k_splitk_reduce(const GemmArgs p, int V4) {
         const long off = pix * p.ldc;
         if (p.bias) v += p.bias[col];
         v = epi_mask(p, pix, col, act_fwd(v, p.act, p.alpha));
-        if (p.beta != 0.f) v += p.beta * p.C[off + col];
-        p.C[off + col] = v;
+        if (p.C) {
+            if (p.beta != 0.f) v += p.beta * p.C[off + col];
+            p.C[off + col] = v;
+        }
         if (p.yp) store_planes1(p.yp, p.ypC, pix, col, v);
     }
 }
@@ -1343,7 +1347,8 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
                       float *C, int ldc, const float *bias, float beta, int act, float alpha,
                       void *ws, size_t ws_bytes, hipStream_t s, const float *mz = nullptr, int ldmz = 0,
                       int mact = DG_ACT_NONE, float malpha = 0.f, const PlaneRefs *pr = nullptr,
-                      unsigned short *yp = nullptr, const PoolOut *po = nullptr) {
+                      unsigned short *yp = nullptr, const PoolOut *po = nullptr,
+                      const unsigned short *mzp = nullptr) {
     const int mode = engine_mode(d, op);
     const OpPlan &pl = d->plan[op];
     const size_t need = d->rc[op].on ? d->rc[op].bytes : pl.gemm_bytes;
@@ -1361,6 +1366,18 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
         DG_ARG(beta == 0.f, "the fused pool overwrites its output (beta must be 0)");
         a.pidx = po->idx; a.pool_y = po->y; a.ldpy = po->ldy;
         a.yp = po->planes; a.ypC = d->g.Co;
+    }
+    if (mzp) {
+        // mask from the hi plane's sign: the small-Cin kernels read fp32 masks only
+        DG_ARG(!mz && !pl.small, "plane mask: not with an fp32 mask, nor on the small-Cin kernels");
+        DG_ARG(mact == DG_ACT_NONE || mact == DG_ACT_RELU || mact == DG_ACT_LRELU,
+               "plane mask needs a sign-determined activation (got %d)", mact);
+        a.mzp = mzp; a.mzpC = mode == MODE_FWD ? d->g.Co : d->g.Ci;
+    }
+    if (!C && !po) {
+        // planes-only output: the GEMM epilogues skip the fp32 store
+        DG_ARG(yp && beta == 0.f && mode != MODE_WGRAD && !pl.narrow && !pl.small && !d->rc[op].on,
+               "output NULL: only a GEMM-path op writing its output planes (beta 0) may omit it");
     }
     if (pl.M == 0 || pl.N == 0) return DG_OK;
     if (yp) {
@@ -1669,8 +1686,8 @@ int dg_conv_op_planes(dg_conv_t d, int op, int *tensors) {
 int dg_conv_fwd_pl(dg_conv_t d, const float *x, int ldx, const float *w, const float *bias, float *y, int ldy,
                    float beta, int act, float alpha, const dg_conv_planes_t *planes, void *ws, size_t ws_bytes,
                    dg_stream_t stream) {
-    DG_ARG(d && x && w && y, "NULL tensor");
-    DG_ARG(ldx >= d->Cin && ldy >= d->Cout, "pixel stride smaller than channels");
+    DG_ARG(d && x && w && (y || (planes && planes->out)), "NULL tensor");
+    DG_ARG(ldx >= d->Cin && (!y || ldy >= d->Cout), "pixel stride smaller than channels");
     dg::PlaneRefs r{};
     const dg::PlaneRefs *pr;
     int e = dg::plane_refs(d, DG_OP_FWD, planes, r, pr);
@@ -1724,6 +1741,23 @@ int dg_conv_bwd_data_pl(dg_conv_t d, const float *dy, int lddy, const float *w, 
     return dg::run_engine(d, DG_OP_BWD_DATA, dy, lddy, w, d->transpose ? d->g.Co : 0, dx, lddx, nullptr, beta,
                           DG_ACT_NONE, 0.f, ws, ws_bytes, (hipStream_t)stream, z, z ? ldz : 0,
                           z ? act : DG_ACT_NONE, alpha, pr, planes ? (unsigned short *)planes->out : nullptr);
+}
+
+int dg_conv_bwd_data_xmask(dg_conv_t d, const float *dy, int lddy, const float *w, float *dx, int lddx, float beta,
+                           int act, float alpha, const dg_conv_planes_t *planes, void *ws, size_t ws_bytes,
+                           dg_stream_t stream) {
+    DG_ARG(d && dy && w && dx && planes && planes->x, "NULL tensor or x planes");
+    DG_ARG((planes->ready & DG_TENSOR_X) != 0, "x planes not ready (written by x's producer or a split)");
+    DG_ARG((((uintptr_t)planes->x) & 7) == 0, "x planes must be 8-byte aligned");
+    DG_ARG(lddy >= d->Cout && lddx >= d->Cin, "pixel stride smaller than channels");
+    DG_ARG(d->Cin % 16 == 0, "x planes need Cin %% 16 == 0");
+    dg::PlaneRefs r{};
+    const dg::PlaneRefs *pr;
+    int e = dg::plane_refs(d, DG_OP_BWD_DATA, planes, r, pr);
+    if (e != DG_OK) return e;
+    return dg::run_engine(d, DG_OP_BWD_DATA, dy, lddy, w, d->transpose ? d->g.Co : 0, dx, lddx, nullptr, beta,
+                          DG_ACT_NONE, 0.f, ws, ws_bytes, (hipStream_t)stream, nullptr, 0, act, alpha, pr,
+                          (unsigned short *)planes->out, nullptr, (const unsigned short *)planes->x);
 }
 
 int dg_conv_bwd_data(dg_conv_t d, const float *dy, int lddy, const float *w, float *dx, int lddx, float beta,

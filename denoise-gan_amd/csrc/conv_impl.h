@@ -43,10 +43,27 @@ struct GemmArgs {
     // of the first maximum (row-major), bit 2 set when the pooled value > 0.
     // C (the full-size output) is not written.
     unsigned char *pidx; float *pool_y; int ldpy;
+    // optional gradient mask from the bf16x6 planes of the activation output
+    // instead of its fp32 values (dg_conv_bwd_data_xmask): act' of a
+    // sign-determined activation from the sign of the hi plane, [pixel][3 mzpC]
+    const unsigned short *mzp; int mzpC;
 };
 
+// hi plane of element (pix, col) of a packed plane tensor, as a float
+__device__ __forceinline__ float hi_plane(const unsigned short *zp, int C, long pix, int col) {
+    return __uint_as_float((unsigned)zp[pix * 3 * C + (col >> 4) * 48 + (col & 15)] << 16);
+}
+// the same for columns col..col+3 (col % 4 == 0): one 8-byte load
+__device__ __forceinline__ f32x4 hi_plane4(const unsigned short *zp, int C, long pix, int col) {
+    const u32x2_t h = *reinterpret_cast<const u32x2_t *>(zp + pix * 3 * C + (col >> 4) * 48 + (col & 15));
+    return f32x4{__uint_as_float(h[0] << 16), __uint_as_float(h[0] & 0xffff0000u), __uint_as_float(h[1] << 16),
+                 __uint_as_float(h[1] & 0xffff0000u)};
+}
+
 __device__ __forceinline__ float epi_mask(const GemmArgs &p, long pix, int col, float v) {
-    return p.mz ? v * act_grad_from_out(p.mz[pix * p.ldmz + col], p.mact, p.malpha) : v;
+    if (p.mz) return v * act_grad_from_out(p.mz[pix * p.ldmz + col], p.mact, p.malpha);
+    if (p.mzp) return v * act_grad_from_out(hi_plane(p.mzp, p.mzpC, pix, col), p.mact, p.malpha);
+    return v;
 }
 
 // Branch-free operand loads: raw buffer loads through a resource whose range
@@ -114,13 +131,13 @@ template <int MODE, int TM, int TN>
 __device__ __forceinline__ void conv_epilogue(const GemmArgs &p, f32x16 (&acc)[TM][TN], int rbase, int cbase,
                                               int Mrows, const PhaseInfo &ph, int phase, int split, int l32, int h2) {
     const ConvGeom &g = p.g;
-#pragma unroll
+#pragma clang loop unroll(full)
     for (int a = 0; a < TM; ++a) {
-#pragma unroll
+#pragma clang loop unroll(full)
         for (int b = 0; b < TN; ++b) {
             const int col = cbase + b * 32 + l32;
             if (col >= p.N) continue;
-#pragma unroll
+#pragma clang loop unroll(full)
             for (int r = 0; r < 16; ++r) {
                 const int row = rbase + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h2;
                 if (row >= Mrows) continue;
@@ -139,8 +156,10 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs &p, f32x16 (&acc)[T
                     if (p.bias) v += p.bias[col];
                     v = act_fwd(v, p.act, p.alpha);
                     v = epi_mask(p, pix, col, v);
-                    if (p.beta != 0.f) v += p.beta * p.C[off + col];
-                    p.C[off + col] = v;
+                    if (p.C) {
+                        if (p.beta != 0.f) v += p.beta * p.C[off + col];
+                        p.C[off + col] = v;
+                    }
                     if (p.yp) store_planes1(p.yp, p.ypC, pix, col, v);
                 }
             }
@@ -175,13 +194,13 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
     const int c4 = lane % C4;
     const int col = cbase + c4 * 4;
     const bool full = col + 3 < p.N;
-#pragma unroll
+#pragma clang loop unroll(full)
     for (int a = 0; a < TM; ++a) {
 #pragma unroll
         for (int b = 0; b < TN; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) stage[(4 * (lane >> 4) + r) * LD + b * 16 + (lane & 15)] = acc[a][b][r];
-#pragma unroll
+#pragma clang loop unroll(full)
         for (int pass = 0; pass < 16 / RPP; ++pass) {
             const int rl = pass * RPP + lane / C4;
             const f32x4 v = *reinterpret_cast<const f32x4 *>(stage + rl * LD + c4 * 4);
@@ -218,8 +237,20 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
                 }
 #pragma unroll
                 for (int q = 0; q < 4; ++q) o[q] *= act_grad_from_out(z[q], p.mact, p.malpha);
+            } else if (p.mzp) {
+                f32x4 z;
+                if (full) {
+                    z = hi_plane4(p.mzp, p.mzpC, pix, col);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) z[q] = (col + q < p.N) ? hi_plane(p.mzp, p.mzpC, pix, col + q) : 0.f;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) o[q] *= act_grad_from_out(z[q], p.mact, p.malpha);
             }
-            if (cvec && full) {
+            if (!p.C) {
+                // planes-only output (dg_conv_fwd_pl with y == NULL, beta 0)
+            } else if (cvec && full) {
                 if (p.beta != 0.f) o += p.beta * *reinterpret_cast<const f32x4 *>(dst);
                 *reinterpret_cast<f32x4 *>(dst) = o;
             } else {

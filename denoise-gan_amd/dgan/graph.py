@@ -441,6 +441,31 @@ class GraphPlan:
                     self.pool_idx[k][midx] = alias.pool_idx[0][midx][:N]
                 else:
                     self.pool_idx[k][midx] = torch.empty(shp[nodes[midx].out.id], dtype=torch.uint8, device=device)
+        # ---- planes-only activations ----
+        # in a plan without parameter gradients (the frozen VGG19), a conv whose
+        # activation output feeds exactly one conv as producer-written planes
+        # skips its fp32 output: the consumer's forward reads the planes, and its
+        # masked input gradient takes act' from the planes' sign
+        # (dg_conv_bwd_data_xmask).  An aliasing plan reads its forward plan's
+        # planes (the first N images' rows).
+        self.nofp32 = set()
+        if alias is not None:
+            self.nofp32 = set(alias.nofp32)
+            for n in conv_nodes:
+                if n.idx not in self.nofp32:
+                    continue
+                c = cons[n.out.id][0]
+                src = alias.cplanes[0][c.idx].x
+                self.cplanes[0][c.idx].x = src.view(self.desc[c.idx].plane_bytes(ops.TENSOR_X))
+        elif not param_grads and feed and not os.environ.get("DG_NO_PLANES_ONLY"):
+            for n in conv_nodes:
+                t = n.out
+                if (n.idx in self.fused_conv or t.id == graph.output.id or t.id not in self.premask
+                        or ops.act_id(n.attrs["act"]) not in (0, 1, 2)):
+                    continue
+                c = cons[t.id][0]
+                if c.kind == "conv" and all(self.cplanes[k][n.idx].fwd_out is not None for k in range(slots)):
+                    self.nofp32.add(n.idx)
         # ---- workspace ----
         ws = [0]
         for n in nodes[1:]:
@@ -527,8 +552,8 @@ class GraphPlan:
                                act=n.attrs["act"], alpha=n.attrs["alpha"], pool_y=s[mp.out.id], ws=ws, planes=P,
                                pool_planes=self.pool_out[slot].get(mp.idx))
                 else:
-                    d.fwd(xin, A.param(f"{n.name}/kernel"), y, bias=bias, act=n.attrs["act"],
-                          alpha=n.attrs["alpha"], ws=ws, planes=P)
+                    d.fwd(xin, A.param(f"{n.name}/kernel"), None if n.idx in self.nofp32 else y, bias=bias,
+                          act=n.attrs["act"], alpha=n.attrs["alpha"], ws=ws, planes=P)
             elif k == "bn":
                 mean, inv = self.saved[slot][n.name]
                 if training:
@@ -619,7 +644,13 @@ class GraphPlan:
                     d.bwd_filter(s[t_in.id], dy, A.grad_of(f"{n.name}/kernel"), dbias=db, beta=param_beta, ws=ws,
                                  planes=P)
                 if need(t_in):
-                    if t_in.id in self.premask:
+                    if t_in.node.idx in self.nofp32:
+                        # (x exists as the planes its producer wrote in the forward)
+                        pa = t_in.node.attrs
+                        P.x.ready = True
+                        d.bwd_data_xmask(dy, A.param(f"{n.name}/kernel"), gr[t_in.id], pa["act"], pa["alpha"],
+                                         beta=beta_of(n, t_in), ws=ws, planes=P)
+                    elif t_in.id in self.premask:
                         pa = t_in.node.attrs
                         d.bwd_data_masked(dy, A.param(f"{n.name}/kernel"), gr[t_in.id], s[t_in.id], pa["act"],
                                           pa["alpha"], beta=beta_of(n, t_in), ws=ws, planes=P)

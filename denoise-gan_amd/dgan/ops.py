@@ -317,7 +317,8 @@ class ConvDesc:
     # planes: optional ConvPlanes (bf16x6 operand planes shared between the
     # ops of this layer, include/dgan.h dg_conv_planes_t)
     def fwd(self, x, w, y, bias=None, act="none", alpha=0.3, beta=0.0, ws=None, planes=None):
-        ldx, ldy = pix_ld(x, self.Cin), pix_ld(y, self.Cout)
+        """y None: only the output's planes (planes.fwd_out) are written."""
+        ldx, ldy = pix_ld(x, self.Cin), (pix_ld(y, self.Cout) if y is not None else 0)
         wp, wn = self._ws(OP_FWD, ws)
         pp, fills = self._pl(OP_FWD, planes)
         ev = _prof_begin()
@@ -369,6 +370,24 @@ class ConvDesc:
     def bwd_data_masked(self, dy, w, dx, z, act, alpha=0.3, beta=0.0, ws=None, planes=None):
         """dx = dL/dx * act'(z) + beta*dx, z = the activation output this conv read as input."""
         return self._bwd_data(dy, w, dx, z, act_id(act), alpha, beta, ws, planes)
+
+    def bwd_data_xmask(self, dy, w, dx, act, alpha=0.3, beta=0.0, ws=None, planes=None):
+        """dx = dL/dx * act'(x) + beta*dx with act' from the sign of x's hi plane
+        (planes.x, ready): the layer input need not exist in fp32."""
+        lddy, lddx = pix_ld(dy, self.Cout), pix_ld(dx, self.Cin)
+        wp, wn = self._ws(OP_BWD_DATA, ws)
+        pp, fills = self._pl(OP_BWD_DATA, planes)
+        if pp is None:
+            pp, fills = ctypes.byref(planes._c(planes.bwd_out)), 0
+        ev = _prof_begin()
+        call("dg_conv_bwd_data_xmask", self._h, _p(dy), lddy, _p(w), _p(dx), lddx, float(beta), act_id(act),
+             float(alpha), pp, wp, wn, _stream())
+        _prof_end(ev, self, "bwd_data")
+        if fills:
+            planes._filled(fills)
+        if planes.bwd_out is not None:
+            planes.bwd_out.ready = True
+        return dx
 
     def _bwd_data(self, dy, w, dx, z, act, alpha, beta, ws, planes):
         lddy, lddx = pix_ld(dy, self.Cout), pix_ld(dx, self.Cin)

@@ -136,6 +136,17 @@ int dg_conv_bwd_data_pl(dg_conv_t d, const float *dy, int lddy, const float *w,
 int dg_conv_bwd_filter_pl(dg_conv_t d, const float *x, int ldx, const float *dy, int lddy,
                           float *dw, float *dbias, float beta,
                           const dg_conv_planes_t *planes, void *ws, size_t ws_bytes, dg_stream_t stream);
+/* dg_conv_bwd_data_pl masked by act'(x) taken from the sign of the hi plane of
+ * x's bf16x6 planes (planes->x, ready: written by x's producer) instead of an
+ * fp32 z, so a layer input that only exists as planes (a VGG19 conv -> conv
+ * chain whose producer wrote no fp32 output: dg_conv_fwd_pl with y NULL) can
+ * be masked (keras VGG19 ReLU, pix2pix.py:53-67).  act NONE / RELU / LRELU;
+ * a positive fp32 value whose bf16 rounding underflows to 0 (|x| < 2^-133)
+ * reads as <= 0.  dg_conv_fwd_pl accepts y == NULL when planes->out is set
+ * and beta == 0: only the output's planes are written. */
+int dg_conv_bwd_data_xmask(dg_conv_t d, const float *dy, int lddy, const float *w, float *dx, int lddx,
+                           float beta, int act, float alpha, const dg_conv_planes_t *planes,
+                           void *ws, size_t ws_bytes, dg_stream_t stream);
 /* Conv2D forward followed by MaxPool2D(2) on its activated output, fused into
  * the forward epilogue (VGG19 blockN_conv{2,4} -> blockN_pool, keras
  * applications VGG19 as built by pix2pix.py:53-67 / srgan.py:70-76; replaces

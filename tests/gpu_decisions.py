@@ -53,6 +53,14 @@ def fused_pool_decisions(idx):
     return arg, (mask.reshape(N, 2 * H2, 2 * W2, C), known.reshape(N, 2 * H2, 2 * W2, C))
 
 
+def plane_positive(pbuf, shape):
+    """x > 0 from the hi plane of a packed bf16x6 plane buffer ([pixel][C/16][3][16]
+    int16; a positive bf16 is a positive int16) for an NHWC shape."""
+    N, H, W, C = shape
+    hi = pbuf.buf[:N * H * W * C * 6].view(torch.int16).reshape(N * H * W, C // 16, 3, 16)[:, :, 0, :]
+    return (hi.reshape(N, H, W, C) > 0)
+
+
 def graph_decisions(plan, slot=0, rows=None):
     """{layer name: mask / argmax} of one dgan.graph.GraphPlan slot; rows: a
     slice of the batch (e.g. one half of a batched forward)."""
@@ -61,9 +69,15 @@ def graph_decisions(plan, slot=0, rows=None):
     sel = (lambda t: t) if rows is None else (lambda t: t[rows])
     out = {}
     fused_conv = getattr(plan, "fused_conv", {})
+    nofp32 = getattr(plan, "nofp32", set())
+    cons = g.consumers() if nofp32 else {}
     for n in g.nodes[1:]:
         k = n.kind
-        if k == "conv" and n.idx in fused_conv:
+        if k == "conv" and n.idx in nofp32:
+            # planes-only activation: the sign of the planes its consumer reads
+            c = cons[n.out.id][0]
+            out[n.name] = sel(plane_positive(plan.cplanes[slot][c.idx].x, plan.shape[n.out.id])).cpu().numpy()
+        elif k == "conv" and n.idx in fused_conv:
             m = fused_conv[n.idx]
             arg, cm = fused_pool_decisions(sel(plan.pool_idx[slot][m.idx]))
             out[m.name] = arg

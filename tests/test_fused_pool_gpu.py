@@ -101,3 +101,39 @@ def test_fused_pool_refuses_ineligible_plans():
             d.fwd_pool(x, w, idx, act="relu", pool_y=py, ws=ops.Workspace())
     d = ops.ConvDesc(16, 64, 64, 32, 64, 3, 1, "same", math="bf16x6")
     assert not d.pool_fusable("tanh")
+
+
+@gpu
+@pytest.mark.parametrize("shape", [(8, 64, 64, 64, 64), (16, 16, 16, 512, 512)], ids=["b1c2like", "b5like_splitk"])
+def test_planes_only_forward_and_plane_mask(shape):
+    """A conv -> conv chain without the fp32 activation (the frozen VGG19's
+    planes-only layers): the producer's planes-only forward writes the same
+    planes as its full forward, and the consumer's input gradient masked by
+    the planes' sign (dg_conv_bwd_data_xmask) equals the fp32-masked one."""
+    N, H, W, C, Co = shape
+    d0 = ops.ConvDesc(N, H, W, C, C, 3, 1, "same", math="bf16x6")   # producer
+    d1 = ops.ConvDesc(N, H, W, C, Co, 3, 1, "same", math="bf16x6")  # consumer
+    x = _rand((N, H, W, C), 11)
+    w0 = _rand(d0.weight_shape, 12, 0.05)
+    w1 = _rand(d1.weight_shape, 13, 0.05)
+    ws = ops.Workspace()
+    nb = N * H * W * C * 6
+    # full forward (fp32 + the consumer's planes) vs planes only
+    z = torch.empty(d0.out_shape, device="cuda")
+    P0 = ops.ConvPlanes(fwd_out=ops.PlaneBuf(nb))
+    d0.fwd(x, w0, z, act="relu", ws=ws, planes=P0)
+    P1 = ops.ConvPlanes(fwd_out=ops.PlaneBuf(nb))
+    d0.fwd(x, w0, None, act="relu", ws=ws, planes=P1)
+    torch.cuda.synchronize()
+    assert torch.equal(_bytes(P0.fwd_out, nb), _bytes(P1.fwd_out, nb))
+    # consumer's input gradient: fp32 mask vs plane mask (x planes = the producer's output planes)
+    dy = _rand(d1.out_shape, 14)
+    dx0 = torch.empty_like(z)
+    d1.bwd_data_masked(dy, w1, dx0, z, "relu", ws=ws)
+    dx1 = torch.full_like(z, float("nan"))
+    Q = ops.ConvPlanes(x=P1.fwd_out)
+    Q.x.ready = True
+    d1.bwd_data_xmask(dy, w1, dx1, "relu", ws=ws, planes=Q)
+    torch.cuda.synchronize()
+    assert (z > 0).float().mean() > 0.2 and (z <= 0).float().mean() > 0.2
+    assert torch.equal(dx0.view(torch.int32), dx1.view(torch.int32))
