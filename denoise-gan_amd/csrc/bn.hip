@@ -14,7 +14,6 @@
 // catastrophic cancellation); chunks are combined with Chan's formula.
 #include "common.h"
 #include <algorithm>
-#include <cstdlib>
 
 namespace dg {
 
@@ -406,7 +405,7 @@ k_bn_bwd_apply(const float *__restrict__ dz, int lddz, const float *__restrict__
 #pragma unroll
         for (int q = 0; q < V; ++q)
             o[q] = A[q] * (dv[q] * act_grad_from_out(zv[q], act, alpha) * dscale) + B[q] * (yv[q] - Mu[q]) + D[q];
-        storev<V>(dy + r * lddy + c, o);
+        if (dy) storev<V>(dy + r * lddy + c, o);
         if constexpr (V == 4) {
             if (dyp) store_planes4(dyp, C, r, c, f32x4{o[0], o[1], o[2], o[3]});
         }
@@ -428,221 +427,6 @@ k_act_bwd(const float *__restrict__ dz, int lddz, const float *__restrict__ z, i
 #pragma unroll
         for (int q = 0; q < V; ++q) o[q] = dv[q] * act_grad_from_out(zv[q], act, alpha);
         storev<V>(dy + r * lddy + c, o);
-    }
-}
-
-// ---- small layers: one launch per BN call ----
-// The deep U-Net layers (pix2pix.py:110-142: down5-8, up1-3; <= ~1M elements)
-// are launch- and latency-bound on the partial -> finalize -> apply chain.
-// Here one block owns a group of SM_CH channels over ALL rows of every
-// segment: pass 1 accumulates the statistics (row lanes in a fixed order,
-// shifted by the segment's first row, then a fixed LDS tree), the block
-// finalises them itself (moving averages in segment order), and pass 2
-// normalises / writes -- the re-read of the rows hits L2.  No cross-block
-// communication; deterministic.
-constexpr int SM_V = 4, SM_SLOTS = 4, SM_CH = SM_V * SM_SLOTS, SM_RL = 256 / SM_SLOTS;
-constexpr int SM_U = 4;                   // rows in flight per lane
-// S * M * C at or below: the one-launch path (DG_BN_SMALL_MAX overrides, for A/B runs)
-static long sm_max_elems() {
-    const char *e = getenv("DG_BN_SMALL_MAX");
-    return e ? atol(e) : (1L << 18);
-}
-
-// sum over the SM_RL row lanes of each slot's SM_V values (fixed order)
-__device__ __forceinline__ void sm_lane_sum(float (&v)[SM_V], float *sh) {
-    const int slot = threadIdx.x % SM_SLOTS, rl = threadIdx.x / SM_SLOTS;
-#pragma unroll
-    for (int q = 0; q < SM_V; ++q) sh[threadIdx.x * SM_V + q] = v[q];
-    __syncthreads();
-    for (int w = SM_RL / 2; w >= 1; w >>= 1) {
-        if (rl < w) {
-#pragma unroll
-            for (int q = 0; q < SM_V; ++q) sh[threadIdx.x * SM_V + q] += sh[(threadIdx.x + w * SM_SLOTS) * SM_V + q];
-        }
-        __syncthreads();
-    }
-#pragma unroll
-    for (int q = 0; q < SM_V; ++q) v[q] = sh[slot * SM_V + q];
-    __syncthreads();
-}
-
-__global__ void __launch_bounds__(256)
-k_bn_fwd_small(const float *__restrict__ y, int ld, long M, int S, int C, const float *gamma, const float *beta,
-               float *save_mean, float *save_invstd, float *mm, float *mv, float momentum, float eps,
-               float *__restrict__ z, int ldz, int act, float alpha, float drop_rate, uint32_t seed,
-               uint32_t seed_stride, const int32_t *step_dev, unsigned short *zp0, int zp0C, int zp0col,
-               unsigned short *zp1, int zp1C, int zp1col) {
-    __shared__ float sh[256 * SM_V];
-    const int slot = threadIdx.x % SM_SLOTS, rl = threadIdx.x / SM_SLOTS;
-    const int c = blockIdx.x * SM_CH + slot * SM_V;
-    const bool cok = c < C;
-    const uint32_t step = step_dev ? (uint32_t)*step_dev : 0u;
-    const float keep_scale = drop_rate > 0.f ? 1.f / (1.f - drop_rate) : 1.f;
-    float mmc[SM_V], mvc[SM_V];
-#pragma unroll
-    for (int q = 0; q < SM_V; ++q) { mmc[q] = cok && mm ? mm[c + q] : 0.f; mvc[q] = cok && mv ? mv[c + q] : 0.f; }
-    for (int sg = 0; sg < S; ++sg) {
-        const float *ys = y + (long)sg * M * ld;
-        float K[SM_V], s1[SM_V], s2[SM_V];
-#pragma unroll
-        for (int q = 0; q < SM_V; ++q) { K[q] = 0.f; s1[q] = s2[q] = 0.f; }
-        if (cok) {
-            loadv<SM_V>(ys + c, K);
-            auto acc = [&](const float (&v)[SM_V]) {
-#pragma unroll
-                for (int q = 0; q < SM_V; ++q) {
-                    const float d = v[q] - K[q];
-                    s1[q] += d;
-                    s2[q] += d * d;
-                }
-            };
-            // SM_U rows' loads in flight per lane, summed in row order
-            long r = rl;
-            for (; r + (SM_U - 1) * SM_RL < M; r += SM_U * SM_RL) {
-                float v[SM_U][SM_V];
-#pragma unroll
-                for (int u = 0; u < SM_U; ++u) loadv<SM_V>(ys + (r + u * SM_RL) * ld + c, v[u]);
-#pragma unroll
-                for (int u = 0; u < SM_U; ++u) acc(v[u]);
-            }
-            for (; r < M; r += SM_RL) {
-                float v[SM_V];
-                loadv<SM_V>(ys + r * ld + c, v);
-                acc(v);
-            }
-        }
-        sm_lane_sum(s1, sh);
-        sm_lane_sum(s2, sh);
-        float sc[SM_V], sf[SM_V];
-        const float n = (float)M;
-#pragma unroll
-        for (int q = 0; q < SM_V; ++q) {
-            const float mu = K[q] + s1[q] / n;
-            const float m2 = fmaxf(s2[q] - s1[q] * s1[q] / n, 0.f);
-            const float var = m2 / n;
-            const float inv = 1.f / sqrtf(var + eps);
-            const float g = cok && gamma ? gamma[c + q] : 1.f;
-            const float b = cok && beta ? beta[c + q] : 0.f;
-            sc[q] = g * inv;
-            sf[q] = b - mu * g * inv;
-            if (cok && rl == 0) {
-                if (save_mean) save_mean[sg * C + c + q] = mu;
-                if (save_invstd) save_invstd[sg * C + c + q] = inv;
-            }
-            mmc[q] -= (mmc[q] - mu) * (1.f - momentum);
-            const float unb = n > 1.f ? m2 / (n - 1.f) : m2;
-            mvc[q] -= (mvc[q] - unb) * (1.f - momentum);
-        }
-        if (!cok) continue;
-        const uint32_t sd = seed + (uint32_t)sg * seed_stride;
-        for (long r = rl; r < M; r += SM_RL) {
-            const long rr = (long)sg * M + r;
-            float v[SM_V], o[SM_V];
-            loadv<SM_V>(y + rr * ld + c, v);
-#pragma unroll
-            for (int q = 0; q < SM_V; ++q) {
-                float t = v[q] * sc[q] + sf[q];
-                if (drop_rate > 0.f)
-                    t = dropout_keep(sd, step, (uint32_t)(r * C + c + q), drop_rate) ? t * keep_scale : 0.f;
-                o[q] = act_fwd(t, act, alpha);
-            }
-            storev<SM_V>(z + rr * ldz + c, o);
-            if (zp0) store_planes4(zp0, zp0C, rr, zp0col + c, f32x4{o[0], o[1], o[2], o[3]});
-            if (zp1) store_planes4(zp1, zp1C, rr, zp1col + c, f32x4{o[0], o[1], o[2], o[3]});
-        }
-    }
-    if (cok && rl == 0) {
-#pragma unroll
-        for (int q = 0; q < SM_V; ++q) {
-            if (mm) mm[c + q] = mmc[q];
-            if (mv) mv[c + q] = mvc[q];
-        }
-    }
-}
-
-__global__ void __launch_bounds__(256)
-k_bn_bwd_small(const float *__restrict__ dz, int lddz, const float *__restrict__ z, int ldz,
-               const float *__restrict__ y, int ldy, long M, int S, int C, const float *gamma,
-               const float *__restrict__ mean, const float *__restrict__ invstd, int act, float alpha, float dscale,
-               float *__restrict__ dy, int lddy, unsigned short *__restrict__ dyp, float *dgamma, float *dbeta,
-               float beta) {
-    __shared__ float sh[256 * SM_V];
-    const int slot = threadIdx.x % SM_SLOTS, rl = threadIdx.x / SM_SLOTS;
-    const int c = blockIdx.x * SM_CH + slot * SM_V;
-    const bool cok = c < C;
-    float t1[SM_V], t2[SM_V];
-#pragma unroll
-    for (int q = 0; q < SM_V; ++q) t1[q] = t2[q] = 0.f;
-    for (int sg = 0; sg < S; ++sg) {
-        const long ro = (long)sg * M;
-        float mu[SM_V], inv[SM_V], a1[SM_V], a2[SM_V];
-#pragma unroll
-        for (int q = 0; q < SM_V; ++q) { a1[q] = a2[q] = 0.f; mu[q] = 0.f; inv[q] = 0.f; }
-        if (cok) {
-            loadv<SM_V>(mean + sg * C + c, mu);
-            loadv<SM_V>(invstd + sg * C + c, inv);
-            auto acc = [&](const float (&dv)[SM_V], const float (&zv)[SM_V], const float (&yv)[SM_V]) {
-#pragma unroll
-                for (int q = 0; q < SM_V; ++q) {
-                    const float dbn = dv[q] * act_grad_from_out(zv[q], act, alpha) * dscale;
-                    a1[q] += dbn;
-                    a2[q] += dbn * (yv[q] - mu[q]) * inv[q];
-                }
-            };
-            long r = rl;
-            for (; r + (SM_U - 1) * SM_RL < M; r += SM_U * SM_RL) {
-                float dv[SM_U][SM_V], zv[SM_U][SM_V], yv[SM_U][SM_V];
-#pragma unroll
-                for (int u = 0; u < SM_U; ++u) {
-                    const long rr = ro + r + u * SM_RL;
-                    loadv<SM_V>(dz + rr * lddz + c, dv[u]);
-                    loadv<SM_V>(z + rr * ldz + c, zv[u]);
-                    loadv<SM_V>(y + rr * ldy + c, yv[u]);
-                }
-#pragma unroll
-                for (int u = 0; u < SM_U; ++u) acc(dv[u], zv[u], yv[u]);
-            }
-            for (; r < M; r += SM_RL) {
-                float dv[SM_V], zv[SM_V], yv[SM_V];
-                loadv<SM_V>(dz + (ro + r) * lddz + c, dv);
-                loadv<SM_V>(z + (ro + r) * ldz + c, zv);
-                loadv<SM_V>(y + (ro + r) * ldy + c, yv);
-                acc(dv, zv, yv);
-            }
-        }
-        sm_lane_sum(a1, sh);
-        sm_lane_sum(a2, sh);
-        if (!cok) continue;
-        float A[SM_V], B[SM_V], D[SM_V];
-#pragma unroll
-        for (int q = 0; q < SM_V; ++q) {
-            t1[q] += a1[q];
-            t2[q] += a2[q];
-            const float g = gamma ? gamma[c + q] : 1.f;
-            const float k1 = g * inv[q];
-            const float m1 = a1[q] / (float)M, m2 = a2[q] / (float)M;
-            A[q] = k1;
-            B[q] = -k1 * m2 * inv[q];
-            D[q] = -k1 * m1;
-        }
-        for (long r = rl; r < M; r += SM_RL) {
-            float dv[SM_V], zv[SM_V], yv[SM_V], o[SM_V];
-            loadv<SM_V>(dz + (ro + r) * lddz + c, dv);
-            loadv<SM_V>(z + (ro + r) * ldz + c, zv);
-            loadv<SM_V>(y + (ro + r) * ldy + c, yv);
-#pragma unroll
-            for (int q = 0; q < SM_V; ++q)
-                o[q] = A[q] * (dv[q] * act_grad_from_out(zv[q], act, alpha) * dscale) + B[q] * (yv[q] - mu[q]) + D[q];
-            storev<SM_V>(dy + (ro + r) * lddy + c, o);
-            if (dyp) store_planes4(dyp, C, ro + r, c, f32x4{o[0], o[1], o[2], o[3]});
-        }
-    }
-    if (cok && rl == 0) {
-#pragma unroll
-        for (int q = 0; q < SM_V; ++q) {
-            if (dbeta) dbeta[c + q] = t1[q] + (beta != 0.f ? beta * dbeta[c + q] : 0.f);
-            if (dgamma) dgamma[c + q] = t2[q] + (beta != 0.f ? beta * dgamma[c + q] : 0.f);
-        }
     }
 }
 
@@ -697,21 +481,6 @@ int dg_bn_fwd_train_seg(int S, int M, int C, const float *y, int ldy, const floa
     DG_ARG(ws_bytes >= dg::bn_ws_floats(M, C, S) * sizeof(float), "workspace too small");
     DG_ARG(drop_rate >= 0.f && drop_rate < 1.f, "bad dropout rate");
     hipStream_t s = (hipStream_t)stream;
-    unsigned short *p0 = (unsigned short *)zp0, *p1 = (unsigned short *)zp1;
-    const bool av4 = dg::vec4_ok(C, {{y, ldy}, {z, ldz}});
-    auto pl_ok = [&](const unsigned short *p, int pc, int col) {
-        return !p || (av4 && pc % 16 == 0 && col % 16 == 0 && C % 16 == 0 && col + C <= pc && (((uintptr_t)p) & 15) == 0);
-    };
-    DG_ARG(pl_ok(p0, zp0C, zp0col) && pl_ok(p1, zp1C, zp1col),
-           "z planes need float4-aligned tensors, C and the column %% 16 == 0, col + C <= planes C, 16-byte alignment");
-    if (av4 && (long)S * M * C <= dg::sm_max_elems()) {
-        hipLaunchKernelGGL(dg::k_bn_fwd_small, dim3(dg_cdiv(C, dg::SM_CH)), dim3(256), 0, s, y, ldy, (long)M, S, C,
-                           gamma, beta, save_mean, save_invstd, moving_mean, moving_var, momentum, eps, z, ldz, act,
-                           alpha, drop_rate, drop_seed, drop_seed_stride, step_dev, p0, zp0C, zp0col, p1, zp1C,
-                           zp1col);
-        DG_LAUNCHED("bn_fwd_small");
-        return DG_OK;
-    }
     dg::BnPlan bp = dg::bn_plan(M, C);
     float *w = (float *)ws;
     const size_t RC = (size_t)S * bp.R * C;
@@ -731,6 +500,13 @@ int dg_bn_fwd_train_seg(int S, int M, int C, const float *y, int ldy, const floa
     hipLaunchKernelGGL(dg::k_bn_stats_final, dim3(dg_cdiv(C, dg::FIN_C)), dim3(256), 0, s, pn, pmean, pm2, bp.R, C, S,
                        gamma, beta, save_mean, save_invstd, moving_mean, moving_var, momentum, eps, scale, shift);
     DG_LAUNCHED("bn_stats_final");
+    const bool av4 = dg::vec4_ok(C, {{y, ldy}, {z, ldz}});
+    unsigned short *p0 = (unsigned short *)zp0, *p1 = (unsigned short *)zp1;
+    auto pl_ok = [&](const unsigned short *p, int pc, int col) {
+        return !p || (av4 && pc % 16 == 0 && col % 16 == 0 && C % 16 == 0 && col + C <= pc && (((uintptr_t)p) & 15) == 0);
+    };
+    DG_ARG(pl_ok(p0, zp0C, zp0col) && pl_ok(p1, zp1C, zp1col),
+           "z planes need float4-aligned tensors, C and the column %% 16 == 0, col + C <= planes C, 16-byte alignment");
     const long MT = (long)S * M;
     if (av4)
         hipLaunchKernelGGL(dg::k_bn_apply<4>, dim3(dg::ew_grid(MT * C / 4)), dim3(256), 0, s, y, ldy, (long)M, S, C,
@@ -775,8 +551,9 @@ int dg_bn_bwd_seg(int S, int M, int C, const float *dz, int lddz, const float *z
                   const float *gamma, const float *save_mean, const float *save_invstd, int act, float alpha,
                   float drop_rate, float *dy, int lddy, void *dy_planes, float *dgamma, float *dbeta, float beta,
                   void *ws, size_t ws_bytes, dg_stream_t stream) {
-    DG_ARG(dz && z && y && save_mean && save_invstd && dy && ws, "NULL tensor");
-    DG_ARG(S >= 1 && S <= 8 && M > 0 && C > 0 && lddz >= C && ldz >= C && ldy >= C && lddy >= C, "bad shape");
+    // dy NULL: only its planes are written (every consumer reads dy_planes)
+    DG_ARG(dz && z && y && save_mean && save_invstd && (dy || dy_planes) && ws, "NULL tensor");
+    DG_ARG(S >= 1 && S <= 8 && M > 0 && C > 0 && lddz >= C && ldz >= C && ldy >= C && (!dy || lddy >= C), "bad shape");
     DG_ARG(ws_bytes >= dg::bn_ws_floats(M, C, S) * sizeof(float), "workspace too small");
     if (drop_rate > 0.f && act != DG_ACT_RELU) {
         dg::set_error("dropout backward needs a ReLU after it (mask recovered from the output)");
@@ -784,19 +561,6 @@ int dg_bn_bwd_seg(int S, int M, int C, const float *dz, int lddz, const float *z
     }
     hipStream_t s = (hipStream_t)stream;
     const float dscale = drop_rate > 0.f ? 1.f / (1.f - drop_rate) : 1.f;
-    {
-        const bool sv4 = dg::vec4_ok(C, {{dz, lddz}, {z, ldz}, {y, ldy}, {dy, lddy}, {save_mean, 4}, {save_invstd, 4}});
-        unsigned short *dyp = (unsigned short *)dy_planes;
-        DG_ARG(!dyp || (sv4 && C % 16 == 0 && (((uintptr_t)dyp) & 15) == 0),
-               "dy planes need C %% 16 == 0, float4-aligned tensors and a 16-byte aligned plane buffer");
-        if (sv4 && (long)S * M * C <= dg::sm_max_elems()) {
-            hipLaunchKernelGGL(dg::k_bn_bwd_small, dim3(dg_cdiv(C, dg::SM_CH)), dim3(256), 0, s, dz, lddz, z, ldz, y,
-                               ldy, (long)M, S, C, gamma, save_mean, save_invstd, act, alpha, dscale, dy, lddy, dyp,
-                               dgamma, dbeta, beta);
-            DG_LAUNCHED("bn_bwd_small");
-            return DG_OK;
-        }
-    }
     dg::BnPlan bp = dg::bn_plan(M, C);
     float *w = (float *)ws;
     const size_t RC = (size_t)S * bp.R * C;

@@ -31,6 +31,7 @@ BN_MOMENTUM = 0.99
 DROP_RATE = 0.5   # pix2pix.py:138
 FEED_DY = not os.environ.get("DG_NO_FEED_DY")  # BN backward writes the conv's dy planes
 FEED_X = not os.environ.get("DG_NO_FEED_X")    # BN forward writes the next convs' x planes
+DY_PLANES_ONLY = not os.environ.get("DG_DY_FP32")  # ... and then skips the fp32 dy (its readers take the planes)
 
 
 def xrows(buf, row0, rows, C):
@@ -401,7 +402,8 @@ class GeneratorPlan:
         feed = P is not None and P.dy is not None
         ops.bn_bwd(dz, z, y, A.param(f"{name}/gamma"), s["mean"][name], s["inv"][name], dy, A.grad_of(f"{name}/gamma"),
                    A.grad_of(f"{name}/beta"), act=act, alpha=ALPHA, drop_rate=drop_rate, beta=beta, ws=ws,
-                   dy_planes=plane_rows(P.dy, dy, 0) if feed else None, segments=self.halves)
+                   dy_planes=plane_rows(P.dy, dy, 0) if feed else None, segments=self.halves,
+                   dy_fp32=not (feed and DY_PLANES_ONLY))
         if feed:
             P._filled(ops.TENSOR_DY)
 
@@ -623,7 +625,7 @@ class DiscriminatorPlan:
                                A.grad_of(f"{name}/gamma") if param_grads else None,
                                A.grad_of(f"{name}/beta") if param_grads else None, act="lrelu", alpha=ALPHA,
                                beta=beta, ws=ws, dy_planes=plane_rows(P.dy, dy, 0) if feed else None,
-                               segments=len(hs))
+                               segments=len(hs), dy_fp32=not (feed and DY_PLANES_ONLY))
                     if feed:
                         P._filled(ops.TENSOR_DY)
                 else:

@@ -506,10 +506,12 @@ def bn_fwd_infer(y, gamma, beta, moving_mean, moving_var, z, act="none", alpha=0
 
 
 def bn_bwd(dz, z, y, gamma, save_mean, save_invstd, dy, dgamma, dbeta, act="none", alpha=0.3, drop_rate=0.0,
-           beta=0.0, ws=None, dy_planes=None, segments=1):
+           beta=0.0, ws=None, dy_planes=None, segments=1, dy_fp32=True):
     """dy_planes: a uint8 device tensor (e.g. a slice of a ConvPlanes' dy
-    PlaneBuf) that also receives dy's bf16x6 planes.  segments: see bn_fwd_train
-    (dg_bn_bwd_seg; dgamma / dbeta summed over the segments)."""
+    PlaneBuf) that also receives dy's bf16x6 planes; dy_fp32=False then skips
+    the fp32 dy (its consumers read the planes; dy only gives the shape).
+    segments: see bn_fwd_train (dg_bn_bwd_seg; dgamma / dbeta summed over the
+    segments)."""
     C = y.shape[-1]
     M = _rows(y)
     if M % segments:
@@ -518,7 +520,8 @@ def bn_bwd(dz, z, y, gamma, save_mean, save_invstd, dy, dgamma, dbeta, act="none
     ws = ws or default_workspace()
     buf, n = ws.get(bn_workspace_bytes(M, C, segments))
     call("dg_bn_bwd_seg", segments, M, C, _p(dz), pix_ld(dz, C), _p(z), pix_ld(z, C), _p(y), pix_ld(y, C), _p(gamma),
-         _p(save_mean), _p(save_invstd), act_id(act), float(alpha), float(drop_rate), _p(dy), pix_ld(dy, C),
+         _p(save_mean), _p(save_invstd), act_id(act), float(alpha), float(drop_rate),
+         _p(dy) if (dy_fp32 or dy_planes is None) else None, pix_ld(dy, C),
          None if dy_planes is None else dy_planes.data_ptr(),
          _p(dgamma), _p(dbeta), float(beta), _p(buf), n, _stream())
     return dy
