@@ -935,8 +935,8 @@ struct OpPlan {
     long x6_ra, x6_rb;
     int x6_ca, x6_cb;
     size_t x6_a_off, x6_b_off;
-    // halo-tiled bf16x6 kernel (stride-1 3x3 FWD / DGRAD, conv_x6h.hip):
-    // cfg = its BN, tiles of 8 x 16 output pixels
+    // halo-tiled bf16x6 kernel (conv_x6h.hip): 1 = stride-1 3x3 FWD / DGRAD,
+    // 2 = stride-2 4x4 DGRAD phases; cfg = its BN, tiles of 8 x 16 output pixels
     int halo, htx, hty;
     // small-Cin 4x4 stride-2 kernels (conv_small.hip); WGRAD: conv-view output rows per block
     int small, small_rows;
@@ -1123,24 +1123,33 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         }
     }
     if (!pl.x6) choose_tiles(pl, kCfgs, kNumCfgs, 157.3e12, "DG_FORCE_CFG", nullptr);
-    if (pl.x6 == 1 && (mode == MODE_FWD || mode == MODE_DGRAD) && g.kh == 3 && g.kw == 3 && g.sh == 1 && g.sw == 1 &&
-        pl.K % 144 == 0 && !getenv("DG_NO_HALO")) {
+    // halo-tiled kernel: 3x3 stride-1 FWD / DGRAD (kt 3), and the sub-pixel
+    // phases of a 4x4 stride-2 DGRAD (kt 2: ConvT forwards, down-block input gradients)
+    const bool h33 = (mode == MODE_FWD || mode == MODE_DGRAD) && g.kh == 3 && g.kw == 3 && g.sh == 1 && g.sw == 1 &&
+                     pl.K % 144 == 0;
+    const bool h22 = mode == MODE_DGRAD && g.kh == 4 && g.kw == 4 && g.sh == 2 && g.sw == 2 && g.Th == 2 &&
+                     g.Tw == 2 && pl.K % 64 == 0 && !getenv("DG_NO_HALO2");
+    if (pl.x6 == 1 && (h33 || h22) && !getenv("DG_NO_HALO")) {
         // each input pixel staged once per 16-channel chunk instead of once per tap
-        const int Hout = mode == MODE_FWD ? g.Ho : g.H, Wout = mode == MODE_FWD ? g.Wo : g.W;
-        pl.halo = 1;
+        const int ntap = h33 ? 9 : 4;
+        int Hout, Wout;
+        if (mode == MODE_FWD) { Hout = g.Ho; Wout = g.Wo; }
+        else if (h33) { Hout = g.H; Wout = g.W; }
+        else { Hout = (g.H + 1) / 2; Wout = (g.W + 1) / 2; }   // phase 0's grid, the largest
+        pl.halo = h33 ? 1 : 2;
         pl.htx = (Wout + 15) / 16;
         pl.hty = (Hout + 7) / 8;
         pl.cfg = pl.N > 64 ? 128 : 64;
         pl.mtiles = g.N * pl.htx * pl.hty;
         pl.ntiles = (pl.N + pl.cfg - 1) / pl.cfg;
         // split-K over channel chunks (at least two per split) until ~2 blocks per CU
-        const long nch = pl.K / 144, blocks = (long)pl.mtiles * pl.ntiles;
+        const long nch = pl.K / (16 * ntap), blocks = (long)pl.mtiles * pl.ntiles * pl.nphase;
         long splits = 1;
         // (same-box A/B of the target: 256 -0.2%, 1024 -0.8% full step vs 512)
         static const long target = getenv("DG_HALO_BLOCKS") ? atol(getenv("DG_HALO_BLOCKS")) : 512;
         while (blocks * splits < target && splits * 4 <= nch) splits *= 2;
         const long cps = (nch + splits - 1) / splits;
-        pl.kchunk = (int)(cps * 144);
+        pl.kchunk = (int)(cps * 16 * ntap);
         pl.splits = (int)((nch + cps - 1) / cps);
     }
     pl.vec = pl.x6 ? 1 : cfg_vec(g, mode, kCfgs[pl.cfg].bk);
@@ -1156,7 +1165,7 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     pl.gemm_bytes = pl.ws_bytes;
     if (getenv("DG_PLAN_DEBUG"))
         fprintf(stderr, "[dg plan] mode %d M=%d N=%d K=%d -> %s cfg %d splits %d\n", mode, pl.M, pl.N, pl.K,
-                pl.halo ? "x6h" : (pl.x6 == 2 ? "f16" : (pl.x6 ? "x6" : "fp32")), pl.cfg, pl.splits);
+                pl.halo == 2 ? "x6h2" : pl.halo ? "x6h" : (pl.x6 == 2 ? "f16" : (pl.x6 ? "x6" : "fp32")), pl.cfg, pl.splits);
     return pl;
 }
 
@@ -1338,7 +1347,7 @@ struct PoolOut {
 // whose derivative is a function of the output's sign
 static bool pool_fusable(const dg_conv_desc_s *d, int act) {
     const OpPlan &pl = d->plan[DG_OP_FWD];
-    return !d->transpose && pl.x6 == 1 && pl.halo && pl.splits == 1 && !d->rc[DG_OP_FWD].on && d->g.Ho % 8 == 0 &&
+    return !d->transpose && pl.x6 == 1 && pl.halo == 1 && pl.splits == 1 && !d->rc[DG_OP_FWD].on && d->g.Ho % 8 == 0 &&
            d->g.Wo % 16 == 0 && d->g.Co % 16 == 0 &&
            (act == DG_ACT_NONE || act == DG_ACT_RELU || act == DG_ACT_LRELU);
 }
@@ -1493,7 +1502,7 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
         fastdiv_magic((unsigned)a.g.Ho, a.mg_ho, a.sh_ho);
         a.B = (const float *)pb; a.ldb = pl.x6_cb; a.b_bytes = (unsigned)(3 * pbs * 2);
         dim3 grid(pl.mtiles * pl.ntiles, pl.nphase * pl.splits);
-        if (pl.halo) launch_gemm_x6h(mode, pl.cfg, grid, a, pl.htx, pl.hty, s);
+        if (pl.halo) launch_gemm_x6h(mode, pl.cfg, pl.halo == 2 ? 2 : 3, grid, a, pl.htx, pl.hty, s);
         else launch_gemm_x6(mode, pl.cfg, grid, a, s);
         DG_LAUNCHED("conv_gemm_x6");
         return finish_splitk(mode, pl, a, s);

@@ -1,43 +1,54 @@
-// Halo-tiled bf16x6 implicit GEMM for stride-1 3x3 convolutions (gfx950):
-// the forward pass of a Conv2D(3, strides=1) and its input gradient -- every
-// VGG19 layer (pix2pix.py:53-67) and the 3x3 convs of the SR family.
+// Halo-tiled bf16x6 implicit GEMM (gfx950) for
+//   KT = 3: stride-1 3x3 convolutions, forward and input gradient -- every
+//           VGG19 layer (pix2pix.py:53-67) and the 3x3 convs of the SR family;
+//   KT = 2: the input gradient of stride-2 4x4 convolutions, one sub-pixel
+//           phase per grid slice (each phase is a stride-1 2x2 conv over dy)
+//           -- the U-Net's Conv2DTranspose forwards (pix2pix.py:128-142) and
+//           the down blocks' / PatchGAN's input gradients (:110-126, :194-211).
 //
 // The generic bf16x6 kernel (conv_x6.hip) stages each K-tile (one filter tap
 // x 16 channels) as BM rows gathered from the activation planes, so each
-// input pixel crosses L2 -> LDS nine times per channel chunk.  Here a block
+// input pixel crosses L2 -> LDS once per tap that reads it.  Here a block
 // owns a PH x PW = 8 x 16 output patch (its 128 GEMM rows) and stages, per
-// 16-channel chunk, the (PH+2) x (PW+2) = 180-pixel input halo ONCE; the nine
+// 16-channel chunk, the (PH+KT-1) x (PW+KT-1) input halo ONCE; the KT*KT
 // taps of the chunk read shifted windows of it.  A fragment of 16 GEMM rows
 // is one patch row, i.e. 16 consecutive halo pixels, so a tap is a constant
 // LDS offset (an immediate on the ds_read) and needs no per-row validity
 // test: padding pixels are fetched out of range and land as zeros.
 //
 // Per block (4 waves, 2x2, wave tile 64 x BN/2 of 16x16 accumulators):
-//   LDS: 2 halo buffers (3 planes x 6 KiB: 180 px x 32 B padded to whole
-//   1-KiB DMAs) + 3 weight K-tile buffers (as conv_x6.hip) = 74.6 KB for
-//   BN = 128, so two blocks share a CU.
-//   Pipeline: weight K-tiles two ahead (three buffers); the halo of chunk
-//   c+1 is fetched during the first five K-tiles of chunk c, one 1-KiB piece
-//   per wave per K-tile, into the other halo buffer.  Every K-tile position
-//   within a chunk is unrolled, so the DMA count of each position -- and so
-//   each s_waitcnt -- is a compile-time constant.
+//   LDS: 2 halo buffers (3 planes x whole 1-KiB DMAs: 180 px -> 6 KiB for
+//   KT 3, 153 px -> 5 KiB for KT 2) + NB weight K-tile buffers (3 for KT 3,
+//   4 for KT 2 so a tap's buffer is fixed) = 74.6 / 79.1 KB for BN = 128, so
+//   two blocks share a CU.
+//   Pipeline: weight K-tiles two ahead; the halo of chunk c+1 is fetched
+//   during the first K-tiles of chunk c, PPT 1-KiB pieces per wave per K-tile,
+//   into the other halo buffer, and has landed by the chunk's last K-tile.
+//   Every K-tile position within a chunk is unrolled, so the DMA count of
+//   each position -- and so each s_waitcnt -- is a compile-time constant.
 //   The epilogue maps patch rows to pixels (ragged patches at the image edge
-//   are masked) and is shared with conv_x6.hip (staged through LDS).
+//   are masked; a phase's pixels are scattered to (sh*hh + ph, sw*ww + pw))
+//   and is shared with conv_x6.hip (staged through LDS).
 //
-// FWD : y[n,ho,wo]  = sum_{a,b} x [n, ho-pt+a, wo-pl+b] . w[a,b]   (halo origin (-pt, -pl))
-// DGRAD: dx[n,h,w] = sum_{a,b} dy[n, h+pt-a, w+pl-b]  . w[a,b]^T  (origin (pt-2, pl-2), taps mirrored)
+// FWD (KT 3):  y[n,ho,wo]  = sum_{a,b} x [n, ho-pt+a, wo-pl+b] . w[a,b]      (halo origin (-pt, -pl))
+// DGRAD:       dx[phase pixel (hh, ww)] = sum_{a,b} dy[n, hh+oh-a, ww+ow-b] . w[i0h+a*sh, i0w+b*sw]^T
+//              (origin (oh-KT+1, ow-KT+1), taps mirrored; stride 1: oh = pt)
 #include "conv_x6.h"
 #include <algorithm>
 #include <type_traits>
+#include <utility>
 
 namespace dg {
 
-constexpr int HX_PH = 8, HX_PW = 16, HX_K = 3;
-constexpr int HX_HH = HX_PH + HX_K - 1, HX_HW = HX_PW + HX_K - 1;  // 10 x 18 halo
-constexpr int HX_HPX = HX_HH * HX_HW;                              // 180 pixels
-constexpr int HX_HPL = 6 * 1024;                                   // bytes per halo plane image
-constexpr int HX_HDMA = 3 * HX_HPL / 1024;                         // 18 one-KiB DMAs per halo
-static_assert(HX_HPX * 32 <= HX_HPL, "halo plane image");
+constexpr int HX_PH = 8, HX_PW = 16;
+template <int KT>
+struct HaloGeom {
+    static constexpr int HH = HX_PH + KT - 1, HW = HX_PW + KT - 1;
+    static constexpr int HPX = HH * HW;
+    static constexpr int HPL = (HPX * 32 + 1023) / 1024 * 1024;  // bytes per halo plane image
+    static constexpr int HDMA = 3 * HPL / 1024;                   // one-KiB DMAs per halo
+    static constexpr int NTAP = KT * KT;
+};
 
 // Forward epilogue fused with the 2x2 max pool that follows the conv (VGG19
 // blockN_conv{2,4} -> blockN_pool, pix2pix.py:53-67 content features): a
@@ -119,24 +130,37 @@ __device__ __forceinline__ void conv_epilogue16_pool(const GemmArgs &p, f32x4 (&
     }
 }
 
-template <int MODE, int BN, bool POOL>
+// f(integral_constant<T>) for T = 0 .. NTAP-1, unrolled at compile time
+template <class F, int... T>
+__device__ __forceinline__ void for_taps(F &&f, std::integer_sequence<int, T...>) {
+    (f(std::integral_constant<int, T>{}), ...);
+}
+
+template <int MODE, int BN, bool POOL, int KT>
 __global__ void __launch_bounds__(256, 2)
 k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "forward or input gradient");
     static_assert(!POOL || MODE == MODE_FWD, "the pool epilogue is a forward epilogue");
+    static_assert(KT == 3 || (KT == 2 && MODE == MODE_DGRAD), "3x3 stride 1, or a stride-2 4x4 input-gradient phase");
+    using HG = HaloGeom<KT>;
+    constexpr int NTAP = HG::NTAP;
+    constexpr int NB = NTAP % 3 == 0 ? 3 : 4;   // weight K-tile buffers: a tap position owns one
+    static_assert(NTAP % NB == 0, "tap positions line up with the weight buffers across chunks");
     constexpr int BK = 16, NW = 4;
     constexpr int WTM = 64, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
     constexpr bool B_KC = MODE == MODE_DGRAD;
     constexpr int BPL = BN * 32 + 96, BBUF = 3 * BPL;
     constexpr int B_SL = 3 * BN / 32, B_NJ = (B_SL + NW - 1) / NW;
-    constexpr int H_NJ = (HX_HDMA + NW - 1) / NW;  // halo pieces per wave (5)
-    static_assert(H_NJ < 9, "the halo of the next chunk is issued within one chunk's K-tiles");
+    constexpr int H_NJ = (HG::HDMA + NW - 1) / NW;          // halo pieces per wave
+    constexpr int PPT = (H_NJ + NTAP - 2) / (NTAP - 1);     // pieces per K-tile, none at the last tap
+    static_assert((H_NJ - 1) / PPT < NTAP - 1, "the next chunk's halo lands by the chunk's last K-tile");
 
-    __shared__ __attribute__((aligned(16))) char hal0[3 * HX_HPL];
-    __shared__ __attribute__((aligned(16))) char hal1[3 * HX_HPL];
+    __shared__ __attribute__((aligned(16))) char hal[2][3 * HG::HPL];
     __shared__ __attribute__((aligned(16))) char bs0[BBUF];
     __shared__ __attribute__((aligned(16))) char bs1[BBUF];
     __shared__ __attribute__((aligned(16))) char bs2[BBUF];
+    __shared__ __attribute__((aligned(16))) char bs3[NB == 4 ? BBUF : 16];
+    char *const hal0 = hal[0], *const hal1 = hal[1];
 
     const ConvGeom &g = p.g;
     const int tid = threadIdx.x;
@@ -144,8 +168,10 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid >> 1, wn = wid & 1;
 
-    int split, tile;
-    xcd_remap(split, tile);
+    int zz, tile;
+    xcd_remap(zz, tile);
+    const int phase = zz / p.splits;
+    const int split = zz - phase * p.splits;
     const int mt = tile / p.ntiles;
     const int nt = tile - mt * p.ntiles;
     const int n0 = nt * BN;
@@ -153,16 +179,40 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     const int t_ = mt / tiles_x;
     const int ty = t_ % tiles_y;
     const int nimg = t_ / tiles_y;
-    // A source (FWD: x; DGRAD: dy) and output extents
+    // A source (FWD: x; DGRAD: dy) extents and the output grid of this block
+    // (DGRAD: the phase's sub-grid; stride 1: the whole dx)
     const int Hin = MODE == MODE_FWD ? g.H : g.Ho, Win = MODE == MODE_FWD ? g.W : g.Wo;
-    const int Hout = MODE == MODE_FWD ? g.Ho : g.H, Wout = MODE == MODE_FWD ? g.Wo : g.W;
-    const int oy = ty * HX_PH + (MODE == MODE_FWD ? -g.pt : g.pt - (HX_K - 1));
-    const int ox = tx * HX_PW + (MODE == MODE_FWD ? -g.pl : g.pl - (HX_K - 1));
-    // channel chunks of this split (kchunk is a multiple of 9 taps x 16 channels)
-    const int nch = p.K / (9 * BK);
-    const int cbeg = split * (p.kchunk / (9 * BK));
-    const int cend = min(nch, cbeg + p.kchunk / (9 * BK));
+    PhaseInfo ph{};
+    int Hout, Wout, oy, ox;
+    if constexpr (MODE == MODE_FWD) {
+        Hout = g.Ho; Wout = g.Wo;
+        oy = ty * HX_PH - g.pt;
+        ox = tx * HX_PW - g.pl;
+    } else {
+        ph = phase_info(g, phase, g.N);
+        Hout = ph.Hp; Wout = ph.Wp;
+        // tap a of the phase reads dy row hh + oh - a (exact: ph + pt - i0h is a multiple of sh)
+        const int oh = (ph.ph + g.pt - ph.i0h) / g.sh, ow = (ph.pw + g.pl - ph.i0w) / g.sw;
+        oy = ty * HX_PH + oh - (KT - 1);
+        ox = tx * HX_PW + ow - (KT - 1);
+    }
+    if (ty * HX_PH >= Hout || tx * HX_PW >= Wout) return;   // block-uniform: a smaller phase grid
+    // channel chunks of this split (kchunk is a multiple of NTAP taps x 16 channels)
+    const int nch = p.K / (NTAP * BK);
+    const int cbeg = split * (p.kchunk / (NTAP * BK));
+    const int cend = min(nch, cbeg + p.kchunk / (NTAP * BK));
     if (cbeg >= cend) return;
+    // filter tap (row-major in w) of tap position T
+    int tap_w[NTAP];
+#pragma unroll
+    for (int T = 0; T < NTAP; ++T) {
+        if constexpr (MODE == MODE_FWD) {
+            tap_w[T] = T;
+        } else {
+            const int i = ph.i0h + (T / KT) * g.sh, j = ph.i0w + (T % KT) * g.sw;
+            tap_w[T] = i * g.kw + j;
+        }
+    }
 
     const rsrc4_t rA = make_rsrc4(p.A, p.a_bytes);
     const rsrc4_t rB = make_rsrc4(p.B, p.b_bytes);
@@ -173,29 +223,30 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         asm volatile("" ::: "memory");
     };
 
-    // ---- halo pieces: wave piece s is DMA d = wid + NW*s of the 18 (plane,
-    // KiB) pieces (d >= 18 repeats piece d - 18: same bytes, same data, and
+    // ---- halo pieces: wave piece s is DMA d = wid + NW*s of the HDMA (plane,
+    // KiB) pieces (d >= HDMA repeats piece d - HDMA: same bytes, same data, and
     // every DMA provably targets the halo buffer); lane L of a piece fetches
     // the 16-byte half-row q = 64k + L of its plane image (halo pixel q/2,
     // channel half q&1).  hoff: byte offset at chunk 0, or -1 outside the
-    // image / past the 180 pixels.
+    // image / past the halo's pixels.
+    constexpr int PER = HG::HPL / 1024;
     int hoff[H_NJ], hdst[H_NJ];
 #pragma unroll
     for (int s = 0; s < H_NJ; ++s) {
-        const int d = (wid + NW * s) % HX_HDMA;
-        const int pl = d / 6, kk = d - pl * 6;
-        hdst[s] = pl * HX_HPL + kk * 1024;
+        const int d = (wid + NW * s) % HG::HDMA;
+        const int pl = d / PER, kk = d - pl * PER;
+        hdst[s] = pl * HG::HPL + kk * 1024;
         hoff[s] = -1;
         const int q = kk * 64 + lane, hp = q >> 1, hh = q & 1;
-        if (hp < HX_HPX) {
-            const int hr = hp / HX_HW, hc = hp - hr * HX_HW;
+        if (hp < HG::HPX) {
+            const int hr = hp / HG::HW, hc = hp - hr * HG::HW;
             const int iy = oy + hr, ix = ox + hc;
             if ((unsigned)iy < (unsigned)Hin && (unsigned)ix < (unsigned)Win)
                 hoff[s] = ((((nimg * Hin + iy) * Win + ix) * (3 * p.lda)) + 16 * pl + 8 * hh) * 2;
         }
     }
-    auto issue_h = [&](int s, int chunk, char *hal) __attribute__((always_inline)) {
-        dma(rA, hal + hdst[s], hoff[s] >= 0 ? (unsigned)(hoff[s] + chunk * 96) : DG_OOB);
+    auto issue_h = [&](int s, int chunk, char *hb) __attribute__((always_inline)) {
+        dma(rA, hb + hdst[s], hoff[s] >= 0 ? (unsigned)(hoff[s] + chunk * 96) : DG_OOB);
     };
 
     // ---- weight K-tile slots (as conv_x6.hip): FWD RC image [16 k][BN],
@@ -225,16 +276,19 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
             bbase[j] = (ci * (3 * p.ldb) + 16 * plane + 8 * c) * 2;
         }
     }
-    // tap t = 3a + b of chunk c: FWD rows (t*Ci + 16c) of w[(a,b,ci)][co];
-    // DGRAD rows ci of w[a,b] at co-chunk c
-    auto issue_b = [&](int t, int chunk, char *bs) __attribute__((always_inline)) {
+    // tap position T of chunk c: FWD rows (tap*Ci + 16c) of w[(a,b,ci)][co];
+    // DGRAD rows ci of w[i,j] at co-chunk c
+    auto issue_b = [&](int T, int chunk, char *bs) __attribute__((always_inline)) {
         int delta;
-        if constexpr (!B_KC) delta = ((t * g.Ci + chunk * BK) * (3 * p.ldb)) * 2;
-        else delta = (t * g.Ci * (3 * p.ldb) + chunk * 48) * 2;
+        if constexpr (!B_KC) delta = ((tap_w[T] * g.Ci + chunk * BK) * (3 * p.ldb)) * 2;
+        else delta = (tap_w[T] * g.Ci * (3 * p.ldb) + chunk * 48) * 2;
 #pragma unroll
         for (int j = 0; j < B_NJ; ++j) {
             dma(rB, bs + bdst[j], bok[j] ? (unsigned)(bbase[j] + delta) : DG_OOB);
         }
+    };
+    auto bbuf = [&](int i) __attribute__((always_inline)) -> char * {
+        return i == 0 ? bs0 : (i == 1 ? bs1 : (i == 2 ? bs2 : bs3));
     };
 
     f32x4 acc[TM][TN];
@@ -243,21 +297,24 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
 #pragma unroll
         for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // one K-tile: tap T of chunk `chunk` from halo `hc`, weights in bs[T % 3];
-    // issues halo piece T of chunk+1 into `hn` (T < H_NJ) and the weight tile
-    // two K-tiles ahead, then the MFMAs, then waits for the next weight tile
+    // one K-tile: tap position T of chunk `chunk` from halo `hc`, weights in
+    // bs[T % NB]; issues halo pieces PPT*T .. of chunk+1 into `hn` and the
+    // weight tile two K-tiles ahead, then the MFMAs, then waits for the next
+    // weight tile (and, at the chunk's last tap, the whole next halo)
     auto ktile = [&](auto TT, int chunk, const char *hc, char *hn) __attribute__((always_inline)) {
         constexpr int T = decltype(TT)::value;
-        constexpr int ta = T / 3, tb = T % 3;
-        constexpr int da = MODE == MODE_FWD ? ta : HX_K - 1 - ta;
-        constexpr int db = MODE == MODE_FWD ? tb : HX_K - 1 - tb;
-        const char *bc = T % 3 == 0 ? bs0 : (T % 3 == 1 ? bs1 : bs2);
-        char *bn = (T + 2) % 3 == 0 ? bs0 : ((T + 2) % 3 == 1 ? bs1 : bs2);
+        constexpr int ta = T / KT, tb = T % KT;
+        constexpr int da = MODE == MODE_FWD ? ta : KT - 1 - ta;
+        constexpr int db = MODE == MODE_FWD ? tb : KT - 1 - tb;
+        constexpr int H0P = T * PPT, H1P = (T + 1) * PPT < H_NJ ? (T + 1) * PPT : H_NJ;
+        constexpr int NH = H1P > H0P ? H1P - H0P : 0;   // halo pieces issued in this K-tile
+        const char *bc = bbuf(T % NB);
+        char *bn = bbuf((T + 2) % NB);
         bf16x8 ahm[TM], ahl[TM], b1[TN], b2[TN], b3[TN];
-        const char *H0 = hc, *H1 = hc + HX_HPL, *H2 = hc + 2 * HX_HPL;
+        const char *H0 = hc, *H1 = hc + HG::HPL, *H2 = hc + 2 * HG::HPL;
 #pragma unroll
         for (int a = 0; a < TM; ++a) {
-            const int r0 = (wm * TM + a + da) * HX_HW + db;
+            const int r0 = (wm * TM + a + da) * HG::HW + db;
             ahm[a] = x6_kc_frag(H0, H1, r0, lane);
             ahl[a] = x6_kc_frag(H0, H2, r0, lane);
         }
@@ -275,9 +332,10 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
                 b3[b] = x6_rc_frag<BN>(B2, B0, c0, lane);
             }
         }
-        if constexpr (T < H_NJ) issue_h(T, chunk + 1, hn);
-        if constexpr (T + 2 < 9) issue_b(T + 2, chunk, bn);
-        else issue_b(T + 2 - 9, chunk + 1, bn);
+#pragma unroll
+        for (int s = H0P; s < H0P + NH; ++s) issue_h(s, chunk + 1, hn);
+        if constexpr (T + 2 < NTAP) issue_b(T + 2, chunk, bn);
+        else issue_b(T + 2 - NTAP, chunk + 1, bn);
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -294,20 +352,13 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
             for (int b = 0; b < TN; ++b)
                 acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahl[a], b3[b], acc[a][b], 0, 0, 0);
         // DMAs issued in this K-tile may stay in flight; everything older
-        // (the next weight tile, and at T = 8 the whole next halo) has landed
-        wait_dma_c<B_NJ + (T < H_NJ ? 1 : 0)>();
+        // (the next weight tile, and at the last tap the whole next halo) has landed
+        wait_dma_c<B_NJ + NH>();
         barrier();
     };
     auto chunk_tiles = [&](int chunk, const char *hc, char *hn) __attribute__((always_inline)) {
-        ktile(std::integral_constant<int, 0>{}, chunk, hc, hn);
-        ktile(std::integral_constant<int, 1>{}, chunk, hc, hn);
-        ktile(std::integral_constant<int, 2>{}, chunk, hc, hn);
-        ktile(std::integral_constant<int, 3>{}, chunk, hc, hn);
-        ktile(std::integral_constant<int, 4>{}, chunk, hc, hn);
-        ktile(std::integral_constant<int, 5>{}, chunk, hc, hn);
-        ktile(std::integral_constant<int, 6>{}, chunk, hc, hn);
-        ktile(std::integral_constant<int, 7>{}, chunk, hc, hn);
-        ktile(std::integral_constant<int, 8>{}, chunk, hc, hn);
+        for_taps([&](auto TT) __attribute__((always_inline)) { ktile(TT, chunk, hc, hn); },
+                 std::make_integer_sequence<int, NTAP>{});
     };
 
     // prologue: the whole halo of the first chunk and its first two weight tiles
@@ -324,40 +375,47 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     }
     if (c < cend) chunk_tiles(c, hal0, hal1);
     // every wave's DMAs (including the harmless ones past the last chunk)
-    // have landed before hal0 becomes the epilogue's staging area
+    // have landed before the halo buffers become the epilogue's staging area
     wait_dma_c<0>();
     barrier();
 
     constexpr int STAGE = 16 * (WTN + 4);
-    static_assert(NW * STAGE * 4 <= 3 * HX_HPL, "epilogue staging fits in a halo buffer");
-    // patch row -> output pixel; slab rows are pixels (the split-K reduce of
-    // FWD / unit-stride DGRAD maps slab row = pixel)
+    static_assert(NW * STAGE * 4 <= 2 * 3 * HG::HPL, "epilogue staging fits in the halo buffers");
+    float *stage = reinterpret_cast<float *>(hal0) + wid * STAGE;
+    // patch row -> output pixel; slab rows: FWD / stride-1 DGRAD pixels, a
+    // phase's GEMM rows otherwise (as k_splitk_reduce maps them)
     auto rowmap = [&](int row) __attribute__((always_inline)) -> RowPix {
         const int ho = ty * HX_PH + (row >> 4), wo = tx * HX_PW + (row & 15);
         if (ho >= Hout || wo >= Wout) return RowPix{-1, -1};
-        const long pix = ((long)nimg * Hout + ho) * Wout + wo;
-        return RowPix{pix, pix};
+        if constexpr (MODE == MODE_DGRAD && KT == 2) {
+            const long pix = ((long)nimg * g.H + ho * g.sh + ph.ph) * g.W + wo * g.sw + ph.pw;
+            return RowPix{((long)nimg * Hout + ho) * Wout + wo, pix};
+        } else {
+            const long pix = ((long)nimg * Hout + ho) * Wout + wo;
+            return RowPix{pix, pix};
+        }
     };
     if constexpr (POOL)
-        conv_epilogue16_pool<TM, TN>(p, acc, wm * TM, n0 + wn * WTN, ty, tx, nimg, lane,
-                                     reinterpret_cast<float *>(hal0) + wid * STAGE);
+        conv_epilogue16_pool<TM, TN>(p, acc, wm * TM, n0 + wn * WTN, ty, tx, nimg, lane, stage);
     else
-        conv_epilogue16<MODE, TM, TN>(p, acc, wm * WTM, n0 + wn * WTN, rowmap, 0, split, lane,
-                                      reinterpret_cast<float *>(hal0) + wid * STAGE);
+        conv_epilogue16<MODE, TM, TN>(p, acc, wm * WTM, n0 + wn * WTN, rowmap, phase, split, lane, stage);
 }
 
-void launch_gemm_x6h(int mode, int bn, dim3 grid, const GemmArgs &a, int tiles_x, int tiles_y, hipStream_t s) {
+void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int tiles_x, int tiles_y, hipStream_t s) {
     const dim3 blk(256);
-#define DG_X6H(M_, B_, P_) hipLaunchKernelGGL((k_conv_gemm_x6h<M_, B_, P_>), grid, blk, 0, s, a, tiles_x, tiles_y)
+#define DG_X6H(M_, B_, P_, K_) hipLaunchKernelGGL((k_conv_gemm_x6h<M_, B_, P_, K_>), grid, blk, 0, s, a, tiles_x, tiles_y)
     if (mode == MODE_FWD && a.pidx) {
-        if (bn == 128) DG_X6H(MODE_FWD, 128, true);
-        else DG_X6H(MODE_FWD, 64, true);
+        if (bn == 128) DG_X6H(MODE_FWD, 128, true, 3);
+        else DG_X6H(MODE_FWD, 64, true, 3);
     } else if (mode == MODE_FWD) {
-        if (bn == 128) DG_X6H(MODE_FWD, 128, false);
-        else DG_X6H(MODE_FWD, 64, false);
+        if (bn == 128) DG_X6H(MODE_FWD, 128, false, 3);
+        else DG_X6H(MODE_FWD, 64, false, 3);
+    } else if (kt == 2) {
+        if (bn == 128) DG_X6H(MODE_DGRAD, 128, false, 2);
+        else DG_X6H(MODE_DGRAD, 64, false, 2);
     } else {
-        if (bn == 128) DG_X6H(MODE_DGRAD, 128, false);
-        else DG_X6H(MODE_DGRAD, 64, false);
+        if (bn == 128) DG_X6H(MODE_DGRAD, 128, false, 3);
+        else DG_X6H(MODE_DGRAD, 64, false, 3);
     }
 #undef DG_X6H
 }

@@ -79,10 +79,14 @@ def _check_step1(d, loss, gen, y, Ga, Da, bnG, bnD, nloss, what, g_rel=0.0, d_re
     return dps, wg, wd
 
 
-def _check_step2(d, loss, Ga, Da, lr_g, lr_d, nloss, what, loss_rtol=5e-4, median=True):
+def _check_step2(d, loss, Ga, Da, lr_g, lr_d, nloss, what, loss_rtol=5e-4, median=True, steps_apart=2.0):
     """median: also hold the median sampled parameter within 5% of one Adam step (variables whose
     step-1 gradient is exactly cancelling in exact arithmetic -- a conv bias feeding a BatchNorm --
-    are skipped: their fp32 gradient is rounding noise that Adam normalises to a full step)."""
+    are skipped: their fp32 gradient is rounding noise that Adam normalises to a full step).
+    steps_apart: the max-abs bound in Adam steps (lr).  Keras Adam's first two updates (beta_1 .5,
+    beta_2 .999) are each at most ~1.05 lr whatever the gradient, so two runs whose gradients
+    differ in sign on an element can end up to ~4.2 lr apart: the content-on fixtures, whose G
+    gradients carry the VGG19 near-tie spread (VGG_TIE_REL), are held to that; the others to 2 lr."""
     got = loss.cpu().double().numpy()
     assert np.allclose(got, d["s2|losses"][:nloss], rtol=loss_rtol, atol=1e-6), (what, got, d["s2|losses"])
     for pre, A, lr in (("s2|pG|", Ga, lr_g), ("s2|pD|", Da, lr_d)):
@@ -91,7 +95,7 @@ def _check_step2(d, loss, Ga, Da, lr_g, lr_d, nloss, what, loss_rtol=5e-4, media
         for n in names(d, pre):
             idx = d[f"{pre}{n}|idx"]
             diff = np.abs(p[n].astype(np.float64).ravel()[idx] - d[f"{pre}{n}|val"])
-            assert diff.max() <= 2 * lr + 1e-6, (what, n, diff.max())
+            assert diff.max() <= steps_apart * lr + 1e-6, (what, n, diff.max())
             g1 = d.get(f"s1|g{pre[4]}|{n}|l2")
             if median and (g1 is None or float(g1) > 1e-6):
                 assert np.median(diff) < 0.05 * lr, (what, n, np.median(diff))
@@ -125,7 +129,8 @@ def test_pix2pix_bs16_matches_golden(case):
     x2, y2 = batch(meta, meta["batch_seeds"][1])
     loss2 = tr.step(torch.from_numpy(x2).to(DEV), torch.from_numpy(y2).to(DEV))
     torch.cuda.synchronize()
-    _check_step2(d, loss2, m.generator.arena, m.discriminator.arena, 2e-4, 2e-4, 8, case)
+    _check_step2(d, loss2, m.generator.arena, m.discriminator.arena, 2e-4, 2e-4, 8, case,
+                 steps_apart=4.2 if content else 2.0)
 
 
 @gpu
