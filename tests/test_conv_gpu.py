@@ -109,7 +109,7 @@ def test_conv_layer(case, math_mode):
         assert err <= 1e-6 * dy.abs().sum(dim=(0, 1, 2)).max().item(), f"{name} dbias: {err:.3e}"
 
 
-# stride-1 3x3 layers on the halo-tiled bf16x6 kernel (csrc/conv_x6h.hip):
+# layers on the halo-tiled bf16x6 kernel (csrc/conv_x6h.hip), stride-1 3x3:
 # ragged 8x16 output patches (H, W not multiples of 8 / 16), 'valid' padding,
 # BN 64 and 128, and split-K over channel chunks (small images, many channels)
 HALO_CASES = [
@@ -118,6 +118,15 @@ HALO_CASES = [
     ("h.splitk", 2, 8, 8, 512, 512, 3, 1, "same", False, False),
     ("h.valid", 2, 20, 21, 64, 64, 3, 1, "valid", False, True),
     ("h.tfpad", 3, 13, 29, 32, 48, 3, 1, (1, 1, 1, 1), False, False),
+    # stride-2 4x4 layers: the input gradient in 4 sub-pixel phases (Conv2D
+    # bwd_data and Conv2DTranspose fwd; ragged patches, odd sizes whose phases
+    # differ in size, BN 64 / 128, split-K)
+    ("h2.down", 2, 32, 32, 64, 128, 4, 2, "same", False, False),
+    ("h2.up", 2, 16, 16, 256, 64, 4, 2, "same", True, False),
+    ("h2.ragged", 3, 26, 40, 32, 64, 4, 2, "same", False, True),
+    ("h2.odd", 2, 17, 15, 16, 32, 4, 2, "same", False, False),
+    ("h2.splitk", 2, 8, 8, 512, 512, 4, 2, "same", False, False),
+    ("h2.valid", 2, 20, 22, 32, 64, 4, 2, "valid", False, True),
 ]
 
 
@@ -125,7 +134,8 @@ HALO_CASES = [
 @pytest.mark.parametrize("case", HALO_CASES, ids=[c[0] for c in HALO_CASES])
 def test_conv_halo_kernel(case, monkeypatch):
     # force the bf16x6 path (the planner keeps small GEMMs on the fp32 kernel);
-    # every stride-1 3x3 bf16x6 FWD / DGRAD plan runs on the halo kernel
+    # every stride-1 3x3 bf16x6 FWD / DGRAD plan and every stride-2 4x4 DGRAD
+    # runs on the halo kernel
     monkeypatch.setenv("DG_FORCE_X6CFG", "0")
     monkeypatch.delenv("DG_NO_HALO", raising=False)
     test_conv_layer(case, "bf16x6")
