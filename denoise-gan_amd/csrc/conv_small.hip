@@ -19,7 +19,11 @@
 // registers one tile ahead and overlap the MFMAs.
 //
 // Geometry (conv view): kh = kw = 4, sh = sw = 2, CI in {3, 6}, Co % 64 == 0,
-// Wo % 32 == 0 (P = 64 when Wo % 64 == 0).
+// Wo % 32 == 0 (P = 64 when Wo % 64 == 0).  The forward also runs VGG19's
+// block1_conv1 (3x3 stride 1 'same' on the 3-channel preprocessed image,
+// pix2pix.py:53-67): the strip is then 4 input rows x (P + 2) columns without
+// the parity split, and the K of 27 is padded to two halves of rows {0, 1} and
+// {2, 3} (row 3's weights are zero), so the same per-half constant offsets apply.
 #include "conv_impl.h"
 #include <algorithm>
 
@@ -32,28 +36,36 @@ constexpr int SC_CH = 8;    // MFMA operands per register chunk
 // 16*CI taps of one pixel on distinct banks (ds_read_b32 banks are a/4 mod 32)
 __host__ __device__ constexpr int sc_up(int x, int r) { return x + (((r - x) % 32) + 32) % 32; }
 
-template <int CI, int P>
+// KW x (up to 4 rows) filter, stride S in {1 (KW 3), 2 (KW 4)}
+template <int CI, int P, int KW = 4, int S = 2>
 struct Strip {
-    static constexpr int COLS = P + 1;                        // columns per parity
-    static constexpr int PAR = sc_up(COLS * CI, 2 * CI);      // parity stride (floats)
-    static constexpr int ROW = sc_up(2 * PAR, 4 * CI);        // input-row stride
+    static_assert((KW == 4 && S == 2) || (KW == 3 && S == 1), "4x4 stride 2 or 3x3 stride 1");
+    static constexpr int COLS = S == 2 ? P + 1 : P + KW - 1;  // columns per parity
+    static constexpr int PAR = S == 2 ? sc_up(COLS * CI, 2 * CI) : 0;   // parity stride (floats)
+    static constexpr int ROW = S == 2 ? sc_up(2 * PAR, 4 * CI) : sc_up(COLS * CI, 4 * CI);  // input-row stride
     static constexpr int SIZE = 4 * ROW;
-    static constexpr int WL = 2 * P + 2;                      // input columns loaded
+    static constexpr int WL = S * P + KW - S;                 // input columns loaded
     static constexpr int NLOAD = 4 * WL * CI;                 // elements loaded per tile
-    // offset of tap k = (i*4 + j)*CI + ci of pixel 0
+    static constexpr int KHALF = 2 * KW * CI;                 // k per MFMA half (filter rows 0-1 | 2-3)
+    // offset of tap k = (i*KW + j)*CI + ci of pixel 0
     __host__ __device__ static constexpr int tap(int k) {
-        return ((k / CI) >> 2) * ROW + (((k / CI) & 3) & 1) * PAR + (((k / CI) & 3) >> 1) * CI + k % CI;
+        return S == 2 ? ((k / CI) >> 2) * ROW + (((k / CI) & 3) & 1) * PAR + (((k / CI) & 3) >> 1) * CI + k % CI
+                      : ((k / CI) / KW) * ROW + ((k / CI) % KW) * CI + k % CI;
+    }
+    // LDS position of loaded element (input row, input column wl, ci)
+    __host__ __device__ static constexpr int pos(int row, int wl, int ci) {
+        return S == 2 ? row * ROW + (wl & 1) * PAR + (wl >> 1) * CI + ci : row * ROW + wl * CI + ci;
     }
 };
 
 // Load the strip of segment (n, ho, wo0) into registers: element e = tid + q*NTHR of
 // [row 0..3][input column 0..WL-1][ci], zero outside the image
-template <int CI, int P, int NTHR>
+template <int CI, int P, int NTHR, int KW = 4, int ST = 2>
 __device__ __forceinline__ void strip_fetch(const GemmArgs &p, int n, int ho, int wo0, int tid,
-                                            float (&r)[(Strip<CI, P>::NLOAD + NTHR - 1) / NTHR]) {
-    using S = Strip<CI, P>;
+                                            float (&r)[(Strip<CI, P, KW, ST>::NLOAD + NTHR - 1) / NTHR]) {
+    using S = Strip<CI, P, KW, ST>;
     const ConvGeom &g = p.g;
-    const int h0 = 2 * ho - g.pt, w0 = 2 * wo0 - g.pl;
+    const int h0 = ST * ho - g.pt, w0 = ST * wo0 - g.pl;
 #pragma unroll
     for (int q = 0; q < (S::NLOAD + NTHR - 1) / NTHR; ++q) {
         const int e = tid + q * NTHR;
@@ -66,16 +78,17 @@ __device__ __forceinline__ void strip_fetch(const GemmArgs &p, int n, int ho, in
     }
 }
 
-template <int CI, int P, int NTHR>
-__device__ __forceinline__ void strip_store(float *s, int tid, const float (&r)[(Strip<CI, P>::NLOAD + NTHR - 1) / NTHR]) {
-    using S = Strip<CI, P>;
+template <int CI, int P, int NTHR, int KW = 4, int ST = 2>
+__device__ __forceinline__ void strip_store(float *s, int tid,
+                                            const float (&r)[(Strip<CI, P, KW, ST>::NLOAD + NTHR - 1) / NTHR]) {
+    using S = Strip<CI, P, KW, ST>;
 #pragma unroll
     for (int q = 0; q < (S::NLOAD + NTHR - 1) / NTHR; ++q) {
         const int e = tid + q * NTHR;
         if ((S::NLOAD % NTHR) != 0 && q == (S::NLOAD + NTHR - 1) / NTHR - 1 && e >= S::NLOAD) break;
         const int row = e / (S::WL * CI), rem = e - row * (S::WL * CI);
         const int wl = rem / CI, ci = rem - wl * CI;
-        s[row * S::ROW + (wl & 1) * S::PAR + (wl >> 1) * CI + ci] = r[q];
+        s[S::pos(row, wl, ci)] = r[q];
     }
 }
 
@@ -130,7 +143,9 @@ __device__ __forceinline__ void small_fwd_epilogue(const GemmArgs &p, const f32x
             if (p.beta != 0.f) o += p.beta * e.c[i];
         }
         float *dst = p.C + pix * p.ldc + col;
-        if (cvec) {
+        if (!p.C) {
+            // planes-only output (dg_conv_fwd_pl with y NULL)
+        } else if (cvec) {
             *reinterpret_cast<f32x4 *>(dst) = o;
         } else {
 #pragma unroll
@@ -147,11 +162,14 @@ __device__ __forceinline__ void small_fwd_epilogue(const GemmArgs &p, const f32x
 // XL: the epilogue reads global operands (gradient mask or beta * y).  Without them the
 // tile loop issues no loads besides the strip prefetch, and no wait ever covers the
 // previous tile's stores.
-template <int CI, int P, bool XL>
+template <int CI, int P, bool XL, int KW = 4, int ST = 2>
 __global__ void __launch_bounds__(128 * (P / 32))
 k_small_fwd(const GemmArgs p) {
-    using S = Strip<CI, P>;
-    constexpr int KH = 8 * CI;
+    using S = Strip<CI, P, KW, ST>;
+    constexpr int KH = S::KHALF;                  // k per half
+    constexpr int KTOT = KW * KW * CI;            // real k (3x3: half 1's row 3 is padding)
+    constexpr int CH = KH % SC_CH == 0 ? SC_CH : 6;
+    static_assert(KH % CH == 0, "operand chunks");
     constexpr int NTHR = 128 * (P / 32);
     constexpr int NL = (S::NLOAD + NTHR - 1) / NTHR;
     __shared__ __attribute__((aligned(16))) float strip[2][S::SIZE];
@@ -163,7 +181,7 @@ k_small_fwd(const GemmArgs p) {
     const int col0 = blockIdx.y * SC_BN + nt * 32;
     float wr[KH];
 #pragma unroll
-    for (int s = 0; s < KH; ++s) wr[s] = p.B[(long)(s + h2 * KH) * p.ldb + col0 + l32];
+    for (int s = 0; s < KH; ++s) wr[s] = s + h2 * KH < KTOT ? p.B[(long)(s + h2 * KH) * p.ldb + col0 + l32] : 0.f;
     const int segs = g.Wo / P;
     const int ntiles = g.N * g.Ho * segs;
     const int abase = h2 * 2 * S::ROW + (sub * 32 + l32) * CI;
@@ -174,8 +192,8 @@ k_small_fwd(const GemmArgs p) {
     if (t >= ntiles) return;
     {
         const int row = t / segs, n = row / g.Ho;
-        strip_fetch<CI, P, NTHR>(p, n, row - n * g.Ho, (t - row * segs) * P, tid, pre);
-        strip_store<CI, P, NTHR>(strip[0], tid, pre);
+        strip_fetch<CI, P, NTHR, KW, ST>(p, n, row - n * g.Ho, (t - row * segs) * P, tid, pre);
+        strip_store<CI, P, NTHR, KW, ST>(strip[0], tid, pre);
     }
     __syncthreads();
     for (int it = 0; t < ntiles; t += gridDim.x, ++it) {
@@ -186,29 +204,29 @@ k_small_fwd(const GemmArgs p) {
         {   // (past the last tile: refetch this one -- straight-line code keeps the waits exact)
             const int tf = tn < ntiles ? tn : t;
             const int rown = tf / segs, n = rown / g.Ho;
-            strip_fetch<CI, P, NTHR>(p, n, rown - n * g.Ho, (tf - rown * segs) * P, tid, pre);
+            strip_fetch<CI, P, NTHR, KW, ST>(p, n, rown - n * g.Ho, (tf - rown * segs) * P, tid, pre);
         }
         const float *sb = strip[it & 1] + abase;
         f32x16 acc;
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-        // operands in chunks of SC_CH, the next chunk's LDS reads in flight under this chunk's MFMAs
-        float a[2][SC_CH];
+        // operands in chunks of CH, the next chunk's LDS reads in flight under this chunk's MFMAs
+        float a[2][CH];
 #pragma unroll
-        for (int u = 0; u < SC_CH; ++u) a[0][u] = sb[S::tap(u)];
+        for (int u = 0; u < CH; ++u) a[0][u] = sb[S::tap(u)];
 #pragma unroll
-        for (int c = 0; c < KH / SC_CH; ++c) {
-            if (c + 1 < KH / SC_CH) {
+        for (int c = 0; c < KH / CH; ++c) {
+            if (c + 1 < KH / CH) {
 #pragma unroll
-                for (int u = 0; u < SC_CH; ++u) a[(c + 1) & 1][u] = sb[S::tap((c + 1) * SC_CH + u)];
+                for (int u = 0; u < CH; ++u) a[(c + 1) & 1][u] = sb[S::tap((c + 1) * CH + u)];
             }
 #pragma unroll
-            for (int u = 0; u < SC_CH; ++u)
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c & 1][u], wr[c * SC_CH + u], acc, 0, 0, 0);
+            for (int u = 0; u < CH; ++u)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c & 1][u], wr[c * CH + u], acc, 0, 0, 0);
         }
         // the prefetched strip goes to LDS before this tile's stores are issued: waiting for the
         // loads then never waits for the stores (one vmcnt counts both)
-        strip_store<CI, P, NTHR>(strip[(it + 1) & 1], tid, pre);
+        strip_store<CI, P, NTHR, KW, ST>(strip[(it + 1) & 1], tid, pre);
         small_fwd_epilogue<XL>(p, acc, rbase, col0, stage[wid], lane, epi);
         __syncthreads();
     }
@@ -328,6 +346,8 @@ k_small_wgrad(const GemmArgs p, int rows_per_block) {
 bool small_conv_ok(const ConvGeom &g, int mode, int lda) {
     (void)lda;
     if (mode != MODE_FWD && mode != MODE_WGRAD) return false;
+    if (g.kh == 3 && g.kw == 3 && g.sh == 1 && g.sw == 1)   // VGG19 block1_conv1 (forward only)
+        return mode == MODE_FWD && g.Ci == 3 && g.Co % SC_BN == 0 && g.Wo % 32 == 0;
     return g.kh == 4 && g.kw == 4 && g.sh == 2 && g.sw == 2 && (g.Ci == 3 || g.Ci == 6) && g.Co % SC_BN == 0 &&
            g.Wo % 32 == 0;
 }
@@ -339,21 +359,23 @@ int small_wgrad_rows_per_block(const ConvGeom &g) {
     return std::max(1, (rows + want - 1) / want);
 }
 
-template <int CI, int P>
+template <int CI, int P, int KW = 4, int ST = 2>
 static void launch_small(int mode, const GemmArgs &a, int rows_per_block, hipStream_t s) {
     const ConvGeom &g = a.g;
     if (mode == MODE_WGRAD) {
-        const int rows = g.N * g.Ho;
-        const dim3 grid((unsigned)((rows + rows_per_block - 1) / rows_per_block), (unsigned)(g.Co / SC_BN));
-        hipLaunchKernelGGL((k_small_wgrad<CI, P>), grid, dim3(128 * ((16 * CI + 31) / 32)), 0, s, a, rows_per_block);
+        if constexpr (KW == 4) {
+            const int rows = g.N * g.Ho;
+            const dim3 grid((unsigned)((rows + rows_per_block - 1) / rows_per_block), (unsigned)(g.Co / SC_BN));
+            hipLaunchKernelGGL((k_small_wgrad<CI, P>), grid, dim3(128 * ((16 * CI + 31) / 32)), 0, s, a, rows_per_block);
+        }
     } else {
         // persistent: as many blocks as are resident at once (a second partial round of
         // grid-stride blocks would leave most CUs idle at the tail)
         static int resident = 0;
         if (!resident) {
             int per_cu = 0, dev = 0, cus = 256;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_small_fwd<CI, P, true>, 128 * (P / 32), 0) !=
-                    hipSuccess ||
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_small_fwd<CI, P, true, KW, ST>, 128 * (P / 32),
+                                                             0) != hipSuccess ||
                 per_cu < 1)
                 per_cu = 1;
             if (hipGetDevice(&dev) != hipSuccess ||
@@ -364,14 +386,17 @@ static void launch_small(int mode, const GemmArgs &a, int rows_per_block, hipStr
         const int ntiles = g.N * g.Ho * (g.Wo / P);
         const int cols = g.Co / SC_BN;
         const dim3 grid((unsigned)std::max(1, std::min(ntiles, resident / cols)), (unsigned)cols);
-        if (a.mz || a.beta != 0.f) hipLaunchKernelGGL((k_small_fwd<CI, P, true>), grid, dim3(128 * (P / 32)), 0, s, a);
-        else hipLaunchKernelGGL((k_small_fwd<CI, P, false>), grid, dim3(128 * (P / 32)), 0, s, a);
+        if (a.mz || a.beta != 0.f) hipLaunchKernelGGL((k_small_fwd<CI, P, true, KW, ST>), grid, dim3(128 * (P / 32)), 0, s, a);
+        else hipLaunchKernelGGL((k_small_fwd<CI, P, false, KW, ST>), grid, dim3(128 * (P / 32)), 0, s, a);
     }
 }
 
 void launch_small_conv(int mode, const GemmArgs &a, int rows_per_block, hipStream_t s) {
     const bool p64 = a.g.Wo % 64 == 0;
-    if (a.g.Ci == 3) {
+    if (a.g.kh == 3) {   // 3x3 stride 1, Ci 3 (small_conv_ok)
+        if (p64) launch_small<3, 64, 3, 1>(mode, a, rows_per_block, s);
+        else launch_small<3, 32, 3, 1>(mode, a, rows_per_block, s);
+    } else if (a.g.Ci == 3) {
         if (p64) launch_small<3, 64>(mode, a, rows_per_block, s);
         else launch_small<3, 32>(mode, a, rows_per_block, s);
     } else {

@@ -50,6 +50,9 @@ CASES = [
     ("small.rows", 3, 384, 64, 3, 64, 4, 2, "same", False, False),
     ("small.valid", 2, 66, 66, 6, 64, 4, 2, "valid", False, True),
     ("small.tlast", 1, 64, 64, 64, 3, 4, 2, "same", True, True),
+    # VGG19 block1_conv1's forward on the small-Cin kernel (3x3 stride 1, Cin 3)
+    ("small.k3", 2, 32, 64, 3, 64, 3, 1, "same", False, True),
+    ("small.k3c128", 3, 24, 32, 3, 128, 3, 1, "same", False, False),
 ]
 
 
