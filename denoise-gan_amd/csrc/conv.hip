@@ -940,6 +940,10 @@ struct OpPlan {
     int halo, htx, hty;
     // small-Cin 4x4 stride-2 kernels (conv_small.hip); WGRAD: conv-view output rows per block
     int small, small_rows;
+    // single-output-channel direct kernels (conv_co1.hip)
+    int co1;
+    // ConvT(3) forward on the fused MFMA + col2im kernel (conv_tlast.hip)
+    int tlast;
 };
 
 // A narrow op (GEMM N <= 8) recast as a 1x1-geometry MFMA GEMM plus a gather:
@@ -1051,6 +1055,14 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         pl.narrow = g.Co < 8;
     }
     pl.vec = cfg_vec(g, mode, 32);
+    if (co1_ok(g, mode) && math != DG_MATH_FP16 && !getenv("DG_NO_CO1")) {
+        // Co == 1 (PatchGAN last layer): direct kernels, exact fp32 FMA chains
+        pl.co1 = 1; pl.narrow = 0;
+        pl.splits = 1; pl.kchunk = pl.K; pl.mtiles = pl.ntiles = 1;
+        pl.slab_bytes = mode == MODE_WGRAD ? (size_t)co1_wgrad_blocks(g) * g.kh * g.kw * g.Ci * sizeof(float) : 0;
+        pl.ws_bytes = pl.gemm_bytes = pl.slab_bytes;
+        return pl;
+    }
     if (pl.narrow) {
         pl.splits = 1; pl.kchunk = pl.K; pl.ws_bytes = 0; pl.slab_bytes = 0;
         if (mode == MODE_WGRAD) {
@@ -1202,6 +1214,10 @@ static void plan_recast(dg_conv_desc_s *d, int op) {
         rc.slab_off = al256(rc.v_off + (size_t)P * ntap * 4);
     } else if (mode == MODE_DGRAD) {
         const int nv = ntap * g.Ci;
+        if (tlast_ok(g) && !getenv("DG_NO_TLAST")) {
+            d->plan[op].tlast = 1;
+            return;
+        }
         if (direct_dgrad_ok(g) && !getenv("DG_NO_DIRECT")) {
             d->plan[op].direct = 1;
             return;
@@ -1408,10 +1424,29 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
         DG_ARG(lda % 4 == 0 && ((uintptr_t)A & 15) == 0, "recast path needs lda%%4==0 and 16B-aligned A");
         return run_recast(d, op, a, (char *)ws, s);
     }
+    if (pl.co1) {
+        const ConvGeom &g = d->g;
+        if (mode == MODE_WGRAD) {
+            DG_ARG(lda % 4 == 0 && ((uintptr_t)A & 15) == 0, "Co == 1 filter gradient needs ldx %% 4 == 0 and 16B-aligned x");
+        } else {
+            DG_ARG(ldb <= 1 && ((uintptr_t)B & 15) == 0, "Co == 1 kernels need a dense 16B-aligned filter");
+            if (mode == MODE_FWD)
+                DG_ARG(lda % 4 == 0 && ((uintptr_t)A & 15) == 0, "Co == 1 forward needs ldx %% 4 == 0 and 16B-aligned x");
+            else
+                DG_ARG((long)g.N * g.H * g.W * g.Ci < (1L << 31), "operand larger than 2^31 elements");
+        }
+        launch_co1(mode, a, s);
+        DG_LAUNCHED("co1");
+        return DG_OK;
+    }
     if (pl.narrow) {
         if (mode == MODE_FWD) {
             hipLaunchKernelGGL(k_narrow_fwd, dim3(dg_cdiv(pl.M, 4)), dim3(256), 0, s, a);
             DG_LAUNCHED("narrow_fwd");
+        } else if (mode == MODE_DGRAD && pl.tlast && !a.mz && !a.mzp && a.lda % 4 == 0 &&
+                   ((((uintptr_t)a.A) | ((uintptr_t)a.B)) & 15) == 0) {
+            launch_tlast_fwd(a, s);
+            DG_LAUNCHED("tlast_fwd");
         } else if (mode == MODE_DGRAD && pl.direct && a.lda % 4 == 0 && ((uintptr_t)a.A & 15) == 0) {
             launch_direct_dgrad(a, s);
             DG_LAUNCHED("direct_dgrad");

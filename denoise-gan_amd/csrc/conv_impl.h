@@ -287,4 +287,12 @@ bool small_conv_ok(const ConvGeom &g, int mode, int lda);
 int small_wgrad_rows_per_block(const ConvGeom &g);
 void launch_small_conv(int mode, const GemmArgs &a, int rows_per_block, hipStream_t s);
 
+// single-output-channel FWD / DGRAD / WGRAD direct kernels (conv_co1.hip)
+bool co1_ok(const ConvGeom &g, int mode);
+int co1_wgrad_blocks(const ConvGeom &g);
+void launch_co1(int mode, const GemmArgs &a, hipStream_t s);
+// Conv2DTranspose(3) forward, 4x4 stride 2, conv-view Co 128: fused MFMA + col2im (conv_tlast.hip)
+bool tlast_ok(const ConvGeom &g);
+void launch_tlast_fwd(const GemmArgs &a, hipStream_t s);
+
 }  // namespace dg

@@ -53,6 +53,17 @@ CASES = [
     # VGG19 block1_conv1's forward on the small-Cin kernel (3x3 stride 1, Cin 3)
     ("small.k3", 2, 32, 64, 3, 64, 3, 1, "same", False, True),
     ("small.k3c128", 3, 24, 32, 3, 128, 3, 1, "same", False, False),
+    # single-output-channel direct input / filter gradients (conv_co1.hip): the
+    # bs16 PatchGAN last layer's geometry, stride 2 and 3x3 (generic tap loops),
+    # a wide row, and a 4-channel input (64 pixel lanes per block)
+    ("co1.full", 4, 31, 31, 512, 1, 4, 1, (1, 1, 1, 1), False, True),
+    ("co1.s2", 2, 19, 23, 64, 1, 4, 2, "same", False, True),
+    ("co1.k3", 2, 9, 300, 128, 1, 3, 1, "same", False, False),
+    ("co1.c4", 2, 11, 13, 4, 1, 4, 1, (1, 1, 1, 1), False, True),
+    # Conv2DTranspose(3) forward on the fused MFMA + col2im kernel (conv_tlast.hip):
+    # ragged 16 x 32 output tiles, and a 128 x 128 output
+    ("tlast.ragged", 2, 13, 21, 128, 3, 4, 2, "same", True, True),
+    ("tlast.big", 1, 64, 64, 128, 3, 4, 2, "same", True, True),
 ]
 
 
