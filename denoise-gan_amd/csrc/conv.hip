@@ -1146,17 +1146,24 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     const bool h22 = mode == MODE_DGRAD && g.kh == 4 && g.kw == 4 && g.sh == 2 && g.sw == 2 && g.Th == 2 &&
                      g.Tw == 2 && pl.K % 64 == 0 &&
                      4L * hp2 * wp2 >= 3L * ((hp2 + 7) / 8 * 8) * ((wp2 + 15) / 16 * 16) && !getenv("DG_NO_HALO2");
-    if (pl.x6 == 1 && (h33 || h22) && !getenv("DG_NO_HALO")) {
+    // (stride-1 4x4: the PatchGAN's 512-channel conv, input gradient only: its
+    // forward measured 0.709 vs 0.668 ms on the generic 128 x 256 tiles at bs16 x2,
+    // the input gradient 0.666 vs 0.690)
+    const bool h44 = mode == MODE_DGRAD && g.kh == 4 && g.kw == 4 && g.sh == 1 && g.sw == 1 &&
+                     pl.K % 256 == 0 && !getenv("DG_NO_HALO4");
+    if (pl.x6 == 1 && (h33 || h22 || h44) && !getenv("DG_NO_HALO")) {
         // each input pixel staged once per 16-channel chunk instead of once per tap
-        const int ntap = h33 ? 9 : 4;
+        const int ntap = h33 ? 9 : (h44 ? 16 : 4);
         int Hout, Wout;
         if (mode == MODE_FWD) { Hout = g.Ho; Wout = g.Wo; }
-        else if (h33) { Hout = g.H; Wout = g.W; }
+        else if (h33 || h44) { Hout = g.H; Wout = g.W; }
         else { Hout = (g.H + 1) / 2; Wout = (g.W + 1) / 2; }   // phase 0's grid, the largest
-        pl.halo = h33 ? 1 : 2;
+        pl.halo = h33 ? 1 : (h44 ? 4 : 2);
         pl.htx = (Wout + 15) / 16;
         pl.hty = (Hout + 7) / 8;
-        pl.cfg = pl.N > 64 ? 128 : 64;
+        // (4x4: BN 128 needs 93 KB of LDS -- one block per CU -- and measured 0.685 vs
+        // 0.666 ms for BN 64, which keeps two)
+        pl.cfg = pl.N > 64 && !h44 ? 128 : 64;
         pl.mtiles = g.N * pl.htx * pl.hty;
         pl.ntiles = (pl.N + pl.cfg - 1) / pl.cfg;
         // split-K over channel chunks (at least two per split) until ~2 blocks per CU
@@ -1543,7 +1550,7 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
         fastdiv_magic((unsigned)a.g.Ho, a.mg_ho, a.sh_ho);
         a.B = (const float *)pb; a.ldb = pl.x6_cb; a.b_bytes = (unsigned)(3 * pbs * 2);
         dim3 grid(pl.mtiles * pl.ntiles, pl.nphase * pl.splits);
-        if (pl.halo) launch_gemm_x6h(mode, pl.cfg, pl.halo == 2 ? 2 : 3, grid, a, pl.htx, pl.hty, s);
+        if (pl.halo) launch_gemm_x6h(mode, pl.cfg, pl.halo == 2 ? 2 : (pl.halo == 4 ? 4 : 3), grid, a, pl.htx, pl.hty, s);
         else launch_gemm_x6(mode, pl.cfg, grid, a, s);
         DG_LAUNCHED("conv_gemm_x6");
         return finish_splitk(mode, pl, a, s);

@@ -1,6 +1,8 @@
 // Halo-tiled bf16x6 implicit GEMM (gfx950) for
 //   KT = 3: stride-1 3x3 convolutions, forward and input gradient -- every
 //           VGG19 layer (pix2pix.py:53-67) and the 3x3 convs of the SR family;
+//   KT = 4: stride-1 4x4 convolutions -- the input gradient of the PatchGAN's
+//           ZeroPadding2D + Conv2D(512, 4) (pix2pix.py:206-208);
 //   KT = 2: the input gradient of stride-2 4x4 convolutions, one sub-pixel
 //           phase per grid slice (each phase is a stride-1 2x2 conv over dy)
 //           -- the U-Net's Conv2DTranspose forwards (pix2pix.py:128-142) and
@@ -141,7 +143,8 @@ __global__ void __launch_bounds__(256, 2)
 k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "forward or input gradient");
     static_assert(!POOL || MODE == MODE_FWD, "the pool epilogue is a forward epilogue");
-    static_assert(KT == 3 || (KT == 2 && MODE == MODE_DGRAD), "3x3 stride 1, or a stride-2 4x4 input-gradient phase");
+    static_assert(KT == 3 || (KT != 3 && MODE == MODE_DGRAD),
+                  "3x3 stride 1, or a stride-1 4x4 / stride-2 4x4-phase input gradient");
     using HG = HaloGeom<KT>;
     constexpr int NTAP = HG::NTAP;
     constexpr int NB = NTAP % 3 == 0 ? 3 : 4;   // weight K-tile buffers: a tap position owns one
@@ -413,6 +416,8 @@ void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int
     } else if (kt == 2) {
         if (bn == 128) DG_X6H(MODE_DGRAD, 128, false, 2);
         else DG_X6H(MODE_DGRAD, 64, false, 2);
+    } else if (kt == 4) {
+        DG_X6H(MODE_DGRAD, 64, false, 4);
     } else {
         if (bn == 128) DG_X6H(MODE_DGRAD, 128, false, 3);
         else DG_X6H(MODE_DGRAD, 64, false, 3);

@@ -11,7 +11,8 @@ import csv
 import sys
 from collections import defaultdict
 
-CONV = ("k_conv_gemm", "k_split3", "k_splitk_reduce", "k_narrow", "k_direct", "k_recast", "k_transpose", "k_colsum")
+CONV = ("k_conv_gemm", "k_split3", "k_splitk_reduce", "k_narrow", "k_direct", "k_recast", "k_transpose", "k_colsum",
+        "k_small", "k_co1", "k_tlast")
 
 
 def load(path, counter):

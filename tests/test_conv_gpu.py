@@ -141,6 +141,11 @@ HALO_CASES = [
     ("h2.odd", 2, 17, 15, 16, 32, 4, 2, "same", False, False),
     ("h2.splitk", 2, 8, 8, 512, 512, 4, 2, "same", False, False),
     ("h2.valid", 2, 20, 22, 32, 64, 4, 2, "valid", False, True),
+    # stride-1 4x4 (the PatchGAN's ZeroPadding2D + Conv2D(512, 4)): the input
+    # gradient on the 11 x 19 halo, ragged patches, 'same' (asymmetric pads)
+    ("h4.pad", 2, 18, 21, 32, 64, 4, 1, (1, 1, 1, 1), False, False),
+    ("h4.same", 3, 11, 17, 16, 32, 4, 1, "same", False, True),
+    ("h4.bn128", 2, 16, 16, 64, 256, 4, 1, (1, 1, 1, 1), False, False),
 ]
 
 
