@@ -989,9 +989,24 @@ static bool cfg_vec(const ConvGeom &g, int mode, int bk) {
 // table; returns the modelled time.  Modelled time of a candidate:
 //   rounds x (blocks per CU x per-block MFMA work) / (CU peak x occupancy efficiency)
 // + split-K slab traffic, where blocks per CU = min(resident limit, blocks / 256).
+// Plan features switched off for same-box A/B runs: DG_PLAN_DISABLE is a
+// comma-separated list of {shortk, small, co1, tlast, direct, halo, halo2, halo4}
+// (read when a descriptor is planned; unset in production runs)
+static bool plan_off(const char *feature) {
+    const char *list = getenv("DG_PLAN_DISABLE");
+    if (!list) return false;
+    const size_t n = strlen(feature);
+    for (const char *q = list; *q;) {
+        const char *e = strchr(q, ',');
+        const size_t len = e ? (size_t)(e - q) : strlen(q);
+        if (len == n && !strncmp(q, feature, n)) return true;
+        if (!e) break;
+        q = e + 1;
+    }
+    return false;
+}
+
 static double choose_tiles(OpPlan &pl, const TileCfg *cfgs, int ncfg, double peak, const char *force_env, void *) {
-    // DG_PLAN_V10=1: the v10 cost model (occupancy in blocks, 128x256 at eff 1.0), for A/B runs
-    static const bool v10 = getenv("DG_PLAN_V10") != nullptr;
     const double cu_flops = peak / 256.0;
     static const double occ_eff[] = {0.0, 0.62, 0.80, 0.88, 0.92};
     int forced = -1;
@@ -1003,7 +1018,7 @@ static double choose_tiles(OpPlan &pl, const TileCfg *cfgs, int ncfg, double pea
     // recast 0.241 -> 0.219); the MFMA-time model misses their prologue /
     // epilogue weight
     if (forced < 0 && cfgs == kCfgs && pl.K <= 256 && pl.N <= 128 && (long)pl.M * pl.nphase >= 65536 &&
-        !getenv("DG_PLAN_NO_SHORTK"))
+        !plan_off("shortk"))
         forced = 6;
     int best = -1; double best_t = 1e30; long best_splits = 1;
     for (int c = 0; c < ncfg; ++c) {
@@ -1019,8 +1034,8 @@ static double choose_tiles(OpPlan &pl, const TileCfg *cfgs, int ncfg, double pea
             long bpc = std::min<long>(t.bpc, (blocks + 255) / 256);
             double rounds = std::ceil((double)blocks / (256.0 * bpc));
             // occupancy in 4-wave units: an 8-wave block counts as two
-            const long occ = v10 ? bpc : std::min<long>(4, bpc * (t.wgm * t.wgn) / 4);
-            const double eff = (v10 && cfgs == kX6Cfgs && c == 5) ? 1.0 : t.eff;
+            const long occ = std::min<long>(4, bpc * (t.wgm * t.wgn) / 4);
+            const double eff = t.eff;
             double tc = rounds * bpc * 2.0 * t.bm * t.bn * kt_per * t.bk * eff / (cu_flops * occ_eff[occ]);
             double ts = splits > 1 ? (double)splits * pl.nphase * pl.M * pl.N * 8.0 / 5.0e12 + 2e-6 : 0.0;
             if (tc + ts < best_t) { best_t = tc + ts; best = c; best_splits = splits; }
@@ -1055,7 +1070,7 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         pl.narrow = g.Co < 8;
     }
     pl.vec = cfg_vec(g, mode, 32);
-    if (co1_ok(g, mode) && math != DG_MATH_FP16 && !getenv("DG_NO_CO1")) {
+    if (co1_ok(g, mode) && math != DG_MATH_FP16 && !plan_off("co1")) {
         // Co == 1 (PatchGAN last layer): direct kernels, exact fp32 FMA chains
         pl.co1 = 1; pl.narrow = 0;
         pl.splits = 1; pl.kchunk = pl.K; pl.mtiles = pl.ntiles = 1;
@@ -1077,7 +1092,7 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         pl.gemm_bytes = pl.ws_bytes;
         return pl;
     }
-    if (small_conv_ok(g, mode, 0) && !getenv("DG_NO_SMALL")) {
+    if (small_conv_ok(g, mode, 0) && !plan_off("small")) {
         // 3 / 6 input channels, 4x4 stride 2 (G.down1, D.down1, G.last's gradients): exact fp32
         // on the 32x32x2 MFMA whatever the math mode (neither low-precision path takes Cin 3 / 6)
         pl.small = 1;
@@ -1145,13 +1160,13 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     const int hp2 = (g.H + 1) / 2, wp2 = (g.W + 1) / 2;
     const bool h22 = mode == MODE_DGRAD && g.kh == 4 && g.kw == 4 && g.sh == 2 && g.sw == 2 && g.Th == 2 &&
                      g.Tw == 2 && pl.K % 64 == 0 &&
-                     4L * hp2 * wp2 >= 3L * ((hp2 + 7) / 8 * 8) * ((wp2 + 15) / 16 * 16) && !getenv("DG_NO_HALO2");
+                     4L * hp2 * wp2 >= 3L * ((hp2 + 7) / 8 * 8) * ((wp2 + 15) / 16 * 16) && !plan_off("halo2");
     // (stride-1 4x4: the PatchGAN's 512-channel conv, input gradient only: its
     // forward measured 0.709 vs 0.668 ms on the generic 128 x 256 tiles at bs16 x2,
     // the input gradient 0.666 vs 0.690)
     const bool h44 = mode == MODE_DGRAD && g.kh == 4 && g.kw == 4 && g.sh == 1 && g.sw == 1 &&
-                     pl.K % 256 == 0 && !getenv("DG_NO_HALO4");
-    if (pl.x6 == 1 && (h33 || h22 || h44) && !getenv("DG_NO_HALO")) {
+                     pl.K % 256 == 0 && !plan_off("halo4");
+    if (pl.x6 == 1 && (h33 || h22 || h44) && !plan_off("halo")) {
         // each input pixel staged once per 16-channel chunk instead of once per tap
         const int ntap = h33 ? 9 : (h44 ? 16 : 4);
         int Hout, Wout;
@@ -1170,7 +1185,7 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         const long nch = pl.K / (16 * ntap), blocks = (long)pl.mtiles * pl.ntiles * pl.nphase;
         long splits = 1;
         // (same-box A/B of the target: 256 -0.2%, 1024 -0.8% full step vs 512)
-        static const long target = getenv("DG_HALO_BLOCKS") ? atol(getenv("DG_HALO_BLOCKS")) : 512;
+        constexpr long target = 512;
         while (blocks * splits < target && splits * 4 <= nch) splits *= 2;
         const long cps = (nch + splits - 1) / splits;
         pl.kchunk = (int)(cps * 16 * ntap);
@@ -1221,11 +1236,11 @@ static void plan_recast(dg_conv_desc_s *d, int op) {
         rc.slab_off = al256(rc.v_off + (size_t)P * ntap * 4);
     } else if (mode == MODE_DGRAD) {
         const int nv = ntap * g.Ci;
-        if (tlast_ok(g) && !getenv("DG_NO_TLAST")) {
+        if (tlast_ok(g) && !plan_off("tlast")) {
             d->plan[op].tlast = 1;
             return;
         }
-        if (direct_dgrad_ok(g) && !getenv("DG_NO_DIRECT")) {
+        if (direct_dgrad_ok(g) && !plan_off("direct")) {
             d->plan[op].direct = 1;
             return;
         }

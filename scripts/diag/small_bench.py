@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Time the small-Cin conv ops (conv_small.hip) at the pix2pix bs16 geometry,
 with and without the bf16x6 output planes, against the generic GEMM path
-(DG_NO_SMALL=1 at plan time).  HIP events around N calls of each op.
+(DG_PLAN_DISABLE=small at plan time).  HIP events around N calls of each op.
 
     python scripts/diag/small_bench.py [--iters 20]
 """
@@ -38,9 +38,9 @@ def timeit(fn, iters):
 def run(iters, generic):
     from dgan import ops
     if generic:
-        os.environ["DG_NO_SMALL"] = "1"
+        os.environ["DG_PLAN_DISABLE"] = "small"
     else:
-        os.environ.pop("DG_NO_SMALL", None)
+        os.environ.pop("DG_PLAN_DISABLE", None)
     out = {}
     for name, N, H, W, Ci, Co, tr in LAYERS:
         d = ops.ConvDesc(N, H, W, Ci, Co, 4, 2, "same", tr)

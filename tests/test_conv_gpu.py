@@ -156,7 +156,7 @@ def test_conv_halo_kernel(case, monkeypatch):
     # every stride-1 3x3 bf16x6 FWD / DGRAD plan and every stride-2 4x4 DGRAD
     # runs on the halo kernel
     monkeypatch.setenv("DG_FORCE_X6CFG", "0")
-    monkeypatch.delenv("DG_NO_HALO", raising=False)
+    monkeypatch.delenv("DG_PLAN_DISABLE", raising=False)
     test_conv_layer(case, "bf16x6")
 
 
