@@ -990,7 +990,7 @@ static bool cfg_vec(const ConvGeom &g, int mode, int bk) {
 //   rounds x (blocks per CU x per-block MFMA work) / (CU peak x occupancy efficiency)
 // + split-K slab traffic, where blocks per CU = min(resident limit, blocks / 256).
 // Plan features switched off for same-box A/B runs: DG_PLAN_DISABLE is a
-// comma-separated list of {shortk, small, co1, tlast, direct, halo, halo2, halo4}
+// comma-separated list of {shortk, small, co1, tlast, direct, halo, halo2, halo4, xcd_phase}
 // (read when a descriptor is planned; unset in production runs)
 static bool plan_off(const char *feature) {
     const char *list = getenv("DG_PLAN_DISABLE");
@@ -1322,6 +1322,7 @@ static GemmArgs make_args(const ConvGeom &g, const OpPlan &pl, const float *A, i
     a.M = pl.M; a.N = pl.N; a.K = pl.K; a.kchunk = pl.kchunk; a.splits = pl.splits;
     a.mtiles = pl.mtiles; a.ntiles = pl.ntiles; a.nphase = pl.nphase;
     a.slab = (float *)slab;
+    a.xcd_plain = plan_off("xcd_phase");
     return a;
 }
 

@@ -47,6 +47,8 @@ struct GemmArgs {
     // instead of its fp32 values (dg_conv_bwd_data_xmask): act' of a
     // sign-determined activation from the sign of the hi plane, [pixel][3 mzpC]
     const unsigned short *mzp; int mzpC;
+    // 1: DGRAD phase blocks in the plain XCD order (A/B switch DG_PLAN_DISABLE=xcd_phase)
+    int xcd_plain;
 };
 
 // hi plane of element (pix, col) of a packed plane tensor, as a float
@@ -87,14 +89,23 @@ __device__ __forceinline__ float bload1(rsrc_t r, unsigned byte_off) {
 // n-tile fastest in the tile id, the n-tiles of one m-tile (which read the
 // same A rows) and neighbouring m-tiles (which share halo rows) then run on
 // one XCD and hit its L2 instead of each XCD fetching them.
-__device__ __forceinline__ void xcd_remap(int &y, int &x) {
-    const int nx = gridDim.x;
-    const int total = nx * gridDim.y;
+// y_fast: decode the contiguous ids with y fastest instead -- for a DGRAD
+// whose grid y runs over sub-pixel phases, the phases of one tile read the
+// same dy rows, so they then run back to back on one XCD (its L2 serves the
+// later ones) instead of on different XCDs that each fetch dy from HBM.
+__device__ __forceinline__ void xcd_remap(int &y, int &x, bool y_fast = false) {
+    const int nx = gridDim.x, ny = gridDim.y;
+    const int total = nx * ny;
     const int lin = blockIdx.y * nx + blockIdx.x;
     const int q = total >> 3, r = total & 7, xcd = lin & 7, idx = lin >> 3;
     const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
-    y = id / nx;
-    x = id - y * nx;
+    if (y_fast) {
+        x = id / ny;
+        y = id - x * ny;
+    } else {
+        y = id / nx;
+        x = id - y * nx;
+    }
 }
 
 // n / d = (umulhi(n, mul) + n) >> shr for 0 <= n < 2^31 (round-up magic number)

@@ -172,7 +172,10 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     const int wm = wid >> 1, wn = wid & 1;
 
     int zz, tile;
-    xcd_remap(zz, tile);
+    // (the 4 phases of a patch back to back on one XCD: down2 input gradient
+    // 0.270 -> 0.257 ms, up7 forward 0.457 -> 0.446 at bs16 x2; the generic
+    // kernel's deep-layer phases gained nothing)
+    xcd_remap(zz, tile, MODE == MODE_DGRAD && p.nphase > 1 && !p.xcd_plain);
     const int phase = zz / p.splits;
     const int split = zz - phase * p.splits;
     const int mt = tile / p.ntiles;
