@@ -536,7 +536,18 @@ class DiscriminatorPlan:
                                 if self.desc_half is not self.desc else self.planes)
         else:
             self.planes = self.planes_half = [None] * len(self.desc)
+        # G path (train_pix2pix.py:64): of dL/d D([inp, G(x)]) only the G(x) channels 3..5
+        # are used, so that input gradient runs as a Cin-3 conv over down1's filter slice
+        # w[:, :, 3:6, :] (copied per step) straight into dL/dG(x) (beta 1); per channel the
+        # sum is the one the 6-channel op computes
+        self.desc_g3 = None
+        if train and halves > 1 and self.specs[0][1] == 6:
+            co1 = self.specs[0][2]
+            self.desc_g3 = ConvDesc(N, H, W, 3, co1, 4, 2, "same")
+            self.desc_g3.label = "D.down1.g"
+            self.w_g3 = _empty((4, 4, 3, co1), device)
         self.ws_bytes = max([d.max_ws() for d in self.desc + self.desc_half] +
+                            ([self.desc_g3.max_ws()] if self.desc_g3 is not None else []) +
                             [ops.bn_workspace_bytes(N * d.Ho * d.Wo, d.Cout, halves) for d in self.desc])
 
     @property
@@ -587,12 +598,13 @@ class DiscriminatorPlan:
             h = z
 
     def backward(self, dlogits, slot=0, param_grads=True, beta=0.0, input_grad=None, input_beta=0.0, ws=None,
-                 on_grads_ready=None, half=None):
+                 on_grads_ready=None, half=None, input_from=0):
         """Backward through D.  half=None: over all halves (dlogits [halves*N]);
         half=h: over that half only (dlogits [N]), e.g. the G-path gradient
         through D(fake).  param_grads: accumulate weight grads (g = new +
         beta*g, summed over the halves covered); input_grad: NHWC view
-        receiving dL/d(input) (+input_beta*old)."""
+        receiving dL/d(input) (+input_beta*old); input_from=3: only the
+        input channels 3..5 (the generator output), input_grad has 3 channels."""
         A = self.arena
         hs = range(self.halves) if half is None else [half]
         desc = self.desc if half is None else self.desc_half
@@ -639,5 +651,9 @@ class DiscriminatorPlan:
                 dz = sub(self.dz[i - 1])
                 d.bwd_data(dy, A.param(f"{name}/kernel"), dz, ws=ws, planes=P)
                 dh = dz
+            elif input_grad is not None and input_from == 3:
+                co = self.specs[0][2]
+                ops.strided_copy(A.param(f"{name}/kernel").view(16, 6 * co)[:, 3 * co:], self.w_g3.view(16, 3 * co))
+                self.desc_g3.bwd_data(dy, self.w_g3, input_grad, beta=input_beta, ws=ws)
             elif input_grad is not None:
                 d.bwd_data(dy, A.param(f"{name}/kernel"), input_grad, beta=input_beta, ws=ws, planes=P)

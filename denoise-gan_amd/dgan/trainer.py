@@ -118,8 +118,11 @@ class Pix2PixTrainer:
         if sync:
             sync.start("D")
         # ---- gen_tape.gradient (train_pix2pix.py:64): through D(fake) into G(x)
-        D.backward(self.dzf_g, half=1, param_grads=False, input_grad=self.dinp, input_beta=0.0, ws=ws)
-        ops.accumulate(self.dinp[..., 3:], dgen, 1.0)
+        if D.desc_g3 is not None:   # dL/dG(x) += channels 3..5 of dL/d D([x, G(x)])
+            D.backward(self.dzf_g, half=1, param_grads=False, input_grad=dgen, input_beta=1.0, ws=ws, input_from=3)
+        else:
+            D.backward(self.dzf_g, half=1, param_grads=False, input_grad=self.dinp, input_beta=0.0, ws=ws)
+            ops.accumulate(self.dinp[..., 3:], dgen, 1.0)
         if self.content is not None:
             self.content.backward(dgen, beta=1.0, ws=ws)
         # both generator calls (G(x), G(y)) in one backward: their gradients sum
