@@ -1076,6 +1076,8 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         pl.splits = 1; pl.kchunk = pl.K; pl.mtiles = pl.ntiles = 1;
         pl.slab_bytes = mode == MODE_WGRAD ? (size_t)co1_wgrad_blocks(g) * g.kh * g.kw * g.Ci * sizeof(float) : 0;
         pl.ws_bytes = pl.gemm_bytes = pl.slab_bytes;
+        if (getenv("DG_PLAN_DEBUG"))
+            fprintf(stderr, "[dg plan] mode %d M=%d N=%d K=%d -> co1\n", mode, pl.M, pl.N, pl.K);
         return pl;
     }
     if (pl.narrow) {
@@ -1204,7 +1206,8 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     pl.gemm_bytes = pl.ws_bytes;
     if (getenv("DG_PLAN_DEBUG"))
         fprintf(stderr, "[dg plan] mode %d M=%d N=%d K=%d -> %s cfg %d splits %d\n", mode, pl.M, pl.N, pl.K,
-                pl.halo == 2 ? "x6h2" : pl.halo ? "x6h" : (pl.x6 == 2 ? "f16" : (pl.x6 ? "x6" : "fp32")), pl.cfg, pl.splits);
+                pl.halo == 2 ? "x6h2" : pl.halo == 4 ? "x6h4" : pl.halo ? "x6h" : (pl.x6 == 2 ? "f16" : (pl.x6 ? "x6" : "fp32")),
+                pl.cfg, pl.splits);
     return pl;
 }
 
@@ -1238,6 +1241,7 @@ static void plan_recast(dg_conv_desc_s *d, int op) {
         const int nv = ntap * g.Ci;
         if (tlast_ok(g) && !plan_off("tlast")) {
             d->plan[op].tlast = 1;
+            if (getenv("DG_PLAN_DEBUG")) fprintf(stderr, "[dg plan] mode %d -> tlast\n", mode);
             return;
         }
         if (direct_dgrad_ok(g) && !plan_off("direct")) {
