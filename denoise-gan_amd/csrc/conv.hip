@@ -723,6 +723,61 @@ static void launch_direct_dgrad(const GemmArgs &a, hipStream_t s) {
     else hipLaunchKernelGGL((k_direct_dgrad<6, 2, 2>), grid, dim3(256), 0, s, a, tx, ty);
 }
 
+// FWD with Co <= 4 and Ci % 4 == 0: one thread per output pixel, the filter in
+// LDS as [tap][ci/4][co][4] (16-byte broadcast reads), 16-byte x loads.
+// (The wave-per-pixel kernel above leaves half the lanes idle at Ci 32 and
+// spends a 6-step shuffle reduction per output: 0.86 ms for FastSRGAN's
+// 3-channel output conv at bs8 512x512.)
+constexpr int NFWD_WMAX = 8192;   // filter floats in LDS
+template <int CO>
+__global__ void __launch_bounds__(256)
+k_narrow_fwd_px(const GemmArgs p) {
+    __shared__ __attribute__((aligned(16))) float wl[NFWD_WMAX];
+    const ConvGeom &g = p.g;
+    const int ci4 = g.Ci / 4, ntap = g.kh * g.kw;
+    for (int e = threadIdx.x; e < ntap * g.Ci * CO; e += 256) {
+        // e = ((tap * ci4 + c4) * CO + co) * 4 + q  <-  w[tap][c4*4 + q][co]
+        const int q = e & 3, co = (e >> 2) % CO, rest = (e >> 2) / CO;
+        const int c4 = rest % ci4, tap = rest / ci4;
+        wl[e] = p.B[((long)tap * g.Ci + c4 * 4 + q) * CO + co];
+    }
+    __syncthreads();
+    for (int m = blockIdx.x * 256 + threadIdx.x; m < p.M; m += gridDim.x * 256) {
+        const int wo = m % g.Wo, t = m / g.Wo, ho = t % g.Ho, n = t / g.Ho;
+        float acc[CO];
+#pragma unroll
+        for (int co = 0; co < CO; ++co) acc[co] = 0.f;
+        for (int i = 0; i < g.kh; ++i) {
+            const int hi = ho * g.sh - g.pt + i;
+            if (hi < 0 || hi >= g.H) continue;
+            for (int j = 0; j < g.kw; ++j) {
+                const int wi = wo * g.sw - g.pl + j;
+                if (wi < 0 || wi >= g.W) continue;
+                const f32x4 *xp = reinterpret_cast<const f32x4 *>(p.A + ((long)(n * g.H + hi) * g.W + wi) * p.lda);
+                const f32x4 *wp = reinterpret_cast<const f32x4 *>(wl) + (long)(i * g.kw + j) * ci4 * CO;
+#pragma unroll 4
+                for (int c = 0; c < ci4; ++c) {
+                    const f32x4 x = xp[c];
+#pragma unroll
+                    for (int co = 0; co < CO; ++co) {
+                        const f32x4 w = wp[c * CO + co];
+                        acc[co] = fmaf(x[0], w[0], fmaf(x[1], w[1], fmaf(x[2], w[2], fmaf(x[3], w[3], acc[co]))));
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int co = 0; co < CO; ++co) {
+            float v = acc[co];
+            if (p.bias) v += p.bias[co];
+            v = epi_mask(p, m, co, act_fwd(v, p.act, p.alpha));
+            const long off = (long)m * p.ldc + co;
+            if (p.beta != 0.f) v += p.beta * p.C[off];
+            p.C[off] = v;
+        }
+    }
+}
+
 // WGRAD with Co < 8: partial[split][k=(tap,ci)][co].  Block (tap, 256-channel
 // chunk, pixel split): 256 threads = CL channels x PL = 256/CL pixel lanes
 // (CL = Ci rounded up to a power of two, at most 256), four pixels' loads in
@@ -1040,7 +1095,7 @@ static bool cfg_vec(const ConvGeom &g, int mode, int bk) {
 //   rounds x (blocks per CU x per-block MFMA work) / (CU peak x occupancy efficiency)
 // + split-K slab traffic, where blocks per CU = min(resident limit, blocks / 256).
 // Plan features switched off for same-box A/B runs: DG_PLAN_DISABLE is a
-// comma-separated list of {shortk, small, co1, tlast, direct, halo, halo2, halo4, xcd_phase}
+// comma-separated list of {shortk, small, co1, tlast, direct, halo, halo2, halo4, xcd_phase, narrow_px}
 // (read when a descriptor is planned; unset in production runs)
 static bool plan_off(const char *feature) {
     const char *list = getenv("DG_PLAN_DISABLE");
@@ -1517,7 +1572,16 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
         return DG_OK;
     }
     if (pl.narrow) {
-        if (mode == MODE_FWD) {
+        const ConvGeom &gg = d->g;
+        const bool px = mode == MODE_FWD && gg.Ci % 4 == 0 && a.lda % 4 == 0 && (((uintptr_t)a.A) & 15) == 0 &&
+                        (gg.Co == 1 || gg.Co == 3) && (long)gg.kh * gg.kw * gg.Ci * gg.Co <= NFWD_WMAX &&
+                        !plan_off("narrow_px");
+        if (px) {
+            const unsigned grid = (unsigned)std::min<long>(dg_cdiv(pl.M, 256), 8192);
+            if (gg.Co == 1) hipLaunchKernelGGL(k_narrow_fwd_px<1>, dim3(grid), dim3(256), 0, s, a);
+            else hipLaunchKernelGGL(k_narrow_fwd_px<3>, dim3(grid), dim3(256), 0, s, a);
+            DG_LAUNCHED("narrow_fwd_px");
+        } else if (mode == MODE_FWD) {
             hipLaunchKernelGGL(k_narrow_fwd, dim3(dg_cdiv(pl.M, 4)), dim3(256), 0, s, a);
             DG_LAUNCHED("narrow_fwd");
         } else if (mode == MODE_DGRAD && pl.tlast && !a.mz && !a.mzp && a.lda % 4 == 0 &&
