@@ -1664,10 +1664,8 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
         DG_ARG(ws != nullptr, "workspace pointer is NULL");
         void *pa = ws + pl.x6_a_off, *pb = ws + pl.x6_b_off;
         const int ldbw = (mode == MODE_DGRAD) ? a.g.Co : ldb;
-        launch_split_f16(A, lda, pl.x6_ra, pl.x6_ca, pa, s);
-        DG_LAUNCHED("split_f16_a");
-        launch_split_f16(B, ldbw, pl.x6_rb, pl.x6_cb, pb, s);
-        DG_LAUNCHED("split_f16_b");
+        launch_split_f16_pair(A, lda, pl.x6_ra, pl.x6_ca, pa, B, ldbw, pl.x6_rb, pl.x6_cb, pb, s);
+        DG_LAUNCHED("split_f16");
         a.A = (const float *)pa; a.lda = pl.x6_ca; a.a_bytes = (unsigned)(2 * pl.x6_ra * pl.x6_ca);
         a.B = (const float *)pb; a.ldb = pl.x6_cb; a.b_bytes = (unsigned)(2 * pl.x6_rb * pl.x6_cb);
         fastdiv_magic((unsigned)a.g.Wo, a.mg_wo, a.sh_wo);

@@ -292,6 +292,8 @@ void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int
 void launch_split3(const float *src, int ld, long rows, int C, unsigned short *dst, hipStream_t s);
 // the fp16 conv math (DG_MATH_FP16): one fp16 plane [rows][C] and its GEMM (kF16Cfgs)
 void launch_split_f16(const float *src, int ld, long rows, int C, void *dst, hipStream_t s);
+void launch_split_f16_pair(const float *a, int lda, long ra, int ca, void *da, const float *b, int ldb, long rb,
+                           int cb, void *db, hipStream_t s);
 void launch_gemm_f16(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s);
 // small-Cin 4x4 stride-2 FWD / WGRAD on fp32 MFMA (conv_small.hip)
 bool small_conv_ok(const ConvGeom &g, int mode, int lda);
