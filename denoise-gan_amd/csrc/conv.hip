@@ -729,6 +729,13 @@ static void launch_direct_dgrad(const GemmArgs &a, hipStream_t s) {
 // spends a 6-step shuffle reduction per output: 0.86 ms for FastSRGAN's
 // 3-channel output conv at bs8 512x512.)
 constexpr int NFWD_WMAX = 8192;   // filter floats in LDS
+// Smallest output (pixels) the thread-per-pixel kernel takes; below it the
+// wave-per-pixel k_narrow_fwd runs.  Set from a same-box A/B of the two
+// kernels over the SR family's narrow layers (scripts/diag/narrow_ab.py,
+// profiles/r3/narrow_ab.txt): px is 8.5x faster at M 2.1M (FastSRGAN's output
+// conv), 5.5x at 295K, 1.3x at 16K, 1.1x at 8K; the two tie at the launch
+// floor below (M 1152: 14.0 vs 13.8 us, M 64: 16.0 vs 14.3 us).
+constexpr long NFWD_PX_MIN_M = 4096;
 template <int CO>
 __global__ void __launch_bounds__(256)
 k_narrow_fwd_px(const GemmArgs p) {
@@ -1590,10 +1597,7 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
         const ConvGeom &gg = d->g;
         const bool px = mode == MODE_FWD && gg.Ci % 4 == 0 && a.lda % 4 == 0 && (((uintptr_t)a.A) & 15) == 0 &&
                         (gg.Co == 1 || gg.Co == 3) && (long)gg.kh * gg.kw * gg.Ci * gg.Co <= NFWD_WMAX &&
-                        pl.M >= 65536 && !plan_off("narrow_px");
-        // (large outputs only -- FastSRGAN's 512x512 output conv: the per-thread order
-        // changes the sums' rounding, and the autoencoder's bs4 golden fixture,
-        // unconditioned by the GPU's activation decisions, sees that through near-ties)
+                        pl.M >= NFWD_PX_MIN_M && !plan_off("narrow_px");
         if (px) {
             const unsigned grid = (unsigned)std::min<long>(dg_cdiv(pl.M, 256), 8192);
             if (gg.Co == 1) hipLaunchKernelGGL(k_narrow_fwd_px<1>, dim3(grid), dim3(256), 0, s, a);

@@ -1,7 +1,8 @@
 """tf.train.Checkpoint / CheckpointManager stand-ins (train_pix2pix.py:156-164, :176-178).
 
 A checkpoint is one .npz holding every tracked network's variables, BN moving
-statistics and Adam slots (m, v, iterations) under Keras-style names."""
+statistics and Adam slots (m, v, iterations; with mixed_float16 also the dynamic
+loss scale: scale, good steps) under Keras-style names."""
 import glob
 import os
 import re
@@ -26,6 +27,9 @@ class Checkpoint:
                 out[f"{key}/m"] = arena.m.cpu().numpy()
                 out[f"{key}/v"] = arena.v.cpu().numpy()
                 out[f"{key}/iterations"] = arena.iterations.cpu().numpy()
+                ls = getattr(obj, "_ls", None)
+                if ls is not None:   # LossScaleOptimizer: current_loss_scale, good_steps (+ flag)
+                    out[f"{key}/loss_scale"] = ls.cpu().numpy()
         return out
 
     def save(self, file_prefix):
@@ -51,6 +55,9 @@ class Checkpoint:
                     arena.m.copy_(torch.as_tensor(sub["m"]))
                     arena.v.copy_(torch.as_tensor(sub["v"]))
                     arena.iterations.copy_(torch.as_tensor(sub["iterations"]))
+                ls = getattr(obj, "_ls", None)
+                if ls is not None and "loss_scale" in sub:
+                    ls.copy_(torch.as_tensor(sub["loss_scale"]))
         m = re.search(r"-(\d+)\.npz$", path)
         if m:
             self.save_counter = int(m.group(1))

@@ -210,6 +210,10 @@ class SRTrainer:
             sync.finish()
         if self.ls_g is not None:
             # LossScaleOptimizer.apply_gradients: are the (all-reduced) gradients finite?
+            # The flag is re-armed here, so a step(apply=False) that saw inf / nan (and ran
+            # no loss_scale_update) does not leave it set for the next step.
+            ops.fill(self.ls_g[2:3], 1.0)
+            ops.fill(self.ls_d[2:3], 1.0)
             ops.check_finite(self.G.arena.grad, self.ls_g)
             ops.check_finite(self.D.arena.grad, self.ls_d)
         # ---- apply_gradients (train_srgan.py:113-114) -----------------------

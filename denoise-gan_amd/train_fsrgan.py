@@ -97,6 +97,8 @@ def parse_args(argv=None):
     args.ckpt = bool(args.ckpt)
     args.fp16 = bool(args.fp16)
     args.model_name = args.model_name + f"_{args.scale}x_{args.jpeg_quality}q"
+    if args.fp16:   # train_fsrgan.py:313-315: fp16 runs export under their own name
+        args.model_name = args.model_name + "_fp16"
     return args
 
 

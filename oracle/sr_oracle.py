@@ -409,8 +409,9 @@ def _train_step(st, x, y, apply, dec):
     disc = bce_logits(zr, 1.0) + bce_logits(zf, 0.0)
     if st.kind == "fsrgan":
         disc = 0.5 * disc
-    dgen = torch.autograd.grad(gen_loss, gen, retain_graph=True)[0]
-    gG = torch.autograd.grad(gen_loss, list(PG.values()), retain_graph=True)   # at G's loss scale
+    # one backward pass for d gen_loss / d G(x) and the G gradients (at G's loss scale)
+    gs = torch.autograd.grad(gen_loss, [gen] + list(PG.values()), retain_graph=True)
+    dgen, gG = gs[0], gs[1:]
     if st.fp16:
         FP16 = {"scale": st.ls["D"][0]}
     gD = torch.autograd.grad(disc, list(PD.values()))

@@ -3,7 +3,7 @@
 CPU oracles (oracle/p2p_oracle.py, oracle/sr_oracle.py) -- test
 infrastructure, run in the build container, never on the GPU box.
 
-    python scripts/gen_golden.py [p2p_bs16] [srgan_bs32] [ae_bs4]
+    python scripts/gen_golden.py [p2p_bs16] [srgan_bs32] [ae_bs4] [fsrgan_bs8]
 
 The reference ships no tests, fixtures or golden vectors and TensorFlow is
 not installable here, so these digests of the oracle at
@@ -31,6 +31,8 @@ Cases (BASELINE.json configs):
               content loss                                           configs[2]
   ae_bs4      conv autoencoder 64x64 grayscale (replicated to 3 channels),
               bs4, VGG19 content loss                                configs[0]
+  fsrgan_bs8  FastSRGAN 128 -> 512, bs8 (the per-GPU shard of the 8-GPU
+              config), VGG19 content loss at 512x512                 configs[4]
 """
 import json
 import math
@@ -60,6 +62,7 @@ CASES = {
                           content=0),
     "srgan_bs32": dict(kind="srgan", N=32, H=96, scale=4, seed=21, batch_seeds=(50, 51), lr=1e-3),
     "ae_bs4": dict(kind="autoencoder", N=4, H=64, scale=1, seed=21, batch_seeds=(50, 51), lr=1e-3, gray=True),
+    "fsrgan_bs8": dict(kind="fsrgan", N=8, H=512, scale=4, seed=21, batch_seeds=(60, 61), lr=1e-3),
 }
 
 
@@ -145,6 +148,9 @@ def gen_sr(cfg):
     kind = cfg["kind"]
     if kind == "srgan":
         gg = zoo.srgan_generator(scale=cfg["scale"])
+        dg = zoo.sr_discriminator(df=32)
+    elif kind == "fsrgan":
+        gg = zoo.fsrgan_generator(gf=32, n_blocks=6)
         dg = zoo.sr_discriminator(df=32)
     else:
         gg = zoo.autoencoder_generator()

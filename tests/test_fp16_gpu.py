@@ -91,7 +91,8 @@ def _synthetic(N, H, scale, seed):
 LS = 2.0 ** 8
 
 
-def _run(model_cls, kind, N, H, **kw):
+def _run(model_cls, kind, N, H, ls=LS, **kw):
+    """ls: the initial loss scale of both optimizers (None: Keras' 2^15 as constructed)."""
     m = model_cls(Args(crop_size=H, **kw))
     assert m.fp16 and m.generator.conv_math == "fp16"
     PG, PD = m.generator.arena.export(), m.discriminator.arena.export()
@@ -101,20 +102,22 @@ def _run(model_cls, kind, N, H, **kw):
     # Keras' initial 2^15 overflows fp16 in these randomly initialised discriminators' backward
     # (Keras would halve it over the first steps, as test_dynamic_loss_scale_skips_and_halves
     # checks); compare at a scale that keeps every fp16 operand finite
-    for t in m.loss_scales:
-        t[0] = LS
+    if ls is not None:
+        for t in m.loss_scales:
+            t[0] = ls
+    LS0 = float(m.loss_scales[0][0])
     loss = tr.step(torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV), apply=False)
     torch.cuda.synchronize()
     got = loss.cpu().double().numpy()
     gen = tr.gen_output.detach().cpu().numpy()
     # the arenas hold the loss-scaled gradients (Adam unscales them); the scales the step
-    # used are 2^15, untouched by apply=False
+    # used are untouched by apply=False, and both gradient sets were finite at them
     sg, sd = (float(t[0]) for t in m.loss_scales)
-    assert sg == sd == LS and float(m.loss_scales[0][2]) == 1.0 and float(m.loss_scales[1][2]) == 1.0
+    assert sg == sd == LS0 and float(m.loss_scales[0][2]) == 1.0 and float(m.loss_scales[1][2]) == 1.0
     gG = {n: m.generator.arena.grad_of(n).cpu().double().numpy() / sg for n, _ in m.generator.arena.var_list}
     gD = {n: m.discriminator.arena.grad_of(n).cpu().double().numpy() / sd for n, _ in m.discriminator.arena.var_list}
     st = S.SRState(kind, PG, PD, PV, scale=4, lr=1e-3, fp16=True)
-    st.ls = {"G": [LS, 0], "D": [LS, 0]}
+    st.ls = {"G": [LS0, 0], "D": [LS0, 0]}
     emu = S.train_step(st, x, y, apply=False)
     ref = S.train_step(S.SRState(kind, PG, PD, PV, scale=4, lr=1e-3), x, y, apply=False)
     assert np.allclose(got, emu["losses"], rtol=1e-3, atol=1e-6), (got, emu["losses"])
@@ -135,6 +138,10 @@ def _run(model_cls, kind, N, H, **kw):
             noise = float(np.linalg.norm(g_ref - fp64[n])) / den
             worst = max(worst, err / max(noise, 1e-2))
             assert err <= max(2.0 * noise, 2e-2), f"{label} {n}: rel-L2 {err:.3e}, fp16 noise {noise:.3e}"
+            # elementwise: within 1e-4 + 2x the emulation's own max-abs distance from fp64
+            emax = float(np.abs(grads[n] - g_ref).max())
+            nmax = float(np.abs(g_ref - fp64[n]).max())
+            assert emax <= 1e-4 + 2.0 * nmax, f"{label} {n}: max-abs {emax:.3e}, fp16 noise {nmax:.3e}"
     # mixed precision vs the fp64 step
     assert abs(psnr(gen, y) - psnr(ref["gen"], y)) < 0.05
     assert np.allclose(got, ref["losses"], rtol=1e-2, atol=1e-5), (got, ref["losses"])
@@ -153,6 +160,29 @@ def test_srgan_fp16_step_matches_mixed_float16_oracle():
 def test_fsrgan_fp16_step_matches_mixed_float16_oracle():
     from fsrgan import FastSRGAN
     _run(FastSRGAN, "fsrgan", N=2, H=64)
+
+
+@gpu
+@pytest.mark.timeout(600)
+def test_srgan_full_config_fp16_at_keras_initial_scale():
+    """BASELINE configs[2] in SRGAN's default mode (train_srgan.py:275 fp16=1, the mode
+    `bench.py --model srgan` times): 24 -> 96, 16 residual blocks, bs32, VGG19 content, both
+    optimizers at Keras' initial dynamic scale 2^15 (srgan.py:64-67).  At this size the scaled
+    fp16 backward stays finite at 2^15 on the device and in the emulation alike, so nothing is
+    halved; the gradients are compared at that scale, then two applied steps each count one
+    good step at 2^15 (DynamicLossScale.update) -- the halving path is
+    test_dynamic_loss_scale_skips_and_halves."""
+    from srgan import SRGAN
+    m = _run(SRGAN, "srgan", N=32, H=96, ls=None)
+    assert m.gen_optimizer.loss_scale == 2.0 ** 15 and m.disc_optimizer.loss_scale == 2.0 ** 15
+    x, y = _synthetic(32, 96, 4, seed=62)
+    tr = m.trainer(x.shape, y.shape)
+    for _ in range(2):
+        tr.step(torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV))
+    torch.cuda.synchronize()
+    for t in m.loss_scales:
+        assert float(t[0]) == 2.0 ** 15 and float(t[1]) == 2.0 and float(t[2]) == 1.0
+    assert int(m.generator.arena.iterations.item()) == 2
 
 
 @gpu
@@ -187,3 +217,60 @@ def test_dynamic_loss_scale_skips_and_halves():
     assert float(lsg[0]) == 2 * LS and float(lsg[1]) == 0.0
     assert m.gen_optimizer.loss_scale == 2 * LS
     assert np.isfinite(m.generator.arena.data.cpu().numpy()).all()
+
+
+@gpu
+def test_nonfinite_apply_false_step_does_not_stick():
+    """A step(apply=False) that sees inf / nan runs no loss_scale_update; the next
+    step re-arms the finite flag itself, so a finite apply=True step after it is
+    applied and counted (not skipped, not halved)."""
+    from srgan import SRGAN
+    m = SRGAN(Args(crop_size=32, vgg_width=8))
+    x, y = _synthetic(2, 32, 4, seed=5)
+    tr = m.trainer(x.shape, y.shape)
+    xd, yd = torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV)
+    lsg, lsd = m.loss_scales
+    lsd[0] = LS
+    lsg[0] = 3.0e38
+    tr.step(xd, yd, apply=False)
+    torch.cuda.synchronize()
+    assert float(lsg[2]) == 0.0 and float(lsg[0]) == float(np.float32(3.0e38))
+    lsg[0] = LS
+    before = m.generator.arena.data.clone()
+    tr.step(xd, yd)
+    torch.cuda.synchronize()
+    assert int(m.generator.arena.iterations.item()) == 1
+    assert not torch.equal(m.generator.arena.data, before)
+    assert float(lsg[0]) == LS and float(lsg[1]) == 1.0 and float(lsg[2]) == 1.0
+
+
+def _srgan_main_args(tmp, epochs, retrain):
+    import train_srgan
+    a = train_srgan.parse_args([])
+    assert a.fp16 and a.model_name.endswith("_fp16")      # train_srgan.py:312-314
+    a.model_dir, a.logdir = str(tmp / "models"), str(tmp / "logs")
+    a.batch_size, a.epochs, a.retrain, a.synthetic, a.steps_per_epoch = 2, epochs, retrain, 1, 2
+    a.crop_size, a.save_iter, a.seed, a.vgg_width = 32, 2, 3, 8
+    return a
+
+
+@gpu
+def test_srgan_fp16_resume_restores_loss_scale(tmp_path):
+    """train_srgan.main with its default fp16=1: 2 epochs == 1 epoch + checkpoint +
+    --retrain + 1 epoch, bit for bit, including each optimizer's dynamic loss scale
+    (Keras' LossScaleOptimizer checkpoints current_loss_scale and good_steps).
+    The initial 2^15 overflows these fresh discriminators, so the scales move."""
+    import train_srgan
+    full = train_srgan.main(_srgan_main_args(tmp_path / "a", 2, 0))
+    train_srgan.main(_srgan_main_args(tmp_path / "b", 1, 0))
+    resumed = train_srgan.main(_srgan_main_args(tmp_path / "b", 1, 1))
+    torch.cuda.synchronize()
+    assert resumed.iterations == full.iterations == 4
+    for la, lb in zip(full.loss_scales, resumed.loss_scales):
+        assert torch.equal(la, lb), (la, lb)
+    assert any(float(t[0]) != 2.0 ** 15 or float(t[1]) != 0.0 for t in full.loss_scales)
+    for na, nb in ((full.generator, resumed.generator), (full.discriminator, resumed.discriminator)):
+        for t in ("data", "m", "v", "iterations"):
+            assert torch.equal(getattr(na.arena, t), getattr(nb.arena, t)), t
+    name = full.model_name
+    assert name.endswith("_fp16") and (tmp_path / "b" / "models" / f"{name}.npz").exists()

@@ -7,7 +7,7 @@ import pytest
 
 from golden_util import batch, load, weights_crc
 
-CASES = ["p2p_bs16", "p2p_bs16_core", "srgan_bs32", "ae_bs4"]
+CASES = ["p2p_bs16", "p2p_bs16_core", "srgan_bs32", "ae_bs4", "fsrgan_bs8"]
 
 
 @pytest.mark.parametrize("case", CASES)
@@ -24,7 +24,8 @@ def test_fixture_loads_and_weights_match(case):
         assert weights_crc(G, meta["gvars"]) == meta["wcrc_G"]
         assert weights_crc(D, meta["dvars"]) == meta["wcrc_D"]
     else:
-        gg = zoo.srgan_generator(scale=meta["scale"]) if meta["kind"] == "srgan" else zoo.autoencoder_generator()
+        gg = {"srgan": lambda: zoo.srgan_generator(scale=meta["scale"]),
+              "fsrgan": lambda: zoo.fsrgan_generator(gf=32, n_blocks=6)}.get(meta["kind"], zoo.autoencoder_generator)()
         dg = zoo.sr_discriminator(df=32)
         G = init_graph_variables(gg, meta["seed"])
         D = init_graph_variables(dg, meta["seed"] + 1)

@@ -63,3 +63,38 @@ def test_plan_kernel_family(layer, expect):
         got.setdefault(mode, kind)
     for mode, kind in expect.items():
         assert got.get(mode) == kind, (layer, got)
+
+
+CSRC = os.path.join(REPO, "denoise-gan_amd", "csrc")
+
+
+def test_no_plan_choice_justified_by_a_fixture():
+    """Kernel selection follows same-box timing, never a test outcome: no csrc/ source may
+    justify a plan choice by a golden fixture (the fixtures are drift pins, tests/test_golden_gpu.py)."""
+    bad = []
+    for f in sorted(os.listdir(CSRC)):
+        with open(os.path.join(CSRC, f)) as fh:
+            for i, line in enumerate(fh, 1):
+                if re.search(r"golden|fixture", line, re.I):
+                    bad.append(f"{f}:{i}: {line.strip()}")
+    assert not bad, bad
+
+
+def test_size_thresholds_cite_a_measurement():
+    """Every named size threshold of the planner (constexpr ... _MIN_ / _MAX_ in csrc/) is preceded by
+    a comment citing the A/B that set it, and the cited profile is committed."""
+    for f in sorted(os.listdir(CSRC)):
+        lines = open(os.path.join(CSRC, f)).read().split("\n")
+        for i, line in enumerate(lines):
+            m = re.match(r"\s*constexpr\s+\w+\s+(\w*_MIN_\w*|\w*_MAX_\w*)\s*=", line)
+            if not m:
+                continue
+            j = i - 1
+            block = []
+            while j >= 0 and lines[j].strip().startswith("//"):
+                block.append(lines[j])
+                j -= 1
+            text = " ".join(block)
+            assert re.search(r"A/B|measured|sweep", text), (f, m.group(1))
+            for ref in re.findall(r"profiles/[\w/.\-]+", text):
+                assert os.path.exists(os.path.join(REPO, ref.rstrip(".,)"))), (f, m.group(1), ref)

@@ -252,6 +252,12 @@ SR_CONVS = [
     ("ae.d5", 4, 16, 16, 32, 64, 3, 1, True, None),
     ("ae.d6", 4, 16, 16, 64, 64, 3, 2, True, None),
     ("odd.7x3", 3, 7, 3, 128, 64, 3, 1, True, None),
+    # thread-per-pixel narrow forward (k_narrow_fwd_px, Co 1 / 3, Ci % 4 == 0) at the sizes
+    # FastSRGAN's 512x512 output conv runs it (M >= 65536), a ragged M and ldx > Ci
+    ("px.fsrgan_out", 1, 512, 512, 32, 3, 3, 1, True, None),
+    ("px.co1.ragged", 1, 257, 263, 32, 1, 3, 1, True, 36),
+    ("px.co3.1x1.ld", 2, 200, 171, 64, 3, 1, 1, True, 68),
+    ("px.co3.small", 3, 9, 13, 32, 3, 3, 1, True, 40),
 ]
 
 
@@ -489,6 +495,17 @@ def test_autoencoder_full_config_parity():
     content loss, mask-conditioned, max-abs 1e-4."""
     from autoencoder import Autoencoder
     _run_step_parity(Autoencoder, "autoencoder", N=4, H=64, scale=1, conditioned=True, gray=True)
+
+
+@gpu
+@pytest.mark.timeout(900)
+def test_fsrgan_full_size_parity():
+    """BASELINE configs[4] at its per-GPU image size: FastSRGAN 128 -> 512, VGG19 content loss at
+    512x512, mask-conditioned, max-abs 1e-4.  bs2 (M = 524,288 output pixels) already fires every
+    size-dependent plan of the bs8 shard: the narrow output conv, the depthwise kernels at 128x128x192,
+    the 512x512 discriminator and VGG19 layers."""
+    from fsrgan import FastSRGAN
+    _run_step_parity(FastSRGAN, "fsrgan", N=2, H=512, scale=4, conditioned=True)
 
 
 @gpu

@@ -32,7 +32,8 @@ def psnr(img, ref):
     return 10 * math.log10(1.0 / mse)
 
 
-def _compare_grads(arena, ref, label, tol=1e-4):
+def _compare_grads(arena, ref, label, tol=1e-4, rtol=0.0):
+    """max-abs `tol` (+ rtol x the variable's max |g|) per variable."""
     worst = (0.0, None, 0.0)
     for name, g_ref in ref.items():
         g = arena.grad_of(name).detach().double().cpu().numpy()
@@ -40,7 +41,8 @@ def _compare_grads(arena, ref, label, tol=1e-4):
         rel = err / (float(np.abs(g_ref).max()) + 1e-30)
         if err > worst[0]:
             worst = (err, name, rel)
-        assert err < tol, f"{label} {name}: max-abs grad diff {err:.3e} (rel {rel:.3e})"
+        t = tol + rtol * float(np.abs(g_ref).max())
+        assert err < t, f"{label} {name}: max-abs grad diff {err:.3e} (rel {rel:.3e}) > {t:.3e}"
     return worst
 
 
@@ -159,19 +161,42 @@ def test_generator_inference_uses_moving_stats():
     assert np.abs(got.cpu().numpy() - ref).max() < 1e-5
 
 
+# fp32 noise floor of the content-on step (scripts/diag/fp32_floor.py ->
+# profiles/r3/fp32_floor_full_width.txt): the torch fp32 CPU restatement, on the fp64
+# run's own decisions, misses fp64 by up to 1.9e-4 x max|g| at full width (G down1/kernel
+# 3.2e-4 of max 2.8: the content gradient -- loss ~48 with the seeded stand-in VGG19 --
+# reaches G.down1 through the VGG19 and U-Net backward).  1e-4 absolute is below what fp32
+# arithmetic holds there; gradients get 1e-4 + 1e-4 x max|g| (44 of 45 G variables and all of
+# D still meet 1e-4 on the fp32 CPU restatement itself).
+FP32_FLOOR_REL = 1e-4
+
+VGG_PARITY_CASES = [
+    # (id, G/D width divisor, VGG19 width divisor, dropout rate)
+    ("narrow", 16, 8, 0.0),
+    # the headline networks at full width (54.4M-parameter G, full VGG19): the full-width VGG19
+    # input-gradient tiles and G's backward under the content gradient, dropout and identity on
+    ("full_width", 1, 1, 0.5),
+]
+
+
 @gpu
-def test_step_parity_with_vgg_content():
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("case", VGG_PARITY_CASES, ids=[c[0] for c in VGG_PARITY_CASES])
+def test_step_parity_with_vgg_content(case):
     """The reference-equivalent step incl. the VGG19 content loss (pix2pix.py:45-51, :87; seeded
-    stand-in VGG weights, channel width /8 to keep the fp64 CPU oracle fast) vs the torch fp64
-    autograd restatement (oracle/torch_p2p.py + oracle/sr_oracle.py's VGG19), mask-conditioned:
-    the oracle takes the HIP path's ReLU / LeakyReLU / max-pool decisions (G(x), G(y), D real,
-    D fake, VGG19 on G(x) and on y; oracle/decisions.py), each override audited to be a near-tie.
-    Losses to 1e-5, |dPSNR| < 0.01 dB, every G and D gradient to max-abs 1e-4."""
+    stand-in VGG weights) vs the torch fp64 autograd restatement (oracle/torch_p2p.py +
+    oracle/sr_oracle.py's VGG19), bs2 256x256, identity pass on, mask-conditioned: the oracle takes
+    the HIP path's ReLU / LeakyReLU / max-pool decisions (G(x), G(y), D real, D fake, VGG19 on G(x)
+    and on y; oracle/decisions.py), each override audited to be a near-tie.
+    Losses to 1e-5, |dPSNR| < 0.01 dB, every G and D gradient to max-abs 1e-4 + 1e-4 x max|g|
+    (north star 1e-4, plus the measured fp32 noise floor FP32_FLOOR_REL)."""
     from gpu_decisions import audit_ok, discriminator_decisions, generator_decisions, graph_decisions, to_oracle
     from oracle import torch_p2p as T
     from pix2pix import Pix2Pix
-    width, seed = 16, 5
-    m = Pix2Pix(Args(width=width, seed=seed, dropout_rate=0.0, content_loss=1, vgg_width=8))
+    _, width, vgg_width, drop = case
+    seed, drop_seed = 5, 4
+    m = Pix2Pix(Args(width=width, seed=seed, dropout_rate=drop, dropout_seed=drop_seed, content_loss=1,
+                     vgg_width=vgg_width))
     G = m.generator.arena.export()
     D = m.discriminator.arena.export()
     PV = m.vgg.arena.export()
@@ -185,13 +210,14 @@ def test_step_parity_with_vgg_content():
            "Vsr": graph_decisions(tr.content.fplan, 0, rows=slice(0, N)),
            "Vhr": graph_decisions(tr.content.fplan, 0, rows=slice(N, 2 * N))}
     dec = {k: to_oracle(v) for k, v in dec.items()}
-    vals, gG, gD, gen_ref = T.step_grads(G, D, x, y, width=width, drop_rate=0.0, PV=PV, dec=dec)
+    vals, gG, gD, gen_ref = T.step_grads(G, D, x, y, width=width, drop_rate=drop, drop_seed=drop_seed, PV=PV,
+                                         dec=dec)
     n_over = audit_ok(dec, 1e-5, "pix2pix+vgg")
     got = loss.cpu().double().numpy()
     assert got[4] > 0.0
     assert np.allclose(got, np.array(vals), rtol=1e-5, atol=1e-7), (got, vals)
     gen = tr.gen_output.cpu().numpy()
     assert abs(psnr(gen, y) - psnr(gen_ref, y)) < 0.01
-    wg = _compare_grads(m.generator.arena, gG, "G")
-    wd = _compare_grads(m.discriminator.arena, gD, "D")
-    print(f"pix2pix+VGG parity: worst G {wg}, worst D {wd}, overridden decisions {n_over}")
+    wg = _compare_grads(m.generator.arena, gG, "G", rtol=FP32_FLOOR_REL)
+    wd = _compare_grads(m.discriminator.arena, gD, "D", rtol=FP32_FLOOR_REL)
+    print(f"pix2pix+VGG parity ({case[0]}): worst G {wg}, worst D {wd}, overridden decisions {n_over}")
