@@ -32,10 +32,10 @@ Prints ONE JSON line (rank 0).  Extra fields:
                 one step / summed conv launch time measured with HIP events on
                 the launching stream, vs the peak of the conv math in use
                 (bf16x6: bf16 dense peak / 6 = 419.4 TF/s; fp32: 157.3 TF/s);
-                `traffic` = HBM bytes per step of those launches from the
-                committed rocprofv3 PMC profile named in `traffic_source`
-                (scripts/gpu_pmc_bench.sh re-measures it; --pmc-leg runs the
-                two PMC passes as child processes and reports them live)
+                `traffic` = HBM bytes per step of those launches, measured
+                live: two rocprofv3 --pmc child runs (FETCH_SIZE, WRITE_SIZE)
+                of the same workload (N=1, rank 0; --no-pmc-leg falls back to
+                the committed profile when its csrc_sha matches this tree)
   cpu_baseline  the CPU restatement of the same step (oracle/, torch fp32
                 autograd) timed on this box's host cores, rank 0, N=1 only,
                 bounded sample of the same workload
@@ -104,8 +104,9 @@ def main():
     ap.add_argument("--no-content", action="store_true", help="drop the VGG19 content term")
     ap.add_argument("--no-core", action="store_true", help="skip the content-free secondary measurement")
     ap.add_argument("--profile-only", action="store_true", help="skip roofline/cpu legs (for rocprofv3 runs)")
-    ap.add_argument("--pmc-leg", action="store_true",
-                    help="measure roofline.traffic now: two rocprofv3 --pmc child runs (FETCH_SIZE, WRITE_SIZE)")
+    ap.add_argument("--no-pmc-leg", action="store_true",
+                    help="do not measure roofline.traffic live (two rocprofv3 --pmc child runs, FETCH_SIZE and "
+                         "WRITE_SIZE, N=1 rank 0 only); use the committed profile if it matches the sources")
     ap.add_argument("--fp16", type=int, default=None,
                     help="SR family: mixed_float16 (fp16 conv GEMMs + dynamic loss scale); default: the "
                          "reference driver's (train_srgan.py fp16=1, the others 0)")
@@ -247,7 +248,7 @@ def main():
         step_flops = conv_flops
         achieved = conv_flops / (conv_ms * 1e-3)
         peak = {"bf16x6": X6_PEAK, "fp16": BF16_MFMA_PEAK}.get(conv_math, FP32_MFMA_PEAK)
-        traffic, source = traffic_of(args, wl, content, batch, rank, world) if not fp16 else (None, None)
+        traffic, source = traffic_of(args, wl, content, batch, rank, world)
         roofline = {"bound": "mfma", "achieved": round(achieved / 1e12, 2), "peak": round(peak / 1e12, 1),
                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
                     "traffic_unit": "HBM bytes per step over the conv-engine launches (rocprofv3 PMC "
@@ -323,7 +324,7 @@ def main():
 
 def traffic_of(args, wl, content, batch, rank, world):
     """(HBM bytes per step of the conv engine, where the number came from)."""
-    if args.pmc_leg and rank == 0 and world == 1:
+    if not args.no_pmc_leg and rank == 0 and world == 1:
         try:
             return pmc_leg(args, batch)
         except Exception as e:  # report and fall back to the committed profile
@@ -333,9 +334,13 @@ def traffic_of(args, wl, content, batch, rank, world):
         return None, None
     with open(path) as f:
         t = json.load(f)
+    sys.path.insert(0, os.path.join(REPO, "scripts"))
+    from pmc_traffic import csrc_sha
+    if t.get("csrc_sha") != csrc_sha():   # measured on other kernels: not this tree's traffic
+        return None, f"profiles/{wl['traffic']} was measured on other library sources; no live PMC leg"
     return (round(t["conv_engine_bytes_per_step"], 0),
-            f"profiles/{wl['traffic']}: {t.get('profile', '?')} (commit {t.get('commit', '?')}), "
-            f"{t.get('method', '')}")
+            f"profiles/{wl['traffic']}: {t.get('profile', '?')} (commit {t.get('commit', '?')}, csrc_sha "
+            f"{t['csrc_sha']} = this tree), {t.get('method', '')}")
 
 
 def pmc_leg(args, batch):
@@ -360,7 +365,9 @@ def pmc_leg(args, batch):
         csvs.append(found[0])
     # the child runs warmup + timed steps + nothing else: count every launch, divide by the step count
     t = summarise(csvs[0], csvs[1], steps + 2)
-    return round(t["conv_engine_bytes_per_step"], 0), f"live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child runs ({t['method']})"
+    return (round(t["conv_engine_bytes_per_step"], 0),
+            f"live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child runs of this workload in this bench run, "
+            f"csrc_sha {t['csrc_sha']} ({t['method']})")
 
 
 def cpu_baseline(args, wl, batch, content):

@@ -1138,6 +1138,9 @@ static double choose_tiles(OpPlan &pl, const TileCfg *cfgs, int ncfg, double pea
     static const double occ_eff[] = {0.0, 0.62, 0.80, 0.88, 0.92};
     int forced = -1;
     if (const char *f = getenv(force_env)) forced = atoi(f);
+    // DG_FORCE_SPLITS: split-K count for sweeps (scripts/diag/deep_sweep.py); unset in production
+    long fsplits = 0;
+    if (const char *f = getenv("DG_FORCE_SPLITS")) fsplits = atol(f);
     // fp32 GEMMs with a short K over many rows (the Cin 3/6 layers and the
     // G.last recast: K 27..128, M >= 64K): per-layer sweep on MI355X (bs32)
     // has the 128x64 BK-16 three-blocks-per-CU tile fastest on every one
@@ -1155,7 +1158,8 @@ static double choose_tiles(OpPlan &pl, const TileCfg *cfgs, int ncfg, double pea
         long mt = (pl.M + t.bm - 1) / t.bm, nt = (pl.N + t.bn - 1) / t.bn;
         long tiles = mt * nt * pl.nphase;
         long ktiles = (pl.K + t.bk - 1) / t.bk;
-        for (long splits = 1; splits <= std::max<long>(1, ktiles / 4); splits *= 2) {
+        for (long splits = 1; splits <= std::max<long>(1, fsplits > 0 ? ktiles : ktiles / 4); splits *= 2) {
+            if (fsplits > 0 && splits != fsplits) continue;
             long kt_per = (ktiles + splits - 1) / splits;
             long blocks = tiles * splits;
             long bpc = std::min<long>(t.bpc, (blocks + 255) / 256);
@@ -1166,7 +1170,7 @@ static double choose_tiles(OpPlan &pl, const TileCfg *cfgs, int ncfg, double pea
             double tc = rounds * bpc * 2.0 * t.bm * t.bn * kt_per * t.bk * eff / (cu_flops * occ_eff[occ]);
             double ts = splits > 1 ? (double)splits * pl.nphase * pl.M * pl.N * 8.0 / 5.0e12 + 2e-6 : 0.0;
             if (tc + ts < best_t) { best_t = tc + ts; best = c; best_splits = splits; }
-            if (blocks >= 1024) break;
+            if (blocks >= 1024 && fsplits <= 0) break;
         }
     }
     if (best < 0) best = 0;

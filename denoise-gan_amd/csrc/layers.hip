@@ -135,15 +135,34 @@ __global__ void __launch_bounds__(256) k_prelu_bwd(long npix, ShufGeom g, const 
     }
 }
 
-// d alpha[c] = sum_q sum_r part[r][q*C + c]  (+ beta * dalpha)
+// d alpha[c] = sum_r sum_q part[r][q*C + c]  (+ beta * dalpha).  Block = 16 channels x
+// 16 row lanes: lane rl sums rows r = rl, rl + 16, ... (the B*B sub-positions of a row
+// together, eight rows' loads in flight), then the lanes are added in lane order.
+// (One thread per channel summing all R*BB partials serially: 357 us per call in
+// FastSRGAN, one block for its 32 channels.)
 __global__ void __launch_bounds__(256) k_prelu_alpha_final(const float *part, int R, int C, int BB, float *dalpha,
                                                           float beta) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
+    __shared__ float red[256];
+    const int cl = threadIdx.x & 15, rl = threadIdx.x >> 4;
+    const int c = blockIdx.x * 16 + cl;
     float s = 0.f;
-    for (int r = 0; r < R; ++r)
-        for (int q = 0; q < BB; ++q) s += part[(long)r * C * BB + q * C + c];
-    dalpha[c] = beta != 0.f ? s + beta * dalpha[c] : s;
+    if (c < C) {
+        const long rs = (long)C * BB;
+#pragma unroll 8
+        for (int r = rl; r < R; r += 16) {
+            const float *pp = part + (long)r * rs + c;
+            float t = pp[0];
+            for (int q = 1; q < BB; ++q) t += pp[q * C];
+            s += t;
+        }
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    if (rl == 0 && c < C) {
+        float t = red[cl];
+        for (int l = 1; l < 16; ++l) t += red[l * 16 + cl];
+        dalpha[c] = beta != 0.f ? t + beta * dalpha[c] : t;
+    }
 }
 
 // --------------------------------------------------------------------------
@@ -395,102 +414,134 @@ __global__ void __launch_bounds__(256) k_upsample_relu_bwd(int N, int H, int W, 
 // kernel k[i][j][c] (Keras [3,3,C,1]).
 //   y[n,h,w,c] = b[c] + sum_ij x[n,h+i-1,w+j-1,c] k[i,j,c]
 // --------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_dw_fwd(int N, int H, int W, int C, const float *__restrict__ x, int ldx,
-                                               const float *__restrict__ k, const float *__restrict__ b,
-                                               float *__restrict__ y, int ldy) {
-    const long total = (long)N * H * W * C;
-    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-        const long p = e / C;
-        const int c = (int)(e - p * C);
-        const int w = (int)(p % W);
-        const long t = p / W;
-        const int h = (int)(t % H);
-        const long n = t / H;
-        float s = 0.f;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int hh = h + i - 1;
-            if (hh < 0 || hh >= H) continue;
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                const int ww = w + j - 1;
-                if (ww < 0 || ww >= W) continue;
-                s = fmaf(x[((n * H + hh) * W + ww) * ldx + c], k[(i * 3 + j) * C + c], s);
-            }
-        }
-        y[p * ldy + c] = s + (b ? b[c] : 0.f);
-    }
+struct DwPlan {
+    int RB, nrc, R;   // rows per chunk, row chunks per image, partial rows
+};
+static DwPlan dw_plan(int N, int H, int W, int C) {
+    DwPlan p;
+    const long cols = (long)dg_cdiv(C, 64) * dg_cdiv(W, 4) * N;
+    int nrc = (int)std::max<long>(1, std::min<long>(H, dg_cdiv(2048, cols)));   // >= 2048 blocks
+    p.RB = dg_cdiv(H, nrc);
+    p.nrc = dg_cdiv(H, p.RB);
+    p.R = N * p.nrc * dg_cdiv(W, 4);
+    return p;
 }
 
-__global__ void __launch_bounds__(256) k_dw_bwd_data(int N, int H, int W, int C, const float *__restrict__ dy,
-                                                    int lddy, const float *__restrict__ k, float *__restrict__ dx,
-                                                    int lddx, float beta) {
-    const long total = (long)N * H * W * C;
-    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-        const long p = e / C;
-        const int c = (int)(e - p * C);
-        const int w = (int)(p % W);
-        const long t = p / W;
-        const int h = (int)(t % H);
-        const long n = t / H;
-        float s = 0.f;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            const int hh = h - i + 1;  // output row that reads x[h] through tap i
-            if (hh < 0 || hh >= H) continue;
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                const int ww = w - j + 1;
-                if (ww < 0 || ww >= W) continue;
-                s = fmaf(dy[((n * H + hh) * W + ww) * lddy + c], k[(i * 3 + j) * C + c], s);
-            }
-        }
-        float *o = dx + p * lddx + c;
-        *o = beta != 0.f ? s + beta * *o : s;
-    }
-}
-
-// partial sums of dk[i][j][c] (9 taps) and db[c] over a row chunk: part[r][10][C]
-__global__ void __launch_bounds__(256) k_dw_bwd_filter(int N, int H, int W, int C, const float *__restrict__ x,
-                                                      int ldx, const float *__restrict__ dy, int lddy, long rows,
-                                                      float *__restrict__ part) {
-    const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+// Forward and input gradient: block (64 channels, 4 image columns, one image and a chunk
+// of RB rows, the geometry of k_dw_bwd_filter below); wave v walks column w down the rows
+// with the 3x3 input window in registers (three new loads per output, no index divisions).
+// The taps are summed in the (i, j) order of the direct formula, padding taps as x * 0.
+// (Thread per (pixel, channel) with nine loads and a div/mod chain per output: 184 /
+// 165 us per call at FastSRGAN's 8 x 128 x 128 x 192, ~4.6x the HBM time.)
+template <bool BWD>
+__global__ void __launch_bounds__(256) k_dw_rows(int N, int H, int W, int C, const float *__restrict__ src, int lds,
+                                                const float *__restrict__ k, const float *__restrict__ b,
+                                                float *__restrict__ dst, int ldd, float beta, int RB, int nrc) {
+    const int cl = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int c = blockIdx.x * 64 + cl;
-    const long M = (long)N * H * W;
-    const long r0 = (long)blockIdx.y * rows;
-    const long r1 = std::min<long>(M, r0 + rows);
+    const int w = blockIdx.y * 4 + wv;
+    if (c >= C || w >= W) return;
+    const int n = blockIdx.z / nrc, rc = blockIdx.z - n * nrc;
+    const int h0 = rc * RB, h1 = min(H, h0 + RB);
+    float kk[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) kk[q] = k[q * C + c];
+    const float bias = (!BWD && b) ? b[c] : 0.f;
+    const bool okl = w > 0, okr = w + 1 < W;
+    const float *sb = src + (long)n * H * W * lds + c;
+    float *db = dst + (long)n * H * W * ldd + c;
+    auto ld3 = [&](int h, float &v0, float &v1, float &v2) {
+        const bool okh = h >= 0 && h < H;
+        const float *r = sb + ((long)h * W + w) * lds;
+        v0 = okh && okl ? r[-lds] : 0.f;
+        v1 = okh ? r[0] : 0.f;
+        v2 = okh && okr ? r[lds] : 0.f;
+    };
+    // window rows: u = row h-1, m = row h, d = row h+1 (columns w-1, w, w+1)
+    float u0, u1, u2, m0, m1, m2;
+    ld3(h0 - 1, u0, u1, u2);
+    ld3(h0, m0, m1, m2);
+    for (int h = h0; h < h1; ++h) {
+        float d0, d1, d2;
+        ld3(h + 1, d0, d1, d2);
+        float s = 0.f;
+        if (!BWD) {   // y[h][w] = sum_ij x[h+i-1][w+j-1] k[i][j]
+            s = fmaf(u0, kk[0], s); s = fmaf(u1, kk[1], s); s = fmaf(u2, kk[2], s);
+            s = fmaf(m0, kk[3], s); s = fmaf(m1, kk[4], s); s = fmaf(m2, kk[5], s);
+            s = fmaf(d0, kk[6], s); s = fmaf(d1, kk[7], s); s = fmaf(d2, kk[8], s);
+            db[((long)h * W + w) * ldd] = s + bias;
+        } else {      // dx[h][w] = sum_ij dy[h-i+1][w-j+1] k[i][j]
+            s = fmaf(d2, kk[0], s); s = fmaf(d1, kk[1], s); s = fmaf(d0, kk[2], s);
+            s = fmaf(m2, kk[3], s); s = fmaf(m1, kk[4], s); s = fmaf(m0, kk[5], s);
+            s = fmaf(u2, kk[6], s); s = fmaf(u1, kk[7], s); s = fmaf(u0, kk[8], s);
+            float *o = db + ((long)h * W + w) * ldd;
+            *o = beta != 0.f ? s + beta * *o : s;
+        }
+        u0 = m0; u1 = m1; u2 = m2;
+        m0 = d0; m1 = d1; m2 = d2;
+    }
+}
+
+// Filter gradient of the depthwise conv: partial sums of dk[i][j][c] (9 taps) and
+// db[c] per block, part[r][10][C].  Block (64 channels, 4 image columns, one image and
+// a chunk of RB rows): wave v walks column w down the rows, keeping the 3x3 window of x
+// around (h, w) in registers -- per output pixel three new x loads (row h+1) and one dy
+// load, 256 B per wave instruction, no index divisions -- and the four waves' sums are
+// added in wave order.  (The row-chunk version -- one thread per (channel, pixel), nine
+// x loads and a div/mod chain per pixel -- took 267 us per call at FastSRGAN's
+// 8 x 128 x 128 x 192.)
+__global__ void __launch_bounds__(256) k_dw_bwd_filter(int N, int H, int W, int C, const float *__restrict__ x,
+                                                      int ldx, const float *__restrict__ dy, int lddy, int RB,
+                                                      int nrc, float *__restrict__ part) {
+    const int cl = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int c = blockIdx.x * 64 + cl;
+    const int w = blockIdx.y * 4 + wv;
+    const int n = blockIdx.z / nrc, rc = blockIdx.z - n * nrc;
+    const int h0 = rc * RB, h1 = min(H, h0 + RB);
     float acc[10];
 #pragma unroll
     for (int q = 0; q < 10; ++q) acc[q] = 0.f;
-    if (c < C) {
-        for (long p = r0 + rl; p < r1; p += 4) {
-            const int w = (int)(p % W);
-            const long t = p / W;
-            const int h = (int)(t % H);
-            const long n = t / H;
-            const float g = dy[p * lddy + c];
+    if (c < C && w < W) {
+        const bool okl = w > 0, okr = w + 1 < W;
+        const float *xb = x + (long)n * H * W * ldx + c;
+        const float *gb = dy + (long)n * H * W * lddy + c;
+        auto ldx3 = [&](int h, float &v0, float &v1, float &v2) {
+            const bool okh = h >= 0 && h < H;
+            const float *r = xb + ((long)h * W + w) * ldx;
+            v0 = okh && okl ? r[-ldx] : 0.f;
+            v1 = okh ? r[0] : 0.f;
+            v2 = okh && okr ? r[ldx] : 0.f;
+        };
+        float a0, a1, a2, b0, b1, b2;
+        ldx3(h0 - 1, a0, a1, a2);
+        ldx3(h0, b0, b1, b2);
+        for (int h = h0; h < h1; ++h) {
+            float c0, c1, c2;
+            ldx3(h + 1, c0, c1, c2);
+            const float g = gb[((long)h * W + w) * lddy];
+            acc[0] = fmaf(a0, g, acc[0]);
+            acc[1] = fmaf(a1, g, acc[1]);
+            acc[2] = fmaf(a2, g, acc[2]);
+            acc[3] = fmaf(b0, g, acc[3]);
+            acc[4] = fmaf(b1, g, acc[4]);
+            acc[5] = fmaf(b2, g, acc[5]);
+            acc[6] = fmaf(c0, g, acc[6]);
+            acc[7] = fmaf(c1, g, acc[7]);
+            acc[8] = fmaf(c2, g, acc[8]);
             acc[9] += g;
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                const int hh = h + i - 1;
-                if (hh < 0 || hh >= H) continue;
-#pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    const int ww = w + j - 1;
-                    if (ww < 0 || ww >= W) continue;
-                    acc[i * 3 + j] = fmaf(x[((n * H + hh) * W + ww) * ldx + c], g, acc[i * 3 + j]);
-                }
-            }
+            a0 = b0; a1 = b1; a2 = b2;
+            b0 = c0; b1 = c1; b2 = c2;
         }
     }
     __shared__ float red[4][10][64];
 #pragma unroll
-    for (int q = 0; q < 10; ++q) red[rl][q][cl] = acc[q];
+    for (int q = 0; q < 10; ++q) red[wv][q][cl] = acc[q];
     __syncthreads();
     if (c < C) {
-        for (int q = rl; q < 10; q += 4) {
+        const long r = (long)blockIdx.z * gridDim.y + blockIdx.y;
+        for (int q = wv; q < 10; q += 4) {
             const float s = red[0][q][cl] + red[1][q][cl] + red[2][q][cl] + red[3][q][cl];
-            part[((long)blockIdx.y * 10 + q) * C + c] = s;
+            part[(r * 10 + q) * C + c] = s;
         }
     }
 }
@@ -728,7 +779,7 @@ int dg_prelu_bwd(int N, int H, int W, int C, int block, const float *y, int ldy,
                        dy, lddy, beta, rp.rows, (float *)ws);
     DG_LAUNCHED("prelu_bwd");
     if (dalpha) {
-        hipLaunchKernelGGL(dg::k_prelu_alpha_final, dim3(dg_cdiv(C, 256)), dim3(256), 0, s, (const float *)ws, rp.R, C,
+        hipLaunchKernelGGL(dg::k_prelu_alpha_final, dim3(dg_cdiv(C, 16)), dim3(256), 0, s, (const float *)ws, rp.R, C,
                            block * block, dalpha, alpha_beta);
         DG_LAUNCHED("prelu_alpha_final");
     }
@@ -871,8 +922,8 @@ int dg_upsample2_relu_bwd(int N, int H, int W, int C, const float *x, int ldx, c
 int dg_dwconv3_workspace_size(int N, int H, int W, int C, size_t *bytes) {
     DG_ARG(bytes, "NULL argument");
     DG_ARG(N > 0 && H > 0 && W > 0 && C > 0, "bad shape");
-    dg::RedPlan rp = dg::red_plan((long)N * H * W);
-    *bytes = (size_t)rp.R * 10 * C * sizeof(float) + 256;
+    const dg::DwPlan dp = dg::dw_plan(N, H, W, C);
+    *bytes = (size_t)dp.R * 10 * C * sizeof(float) + 256;
     return DG_OK;
 }
 
@@ -880,8 +931,9 @@ int dg_dwconv3_fwd(int N, int H, int W, int C, const float *x, int ldx, const fl
                    int ldy, dg_stream_t stream) {
     DG_ARG(x && k && y, "NULL tensor");
     DG_ARG(N > 0 && H > 0 && W > 0 && C > 0 && ldx >= C && ldy >= C, "bad shape");
-    hipLaunchKernelGGL(dg::k_dw_fwd, dim3(dg::lgrid((long)N * H * W * C)), dim3(256), 0, (hipStream_t)stream, N, H, W,
-                       C, x, ldx, k, bias, y, ldy);
+    const dg::DwPlan dp = dg::dw_plan(N, H, W, C);
+    hipLaunchKernelGGL(dg::k_dw_rows<false>, dim3(dg_cdiv(C, 64), dg_cdiv(W, 4), N * dp.nrc), dim3(256), 0,
+                       (hipStream_t)stream, N, H, W, C, x, ldx, k, bias, y, ldy, 0.f, dp.RB, dp.nrc);
     DG_LAUNCHED("dwconv_fwd");
     return DG_OK;
 }
@@ -890,8 +942,10 @@ int dg_dwconv3_bwd_data(int N, int H, int W, int C, const float *dy, int lddy, c
                         float beta, dg_stream_t stream) {
     DG_ARG(dy && k && dx, "NULL tensor");
     DG_ARG(N > 0 && H > 0 && W > 0 && C > 0 && lddy >= C && lddx >= C, "bad shape");
-    hipLaunchKernelGGL(dg::k_dw_bwd_data, dim3(dg::lgrid((long)N * H * W * C)), dim3(256), 0, (hipStream_t)stream, N, H,
-                       W, C, dy, lddy, k, dx, lddx, beta);
+    const dg::DwPlan dp = dg::dw_plan(N, H, W, C);
+    hipLaunchKernelGGL(dg::k_dw_rows<true>, dim3(dg_cdiv(C, 64), dg_cdiv(W, 4), N * dp.nrc), dim3(256), 0,
+                       (hipStream_t)stream, N, H, W, C, dy, lddy, k, (const float *)nullptr, dx, lddx, beta, dp.RB,
+                       dp.nrc);
     DG_LAUNCHED("dwconv_bwd_data");
     return DG_OK;
 }
@@ -903,14 +957,14 @@ int dg_dwconv3_bwd_filter(int N, int H, int W, int C, const float *x, int ldx, c
     size_t need;
     dg_dwconv3_workspace_size(N, H, W, C, &need);
     DG_ARG(ws_bytes >= need, "workspace too small");
-    dg::RedPlan rp = dg::red_plan((long)N * H * W);
+    const dg::DwPlan dp = dg::dw_plan(N, H, W, C);
     hipStream_t s = (hipStream_t)stream;
     float *part = (float *)ws;
-    hipLaunchKernelGGL(dg::k_dw_bwd_filter, dim3(dg_cdiv(C, 64), rp.R), dim3(256), 0, s, N, H, W, C, x, ldx, dy, lddy,
-                       rp.rows, part);
+    hipLaunchKernelGGL(dg::k_dw_bwd_filter, dim3(dg_cdiv(C, 64), dg_cdiv(W, 4), N * dp.nrc), dim3(256), 0, s, N, H, W,
+                       C, x, ldx, dy, lddy, dp.RB, dp.nrc, part);
     DG_LAUNCHED("dwconv_bwd_filter");
-    // dk[q][c] (q = tap i*3+j) and dbias[c] (q = 9): ordered sums over the row chunks
-    hipLaunchKernelGGL(dg::k_rows_final10, dim3(10, dg_cdiv(C, 16)), dim3(256), 0, s, (const float *)part, rp.R, C, dk,
+    // dk[q][c] (q = tap i*3+j) and dbias[c] (q = 9): ordered sums over the blocks' partials
+    hipLaunchKernelGGL(dg::k_rows_final10, dim3(10, dg_cdiv(C, 16)), dim3(256), 0, s, (const float *)part, dp.R, C, dk,
                        dbias, beta);
     DG_LAUNCHED("dwconv_filter_final");
     return DG_OK;

@@ -2,7 +2,11 @@
 """Per-layer conv table of one pix2pix bs16 training step (HIP events per conv
 call, dgan.ops.ConvProfile), grouped by layer geometry and op, as a markdown
 table: GFLOP, ms, TF/s (fp32-equivalent) and the fraction of the bf16x6
-basis (bf16 dense peak / 6 = 419.4 TF/s).
+basis (bf16 dense peak / 6 = 419.4 TF/s), plus each op's own roofline: the
+larger of its MFMA time at the basis and its HBM time for the algorithmic fp32
+operand bytes (x, w, y once each) at 8 TB/s -- narrow layers (Cin 3/6, Cout
+1/3) and the deep U-Net layers (M = 32..512 rows) are HBM- or weight-bound,
+and `roof` is their fraction of that bound.
 
     python scripts/layer_table.py [--content 0|1] [--steps 3] > profiles/...md
 """
@@ -17,6 +21,7 @@ sys.path[:0] = [os.path.join(REPO, "denoise-gan_amd"), REPO]
 import torch  # noqa: E402
 
 BASIS = 2516.6e12 / 6
+HBM = 8.0e12
 
 
 def main():
@@ -35,7 +40,7 @@ def main():
     for _ in range(3):
         tr.step(x, y)
     torch.cuda.synchronize()
-    agg = defaultdict(lambda: [0, 0.0, 0.0])
+    agg = defaultdict(lambda: [0, 0.0, 0.0, 0.0])
     for _ in range(a.steps):
         with ops.ConvProfile() as prof:
             tr.step(x, y)
@@ -47,16 +52,21 @@ def main():
             agg[key][0] += 1
             agg[key][1] += r["flops"]
             agg[key][2] += r["ms"]
+            agg[key][3] += r["bytes"]
     rows = sorted(agg.items(), key=lambda kv: -kv[1][2])
     tot = defaultdict(lambda: [0.0, 0.0])
-    print(f"| net | layer | op | N | H x W | Cin -> Cout | k/s | calls/step | GFLOP/step | ms/step | TF/s | frac |")
-    print("|---|---|---|---|---|---|---|---|---|---|---|---|")
-    for (net, kind, op, N, H, W, Ci, Co, k, s), (n, fl, ms) in rows:
-        fl /= a.steps; ms /= a.steps
+    print(f"| net | layer | op | N | H x W | Cin -> Cout | k/s | calls/step | GFLOP/step | MB/step | ms/step | TF/s | "
+          f"frac | bound | roof |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|")
+    for (net, kind, op, N, H, W, Ci, Co, k, s), (n, fl, ms, by) in rows:
+        fl /= a.steps; ms /= a.steps; by /= a.steps
         tot[net][0] += fl; tot[net][1] += ms
         tf = fl / (ms * 1e-3) / 1e12
+        t_mfma, t_hbm = fl / BASIS, by / HBM
+        bound = "mfma" if t_mfma >= t_hbm else "hbm"
+        roof = max(t_mfma, t_hbm) / (ms * 1e-3)
         print(f"| {net} | {kind} | {op} | {N} | {H}x{W} | {Ci}->{Co} | {k}/{s} | {n // a.steps} | {fl / 1e9:.1f} | "
-              f"{ms:.3f} | {tf:.1f} | {tf * 1e12 / BASIS:.3f} |")
+              f"{by / 1e6:.0f} | {ms:.3f} | {tf:.1f} | {tf * 1e12 / BASIS:.3f} | {bound} | {roof:.3f} |")
     print()
     for net, (fl, ms) in sorted(tot.items()):
         tf = fl / (ms * 1e-3) / 1e12

@@ -5,11 +5,29 @@ doubled: on gfx950 it reports half the bytes of 16-B-per-lane streaming
 reads (MI355X_MICROARCH.md, HBM section), the access width of the conv
 engine's operand loads (buffer_load ... lds dwordx4) and split passes.
 
-usage: pmc_traffic.py FETCH_CSV WRITE_CSV STEPS [OUT_JSON [PROFILE_LABEL [COMMIT]]]"""
-import json
+usage: pmc_traffic.py FETCH_CSV WRITE_CSV STEPS [OUT_JSON [PROFILE_LABEL [COMMIT]]]
+
+The JSON carries csrc_sha (csrc_sha() of the measured tree)."""
 import csv
+import hashlib
+import json
+import os
 import sys
 from collections import defaultdict
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def csrc_sha():
+    """sha256 over the library sources (denoise-gan_amd/csrc/*, include/dgan.h): the stamp that
+    ties a committed traffic profile to the kernels it measured (tests/test_profiles.py)."""
+    h = hashlib.sha256()
+    csrc = os.path.join(REPO, "denoise-gan_amd", "csrc")
+    for path in [os.path.join(csrc, f) for f in sorted(os.listdir(csrc))] + [os.path.join(REPO, "include", "dgan.h")]:
+        h.update(os.path.basename(path).encode())
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 CONV = ("k_conv_gemm", "k_split3", "k_splitk_reduce", "k_narrow", "k_direct", "k_recast", "k_transpose", "k_colsum",
         "k_small", "k_co1", "k_tlast")
@@ -39,7 +57,7 @@ def summarise(fetch_csv, write_csv, steps):
     tot_f = sum(v for k, v in fe.items() if any(c in k for c in CONV)) * 2.0
     tot_w = sum(v for k, v in wr.items() if any(c in k for c in CONV))
     return {"conv_engine_bytes_per_step": (tot_f + tot_w) / steps, "read_bytes_per_step": tot_f / steps,
-            "write_bytes_per_step": tot_w / steps, "steps": steps, "method": METHOD}
+            "write_bytes_per_step": tot_w / steps, "steps": steps, "method": METHOD, "csrc_sha": csrc_sha()}
 
 
 def main(fetch_csv, write_csv, steps, out_json=None, profile=None, commit=None):
