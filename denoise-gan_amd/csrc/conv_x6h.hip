@@ -43,6 +43,14 @@
 namespace dg {
 
 constexpr int HX_PH = 8, HX_PW = 16;
+// tap positions column-major with A fragments kept across a filter column (the
+// default); DG_X6H_TAPS_ROWMAJOR builds the row-major order that reloads all TM
+// fragments per tap, for same-box A/B runs (scripts/build_variant.py)
+#ifdef DG_X6H_TAPS_ROWMAJOR
+constexpr bool kTapsColMajor = false;
+#else
+constexpr bool kTapsColMajor = true;
+#endif
 template <int KT>
 struct HaloGeom {
     static constexpr int HH = HX_PH + KT - 1, HW = HX_PW + KT - 1;
@@ -208,14 +216,18 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     const int cbeg = split * (p.kchunk / (NTAP * BK));
     const int cend = min(nch, cbeg + p.kchunk / (NTAP * BK));
     if (cbeg >= cend) return;
-    // filter tap (row-major in w) of tap position T
+    // filter tap (row-major in w) of tap position T.  Tap positions run
+    // column-major (ta = T % KT fastest): the KT taps of one filter column read
+    // halo windows one patch row apart, so each wave keeps its A fragments in
+    // registers across them and reads one new patch row per tap instead of TM
     int tap_w[NTAP];
 #pragma unroll
     for (int T = 0; T < NTAP; ++T) {
+        const int ta = kTapsColMajor ? T % KT : T / KT, tb = kTapsColMajor ? T / KT : T % KT;
         if constexpr (MODE == MODE_FWD) {
-            tap_w[T] = T;
+            tap_w[T] = ta * g.kw + tb;
         } else {
-            const int i = ph.i0h + (T / KT) * g.sh, j = ph.i0w + (T % KT) * g.sw;
+            const int i = ph.i0h + ta * g.sh, j = ph.i0w + tb * g.sw;
             tap_w[T] = i * g.kw + j;
         }
     }
@@ -307,22 +319,30 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     // bs[T % NB]; issues halo pieces PPT*T .. of chunk+1 into `hn` and the
     // weight tile two K-tiles ahead, then the MFMAs, then waits for the next
     // weight tile (and, at the chunk's last tap, the whole next halo)
+    // A fragments of patch rows wm*TM + r (r = a + da, 0 <= r < TM + KT - 1) of the
+    // current filter column: {hi|mid} and {hi|lo} of 16 halo pixels
+    bf16x8 fm[TM + KT - 1], fl[TM + KT - 1];
     auto ktile = [&](auto TT, int chunk, const char *hc, char *hn) __attribute__((always_inline)) {
         constexpr int T = decltype(TT)::value;
-        constexpr int ta = T / KT, tb = T % KT;
+        constexpr int ta = kTapsColMajor ? T % KT : T / KT, tb = kTapsColMajor ? T / KT : T % KT;
         constexpr int da = MODE == MODE_FWD ? ta : KT - 1 - ta;
         constexpr int db = MODE == MODE_FWD ? tb : KT - 1 - tb;
         constexpr int H0P = T * PPT, H1P = (T + 1) * PPT < H_NJ ? (T + 1) * PPT : H_NJ;
         constexpr int NH = H1P > H0P ? H1P - H0P : 0;   // halo pieces issued in this K-tile
         const char *bc = bbuf(T % NB);
         char *bn = bbuf((T + 2) % NB);
-        bf16x8 ahm[TM], ahl[TM], b1[TN], b2[TN], b3[TN];
+        bf16x8 b1[TN], b2[TN], b3[TN];
         const char *H0 = hc, *H1 = hc + HG::HPL, *H2 = hc + 2 * HG::HPL;
+        auto load_row = [&](int r) __attribute__((always_inline)) {
+            const int r0 = (wm * TM + r) * HG::HW + db;
+            fm[r] = x6_kc_frag(H0, H1, r0, lane);
+            fl[r] = x6_kc_frag(H0, H2, r0, lane);
+        };
+        if constexpr (ta == 0 || !kTapsColMajor) {   // a new filter column: its first tap's TM rows
 #pragma unroll
-        for (int a = 0; a < TM; ++a) {
-            const int r0 = (wm * TM + a + da) * HG::HW + db;
-            ahm[a] = x6_kc_frag(H0, H1, r0, lane);
-            ahl[a] = x6_kc_frag(H0, H2, r0, lane);
+            for (int a = 0; a < TM; ++a) load_row(a + da);
+        } else {                   // one row beyond the previous tap's window
+            load_row(MODE == MODE_FWD ? da + TM - 1 : da);
         }
         const char *B0 = bc, *B1 = bc + BPL, *B2 = bc + 2 * BPL;
 #pragma unroll
@@ -346,17 +366,17 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         for (int a = 0; a < TM; ++a)
 #pragma unroll
             for (int b = 0; b < TN; ++b)
-                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahm[a], b1[b], acc[a][b], 0, 0, 0);
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fm[a + da], b1[b], acc[a][b], 0, 0, 0);
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
             for (int b = 0; b < TN; ++b)
-                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahm[a], b2[b], acc[a][b], 0, 0, 0);
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fm[a + da], b2[b], acc[a][b], 0, 0, 0);
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
             for (int b = 0; b < TN; ++b)
-                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahl[a], b3[b], acc[a][b], 0, 0, 0);
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fl[a + da], b3[b], acc[a][b], 0, 0, 0);
         // DMAs issued in this K-tile may stay in flight; everything older
         // (the next weight tile, and at the last tap the whole next halo) has landed
         wait_dma_c<B_NJ + NH>();

@@ -3,7 +3,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 L=denoise-gan_amd/lib
-B="python bench.py --steps 30 --warmup 8 --no-cpu-baseline --no-core"
+B="python bench.py --steps 30 --warmup 8 --no-cpu-baseline --no-core --no-pmc-leg"
 for r in 1 2; do
   for v in base "$@"; do
     if [ "$v" = base ]; then lib=""; else lib="$PWD/$L/libdgan_$v.so"; fi
