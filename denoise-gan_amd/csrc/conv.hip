@@ -860,6 +860,126 @@ k_narrow_wgrad(const GemmArgs p) {
         p.slab[((long)split * p.M + krow) * p.N + co] = acc[co];
 }
 
+// WGRAD with Co <= 4 at stride 1 (the SR family's 3-channel output convs,
+// e.g. FastSRGAN's 3x3 32 -> 3 at 512x512): dW[(tap, ci)][co] = sum over output
+// pixels of x[pixel + tap][ci] * dy[pixel][co].  A block walks output row
+// segments of NWT_TP pixels: it stages the kh x (NWT_TP + kw - 1) x Ci input
+// window and the segment's dy (4 floats per pixel) in LDS once, and thread q
+// owns filter rows q, q + 256, ... (tap, ci) with their Co sums in registers
+// -- per pixel one conflict-free ds_read_b32 of x and one broadcast float4 of
+// dy, and every x element staged once per segment instead of once per tap.
+// Partials per block [block][Q][4] are summed in block order by
+// k_narrow_wgrad_final.  (k_narrow_wgrad above -- one block per tap, each lane
+// a chain of 4 pixels' loads in flight -- took 1.04 ms for FastSRGAN's output
+// conv at bs8.)
+constexpr int NWT_TP = 64;
+constexpr int NWT_QMAX = 4;    // filter rows per thread: Q = kh*kw*Ci <= 1024
+static bool narrow_tile_ok(const ConvGeom &g) {
+    const long Q = (long)g.kh * g.kw * g.Ci;
+    const long lds = ((long)g.kh * (NWT_TP + g.kw - 1) * g.Ci + 4L * NWT_TP) * 4;
+    return g.sh == 1 && g.sw == 1 && g.Co <= 4 && g.Ci % 4 == 0 && Q <= 256L * NWT_QMAX && lds <= 64 * 1024;
+}
+static size_t narrow_tile_lds(const ConvGeom &g) {
+    return ((size_t)g.kh * (NWT_TP + g.kw - 1) * g.Ci + 4 * NWT_TP) * sizeof(float);
+}
+static int narrow_tile_segments(const ConvGeom &g) {
+    return g.N * g.Ho * ((g.Wo + NWT_TP - 1) / NWT_TP);
+}
+
+__global__ void __launch_bounds__(256)
+k_narrow_wgrad_tile(const GemmArgs p, int nseg, float *__restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    const ConvGeom &g = p.g;
+    const int Ci = g.Ci, KW = g.kw, KH = g.kh, Co = g.Co;
+    const int XW = NWT_TP + KW - 1;
+    const int ci4 = Ci >> 2;
+    const int XV = KH * XW * ci4;                            // staged x float4s
+    float *xs = sm;                                          // [KH][XW][Ci]
+    f32x4 *ds = reinterpret_cast<f32x4 *>(sm + 4 * XV);      // [NWT_TP] dy, co 0..3
+    const int Q = KH * KW * Ci;
+    const int segw = (g.Wo + NWT_TP - 1) / NWT_TP;
+    f32x4 acc[NWT_QMAX];
+#pragma unroll
+    for (int u = 0; u < NWT_QMAX; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+        const int sx = seg % segw, t = seg / segw;
+        const int ho = t % g.Ho, n = t / g.Ho;
+        const int wo0 = sx * NWT_TP;
+        for (int e = threadIdx.x; e < XV; e += 256) {
+            const int c4 = e % ci4, r = e / ci4;
+            const int col = r % XW, i = r / XW;
+            const int hi = ho - g.pt + i, wi = wo0 - g.pl + col;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            if ((unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W)
+                v = *reinterpret_cast<const f32x4 *>(p.A + ((long)(n * g.H + hi) * g.W + wi) * p.lda + 4 * c4);
+            reinterpret_cast<f32x4 *>(xs)[e] = v;
+        }
+        if (threadIdx.x < NWT_TP) {
+            const int wo = wo0 + threadIdx.x;
+            f32x4 d = {0.f, 0.f, 0.f, 0.f};
+            if (wo < g.Wo) {
+                const float *dp = p.B + ((long)(n * g.Ho + ho) * g.Wo + wo) * p.ldb;
+#pragma unroll
+                for (int co = 0; co < 4; ++co)
+                    if (co < Co) d[co] = dp[co];
+            }
+            ds[threadIdx.x] = d;
+        }
+        __syncthreads();
+        const int npx = min(NWT_TP, g.Wo - wo0);
+#pragma unroll
+        for (int u = 0; u < NWT_QMAX; ++u) {
+            const int q = threadIdx.x + 256 * u;
+            if (q < Q) {
+                const int tap = q / Ci, c = q - tap * Ci;
+                const int i = tap / KW, j = tap - i * KW;
+                const float *xr = xs + (i * XW + j) * Ci + c;
+                f32x4 a = acc[u];
+                for (int px = 0; px < npx; ++px) {
+                    const float xv = xr[px * Ci];
+                    const f32x4 d = ds[px];
+#pragma unroll
+                    for (int co = 0; co < 4; ++co) a[co] = fmaf(xv, d[co], a[co]);
+                }
+                acc[u] = a;
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int u = 0; u < NWT_QMAX; ++u) {
+        const int q = threadIdx.x + 256 * u;
+        if (q < Q) reinterpret_cast<f32x4 *>(part)[(long)blockIdx.x * Q + q] = acc[u];
+    }
+}
+
+// dW[q][co] = sum over the R partial blocks of part[r][q][co] (+ beta dW): block = 16
+// (q, co) outputs x 16 row lanes summing rows r = lane, lane + 16, ... in order, then the
+// lanes in lane order
+__global__ void __launch_bounds__(256)
+k_narrow_wgrad_final(const GemmArgs p, int R, const float *__restrict__ part) {
+    __shared__ float red[256];
+    const int Q4 = p.M * 4;
+    const int ol = threadIdx.x & 15, rl = threadIdx.x >> 4;
+    const int o = blockIdx.x * 16 + ol;
+    float sacc = 0.f;
+    if (o < Q4) {
+#pragma unroll 8
+        for (int r = rl; r < R; r += 16) sacc += part[(long)r * Q4 + o];
+    }
+    red[threadIdx.x] = sacc;
+    __syncthreads();
+    if (rl == 0 && o < Q4) {
+        const int q = o >> 2, co = o & 3;
+        if (co < p.N) {
+            float t = red[ol];
+            for (int l = 1; l < 16; ++l) t += red[l * 16 + ol];
+            float *dst = p.C + (long)q * p.ldc + co;
+            *dst = p.beta != 0.f ? t + p.beta * *dst : t;
+        }
+    }
+}
+
 // column sum for bias gradients: out[c] = sum_r dy[r*ld + c] + beta*out[c].
 // Block (row chunk, channel chunk): 256 threads = CC channels (adjacent lanes
 // read adjacent channels of one row) x RL = 256/CC row lanes, each summing its
@@ -1071,6 +1191,8 @@ struct OpPlan {
     int co1;
     // ConvT(3) forward on the fused MFMA + col2im kernel (conv_tlast.hip)
     int tlast;
+    // narrow stride-1 filter gradient on row segments (k_narrow_wgrad_tile): partial blocks
+    int ntile;
 };
 
 // A narrow op (GEMM N <= 8) recast as a 1x1-geometry MFMA GEMM plus a gather:
@@ -1117,7 +1239,7 @@ static bool cfg_vec(const ConvGeom &g, int mode, int bk) {
 //   rounds x (blocks per CU x per-block MFMA work) / (CU peak x occupancy efficiency)
 // + split-K slab traffic, where blocks per CU = min(resident limit, blocks / 256).
 // Plan features switched off for same-box A/B runs: DG_PLAN_DISABLE is a
-// comma-separated list of {shortk, small, co1, tlast, direct, halo, halo2, halo4, xcd_phase, narrow_px}
+// comma-separated list of {shortk, small, co1, tlast, direct, halo, halo2, halo4, xcd_phase, narrow_px, ntile}
 // (read when a descriptor is planned; unset in production runs)
 static bool plan_off(const char *feature) {
     const char *list = getenv("DG_PLAN_DISABLE");
@@ -1213,7 +1335,12 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     }
     if (pl.narrow) {
         pl.splits = 1; pl.kchunk = pl.K; pl.ws_bytes = 0; pl.slab_bytes = 0;
-        if (mode == MODE_WGRAD) {
+        if (mode == MODE_WGRAD && narrow_tile_ok(g) && !plan_off("ntile")) {
+            pl.ntile = 1;
+            pl.splits = std::min(1024, narrow_tile_segments(g));   // partial blocks
+            pl.slab_bytes = (size_t)pl.splits * pl.M * 4 * sizeof(float);
+            pl.ws_bytes = pl.slab_bytes;
+        } else if (mode == MODE_WGRAD) {
             // pixels split so that taps*ci_chunks*splits ~ 1024 blocks
             long blocks = (long)g.kh * g.kw * ((g.Ci + 255) / 256);
             int s = (int)std::max<long>(1, std::min<long>(1024 / std::max<long>(blocks, 1), pl.K / 64));
@@ -1622,7 +1749,17 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
             int in_lds = wbytes <= 64 * 1024;
             hipLaunchKernelGGL(k_narrow_dgrad, dim3(dg_cdiv(pl.M, 256), pl.nphase), dim3(256), in_lds ? wbytes : 0, s, a, in_lds);
             DG_LAUNCHED("narrow_dgrad");
+        } else if (pl.ntile && a.lda % 4 == 0 && ((uintptr_t)a.A & 15) == 0) {
+            float *part = a.slab;
+            DG_ARG(part != nullptr, "workspace pointer is NULL");
+            hipLaunchKernelGGL(k_narrow_wgrad_tile, dim3(pl.splits), dim3(256), narrow_tile_lds(d->g), s, a,
+                               narrow_tile_segments(d->g), part);
+            DG_LAUNCHED("narrow_wgrad_tile");
+            hipLaunchKernelGGL(k_narrow_wgrad_final, dim3(dg_cdiv(pl.M * 4, 16)), dim3(256), 0, s, a, pl.splits,
+                               (const float *)part);
+            DG_LAUNCHED("narrow_wgrad_final");
         } else {
+            DG_ARG(!pl.ntile, "the narrow filter-gradient tile kernel needs ldx %% 4 == 0 and a 16-byte aligned x");
             a.splits = pl.splits; a.kchunk = pl.kchunk;
             hipLaunchKernelGGL(k_narrow_wgrad, dim3(d->g.kh * d->g.kw * ((d->g.Ci + 255) / 256), pl.splits), dim3(256), 0, s, a);
             DG_LAUNCHED("narrow_wgrad");
