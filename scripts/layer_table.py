@@ -28,15 +28,31 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--content", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--model", default="pix2pix", choices=("pix2pix", "srgan", "fsrgan", "autoencoder"))
+    ap.add_argument("--fp16", type=int, default=None, help="SR family: mixed_float16 (default: the driver's)")
     a = ap.parse_args()
     from bench import Args, WORKLOADS, synthetic_batch
     from dgan import ops
-    from pix2pix import Pix2Pix
-    m = Pix2Pix(Args(crop_size=256, retrain=0, width=1, seed=1234, dropout_seed=0, identity_loss=1,
+    wl = WORKLOADS[a.model]
+    batch = a.batch or wl["batch"]
+    global BASIS
+    if a.model == "pix2pix":
+        from pix2pix import Pix2Pix
+        m = Pix2Pix(Args(crop_size=256, retrain=0, width=1, seed=1234, dropout_seed=0, identity_loss=1,
+                         content_loss=a.content))
+    else:
+        from autoencoder import Autoencoder
+        from fsrgan import FastSRGAN
+        from srgan import SRGAN
+        fp16 = int(wl.get("fp16", 0) if a.fp16 is None else a.fp16)
+        if fp16:
+            BASIS = 2516.6e12   # fp16 GEMMs: the dense fp16 MFMA peak
+        cls = {"srgan": SRGAN, "fsrgan": FastSRGAN, "autoencoder": Autoencoder}[a.model]
+        m = cls(Args(crop_size=wl["size"], scale=wl["scale"], lr=1e-3, fp16=fp16, retrain=0, seed=1234,
                      content_loss=a.content))
-    x, y = (torch.from_numpy(t).cuda() for t in synthetic_batch(WORKLOADS["pix2pix"], a.batch, 1000))
-    tr = m.trainer(x.shape)
+    x, y = (torch.from_numpy(t).cuda() for t in synthetic_batch(wl, batch, 1000))
+    tr = m.trainer(x.shape) if a.model == "pix2pix" else m.trainer(x.shape, y.shape)
     for _ in range(3):
         tr.step(x, y)
     torch.cuda.synchronize()
