@@ -1150,18 +1150,23 @@ static const TileCfg kCfgs[] = {
     {128, 128, 2, 2, 32, 2, 2, 1.00}, {128, 64, 2, 2, 32, 2, 2, 1.12}, {64, 128, 2, 2, 32, 2, 2, 1.12},
     {64, 64, 2, 2, 32, 2, 3, 1.35},   {32, 128, 1, 4, 32, 2, 3, 1.50}, {128, 128, 2, 2, 16, 3, 3, 1.00},
     {128, 64, 2, 2, 16, 3, 3, 1.12},
+    // 32-wide tiles for the 32-channel layers of the SR discriminators (srgan.py:232-272):
+    // a 64-wide tile computes half zeros there
+    {128, 32, 4, 1, 32, 2, 3, 1.40}, {256, 32, 4, 1, 32, 2, 2, 1.30},
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 // bf16x6 kernel configs (conv_x6.hip launch_gemm_x6), K-tile 16
 static const TileCfg kX6Cfgs[] = {
     {128, 128, 2, 2, 16, 2, 2, 1.00}, {128, 64, 2, 2, 16, 2, 2, 1.15}, {64, 128, 2, 2, 16, 2, 2, 1.15},
     {64, 64, 2, 2, 16, 3, 4, 1.40},   {256, 128, 4, 2, 16, 2, 1, 1.00}, {128, 256, 2, 4, 16, 2, 1, 0.90},
+    {128, 32, 4, 1, 16, 3, 4, 1.45},   // 32-wide (SR discriminators' 32-channel layers)
 };
 constexpr int kNumX6Cfgs = sizeof(kX6Cfgs) / sizeof(kX6Cfgs[0]);
 // fp16 kernel configs (conv_x6.hip launch_gemm_f16: the same tiles, K-tile 32)
 static const TileCfg kF16Cfgs[] = {
     {128, 128, 2, 2, 32, 2, 2, 1.00}, {128, 64, 2, 2, 32, 2, 2, 1.15}, {64, 128, 2, 2, 32, 2, 2, 1.15},
     {64, 64, 2, 2, 32, 3, 4, 1.40},   {256, 128, 4, 2, 32, 2, 1, 1.00}, {128, 256, 2, 4, 32, 2, 1, 0.90},
+    {128, 32, 4, 1, 32, 3, 4, 1.45},   // 32-wide (SR discriminators' 32-channel layers)
 };
 constexpr int kNumF16Cfgs = sizeof(kF16Cfgs) / sizeof(kF16Cfgs[0]);
 
@@ -1239,7 +1244,8 @@ static bool cfg_vec(const ConvGeom &g, int mode, int bk) {
 //   rounds x (blocks per CU x per-block MFMA work) / (CU peak x occupancy efficiency)
 // + split-K slab traffic, where blocks per CU = min(resident limit, blocks / 256).
 // Plan features switched off for same-box A/B runs: DG_PLAN_DISABLE is a
-// comma-separated list of {shortk, small, co1, tlast, direct, halo, halo2, halo4, xcd_phase, narrow_px, ntile}
+// comma-separated list of {shortk, small, co1, tlast, direct, halo, halo2, halo4, xcd_phase, narrow_px, ntile,
+// tile32, f16planes}
 // (read when a descriptor is planned; unset in production runs)
 static bool plan_off(const char *feature) {
     const char *list = getenv("DG_PLAN_DISABLE");
@@ -1277,6 +1283,7 @@ static double choose_tiles(OpPlan &pl, const TileCfg *cfgs, int ncfg, double pea
         const TileCfg &t = cfgs[c];
         if (forced >= 0 && c != forced) continue;
         if (forced < 0 && pl.N <= 64 && t.bn > 64) continue;
+        if (forced < 0 && t.bn == 32 && plan_off("tile32")) continue;
         long mt = (pl.M + t.bm - 1) / t.bm, nt = (pl.N + t.bn - 1) / t.bn;
         long tiles = mt * nt * pl.nphase;
         long ktiles = (pl.K + t.bk - 1) / t.bk;
@@ -1572,6 +1579,8 @@ static void launch_gemm(int cfg, int vec, dim3 grid, const GemmArgs &a, hipStrea
         DG_L(4, 32, 128, 1, 4, 32, 2)
         DG_L(5, 128, 128, 2, 2, 16, 3)
         DG_L(6, 128, 64, 2, 2, 16, 3)
+        DG_L(7, 128, 32, 4, 1, 32, 2)
+        DG_L(8, 256, 32, 4, 1, 32, 2)
     }
 #undef DG_L
 }
@@ -1804,13 +1813,26 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
         a.b_bytes = (unsigned)bb;
     }
     if (pl.x6 == 2) {
-        // fp16: round both operands into one fp16 plane each in the workspace
+        // fp16: round the operands into one fp16 plane each -- the caller-held
+        // copies (dg_conv_planes_t: a layer's x, dy and w are converted once
+        // and shared by the ops that read them) or the workspace
         char *ws = (char *)a.slab;
         DG_ARG(ws != nullptr, "workspace pointer is NULL");
         void *pa = ws + pl.x6_a_off, *pb = ws + pl.x6_b_off;
         const int ldbw = (mode == MODE_DGRAD) ? a.g.Co : ldb;
-        launch_split_f16_pair(A, lda, pl.x6_ra, pl.x6_ca, pa, B, ldbw, pl.x6_rb, pl.x6_cb, pb, s);
-        DG_LAUNCHED("split_f16");
+        if (pr && pr->a) pa = pr->a;
+        if (pr && pr->b) pb = pr->b;
+        const bool need_a = !(pr && pr->a && pr->a_ready), need_b = !(pr && pr->b && pr->b_ready);
+        if (need_a && need_b) {
+            launch_split_f16_pair(A, lda, pl.x6_ra, pl.x6_ca, pa, B, ldbw, pl.x6_rb, pl.x6_cb, pb, s);
+            DG_LAUNCHED("split_f16");
+        } else if (need_a) {
+            launch_split_f16(A, lda, pl.x6_ra, pl.x6_ca, pa, s);
+            DG_LAUNCHED("split_f16_a");
+        } else if (need_b) {
+            launch_split_f16(B, ldbw, pl.x6_rb, pl.x6_cb, pb, s);
+            DG_LAUNCHED("split_f16_b");
+        }
         a.A = (const float *)pa; a.lda = pl.x6_ca; a.a_bytes = (unsigned)(2 * pl.x6_ra * pl.x6_ca);
         a.B = (const float *)pb; a.ldb = pl.x6_cb; a.b_bytes = (unsigned)(2 * pl.x6_rb * pl.x6_cb);
         fastdiv_magic((unsigned)a.g.Wo, a.mg_wo, a.sh_wo);
@@ -1921,10 +1943,14 @@ static size_t tensor_plane_bytes(const dg_conv_desc_s *d, int t) {
     return (size_t)6 * d->g.kh * d->g.kw * d->Cin * d->Cout;
 }
 
-// tensors op reads as bf16x6 planes (0 for fp32 / narrow / recast plans)
+// tensors op reads as operand planes: bf16x6 planes (x6 1) or the fp16 copy
+// (x6 2, DG_MATH_FP16: [rows][C] fp16, the same for every op that reads the
+// tensor); 0 for fp32 / narrow / recast plans.  A descriptor's ops never mix
+// the two formats (an fp16 descriptor's other ops run fp32).
 static int op_plane_mask(const dg_conv_desc_s *d, int op) {
     const OpPlan &pl = d->plan[op];
-    if (pl.x6 != 1 || pl.narrow || d->rc[op].on || pl.M == 0 || pl.N == 0) return 0;
+    if ((pl.x6 != 1 && pl.x6 != 2) || pl.narrow || d->rc[op].on || pl.M == 0 || pl.N == 0) return 0;
+    if (pl.x6 == 2 && plan_off("f16planes")) return 0;
     int ta, tb;
     op_tensors(d, op, ta, tb);
     return ta | tb;

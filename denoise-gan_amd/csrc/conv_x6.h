@@ -19,12 +19,18 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 //   RC image [16 k][COLS], read transposed (ds_read_b64_tr_b16): the 8-dword
 //   blocks of k-row k are XOR-swizzled by f(k) so the eight k-rows one 32-lane
 //   half touches (k and k+8 for 4 consecutive k) land on distinct banks.
-// (Both verified exhaustively against the gfx950 bank model for 64/128/256.)
+// (Both verified exhaustively against the gfx950 bank model for 64/128/256;
+// the 32-column images of the 32-wide tiles keep a row-local swap.)
 __device__ __forceinline__ int x6_off(int row, int half) { return row * 32 + 16 * half; }
 
+// (a 32-column image has 16 dwords per k-row: only the 0 / 8 swap stays inside it)
+__device__ __forceinline__ int x6_rc_swz_cols(int cols, int k) {  // in dwords
+    return cols >= 128 ? 8 * ((k & 3) | (((k >> 3) & 1) << 2))
+                       : (cols >= 64 ? 8 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1)) : 8 * ((k >> 1) & 1));
+}
 template <int COLS>
 __device__ __forceinline__ int x6_rc_swz(int k) {  // in dwords
-    return COLS >= 128 ? 8 * ((k & 3) | (((k >> 3) & 1) << 2)) : 8 * (((k >> 1) & 1) | (((k >> 3) & 1) << 1));
+    return x6_rc_swz_cols(COLS, k);
 }
 // byte offset of bf16 element (k, col) in a [16][COLS] plane image (col even)
 template <int COLS>

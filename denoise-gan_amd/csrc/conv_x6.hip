@@ -186,9 +186,7 @@ k_conv_gemm_x6(const GemmArgs p) {
         } else {
             sl.r = pos / (2 * X);
             const int pdw = (pos - sl.r * 2 * X) >> 2;
-            const int swz = X >= 128 ? 8 * ((sl.r & 3) | (((sl.r >> 3) & 1) << 2))
-                                     : 8 * (((sl.r >> 1) & 1) | (((sl.r >> 3) & 1) << 1));
-            sl.c = 2 * (pdw ^ swz);
+            sl.c = 2 * (pdw ^ x6_rc_swz_cols(X, sl.r));
         }
         return sl;
     };
@@ -596,6 +594,7 @@ static void launch_gemm_planes(int mode, int cfg, dim3 grid, const GemmArgs &a, 
         DG_X6(3, 64, 64, 2, 2, 3, 3)
         DG_X6(4, 256, 128, 4, 2, 2, 3)
         DG_X6(5, 128, 256, 2, 4, 2, 3)
+        DG_X6(6, 128, 32, 4, 1, 3, 3)
     }
 #undef DG_X6
 }

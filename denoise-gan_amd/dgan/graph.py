@@ -366,6 +366,9 @@ class GraphPlan:
         self.pool_out = [dict() for _ in range(slots)]    # maxpool node -> consumer conv's x planes
         self.pool_gout = [dict() for _ in range(slots)]   # maxpool node -> producer conv's dy planes
         feed = not os.environ.get("DG_NO_FEED")
+        # (producer-written planes are bf16x6 planes: an fp16 descriptor's planes are
+        # the fp16 copies its own ops convert, so neither end of a feed may be fp16)
+        x6 = lambda d: d.math == ops.MATH_BF16X6   # noqa: E731
         for m in (nodes[1:] if feed else []):
             # max pool between two convs: its output is the next conv's input,
             # its input gradient the previous conv's dy (premask: act' folded in)
@@ -375,7 +378,7 @@ class GraphPlan:
             if len(cs) == 1 and cs[0].kind == "conv" and m.out.id not in self.slice_of:
                 c = cs[0]
                 dc = self.desc[c.idx]
-                if dc.plane_mask[ops.OP_FWD] & ops.TENSOR_X:
+                if dc.plane_mask[ops.OP_FWD] & ops.TENSOR_X and x6(dc):
                     for k in range(slots):
                         pc = self.cplanes[k][c.idx]
                         if pc.x is None:
@@ -386,7 +389,7 @@ class GraphPlan:
             n = t_in.node
             if train and n.kind == "conv" and t_in.id in self.premask:
                 dn = self.desc[n.idx]
-                if (dn.plane_mask[ops.OP_BWD_DATA] | dn.plane_mask[ops.OP_BWD_FILTER]) & ops.TENSOR_DY:
+                if (dn.plane_mask[ops.OP_BWD_DATA] | dn.plane_mask[ops.OP_BWD_FILTER]) & ops.TENSOR_DY and x6(dn):
                     for k in range(slots):
                         pn = self.cplanes[k][n.idx]
                         pn.dy = ops.PlaneBuf(dn.plane_bytes(ops.TENSOR_DY), device)
@@ -398,7 +401,7 @@ class GraphPlan:
                 continue
             c = cons[t.id][0]
             dn, dc = self.desc[n.idx], self.desc[c.idx]
-            if dn.Cout % 16:
+            if dn.Cout % 16 or not (x6(dn) and x6(dc)):
                 continue
             if dc.plane_mask[ops.OP_FWD] & ops.TENSOR_X:
                 for k in range(slots):

@@ -115,7 +115,10 @@ int dg_conv_bwd_filter(dg_conv_t d, const float *x, int ldx, const float *dy, in
  * without touching the fp32 tensor.  NULL buffers fall back to the workspace.
  * The caller owns validity: set a ready bit only after an op whose
  * dg_conv_op_planes mask holds that tensor has run on the same stream, and
- * clear it when the tensor changes. */
+ * clear it when the tensor changes.  Under DG_MATH_FP16 the same buffers hold
+ * the tensor's fp16 copy ([rows][C], 2 B per element) that the fp16 GEMMs
+ * read, converted once per tensor in the same way; `out` (producer-written
+ * planes) is bf16x6-only. */
 enum { DG_TENSOR_X = 1, DG_TENSOR_DY = 2, DG_TENSOR_W = 4 };
 typedef struct dg_conv_planes {
     void *x, *dy, *w;  /* plane buffers (NULL: split into the workspace) */

@@ -33,6 +33,9 @@ F16_CONVS = [
     ("fsrgan.project", 2, 16, 16, 192, 32, 1, 1),
     ("vgg.b3", 2, 12, 12, 256, 256, 3, 1),
     ("odd.7x5", 3, 7, 5, 64, 96, 3, 1),
+    # fp16 128x32 tiles in all three ops (32-column RC images)
+    ("tile32.s1", 2, 128, 128, 32, 32, 3, 1),
+    ("tile32.s2", 4, 96, 96, 32, 32, 3, 2),
 ]
 
 

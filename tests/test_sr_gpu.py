@@ -258,6 +258,11 @@ SR_CONVS = [
     ("px.co1.ragged", 1, 257, 263, 32, 1, 3, 1, True, 36),
     ("px.co3.1x1.ld", 2, 200, 171, 64, 3, 1, 1, True, 68),
     ("px.co3.small", 3, 9, 13, 32, 3, 3, 1, True, 40),
+    # 32-wide GEMM tiles (the SR discriminators' 32-channel layers): fp32 128x32 in all three
+    # ops, bf16x6 128x32 input gradient (RC images of 32 columns), fp32 256x32 forward
+    ("tile32.s1", 2, 128, 128, 32, 32, 3, 1, True, None),
+    ("tile32.s2", 4, 128, 128, 32, 32, 3, 2, True, None),
+    ("tile32.fwd256", 8, 256, 256, 32, 32, 3, 2, True, None),
 ]
 
 
