@@ -860,27 +860,30 @@ k_narrow_wgrad(const GemmArgs p) {
         p.slab[((long)split * p.M + krow) * p.N + co] = acc[co];
 }
 
-// WGRAD with Co <= 4 at stride 1 (the SR family's 3-channel output convs,
-// e.g. FastSRGAN's 3x3 32 -> 3 at 512x512): dW[(tap, ci)][co] = sum over output
-// pixels of x[pixel + tap][ci] * dy[pixel][co].  A block walks output row
-// segments of NWT_TP pixels: it stages the kh x (NWT_TP + kw - 1) x Ci input
-// window and the segment's dy (4 floats per pixel) in LDS once, and thread q
-// owns filter rows q, q + 256, ... (tap, ci) with their Co sums in registers
-// -- per pixel one conflict-free ds_read_b32 of x and one broadcast float4 of
-// dy, and every x element staged once per segment instead of once per tap.
-// Partials per block [block][Q][4] are summed in block order by
-// k_narrow_wgrad_final.  (k_narrow_wgrad above -- one block per tap, each lane
-// a chain of 4 pixels' loads in flight -- took 1.04 ms for FastSRGAN's output
-// conv at bs8.)
+// WGRAD at stride 1 with few filter rows x output channels: the SR family's
+// 3-channel output convs (e.g. FastSRGAN's 3x3 32 -> 3 at 512x512) and the
+// 3-channel input convs of the SR discriminators (3x3 3 -> 32 at 512x512):
+// dW[(tap, ci)][co] = sum over output pixels of x[pixel + tap][ci] * dy[pixel][co].
+// A block walks output row segments of NWT_TP pixels: it stages the
+// kh x (NWT_TP + kw - 1) x Ci input window and the segment's dy (CG groups of
+// 4 channels per pixel) in LDS once; thread t owns slots s = t, t + 256, ...,
+// slot s = (filter row q = s / CG, channel group s % CG) with 4 sums in
+// registers -- per pixel one ds_read_b32 of x (shared by the CG lanes of a
+// row) and one float4 of dy, every x element staged once per segment instead
+// of once per tap.  Partials per block [block][Q * CG][4] are summed in block
+// order by k_narrow_wgrad_final.  (k_narrow_wgrad above -- one block per tap,
+// each lane a chain of 4 pixels' loads in flight -- took 1.04 ms for
+// FastSRGAN's output conv at bs8; the 3 -> 32 input conv's filter gradient ran
+// 455 us per call on 64 x 64 fp32 tiles, 27 of whose 64 rows exist.)
 constexpr int NWT_TP = 64;
-constexpr int NWT_QMAX = 4;    // filter rows per thread: Q = kh*kw*Ci <= 1024
-static bool narrow_tile_ok(const ConvGeom &g) {
-    const long Q = (long)g.kh * g.kw * g.Ci;
-    const long lds = ((long)g.kh * (NWT_TP + g.kw - 1) * g.Ci + 4L * NWT_TP) * 4;
-    return g.sh == 1 && g.sw == 1 && g.Co <= 4 && g.Ci % 4 == 0 && Q <= 256L * NWT_QMAX && lds <= 64 * 1024;
-}
+constexpr int NWT_QMAX = 4;    // slots per thread: Q * CG <= 1024
+static int narrow_tile_groups(const ConvGeom &g) { return (g.Co + 3) / 4; }
 static size_t narrow_tile_lds(const ConvGeom &g) {
-    return ((size_t)g.kh * (NWT_TP + g.kw - 1) * g.Ci + 4 * NWT_TP) * sizeof(float);
+    return ((size_t)g.kh * (NWT_TP + g.kw - 1) * g.Ci + 4 * NWT_TP * (size_t)narrow_tile_groups(g)) * sizeof(float);
+}
+static bool narrow_tile_ok(const ConvGeom &g) {
+    const long S = (long)g.kh * g.kw * g.Ci * narrow_tile_groups(g);
+    return g.sh == 1 && g.sw == 1 && S <= 256L * NWT_QMAX && narrow_tile_lds(g) <= 64 * 1024;
 }
 static int narrow_tile_segments(const ConvGeom &g) {
     return g.N * g.Ho * ((g.Wo + NWT_TP - 1) / NWT_TP);
@@ -891,12 +894,14 @@ k_narrow_wgrad_tile(const GemmArgs p, int nseg, float *__restrict__ part) {
     extern __shared__ __attribute__((aligned(16))) float sm[];
     const ConvGeom &g = p.g;
     const int Ci = g.Ci, KW = g.kw, KH = g.kh, Co = g.Co;
+    const int CG = (Co + 3) >> 2;
     const int XW = NWT_TP + KW - 1;
-    const int ci4 = Ci >> 2;
-    const int XV = KH * XW * ci4;                            // staged x float4s
+    const int XE = KH * XW * Ci;                             // staged x floats
     float *xs = sm;                                          // [KH][XW][Ci]
-    f32x4 *ds = reinterpret_cast<f32x4 *>(sm + 4 * XV);      // [NWT_TP] dy, co 0..3
-    const int Q = KH * KW * Ci;
+    f32x4 *ds = reinterpret_cast<f32x4 *>(sm + ((XE + 3) & ~3));   // [NWT_TP][CG] dy
+    const bool xv4 = (Ci & 3) == 0 && (p.lda & 3) == 0 && (((uintptr_t)p.A) & 15) == 0;
+    const bool dv4 = (Co & 3) == 0 && (p.ldb & 3) == 0 && (((uintptr_t)p.B) & 15) == 0;
+    const int S = KH * KW * Ci * CG;
     const int segw = (g.Wo + NWT_TP - 1) / NWT_TP;
     f32x4 acc[NWT_QMAX];
 #pragma unroll
@@ -905,39 +910,57 @@ k_narrow_wgrad_tile(const GemmArgs p, int nseg, float *__restrict__ part) {
         const int sx = seg % segw, t = seg / segw;
         const int ho = t % g.Ho, n = t / g.Ho;
         const int wo0 = sx * NWT_TP;
-        for (int e = threadIdx.x; e < XV; e += 256) {
-            const int c4 = e % ci4, r = e / ci4;
-            const int col = r % XW, i = r / XW;
-            const int hi = ho - g.pt + i, wi = wo0 - g.pl + col;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            if ((unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W)
-                v = *reinterpret_cast<const f32x4 *>(p.A + ((long)(n * g.H + hi) * g.W + wi) * p.lda + 4 * c4);
-            reinterpret_cast<f32x4 *>(xs)[e] = v;
+        if (xv4) {
+            const int ci4 = Ci >> 2;
+            for (int e = threadIdx.x; e < XE / 4; e += 256) {
+                const int c4 = e % ci4, r = e / ci4;
+                const int col = r % XW, i = r / XW;
+                const int hi = ho - g.pt + i, wi = wo0 - g.pl + col;
+                f32x4 v = {0.f, 0.f, 0.f, 0.f};
+                if ((unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W)
+                    v = *reinterpret_cast<const f32x4 *>(p.A + ((long)(n * g.H + hi) * g.W + wi) * p.lda + 4 * c4);
+                reinterpret_cast<f32x4 *>(xs)[e] = v;
+            }
+        } else {
+            for (int e = threadIdx.x; e < XE; e += 256) {
+                const int c = e % Ci, r = e / Ci;
+                const int col = r % XW, i = r / XW;
+                const int hi = ho - g.pt + i, wi = wo0 - g.pl + col;
+                xs[e] = ((unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W)
+                            ? p.A[((long)(n * g.H + hi) * g.W + wi) * p.lda + c] : 0.f;
+            }
         }
-        if (threadIdx.x < NWT_TP) {
-            const int wo = wo0 + threadIdx.x;
+        for (int e = threadIdx.x; e < NWT_TP * CG; e += 256) {
+            const int px = e / CG, cg = e - px * CG;
+            const int wo = wo0 + px;
             f32x4 d = {0.f, 0.f, 0.f, 0.f};
             if (wo < g.Wo) {
-                const float *dp = p.B + ((long)(n * g.Ho + ho) * g.Wo + wo) * p.ldb;
+                const float *dp = p.B + ((long)(n * g.Ho + ho) * g.Wo + wo) * p.ldb + 4 * cg;
+                if (dv4) {
+                    d = *reinterpret_cast<const f32x4 *>(dp);
+                } else {
 #pragma unroll
-                for (int co = 0; co < 4; ++co)
-                    if (co < Co) d[co] = dp[co];
+                    for (int co = 0; co < 4; ++co)
+                        if (4 * cg + co < Co) d[co] = dp[co];
+                }
             }
-            ds[threadIdx.x] = d;
+            ds[e] = d;
         }
         __syncthreads();
         const int npx = min(NWT_TP, g.Wo - wo0);
 #pragma unroll
         for (int u = 0; u < NWT_QMAX; ++u) {
-            const int q = threadIdx.x + 256 * u;
-            if (q < Q) {
+            const int sl = threadIdx.x + 256 * u;
+            if (sl < S) {
+                const int q = sl / CG, cg = sl - q * CG;
                 const int tap = q / Ci, c = q - tap * Ci;
                 const int i = tap / KW, j = tap - i * KW;
                 const float *xr = xs + (i * XW + j) * Ci + c;
+                const f32x4 *dr = ds + cg;
                 f32x4 a = acc[u];
                 for (int px = 0; px < npx; ++px) {
                     const float xv = xr[px * Ci];
-                    const f32x4 d = ds[px];
+                    const f32x4 d = dr[px * CG];
 #pragma unroll
                     for (int co = 0; co < 4; ++co) a[co] = fmaf(xv, d[co], a[co]);
                 }
@@ -948,29 +971,30 @@ k_narrow_wgrad_tile(const GemmArgs p, int nseg, float *__restrict__ part) {
     }
 #pragma unroll
     for (int u = 0; u < NWT_QMAX; ++u) {
-        const int q = threadIdx.x + 256 * u;
-        if (q < Q) reinterpret_cast<f32x4 *>(part)[(long)blockIdx.x * Q + q] = acc[u];
+        const int sl = threadIdx.x + 256 * u;
+        if (sl < S) reinterpret_cast<f32x4 *>(part)[(long)blockIdx.x * S + sl] = acc[u];
     }
 }
 
-// dW[q][co] = sum over the R partial blocks of part[r][q][co] (+ beta dW): block = 16
-// (q, co) outputs x 16 row lanes summing rows r = lane, lane + 16, ... in order, then the
-// lanes in lane order
+// dW[q][co] = sum over the R partial blocks of part[r][q][co] (+ beta dW), with
+// part rows of 4 * CG floats per filter row q: block = 16 outputs x 16 row lanes
+// summing rows r = lane, lane + 16, ... in order, then the lanes in lane order
 __global__ void __launch_bounds__(256)
 k_narrow_wgrad_final(const GemmArgs p, int R, const float *__restrict__ part) {
     __shared__ float red[256];
-    const int Q4 = p.M * 4;
+    const int CG4 = 4 * ((p.N + 3) >> 2);
+    const int T = p.M * CG4;
     const int ol = threadIdx.x & 15, rl = threadIdx.x >> 4;
     const int o = blockIdx.x * 16 + ol;
     float sacc = 0.f;
-    if (o < Q4) {
+    if (o < T) {
 #pragma unroll 8
-        for (int r = rl; r < R; r += 16) sacc += part[(long)r * Q4 + o];
+        for (int r = rl; r < R; r += 16) sacc += part[(long)r * T + o];
     }
     red[threadIdx.x] = sacc;
     __syncthreads();
-    if (rl == 0 && o < Q4) {
-        const int q = o >> 2, co = o & 3;
+    if (rl == 0 && o < T) {
+        const int q = o / CG4, co = o - q * CG4;
         if (co < p.N) {
             float t = red[ol];
             for (int l = 1; l < 16; ++l) t += red[l * 16 + ol];
@@ -1277,7 +1301,7 @@ static double choose_tiles(OpPlan &pl, const TileCfg *cfgs, int ncfg, double pea
     // epilogue weight
     if (forced < 0 && cfgs == kCfgs && pl.K <= 256 && pl.N <= 128 && (long)pl.M * pl.nphase >= 65536 &&
         !plan_off("shortk"))
-        forced = 6;
+        forced = (pl.N <= 32 && !plan_off("tile32")) ? 7 : 6;   // (32 columns: the 128 x 32 tile)
     int best = -1; double best_t = 1e30; long best_splits = 1;
     for (int c = 0; c < ncfg; ++c) {
         const TileCfg &t = cfgs[c];
@@ -1345,7 +1369,7 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         if (mode == MODE_WGRAD && narrow_tile_ok(g) && !plan_off("ntile")) {
             pl.ntile = 1;
             pl.splits = std::min(1024, narrow_tile_segments(g));   // partial blocks
-            pl.slab_bytes = (size_t)pl.splits * pl.M * 4 * sizeof(float);
+            pl.slab_bytes = (size_t)pl.splits * pl.M * 4 * narrow_tile_groups(g) * sizeof(float);
             pl.ws_bytes = pl.slab_bytes;
         } else if (mode == MODE_WGRAD) {
             // pixels split so that taps*ci_chunks*splits ~ 1024 blocks
@@ -1357,6 +1381,18 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
             pl.ws_bytes = pl.slab_bytes;
         }
         pl.gemm_bytes = pl.ws_bytes;
+        return pl;
+    }
+    if (mode == MODE_WGRAD && g.Ci < 8 && narrow_tile_ok(g) && !plan_off("ntile")) {
+        // 1-7 input channels at stride 1 (the SR discriminators' 3 -> 32 input conv): the
+        // filter-gradient GEMM has Q = kh*kw*Ci <= 63 rows; the row-segment kernel instead
+        pl.ntile = 1;
+        pl.splits = std::min(1024, narrow_tile_segments(g));
+        pl.kchunk = pl.K; pl.mtiles = pl.ntiles = 1;
+        pl.slab_bytes = (size_t)pl.splits * pl.M * 4 * narrow_tile_groups(g) * sizeof(float);
+        pl.ws_bytes = pl.gemm_bytes = pl.slab_bytes;
+        if (getenv("DG_PLAN_DEBUG"))
+            fprintf(stderr, "[dg plan] mode %d M=%d N=%d K=%d -> ntile blocks %d\n", mode, pl.M, pl.N, pl.K, pl.splits);
         return pl;
     }
     if (small_conv_ok(g, mode, 0) && !plan_off("small")) {
@@ -1733,6 +1769,17 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
         DG_LAUNCHED("co1");
         return DG_OK;
     }
+    if (pl.ntile) {   // (mode == MODE_WGRAD)
+        float *part = a.slab;
+        DG_ARG(part != nullptr, "workspace pointer is NULL");
+        hipLaunchKernelGGL(k_narrow_wgrad_tile, dim3(pl.splits), dim3(256), narrow_tile_lds(d->g), s, a,
+                           narrow_tile_segments(d->g), part);
+        DG_LAUNCHED("narrow_wgrad_tile");
+        hipLaunchKernelGGL(k_narrow_wgrad_final, dim3(dg_cdiv(pl.M * 4 * narrow_tile_groups(d->g), 16)), dim3(256), 0,
+                           s, a, pl.splits, (const float *)part);
+        DG_LAUNCHED("narrow_wgrad_final");
+        return DG_OK;
+    }
     if (pl.narrow) {
         const ConvGeom &gg = d->g;
         const bool px = mode == MODE_FWD && gg.Ci % 4 == 0 && a.lda % 4 == 0 && (((uintptr_t)a.A) & 15) == 0 &&
@@ -1758,17 +1805,7 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
             int in_lds = wbytes <= 64 * 1024;
             hipLaunchKernelGGL(k_narrow_dgrad, dim3(dg_cdiv(pl.M, 256), pl.nphase), dim3(256), in_lds ? wbytes : 0, s, a, in_lds);
             DG_LAUNCHED("narrow_dgrad");
-        } else if (pl.ntile && a.lda % 4 == 0 && ((uintptr_t)a.A & 15) == 0) {
-            float *part = a.slab;
-            DG_ARG(part != nullptr, "workspace pointer is NULL");
-            hipLaunchKernelGGL(k_narrow_wgrad_tile, dim3(pl.splits), dim3(256), narrow_tile_lds(d->g), s, a,
-                               narrow_tile_segments(d->g), part);
-            DG_LAUNCHED("narrow_wgrad_tile");
-            hipLaunchKernelGGL(k_narrow_wgrad_final, dim3(dg_cdiv(pl.M * 4, 16)), dim3(256), 0, s, a, pl.splits,
-                               (const float *)part);
-            DG_LAUNCHED("narrow_wgrad_final");
         } else {
-            DG_ARG(!pl.ntile, "the narrow filter-gradient tile kernel needs ldx %% 4 == 0 and a 16-byte aligned x");
             a.splits = pl.splits; a.kchunk = pl.kchunk;
             hipLaunchKernelGGL(k_narrow_wgrad, dim3(d->g.kh * d->g.kw * ((d->g.Ci + 255) / 256), pl.splits), dim3(256), 0, s, a);
             DG_LAUNCHED("narrow_wgrad");

@@ -263,6 +263,9 @@ SR_CONVS = [
     ("tile32.s1", 2, 128, 128, 32, 32, 3, 1, True, None),
     ("tile32.s2", 4, 128, 128, 32, 32, 3, 2, True, None),
     ("tile32.fwd256", 8, 256, 256, 32, 32, 3, 2, True, None),
+    # 3-channel input conv (SR discriminators' d1): filter gradient on the row-segment kernel
+    ("ntile.in3", 2, 128, 128, 3, 32, 3, 1, True, None),
+    ("ntile.in3.ragged", 3, 37, 101, 3, 48, 3, 1, True, None),
 ]
 
 
