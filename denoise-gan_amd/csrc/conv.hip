@@ -1268,7 +1268,7 @@ static bool cfg_vec(const ConvGeom &g, int mode, int bk) {
 //   rounds x (blocks per CU x per-block MFMA work) / (CU peak x occupancy efficiency)
 // + split-K slab traffic, where blocks per CU = min(resident limit, blocks / 256).
 // Plan features switched off for same-box A/B runs: DG_PLAN_DISABLE is a
-// comma-separated list of {shortk, small, co1, tlast, direct, halo, halo2, halo4, xcd_phase, narrow_px, ntile,
+// comma-separated list of {shortk, small, co1, tlast, direct, halo, halo2, halo4, halo_f16, xcd_phase, narrow_px, ntile,
 // tile32, f16planes}
 // (read when a descriptor is planned; unset in production runs)
 static bool plan_off(const char *feature) {
@@ -1469,9 +1469,12 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     // the input gradient 0.666 vs 0.690)
     const bool h44 = mode == MODE_DGRAD && g.kh == 4 && g.kw == 4 && g.sh == 1 && g.sw == 1 &&
                      pl.K % 256 == 0 && !plan_off("halo4");
-    if (pl.x6 == 1 && (h33 || h22 || h44) && !plan_off("halo")) {
-        // each input pixel staged once per 16-channel chunk instead of once per tap
+    // (fp16: 3x3 only, 32-channel chunks; the forward's pool epilogue stays bf16x6)
+    const bool hf16 = pl.x6 == 2 && h33 && pl.K % 288 == 0 && pl.N % 16 == 0 && !plan_off("halo_f16");
+    if ((pl.x6 == 1 && (h33 || h22 || h44) || hf16) && !plan_off("halo")) {
+        // each input pixel staged once per channel chunk instead of once per tap
         const int ntap = h33 ? 9 : (h44 ? 16 : 4);
+        const int bkc = pl.x6 == 2 ? 32 : 16;   // channels per chunk
         int Hout, Wout;
         if (mode == MODE_FWD) { Hout = g.Ho; Wout = g.Wo; }
         else if (h33 || h44) { Hout = g.H; Wout = g.W; }
@@ -1485,13 +1488,13 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         pl.mtiles = g.N * pl.htx * pl.hty;
         pl.ntiles = (pl.N + pl.cfg - 1) / pl.cfg;
         // split-K over channel chunks (at least two per split) until ~2 blocks per CU
-        const long nch = pl.K / (16 * ntap), blocks = (long)pl.mtiles * pl.ntiles * pl.nphase;
+        const long nch = pl.K / (bkc * ntap), blocks = (long)pl.mtiles * pl.ntiles * pl.nphase;
         long splits = 1;
         // (same-box A/B of the target: 256 -0.2%, 1024 -0.8% full step vs 512)
         constexpr long target = 512;
         while (blocks * splits < target && splits * 4 <= nch) splits *= 2;
         const long cps = (nch + splits - 1) / splits;
-        pl.kchunk = (int)(cps * 16 * ntap);
+        pl.kchunk = (int)(cps * bkc * ntap);
         pl.splits = (int)((nch + cps - 1) / cps);
     }
     pl.vec = pl.x6 ? 1 : cfg_vec(g, mode, kCfgs[pl.cfg].bk);
@@ -1507,7 +1510,7 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     pl.gemm_bytes = pl.ws_bytes;
     if (getenv("DG_PLAN_DEBUG"))
         fprintf(stderr, "[dg plan] mode %d M=%d N=%d K=%d -> %s cfg %d splits %d\n", mode, pl.M, pl.N, pl.K,
-                pl.halo == 2 ? "x6h2" : pl.halo == 4 ? "x6h4" : pl.halo ? "x6h" : (pl.x6 == 2 ? "f16" : (pl.x6 ? "x6" : "fp32")),
+                pl.halo == 2 ? "x6h2" : pl.halo == 4 ? "x6h4" : pl.halo ? (pl.x6 == 2 ? "f16h" : "x6h") : (pl.x6 == 2 ? "f16" : (pl.x6 ? "x6" : "fp32")),
                 pl.cfg, pl.splits);
     return pl;
 }
@@ -1876,7 +1879,8 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
         fastdiv_magic((unsigned)a.g.Ho, a.mg_ho, a.sh_ho);
         DG_ARG(a.yp == nullptr, "fp16 conv math writes no bf16x6 output planes");
         dim3 grid(pl.mtiles * pl.ntiles, pl.nphase * pl.splits);
-        launch_gemm_f16(mode, pl.cfg, grid, a, s);
+        if (pl.halo) launch_gemm_x6h(mode, pl.cfg, 3, grid, a, pl.htx, pl.hty, s, 2);
+        else launch_gemm_f16(mode, pl.cfg, grid, a, s);
         DG_LAUNCHED("conv_gemm_f16");
         return finish_splitk(mode, pl, a, s);
     }

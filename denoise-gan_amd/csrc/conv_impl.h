@@ -287,7 +287,8 @@ void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t
 // the halo-tiled bf16x6 kernel (conv_x6h.hip): kt 3 = stride-1 3x3 FWD / DGRAD, kt 2 = the
 // sub-pixel phases of a stride-2 4x4 DGRAD (grid y = phase * splits + split); bn = 64 | 128.
 // a.pidx != NULL selects the fused max-pool epilogue (FWD, one split, output Ho % 8 == 0, Wo % 16 == 0)
-void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int tiles_x, int tiles_y, hipStream_t s);
+void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int tiles_x, int tiles_y, hipStream_t s,
+                     int ni = 3);
 // fp32 [rows][ld] (first C columns, C % 8 == 0) -> bf16 hi/mid/lo planes [rows][C]
 void launch_split3(const float *src, int ld, long rows, int C, unsigned short *dst, hipStream_t s);
 // the fp16 conv math (DG_MATH_FP16): one fp16 plane [rows][C] and its GEMM (kF16Cfgs)

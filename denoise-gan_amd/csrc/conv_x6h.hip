@@ -51,12 +51,12 @@ constexpr bool kTapsColMajor = false;
 #else
 constexpr bool kTapsColMajor = true;
 #endif
-template <int KT>
+template <int KT, int NPL = 3>
 struct HaloGeom {
     static constexpr int HH = HX_PH + KT - 1, HW = HX_PW + KT - 1;
     static constexpr int HPX = HH * HW;
     static constexpr int HPL = (HPX * 32 + 1023) / 1024 * 1024;  // bytes per halo plane image
-    static constexpr int HDMA = 3 * HPL / 1024;                   // one-KiB DMAs per halo
+    static constexpr int HDMA = NPL * HPL / 1024;                 // one-KiB DMAs per halo
     static constexpr int NTAP = KT * KT;
 };
 
@@ -146,27 +146,33 @@ __device__ __forceinline__ void for_taps(F &&f, std::integer_sequence<int, T...>
     (f(std::integral_constant<int, T>{}), ...);
 }
 
-template <int MODE, int BN, bool POOL, int KT>
+// NI = 3: bf16x6 (three bf16 plane images per 16-channel chunk, three MFMAs
+// per fragment pair); NI = 2: fp16 (mixed_float16 policy): a chunk is 32
+// channels, its two 16-channel halves are the two plane images and one
+// v_mfma_f32_16x16x32_f16 covers them
+template <int MODE, int BN, bool POOL, int KT, int NI = 3>
 __global__ void __launch_bounds__(256, 2)
 k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "forward or input gradient");
     static_assert(!POOL || MODE == MODE_FWD, "the pool epilogue is a forward epilogue");
     static_assert(KT == 3 || (KT != 3 && MODE == MODE_DGRAD),
                   "3x3 stride 1, or a stride-1 4x4 / stride-2 4x4-phase input gradient");
-    using HG = HaloGeom<KT>;
+    static_assert(NI == 3 || (NI == 2 && KT == 3 && !POOL), "fp16: 3x3 stride 1, no pool epilogue");
+    constexpr int NPL = NI == 3 ? 3 : 2;        // plane images per chunk
+    using HG = HaloGeom<KT, NPL>;
     constexpr int NTAP = HG::NTAP;
     constexpr int NB = NTAP % 3 == 0 ? 3 : 4;   // weight K-tile buffers: a tap position owns one
     static_assert(NTAP % NB == 0, "tap positions line up with the weight buffers across chunks");
-    constexpr int BK = 16, NW = 4;
+    constexpr int BK = NI == 3 ? 16 : 32, NW = 4;   // channels per chunk
     constexpr int WTM = 64, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
     constexpr bool B_KC = MODE == MODE_DGRAD;
-    constexpr int BPL = BN * 32 + 96, BBUF = 3 * BPL;
-    constexpr int B_SL = 3 * BN / 32, B_NJ = (B_SL + NW - 1) / NW;
+    constexpr int BPL = BN * 32 + 96, BBUF = NPL * BPL;
+    constexpr int B_SL = NPL * BN / 32, B_NJ = (B_SL + NW - 1) / NW;
     constexpr int H_NJ = (HG::HDMA + NW - 1) / NW;          // halo pieces per wave
     constexpr int PPT = (H_NJ + NTAP - 2) / (NTAP - 1);     // pieces per K-tile, none at the last tap
     static_assert((H_NJ - 1) / PPT < NTAP - 1, "the next chunk's halo lands by the chunk's last K-tile");
 
-    __shared__ __attribute__((aligned(16))) char hal[2][3 * HG::HPL];
+    __shared__ __attribute__((aligned(16))) char hal[2][NPL * HG::HPL];
     __shared__ __attribute__((aligned(16))) char bs0[BBUF];
     __shared__ __attribute__((aligned(16))) char bs1[BBUF];
     __shared__ __attribute__((aligned(16))) char bs2[BBUF];
@@ -211,7 +217,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         ox = tx * HX_PW + ow - (KT - 1);
     }
     if (ty * HX_PH >= Hout || tx * HX_PW >= Wout) return;   // block-uniform: a smaller phase grid
-    // channel chunks of this split (kchunk is a multiple of NTAP taps x 16 channels)
+    // channel chunks of this split (kchunk is a multiple of NTAP taps x BK channels)
     const int nch = p.K / (NTAP * BK);
     const int cbeg = split * (p.kchunk / (NTAP * BK));
     const int cend = min(nch, cbeg + p.kchunk / (NTAP * BK));
@@ -259,12 +265,14 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         if (hp < HG::HPX) {
             const int hr = hp / HG::HW, hc = hp - hr * HG::HW;
             const int iy = oy + hr, ix = ox + hc;
+            // (bf16x6 pixel rows: per 16 channels 3 x 16 plane values; fp16: the
+            // channel row itself, plane image pl = channel half pl of the chunk)
             if ((unsigned)iy < (unsigned)Hin && (unsigned)ix < (unsigned)Win)
-                hoff[s] = ((((nimg * Hin + iy) * Win + ix) * (3 * p.lda)) + 16 * pl + 8 * hh) * 2;
+                hoff[s] = ((((nimg * Hin + iy) * Win + ix) * (NI == 3 ? 3 * p.lda : p.lda)) + 16 * pl + 8 * hh) * 2;
         }
     }
     auto issue_h = [&](int s, int chunk, char *hb) __attribute__((always_inline)) {
-        dma(rA, hb + hdst[s], hoff[s] >= 0 ? (unsigned)(hoff[s] + chunk * 96) : DG_OOB);
+        dma(rA, hb + hdst[s], hoff[s] >= 0 ? (unsigned)(hoff[s] + chunk * (NI == 3 ? 96 : 64)) : DG_OOB);
     };
 
     // ---- weight K-tile slots (as conv_x6.hip): FWD RC image [16 k][BN],
@@ -286,20 +294,22 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
             const int swz = BN >= 128 ? 8 * ((r & 3) | (((r >> 3) & 1) << 2)) : 8 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
             const int col = n0 + 2 * (pdw ^ swz);
             bok[j] = col < p.N;
-            bbase[j] = (r * (3 * p.ldb) + (col >> 4) * 48 + 16 * plane + (col & 8)) * 2;
+            if constexpr (NI == 3) bbase[j] = (r * (3 * p.ldb) + (col >> 4) * 48 + 16 * plane + (col & 8)) * 2;
+            else bbase[j] = ((16 * plane + r) * p.ldb + col) * 2;   // image = k rows 16 plane ..
         } else {
             const int r = pos >> 5, c = (pos >> 4) & 1;
             const int ci = n0 + r;
             bok[j] = ci < p.N;
-            bbase[j] = (ci * (3 * p.ldb) + 16 * plane + 8 * c) * 2;
+            bbase[j] = (ci * (NI == 3 ? 3 * p.ldb : p.ldb) + 16 * plane + 8 * c) * 2;
         }
     }
     // tap position T of chunk c: FWD rows (tap*Ci + 16c) of w[(a,b,ci)][co];
     // DGRAD rows ci of w[i,j] at co-chunk c
     auto issue_b = [&](int T, int chunk, char *bs) __attribute__((always_inline)) {
         int delta;
-        if constexpr (!B_KC) delta = ((tap_w[T] * g.Ci + chunk * BK) * (3 * p.ldb)) * 2;
-        else delta = (tap_w[T] * g.Ci * (3 * p.ldb) + chunk * 48) * 2;
+        constexpr int LW = NI == 3 ? 3 : 1;   // weight row stride in units of ldb
+        if constexpr (!B_KC) delta = ((tap_w[T] * g.Ci + chunk * BK) * (LW * p.ldb)) * 2;
+        else delta = (tap_w[T] * g.Ci * (LW * p.ldb) + chunk * (NI == 3 ? 48 : 32)) * 2;
 #pragma unroll
         for (int j = 0; j < B_NJ; ++j) {
             dma(rB, bs + bdst[j], bok[j] ? (unsigned)(bbase[j] + delta) : DG_OOB);
@@ -336,7 +346,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         auto load_row = [&](int r) __attribute__((always_inline)) {
             const int r0 = (wm * TM + r) * HG::HW + db;
             fm[r] = x6_kc_frag(H0, H1, r0, lane);
-            fl[r] = x6_kc_frag(H0, H2, r0, lane);
+            if constexpr (NI == 3) fl[r] = x6_kc_frag(H0, H2, r0, lane);
         };
         if constexpr (ta == 0 || !kTapsColMajor) {   // a new filter column: its first tap's TM rows
 #pragma unroll
@@ -350,33 +360,46 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
             const int c0 = wn * WTN + b * 16;
             if constexpr (B_KC) {
                 b1[b] = x6_kc_frag(B0, B1, c0, lane);
-                b2[b] = x6_kc_frag(B1, B0, c0, lane);
-                b3[b] = x6_kc_frag(B2, B0, c0, lane);
+                if constexpr (NI == 3) {
+                    b2[b] = x6_kc_frag(B1, B0, c0, lane);
+                    b3[b] = x6_kc_frag(B2, B0, c0, lane);
+                }
             } else {
                 b1[b] = x6_rc_frag<BN>(B0, B1, c0, lane);
-                b2[b] = x6_rc_frag<BN>(B1, B0, c0, lane);
-                b3[b] = x6_rc_frag<BN>(B2, B0, c0, lane);
+                if constexpr (NI == 3) {
+                    b2[b] = x6_rc_frag<BN>(B1, B0, c0, lane);
+                    b3[b] = x6_rc_frag<BN>(B2, B0, c0, lane);
+                }
             }
         }
 #pragma unroll
         for (int s = H0P; s < H0P + NH; ++s) issue_h(s, chunk + 1, hn);
         if constexpr (T + 2 < NTAP) issue_b(T + 2, chunk, bn);
         else issue_b(T + 2 - NTAP, chunk + 1, bn);
+        if constexpr (NI == 2) {
 #pragma unroll
-        for (int a = 0; a < TM; ++a)
+            for (int a = 0; a < TM; ++a)
 #pragma unroll
-            for (int b = 0; b < TN; ++b)
-                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fm[a + da], b1[b], acc[a][b], 0, 0, 0);
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fm[a + da]),
+                                                                      __builtin_bit_cast(f16x8, b1[b]), acc[a][b], 0, 0, 0);
+        } else {
 #pragma unroll
-        for (int a = 0; a < TM; ++a)
+            for (int a = 0; a < TM; ++a)
 #pragma unroll
-            for (int b = 0; b < TN; ++b)
-                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fm[a + da], b2[b], acc[a][b], 0, 0, 0);
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fm[a + da], b1[b], acc[a][b], 0, 0, 0);
 #pragma unroll
-        for (int a = 0; a < TM; ++a)
+            for (int a = 0; a < TM; ++a)
 #pragma unroll
-            for (int b = 0; b < TN; ++b)
-                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fl[a + da], b3[b], acc[a][b], 0, 0, 0);
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fm[a + da], b2[b], acc[a][b], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fl[a + da], b3[b], acc[a][b], 0, 0, 0);
+        }
         // DMAs issued in this K-tile may stay in flight; everything older
         // (the next weight tile, and at the last tap the whole next halo) has landed
         wait_dma_c<B_NJ + NH>();
@@ -406,7 +429,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     barrier();
 
     constexpr int STAGE = 16 * (WTN + 4);
-    static_assert(NW * STAGE * 4 <= 2 * 3 * HG::HPL, "epilogue staging fits in the halo buffers");
+    static_assert(NW * STAGE * 4 <= 2 * NPL * HG::HPL, "epilogue staging fits in the halo buffers");
     float *stage = reinterpret_cast<float *>(hal0) + wid * STAGE;
     // patch row -> output pixel; slab rows: FWD / stride-1 DGRAD pixels, a
     // phase's GEMM rows otherwise (as k_splitk_reduce maps them)
@@ -427,10 +450,20 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         conv_epilogue16<MODE, TM, TN>(p, acc, wm * WTM, n0 + wn * WTN, rowmap, phase, split, lane, stage);
 }
 
-void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int tiles_x, int tiles_y, hipStream_t s) {
+void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int tiles_x, int tiles_y, hipStream_t s,
+                     int ni) {
     const dim3 blk(256);
 #define DG_X6H(M_, B_, P_, K_) hipLaunchKernelGGL((k_conv_gemm_x6h<M_, B_, P_, K_>), grid, blk, 0, s, a, tiles_x, tiles_y)
-    if (mode == MODE_FWD && a.pidx) {
+#define DG_F16H(M_, B_) hipLaunchKernelGGL((k_conv_gemm_x6h<M_, B_, false, 3, 2>), grid, blk, 0, s, a, tiles_x, tiles_y)
+    if (ni == 2) {   // fp16: 3x3 stride 1, forward or input gradient
+        if (mode == MODE_FWD) {
+            if (bn == 128) DG_F16H(MODE_FWD, 128);
+            else DG_F16H(MODE_FWD, 64);
+        } else {
+            if (bn == 128) DG_F16H(MODE_DGRAD, 128);
+            else DG_F16H(MODE_DGRAD, 64);
+        }
+    } else if (mode == MODE_FWD && a.pidx) {
         if (bn == 128) DG_X6H(MODE_FWD, 128, true, 3);
         else DG_X6H(MODE_FWD, 64, true, 3);
     } else if (mode == MODE_FWD) {
@@ -446,6 +479,7 @@ void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int
         else DG_X6H(MODE_DGRAD, 64, false, 3);
     }
 #undef DG_X6H
+#undef DG_F16H
 }
 
 }  // namespace dg

@@ -9,6 +9,6 @@ for r in 1 2; do
     tag=$(echo "$v" | tr -c 'A-Za-z0-9_\n' '_')
     if [ "$v" = base ]; then envs=""; else envs="$v"; fi
     env $envs timeout -k 10 300 $B > gpurun_out/ab_${tag}_$r.json 2> gpurun_out/ab_${tag}_$r.err || exit 1
-    echo "$v $r $(python -c "import json;d=json.loads(open('gpurun_out/ab_${tag}_$r.json').read().strip().splitlines()[-1]);print(d['value'],d.get('core',{}).get('value'),d['roofline']['conv_launch_ms_per_step'])")"
+    echo "$v $r $(python -c "import json;d=json.loads(open('gpurun_out/ab_${tag}_$r.json').read().strip().splitlines()[-1]);print(d['value'],(d.get('core') or {}).get('value'),d['roofline']['conv_launch_ms_per_step'])")"
   done
 done

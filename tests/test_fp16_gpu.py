@@ -36,6 +36,11 @@ F16_CONVS = [
     # fp16 128x32 tiles in all three ops (32-column RC images)
     ("tile32.s1", 2, 128, 128, 32, 32, 3, 1),
     ("tile32.s2", 4, 96, 96, 32, 32, 3, 2),
+    # fp16 halo tiles (conv_x6h.hip NI = 2): ragged 8 x 16 patches, several 32-channel
+    # chunks, split-K over chunks on a small grid, BN 64 and 128
+    ("f16h.ragged", 2, 20, 37, 96, 64, 3, 1),
+    ("f16h.splitk", 1, 6, 6, 512, 512, 3, 1),
+    ("f16h.bn128", 2, 24, 24, 128, 160, 3, 1),
 ]
 
 

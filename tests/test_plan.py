@@ -21,14 +21,17 @@ LAYERS = {
     "G.up7": (32, 64, 64, 256, 64, 4, 2, "same", True),
     "G.down1": (32, 256, 256, 3, 64, 4, 2, "same", False),
     "V.b3c2": (32, 64, 64, 256, 256, 3, 1, "same", False),
+    # SRGAN's VGG19 under mixed_float16 (bs32: generated + real batches, 96^2)
+    "S.vgg_f16": (64, 96, 96, 128, 128, 3, 1, "same", False, "fp16"),
+    "S.res_f16": (32, 24, 24, 64, 64, 3, 1, "same", False, "fp16"),
 }
 
 SCRIPT = r"""
 import sys
 sys.path[:0] = [sys.argv[1]]
 from dgan.ops import ConvDesc
-N, H, W, ci, co, k, s, pad, tr = eval(sys.argv[2])
-ConvDesc(N, H, W, ci, co, k, s, pad, tr)
+N, H, W, ci, co, k, s, pad, tr, *math = eval(sys.argv[2])
+ConvDesc(N, H, W, ci, co, k, s, pad, tr, math=math[0] if math else None)
 """
 
 
@@ -56,11 +59,17 @@ def _plans(spec):
     ("G.down1", {"0": "small", "2": "small"}),
     # VGG19 3x3: halo tiles both ways
     ("V.b3c2", {"0": "x6h", "1": "x6h"}),
+    # fp16 3x3 stride 1 (32-channel chunks): the halo tiles' fp16 variant both ways
+    ("S.vgg_f16", {"0": "f16h", "1": "f16h"}),
+    ("S.res_f16", {"0": "f16h", "1": "f16h"}),
 ])
 def test_plan_kernel_family(layer, expect):
     got = {}
     for mode, kind in _plans(LAYERS[layer]):
-        got.setdefault(mode, kind)
+        if len(LAYERS[layer]) > 9:
+            got[mode] = kind   # a math= descriptor plans the default math first, its own last
+        else:
+            got.setdefault(mode, kind)
     for mode, kind in expect.items():
         assert got.get(mode) == kind, (layer, got)
 
