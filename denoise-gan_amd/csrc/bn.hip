@@ -218,86 +218,6 @@ k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, i
     }
 }
 
-// The same finalize over row-group partials written by the producing conv's
-// epilogue (dg_conv_fwd_bnstats): channel-major [3][C][R] (n, mean, M2) and
-// segs[R], the segment of each group (-1: no rows).  L lanes per channel
-// (32, or 256 for long partial rows), lane sums combined in a fixed order.
-template <int L>
-__device__ __forceinline__ float lane_sum_l(float v, float *sh) {
-    constexpr int W = L < 64 ? L : 64;   // lanes of one channel inside a wave
-#pragma unroll
-    for (int o = 1; o < W; o <<= 1) v += __shfl_xor(v, o);
-    if constexpr (L <= 64) {
-        // (every lane of the group holds a sum; all take the first lane's)
-        return __shfl(v, (threadIdx.x & 63) & ~(W - 1));
-    } else {
-        __syncthreads();
-        if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
-        __syncthreads();
-        float s = 0.f;
-#pragma unroll
-        for (int w = 0; w < L / 64; ++w) s += sh[w];
-        return s;
-    }
-}
-
-template <int L>
-__global__ void __launch_bounds__(256)
-k_bn_stats_final_g(const float *st, const int *segs, int R, int C, int S, const float *gamma, const float *beta,
-                   float *save_mean, float *save_invstd, float *mm, float *mv, float momentum, float eps,
-                   float *scale, float *shift) {
-    __shared__ float sh[8];
-    constexpr int CPB = 256 / L;
-    const int cl = threadIdx.x / L, ln = threadIdx.x % L;
-    const int c = blockIdx.x * CPB + cl;
-    const bool cok = c < C;
-    const long NC = (long)C * R;
-    const float *pn = st + (long)c * R, *pmean = pn + NC, *pm2 = pn + 2 * NC;
-    float mmc = 0.f, mvc = 0.f;
-    if (ln == 0 && cok) {
-        if (mm) mmc = mm[c];
-        if (mv) mvc = mv[c];
-    }
-    for (int sg = 0; sg < S; ++sg) {
-        float sn = 0.f, sm = 0.f;
-        if (cok)
-            for (int r = ln; r < R; r += L)
-                if (segs[r] == sg) {
-                    const float n = pn[r];
-                    sn += n;
-                    sm += n * pmean[r];
-                }
-        const float n = lane_sum_l<L>(sn, sh);
-        const float msum = lane_sum_l<L>(sm, sh);
-        const float mu = n > 0.f ? msum / n : 0.f;
-        float q = 0.f;
-        if (cok)
-            for (int r = ln; r < R; r += L)
-                if (segs[r] == sg) {
-                    const float d = pmean[r] - mu;
-                    q += pm2[r] + pn[r] * d * d;
-                }
-        const float m2 = lane_sum_l<L>(q, sh);
-        if (ln != 0 || !cok) continue;
-        const float var = n > 0.f ? m2 / n : 0.f;
-        const float inv = 1.f / sqrtf(var + eps);
-        const int sc = sg * C + c;
-        if (save_mean) save_mean[sc] = mu;
-        if (save_invstd) save_invstd[sc] = inv;
-        const float g = gamma ? gamma[c] : 1.f;
-        const float b = beta ? beta[c] : 0.f;
-        scale[sc] = g * inv;
-        shift[sc] = b - mu * g * inv;
-        mmc -= (mmc - mu) * (1.f - momentum);
-        const float unb = n > 1.f ? m2 / (n - 1.f) : m2;
-        mvc -= (mvc - unb) * (1.f - momentum);
-    }
-    if (ln == 0 && cok) {
-        if (mm) mm[c] = mmc;
-        if (mv) mv[c] = mvc;
-    }
-}
-
 // S segments of M rows: segment s uses its own scale / shift ([S][C]) and
 // dropout seed (seed + s * seed_stride; the mask index restarts per segment)
 template <int V>
@@ -520,32 +440,6 @@ static bool vec4_ok(int C, std::initializer_list<std::pair<const void *, int>> t
     return true;
 }
 
-// the apply pass of a training forward: normalise with [S][C] scale / shift, act,
-// dropout, z and up to two consumers' bf16x6 planes
-static int bn_apply_launch(int S, int M, int C, const float *y, int ldy, const float *scale, const float *shift,
-                           float *z, int ldz, int act, float alpha, float drop_rate, uint32_t drop_seed,
-                           uint32_t drop_seed_stride, const int32_t *step_dev, void *zp0, int zp0C, int zp0col,
-                           void *zp1, int zp1C, int zp1col, hipStream_t s) {
-    const bool av4 = vec4_ok(C, {{y, ldy}, {z, ldz}});
-    unsigned short *p0 = (unsigned short *)zp0, *p1 = (unsigned short *)zp1;
-    auto pl_ok = [&](const unsigned short *p, int pc, int col) {
-        return !p || (av4 && pc % 16 == 0 && col % 16 == 0 && C % 16 == 0 && col + C <= pc && (((uintptr_t)p) & 15) == 0);
-    };
-    DG_ARG(pl_ok(p0, zp0C, zp0col) && pl_ok(p1, zp1C, zp1col),
-           "z planes need float4-aligned tensors, C and the column %% 16 == 0, col + C <= planes C, 16-byte alignment");
-    const long MT = (long)S * M;
-    if (av4)
-        hipLaunchKernelGGL(k_bn_apply<4>, dim3(ew_grid(MT * C / 4)), dim3(256), 0, s, y, ldy, (long)M, S, C, scale,
-                           shift, z, ldz, act, alpha, drop_rate, drop_seed, drop_seed_stride, step_dev, p0, zp0C,
-                           zp0col, p1, zp1C, zp1col);
-    else
-        hipLaunchKernelGGL(k_bn_apply<1>, dim3(ew_grid(MT * C)), dim3(256), 0, s, y, ldy, (long)M, S, C, scale, shift,
-                           z, ldz, act, alpha, drop_rate, drop_seed, drop_seed_stride, step_dev, p0, zp0C, zp0col,
-                           p1, zp1C, zp1col);
-    DG_LAUNCHED("bn_apply");
-    return DG_OK;
-}
-
 }  // namespace dg
 
 extern "C" {
@@ -606,32 +500,24 @@ int dg_bn_fwd_train_seg(int S, int M, int C, const float *y, int ldy, const floa
     hipLaunchKernelGGL(dg::k_bn_stats_final, dim3(dg_cdiv(C, dg::FIN_C)), dim3(256), 0, s, pn, pmean, pm2, bp.R, C, S,
                        gamma, beta, save_mean, save_invstd, moving_mean, moving_var, momentum, eps, scale, shift);
     DG_LAUNCHED("bn_stats_final");
-    return dg::bn_apply_launch(S, M, C, y, ldy, scale, shift, z, ldz, act, alpha, drop_rate, drop_seed,
-                               drop_seed_stride, step_dev, zp0, zp0C, zp0col, zp1, zp1C, zp1col, s);
-}
-
-int dg_bn_fwd_train_stats(int S, int M, int C, const float *stats, const int *segs, int R, const float *y, int ldy,
-                          const float *gamma, const float *beta, float *save_mean, float *save_invstd,
-                          float *moving_mean, float *moving_var, float momentum, float eps, float *z, int ldz,
-                          int act, float alpha, float drop_rate, uint32_t drop_seed, uint32_t drop_seed_stride,
-                          const int32_t *step_dev, void *zp0, int zp0C, int zp0col, void *zp1, int zp1C, int zp1col,
-                          void *ws, size_t ws_bytes, dg_stream_t stream) {
-    DG_ARG(y && z && ws && stats && segs, "NULL tensor");
-    DG_ARG(S >= 1 && S <= 8 && M > 0 && C > 0 && R > 0 && ldy >= C && ldz >= C, "bad shape");
-    DG_ARG(ws_bytes >= (size_t)2 * S * C * sizeof(float), "workspace too small");
-    DG_ARG(drop_rate >= 0.f && drop_rate < 1.f, "bad dropout rate");
-    hipStream_t s = (hipStream_t)stream;
-    float *scale = (float *)ws, *shift = scale + (size_t)S * C;
-    // (256 lanes per channel once a lane would walk more than 32 groups)
-    if (R > 1024)
-        hipLaunchKernelGGL(dg::k_bn_stats_final_g<256>, dim3(C), dim3(256), 0, s, stats, segs, R, C, S, gamma, beta,
-                           save_mean, save_invstd, moving_mean, moving_var, momentum, eps, scale, shift);
+    const bool av4 = dg::vec4_ok(C, {{y, ldy}, {z, ldz}});
+    unsigned short *p0 = (unsigned short *)zp0, *p1 = (unsigned short *)zp1;
+    auto pl_ok = [&](const unsigned short *p, int pc, int col) {
+        return !p || (av4 && pc % 16 == 0 && col % 16 == 0 && C % 16 == 0 && col + C <= pc && (((uintptr_t)p) & 15) == 0);
+    };
+    DG_ARG(pl_ok(p0, zp0C, zp0col) && pl_ok(p1, zp1C, zp1col),
+           "z planes need float4-aligned tensors, C and the column %% 16 == 0, col + C <= planes C, 16-byte alignment");
+    const long MT = (long)S * M;
+    if (av4)
+        hipLaunchKernelGGL(dg::k_bn_apply<4>, dim3(dg::ew_grid(MT * C / 4)), dim3(256), 0, s, y, ldy, (long)M, S, C,
+                           scale, shift, z, ldz, act, alpha, drop_rate, drop_seed, drop_seed_stride, step_dev, p0,
+                           zp0C, zp0col, p1, zp1C, zp1col);
     else
-        hipLaunchKernelGGL(dg::k_bn_stats_final_g<32>, dim3(dg_cdiv(C, 8)), dim3(256), 0, s, stats, segs, R, C, S,
-                           gamma, beta, save_mean, save_invstd, moving_mean, moving_var, momentum, eps, scale, shift);
-    DG_LAUNCHED("bn_stats_final_g");
-    return dg::bn_apply_launch(S, M, C, y, ldy, scale, shift, z, ldz, act, alpha, drop_rate, drop_seed,
-                               drop_seed_stride, step_dev, zp0, zp0C, zp0col, zp1, zp1C, zp1col, s);
+        hipLaunchKernelGGL(dg::k_bn_apply<1>, dim3(dg::ew_grid(MT * C)), dim3(256), 0, s, y, ldy, (long)M, S, C, scale,
+                           shift, z, ldz, act, alpha, drop_rate, drop_seed, drop_seed_stride, step_dev, p0, zp0C,
+                           zp0col, p1, zp1C, zp1col);
+    DG_LAUNCHED("bn_apply");
+    return DG_OK;
 }
 
 int dg_bn_fwd_infer(int M, int C, const float *y, int ldy, const float *gamma, const float *beta,

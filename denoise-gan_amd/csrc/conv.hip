@@ -1269,7 +1269,7 @@ static bool cfg_vec(const ConvGeom &g, int mode, int bk) {
 // + split-K slab traffic, where blocks per CU = min(resident limit, blocks / 256).
 // Plan features switched off for same-box A/B runs: DG_PLAN_DISABLE is a
 // comma-separated list of {shortk, small, co1, tlast, direct, halo, halo2, halo4, halo_f16, xcd_phase, narrow_px, ntile,
-// tile32, f16planes, bnstats}
+// tile32, f16planes}
 // (read when a descriptor is planned; unset in production runs)
 static bool plan_off(const char *feature) {
     const char *list = getenv("DG_PLAN_DISABLE");
@@ -1706,43 +1706,12 @@ static bool pool_fusable(const dg_conv_desc_s *d, int act) {
            (act == DG_ACT_NONE || act == DG_ACT_RELU || act == DG_ACT_LRELU);
 }
 
-// BatchNorm statistics of a forward's output from its GEMM epilogue (dg_conv_fwd_bnstats)
-struct BnsOut {
-    float *stats;
-    int *segs;
-    int S;
-};
-
-// row groups of the forward plan's BatchNorm statistics for S image segments, 0 when
-// the plan cannot write them: a one-split tiled bf16x6 / fp16 GEMM (the halo-tiled
-// kernel's patches lie inside one image; a generic tile's row groups -- WTM rows of a
-// phase -- must not straddle a segment boundary)
-static long bnstats_groups(const dg_conv_desc_s *d, int S) {
-    const OpPlan &pl = d->plan[DG_OP_FWD];
-    const ConvGeom &g = d->g;
-    if ((pl.x6 != 1 && pl.x6 != 2) || pl.splits != 1 || pl.narrow || pl.small || pl.co1 || pl.tlast || pl.ntile ||
-        pl.direct || d->rc[DG_OP_FWD].on || S < 1 || g.N % S || plan_off("bnstats"))
-        return 0;
-    if (pl.halo) return (long)pl.nphase * pl.mtiles * 2;
-    const TileCfg &t = (pl.x6 == 2 ? kF16Cfgs : kX6Cfgs)[pl.cfg];
-    const int wtm = t.bm / t.wgm;
-    long seg_rows;
-    if (engine_mode(d, DG_OP_FWD) == MODE_FWD) {
-        seg_rows = (long)(g.N / S) * g.Ho * g.Wo;
-    } else {
-        if (g.H % g.sh || g.W % g.sw) return 0;   // equal phase grids
-        seg_rows = (long)(g.N / S) * (g.H / g.sh) * (g.W / g.sw);
-    }
-    if (seg_rows % wtm) return 0;
-    return (long)pl.nphase * pl.mtiles * t.wgm;
-}
-
 static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, const float *B, int ldb,
                       float *C, int ldc, const float *bias, float beta, int act, float alpha,
                       void *ws, size_t ws_bytes, hipStream_t s, const float *mz = nullptr, int ldmz = 0,
                       int mact = DG_ACT_NONE, float malpha = 0.f, const PlaneRefs *pr = nullptr,
                       unsigned short *yp = nullptr, const PoolOut *po = nullptr,
-                      const unsigned short *mzp = nullptr, const BnsOut *bo = nullptr) {
+                      const unsigned short *mzp = nullptr) {
     const int mode = engine_mode(d, op);
     const OpPlan &pl = d->plan[op];
     const size_t need = d->rc[op].on ? d->rc[op].bytes : pl.gemm_bytes;
@@ -1760,14 +1729,6 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
         DG_ARG(beta == 0.f, "the fused pool overwrites its output (beta must be 0)");
         a.pidx = po->idx; a.pool_y = po->y; a.ldpy = po->ldy;
         a.yp = po->planes; a.ypC = d->g.Co;
-    }
-    if (bo) {
-        const long R = bnstats_groups(d, bo->S);
-        DG_ARG(op == DG_OP_FWD && R > 0 && R < (1L << 31) && C && beta == 0.f && !po && bo->stats && bo->segs,
-               "this forward plan cannot write BatchNorm statistics (dg_conv_bnstats_groups), or no output / beta != 0");
-        a.bns = bo->stats; a.bnseg = bo->segs; a.bnsR = (int)R;
-        a.bns_img = d->g.N / bo->S;
-        a.bns_hw = engine_mode(d, op) == MODE_FWD ? d->g.Ho * d->g.Wo : d->g.H * d->g.W;
     }
     if (mzp) {
         // mask from the hi plane's sign: the small-Cin kernels read fp32 masks only
@@ -2156,32 +2117,6 @@ int dg_conv_fwd_pl(dg_conv_t d, const float *x, int ldx, const float *w, const f
     return dg::run_engine(d, DG_OP_FWD, x, ldx, w, d->transpose ? 0 : d->Cout, y, ldy, bias, beta, act, alpha, ws,
                           ws_bytes, (hipStream_t)stream, nullptr, 0, DG_ACT_NONE, 0.f, pr,
                           planes ? (unsigned short *)planes->out : nullptr);
-}
-
-int dg_conv_bnstats_groups(dg_conv_t d, int S, int *R) {
-    DG_ARG(d && R, "NULL argument");
-    *R = (int)dg::bnstats_groups(d, S);
-    return DG_OK;
-}
-
-int dg_conv_fwd_bnstats(dg_conv_t d, const float *x, int ldx, const float *w, const float *bias, float *y, int ldy,
-                        int act, float alpha, const dg_conv_planes_t *planes, int S, float *stats, int *segs,
-                        void *ws, size_t ws_bytes, dg_stream_t stream) {
-    DG_ARG(d && x && w && y && stats && segs, "NULL tensor");
-    DG_ARG(ldx >= d->Cin && ldy >= d->Cout, "pixel stride smaller than channels");
-    DG_ARG(act >= DG_ACT_NONE && act <= DG_ACT_SIGMOID, "unknown activation %d", act);
-    if (dg::bnstats_groups(d, S) <= 0) {
-        dg::set_error("forward plan cannot write BatchNorm statistics for %d segments (dg_conv_bnstats_groups)", S);
-        return DG_ERR_UNSUPPORTED;
-    }
-    dg::PlaneRefs r{};
-    const dg::PlaneRefs *pr;
-    int e = dg::plane_refs(d, DG_OP_FWD, planes, r, pr);
-    if (e != DG_OK) return e;
-    dg::BnsOut bo{stats, segs, S};
-    return dg::run_engine(d, DG_OP_FWD, x, ldx, w, d->transpose ? 0 : d->Cout, y, ldy, bias, 0.f, act, alpha, ws,
-                          ws_bytes, (hipStream_t)stream, nullptr, 0, DG_ACT_NONE, 0.f, pr,
-                          planes ? (unsigned short *)planes->out : nullptr, nullptr, nullptr, &bo);
 }
 
 int dg_conv_fwd_pool_ok(dg_conv_t d, int act, int *ok) {

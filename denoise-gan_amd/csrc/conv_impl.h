@@ -49,19 +49,7 @@ struct GemmArgs {
     const unsigned short *mzp; int mzpC;
     // 1: DGRAD phase blocks in the plain XCD order (A/B switch DG_PLAN_DISABLE=xcd_phase)
     int xcd_plain;
-    // optional BatchNorm statistics of the output, written by the epilogue of a
-    // one-split FWD / DGRAD GEMM (dg_conv_fwd_bnstats): per row group g (one
-    // wave's rows of a block tile, numbered by the kernel) and output column c,
-    // the valid rows' count, mean and M2 at bns[(k * N + c) * bnsR + g] for
-    // k = 0, 1, 2, and bnseg[g] = the image segment of the group's rows (image
-    // = pixel / bns_hw, segment = image / bns_img; -1: no rows)
-    float *bns; int *bnseg; int bnsR, bns_hw, bns_img;
 };
-
-// group g of a block with no output rows (a block-uniform early exit): no statistics
-__device__ __forceinline__ void bnstats_empty(const GemmArgs &p, int g0, int groups) {
-    if (p.bns && p.splits == 1 && (int)threadIdx.x < groups) p.bnseg[g0 + threadIdx.x] = -1;
-}
 
 // hi plane of element (pix, col) of a packed plane tensor, as a float
 __device__ __forceinline__ float hi_plane(const unsigned short *zp, int C, long pix, int col) {
@@ -203,16 +191,9 @@ struct RowPix {
 // 16 bytes per lane (C, the split-K slab, beta*C and the gradient mask) and
 // the row -> pixel map (`rowmap(rbase + local row)` -> RowPix) is evaluated
 // once per row per lane.
-//
-// bng: the wave's row group for the BatchNorm statistics (p.bns, one split):
-// each lane keeps count / shifted sums of its 4 columns over the rows it
-// stores (shift = its first value, as k_bn_stats_partial), the lanes of a
-// column combine by Chan's formula in a fixed butterfly order, and lane
-// c4 < C4 writes the wave's (n, mean, M2) of columns col .. col + 3.
 template <int MODE, int TM, int TN, class RowMap>
 __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[TM][TN], int rbase, int cbase,
-                                                RowMap rowmap, int phase, int split, int lane, float *stage,
-                                                int bng = 0) {
+                                                RowMap rowmap, int phase, int split, int lane, float *stage) {
     constexpr int WTN = 16 * TN;
     constexpr int LD = WTN + 4;   // padded staging row (floats): conflict-free writes
     constexpr int C4 = WTN / 4;   // float4 per row
@@ -224,10 +205,6 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
     const int c4 = lane % C4;
     const int col = cbase + c4 * 4;
     const bool full = col + 3 < p.N;
-    constexpr bool BNS = MODE != MODE_WGRAD;
-    const bool stats = BNS && p.bns != nullptr && p.splits == 1;
-    int sn = 0, spix = 0;
-    f32x4 sk = {0.f, 0.f, 0.f, 0.f}, s1 = sk, s2 = sk;
 #pragma clang loop unroll(full)
     for (int a = 0; a < TM; ++a) {
 #pragma unroll
@@ -301,67 +278,7 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
                         if (col + q < p.N) store_planes1(p.yp, p.ypC, pix, col + q, o[q]);
                 }
             }
-            if constexpr (BNS) {
-                if (stats) {
-                    if (sn == 0) {
-                        sk = o;
-                        spix = (int)pix;
-                    }
-                    ++sn;
-                    const f32x4 d = o - sk;
-                    s1 += d;
-                    s2 += d * d;
-                }
-            }
         }
-    }
-    if constexpr (BNS) {
-        if (!stats) return;
-        float n = (float)sn;
-        f32x4 mean = {0.f, 0.f, 0.f, 0.f}, m2 = mean;
-        if (sn > 0) {
-            mean = sk + s1 / n;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) m2[q] = fmaxf(s2[q] - s1[q] * s1[q] / n, 0.f);
-        }
-        int seg = sn > 0 ? (spix / p.bns_hw) / p.bns_img : -1;
-        // lanes lane ^ off (off >= C4) hold the same columns: fixed-order butterfly,
-        // the lower lane of each pair combining (itself, partner)
-#pragma unroll
-        for (int off = C4; off < 64; off <<= 1) {
-            const float nb = __shfl_xor(n, off);
-            f32x4 mb, qb;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                mb[q] = __shfl_xor(mean[q], off);
-                qb[q] = __shfl_xor(m2[q], off);
-            }
-            seg = max(seg, __shfl_xor(seg, off));
-            if ((lane & off) == 0 && nb > 0.f) {
-                if (n == 0.f) {
-                    mean = mb;
-                    m2 = qb;
-                } else {
-                    const float nt = n + nb, f = nb / nt;
-                    const f32x4 dd = mb - mean;
-                    mean += dd * f;
-                    m2 += qb + dd * dd * (n * f);
-                }
-                n += nb;
-            }
-        }
-        if (lane < C4) {
-            const long R = p.bnsR, NC = (long)p.N * R;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (col + q >= p.N) continue;
-                float *e = p.bns + (long)(col + q) * R + bng;
-                e[0] = n;
-                e[NC] = mean[q];
-                e[2 * NC] = m2[q];
-            }
-        }
-        if (lane == 0) p.bnseg[bng] = seg;
     }
 }
 

@@ -159,10 +159,7 @@ k_conv_gemm_x6(const GemmArgs p) {
     if constexpr (MODE == MODE_DGRAD) {
         ph = phase_info(g, phase, g.N);
         Mrows = ph.Mp;
-        if (m0 >= Mrows) {
-            bnstats_empty(p, (phase * p.mtiles + mt) * WGM, WGM);
-            return;
-        }
+        if (m0 >= Mrows) return;
     }
     const int kbeg = split * p.kchunk;
     const int kend = min(p.K, kbeg + p.kchunk);
@@ -517,7 +514,7 @@ k_conv_gemm_x6(const GemmArgs p) {
         return RowPix{row, pix};
     };
     conv_epilogue16<MODE, TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, rowmap, phase, split, lane,
-                                  reinterpret_cast<float *>(smem0) + wid * STAGE, (phase * p.mtiles + mt) * WGM + wm);
+                                  reinterpret_cast<float *>(smem0) + wid * STAGE);
 }
 
 void launch_split3(const float *src, int ld, long rows, int C, unsigned short *dst, hipStream_t s) {

@@ -216,10 +216,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         oy = ty * HX_PH + oh - (KT - 1);
         ox = tx * HX_PW + ow - (KT - 1);
     }
-    if (ty * HX_PH >= Hout || tx * HX_PW >= Wout) {   // block-uniform: a smaller phase grid
-        bnstats_empty(p, (phase * p.mtiles + mt) * 2, 2);
-        return;
-    }
+    if (ty * HX_PH >= Hout || tx * HX_PW >= Wout) return;   // block-uniform: a smaller phase grid
     // channel chunks of this split (kchunk is a multiple of NTAP taps x BK channels)
     const int nch = p.K / (NTAP * BK);
     const int cbeg = split * (p.kchunk / (NTAP * BK));
@@ -450,8 +447,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     if constexpr (POOL)
         conv_epilogue16_pool<TM, TN>(p, acc, wm * TM, n0 + wn * WTN, ty, tx, nimg, lane, stage);
     else
-        conv_epilogue16<MODE, TM, TN>(p, acc, wm * WTM, n0 + wn * WTN, rowmap, phase, split, lane, stage,
-                                      (phase * p.mtiles + mt) * 2 + wm);
+        conv_epilogue16<MODE, TM, TN>(p, acc, wm * WTM, n0 + wn * WTN, rowmap, phase, split, lane, stage);
 }
 
 void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int tiles_x, int tiles_y, hipStream_t s,

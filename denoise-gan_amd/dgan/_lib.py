@@ -88,12 +88,6 @@ _SIGS = {
                                     c_size_t, _P]),
     "dg_conv_bwd_filter_pl": (c_int, [c_void_p, _P, c_int, _P, c_int, _P, _P, c_float, _P, _P, c_size_t, _P]),
     "dg_conv_fwd_pool_ok": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int)]),
-    "dg_conv_bnstats_groups": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int)]),
-    "dg_conv_fwd_bnstats": (c_int, [c_void_p, _P, c_int, _P, _P, _P, c_int, c_int, c_float, _P, c_int, _P, _P, _P,
-                                    c_size_t, _P]),
-    "dg_bn_fwd_train_stats": (c_int, [c_int, c_int, c_int, _P, _P, c_int, _P, c_int, _P, _P, _P, _P, _P, _P, c_float,
-                                      c_float, _P, c_int, c_int, c_float, c_float, c_uint32, c_uint32, _P, _P, c_int,
-                                      c_int, _P, c_int, c_int, _P, c_size_t, _P]),
     "dg_conv_bwd_data_xmask": (c_int, [c_void_p, _P, c_int, _P, _P, c_int, c_float, c_int, c_float, _P, _P, c_size_t,
                                        _P]),
     "dg_conv_fwd_pool": (c_int, [c_void_p, _P, c_int, _P, _P, c_int, c_float, _P, c_int, _P, _P, _P, c_size_t, _P]),

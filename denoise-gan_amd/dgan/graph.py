@@ -469,18 +469,6 @@ class GraphPlan:
                 c = cons[t.id][0]
                 if c.kind == "conv" and all(self.cplanes[k][n.idx].fwd_out is not None for k in range(slots)):
                     self.nofp32.add(n.idx)
-        # ---- BatchNorm statistics from the producing conv's epilogue ----
-        # a conv whose output is read only by the BN node that follows it (the next
-        # node) and whose forward plan can write them (dg_conv_bnstats_groups)
-        self.bn_after = set()
-        self.bns = ops.BnStatsBuf(device)
-        if train and not os.environ.get("DG_NO_BN_EPI_STATS"):
-            for i, n in enumerate(nodes[1:-1], start=1):
-                nxt = nodes[i + 1]
-                if (n.kind == "conv" and nxt.kind == "bn" and nxt.ins[0].id == n.out.id
-                        and len(cons[n.out.id]) == 1 and n.out.id not in self.slice_of
-                        and self.bns.reserve(self.desc[n.idx]) > 0):
-                    self.bn_after.add(n.idx)
         # ---- workspace ----
         ws = [0]
         for n in nodes[1:]:
@@ -551,7 +539,6 @@ class GraphPlan:
             self._wver = A.version
         if out is not None:
             s[g.output.id] = out
-        bn_st = None
         for n in g.nodes[1:]:
             xin = s[n.ins[0].id]
             y = s[n.out.id]
@@ -563,12 +550,6 @@ class GraphPlan:
                 # (a fed input's planes were written by its producer in this pass)
                 P.invalidate(wbit | (0 if n.idx in self.fed_x else ops.TENSOR_X))
                 mp = self.fused_conv.get(n.idx)
-                if training and n.idx in self.bn_after and n.idx not in self.nofp32 and mp is None:
-                    # the BN that follows takes its statistics from this conv's epilogue
-                    bn_st = self.bns.for_conv(d)
-                    d.fwd(xin, A.param(f"{n.name}/kernel"), y, bias=bias, act=n.attrs["act"],
-                          alpha=n.attrs["alpha"], ws=ws, planes=P, bn_stats=bn_st)
-                    continue
                 if mp is not None:
                     d.fwd_pool(xin, A.param(f"{n.name}/kernel"), self.pool_idx[slot][mp.idx], bias=bias,
                                act=n.attrs["act"], alpha=n.attrs["alpha"], pool_y=s[mp.out.id], ws=ws, planes=P,
@@ -579,12 +560,10 @@ class GraphPlan:
             elif k == "bn":
                 mean, inv = self.saved[slot][n.name]
                 if training:
-                    st = bn_st if n.ins[0].node.idx in self.bn_after else None
-                    bn_st = None
                     ops.bn_fwd_train(xin, A.param(f"{n.name}/gamma"), A.param(f"{n.name}/beta"), mean, inv,
                                      self.bn.mean[n.name], self.bn.var[n.name], y, act=n.attrs["act"],
                                      alpha=n.attrs["alpha"], momentum=n.attrs["momentum"], eps=n.attrs["eps"],
-                                     ws=ws, stats=st)
+                                     ws=ws)
                 else:
                     ops.bn_fwd_infer(xin, A.param(f"{n.name}/gamma"), A.param(f"{n.name}/beta"),
                                      self.bn.mean[n.name], self.bn.var[n.name], y, act=n.attrs["act"],

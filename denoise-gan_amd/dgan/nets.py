@@ -32,8 +32,6 @@ DROP_RATE = 0.5   # pix2pix.py:138
 FEED_DY = not os.environ.get("DG_NO_FEED_DY")  # BN backward writes the conv's dy planes
 FEED_X = not os.environ.get("DG_NO_FEED_X")    # BN forward writes the next convs' x planes
 DY_PLANES_ONLY = not os.environ.get("DG_DY_FP32")  # ... and then skips the fp32 dy (its readers take the planes)
-# the producing conv's epilogue writes the BN forward statistics (no statistics pass over y)
-BN_EPILOGUE_STATS = not os.environ.get("DG_NO_BN_EPI_STATS")
 
 
 def xrows(buf, row0, rows, C):
@@ -276,8 +274,6 @@ class GeneratorPlan:
         if train and FEED_X and self.planes[1].x is not None:
             self.planes[0].fwd_out = self.planes[1].x
         self.ws_bytes = max([d.max_ws() for d in self.ddesc + self.udesc + [self.ldesc]] + [self._bn_ws_max()])
-        # BatchNorm statistics from the producing conv's epilogue (training forwards)
-        self.bns = ops.BnStatsBuf(device) if train and BN_EPILOGUE_STATS else None
 
     @property
     def slots(self):
@@ -330,8 +326,7 @@ class GeneratorPlan:
                 d.fwd(h, A.param(f"{name}/kernel"), z, act="lrelu", alpha=ALPHA, ws=ws, planes=P[l])
             else:
                 y = s["yd"][l]
-                st = self.bns.for_conv(d, self.halves) if (self.bns is not None and training) else None
-                d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws, planes=P[l], bn_stats=st)
+                d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws, planes=P[l])
                 # z feeds the next down conv (plane index l+1; down8's z8 feeds
                 # up1, index 8) and, as the skip half of cat[6-l], the up conv
                 # reading that concat (index 15-l, its columns after up 6-l's)
@@ -339,15 +334,14 @@ class GeneratorPlan:
                 outs = [(nxt, co, 0)] if xplanes(nxt) is not None else []
                 if 1 <= l <= 6 and xplanes(15 - l) is not None:
                     outs.append((15 - l, self.ups[7 - l][1], self.ups[6 - l][2]))
-                self._bn_fwd(s, name, y, z, "lrelu", training, ws, outs=outs, stats=st)
+                self._bn_fwd(s, name, y, z, "lrelu", training, ws, outs=outs)
                 if xplanes(nxt) is not None:
                     P[nxt]._filled(ops.TENSOR_X)
             h = z
         for u, (name, ci, co, drop) in enumerate(self.ups):
             d = self.udesc[u]
             y = s["yu"][u]
-            st = self.bns.for_conv(d, self.halves) if (self.bns is not None and training) else None
-            d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws, planes=P[8 + u], bn_stats=st)
+            d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws, planes=P[8 + u])
             z = s["cat"][u][..., :co]
             rate = drop_rate if (drop and training) else 0.0
             # z is the first half of cat[u], read by plane index 9+u (up u+1, or
@@ -358,7 +352,7 @@ class GeneratorPlan:
             if u <= 5 and xplanes(k) is not None:
                 outs.append((k, self.ups[u + 1][1], 0))
             self._bn_fwd(s, name, y, z, "relu", training, ws, rate, lambda hv: dropout_seed(drop_seed, u, hv),
-                         step_dev, outs=outs, stats=st)
+                         step_dev, outs=outs)
             if outs:
                 P[k]._filled(ops.TENSOR_X)
             h = s["cat"][u]
@@ -378,8 +372,7 @@ class GeneratorPlan:
             p.invalidate(ops.TENSOR_DY)
         return p
 
-    def _bn_fwd(self, s, name, y, z, act, training, ws, drop_rate=0.0, seed_of=None, step_dev=None, outs=(),
-                stats=None):
+    def _bn_fwd(self, s, name, y, z, act, training, ws, drop_rate=0.0, seed_of=None, step_dev=None, outs=()):
         """outs: (plane index k, its x channel count, column) -- the BN output is
         also written into plane k's kept x planes at that column (training).
         Training: one segmented call, each half normalised by its own statistics
@@ -394,7 +387,7 @@ class GeneratorPlan:
             ops.bn_fwd_train(y, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), s["mean"][name], s["inv"][name],
                              self.bn.mean[name], self.bn.var[name], z, act=act, alpha=ALPHA, momentum=BN_MOMENTUM,
                              eps=BN_EPS, drop_rate=drop_rate, drop_seed=seed0, step_dev=step_dev, ws=ws, z_planes=zp,
-                             segments=self.halves, drop_seed_stride=stride, stats=stats)
+                             segments=self.halves, drop_seed_stride=stride)
             return
         for hv in range(self.halves):
             ops.bn_fwd_infer(self._half(y, hv), A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.bn.mean[name],
@@ -547,7 +540,6 @@ class DiscriminatorPlan:
         # are used, so that input gradient runs as a Cin-3 conv over down1's filter slice
         # w[:, :, 3:6, :] (copied per step) straight into dL/dG(x) (beta 1); per channel the
         # sum is the one the 6-channel op computes
-        self.bns = ops.BnStatsBuf(device) if train and BN_EPILOGUE_STATS else None
         self.desc_g3 = None
         if train and halves > 1 and self.specs[0][1] == 6:
             co1 = self.specs[0][2]
@@ -585,8 +577,7 @@ class DiscriminatorPlan:
                 d.fwd(h, A.param(f"{name}/kernel"), z, act="lrelu", alpha=ALPHA, ws=ws, planes=P)
             else:
                 y = self.y[i]
-                st = self.bns.for_conv(d, self.halves) if (self.bns is not None and training) else None
-                d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws, planes=P, bn_stats=st)
+                d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws, planes=P)
                 # z feeds the next conv's kept x planes (training)
                 Pn = self.planes[i + 1]
                 xp = Pn.x if FEED_X and training and Pn is not None else None
@@ -596,7 +587,7 @@ class DiscriminatorPlan:
                                      self.inv[name], self.bn.mean[name], self.bn.var[name], z, act="lrelu",
                                      alpha=ALPHA, momentum=BN_MOMENTUM, eps=BN_EPS, ws=ws,
                                      z_planes=[(xrows(xp, 0, rows, co), co, 0)] if xp is not None else (),
-                                     segments=self.halves, stats=st)
+                                     segments=self.halves)
                 else:
                     for hv in range(self.halves):
                         ops.bn_fwd_infer(self._half(y, hv), A.param(f"{name}/gamma"), A.param(f"{name}/beta"),

@@ -314,31 +314,16 @@ class ConvDesc:
         w = self.kh * self.kw * self.Cin * self.Cout
         return 4 * (xin + yout + w)
 
-    def bnstats_groups(self, segments=1):
-        """Row groups of the BatchNorm statistics this layer's forward epilogue can
-        write for `segments` image segments (dg_conv_bnstats_groups), 0 if none."""
-        r = ctypes.c_int()
-        call("dg_conv_bnstats_groups", self._h, int(segments), ctypes.byref(r))
-        return r.value
-
     # planes: optional ConvPlanes (bf16x6 operand planes shared between the
     # ops of this layer, include/dgan.h dg_conv_planes_t)
-    def fwd(self, x, w, y, bias=None, act="none", alpha=0.3, beta=0.0, ws=None, planes=None, bn_stats=None):
-        """y None: only the output's planes (planes.fwd_out) are written.
-        bn_stats: a BnStats (from BnStatsBuf.for_conv) that receives the BatchNorm
-        statistics of y from the GEMM epilogue (dg_conv_fwd_bnstats; beta 0)."""
+    def fwd(self, x, w, y, bias=None, act="none", alpha=0.3, beta=0.0, ws=None, planes=None):
+        """y None: only the output's planes (planes.fwd_out) are written."""
         ldx, ldy = pix_ld(x, self.Cin), (pix_ld(y, self.Cout) if y is not None else 0)
         wp, wn = self._ws(OP_FWD, ws)
         pp, fills = self._pl(OP_FWD, planes)
         ev = _prof_begin()
-        if bn_stats is not None:
-            if beta != 0.0:
-                raise DGError("conv forward with BatchNorm statistics needs beta 0")
-            call("dg_conv_fwd_bnstats", self._h, _p(x), ldx, _p(w), _p(bias), _p(y), ldy, act_id(act), float(alpha),
-                 pp, bn_stats.S, _p(bn_stats.stats), _p(bn_stats.segs), wp, wn, _stream())
-        else:
-            call("dg_conv_fwd_pl", self._h, _p(x), ldx, _p(w), _p(bias), _p(y), ldy,
-                 float(beta), act_id(act), float(alpha), pp, wp, wn, _stream())
+        call("dg_conv_fwd_pl", self._h, _p(x), ldx, _p(w), _p(bias), _p(y), ldy,
+             float(beta), act_id(act), float(alpha), pp, wp, wn, _stream())
         _prof_end(ev, self, "fwd")
         if fills:
             planes._filled(fills)
@@ -480,45 +465,6 @@ def _prof_end(e0, desc, op):
     _PROF.records.append((e0, e1, desc, op))
 
 
-class BnStats:
-    """BatchNorm partials of one conv forward (dg_conv_fwd_bnstats): stats
-    [3, C, R] float32 (rows n, mean, M2 per row group and channel) and segs [R]
-    int32 (the group's segment), consumed by bn_fwd_train(stats=...)."""
-
-    __slots__ = ("stats", "segs", "R", "S")
-
-    def __init__(self, stats, segs, R, S):
-        self.stats, self.segs, self.R, self.S = stats, segs, R, S
-
-
-class BnStatsBuf:
-    """One scratch for the BatchNorm partials of a network's conv -> BN pairs
-    (each pair's partials are consumed by the BN right after its conv)."""
-
-    def __init__(self, device=None):
-        self.device = device or "cuda"
-        self.f = torch.empty(0, dtype=torch.float32, device=self.device)
-        self.i = torch.empty(0, dtype=torch.int32, device=self.device)
-
-    def reserve(self, desc, segments=1):
-        """Grow for desc's forward; -> its row-group count (0: no epilogue statistics)."""
-        R = desc.bnstats_groups(segments)
-        if R:
-            nf, ni = 3 * desc.Cout * R, R
-            if self.f.numel() < nf:
-                self.f = torch.empty(nf, dtype=torch.float32, device=self.device)
-            if self.i.numel() < ni:
-                self.i = torch.empty(ni, dtype=torch.int32, device=self.device)
-        return R
-
-    def for_conv(self, desc, segments=1):
-        """A BnStats for desc's forward, or None when its plan cannot write them."""
-        R = self.reserve(desc, segments)
-        if not R:
-            return None
-        return BnStats(self.f[:3 * desc.Cout * R], self.i[:R], R, segments)
-
-
 def bn_workspace_bytes(M, C, segments=1):
     n = ctypes.c_size_t()
     call("dg_bn_workspace_size_seg", segments, M, C, ctypes.byref(n))
@@ -531,13 +477,11 @@ def _rows(t):
 
 def bn_fwd_train(y, gamma, beta, save_mean, save_invstd, moving_mean, moving_var, z, act="none", alpha=0.3,
                  momentum=0.99, eps=1e-3, drop_rate=0.0, drop_seed=0, step_dev=None, ws=None, z_planes=(),
-                 segments=1, drop_seed_stride=0, stats=None):
+                 segments=1, drop_seed_stride=0):
     """z_planes: up to two (uint8 device tensor, planes C, column) -- packed x
     planes of consuming convs that also receive z.  segments: the rows are that
     many consecutive independent BN calls (dg_bn_fwd_train_seg; save_mean /
-    save_invstd [segments, C], dropout seed drop_seed + s * drop_seed_stride).
-    stats: the BnStats y's producing conv wrote (dg_bn_fwd_train_stats: no
-    statistics pass over y)."""
+    save_invstd [segments, C], dropout seed drop_seed + s * drop_seed_stride)."""
     C = y.shape[-1]
     M = _rows(y)
     if M % segments:
@@ -546,17 +490,11 @@ def bn_fwd_train(y, gamma, beta, save_mean, save_invstd, moving_mean, moving_var
     ws = ws or default_workspace()
     buf, n = ws.get(bn_workspace_bytes(M, C, segments))
     zp = [(t.data_ptr(), int(pc), int(col)) for t, pc, col in z_planes] + [(None, 0, 0)] * (2 - len(z_planes))
-    tail = (float(momentum), float(eps), _p(z), pix_ld(z, C), act_id(act), float(alpha), float(drop_rate),
-            ctypes.c_uint32(drop_seed & 0xFFFFFFFF), ctypes.c_uint32(drop_seed_stride & 0xFFFFFFFF), _p(step_dev),
-            zp[0][0], zp[0][1], zp[0][2], zp[1][0], zp[1][1], zp[1][2], _p(buf), n, _stream())
-    if stats is not None:
-        if stats.S != segments:
-            raise DGError(f"BatchNorm partials for {stats.S} segments, call has {segments}")
-        call("dg_bn_fwd_train_stats", segments, M, C, _p(stats.stats), _p(stats.segs), stats.R, _p(y), pix_ld(y, C),
-             _p(gamma), _p(beta), _p(save_mean), _p(save_invstd), _p(moving_mean), _p(moving_var), *tail)
-    else:
-        call("dg_bn_fwd_train_seg", segments, M, C, _p(y), pix_ld(y, C), _p(gamma), _p(beta), _p(save_mean),
-             _p(save_invstd), _p(moving_mean), _p(moving_var), *tail)
+    call("dg_bn_fwd_train_seg", segments, M, C, _p(y), pix_ld(y, C), _p(gamma), _p(beta), _p(save_mean),
+         _p(save_invstd), _p(moving_mean), _p(moving_var), float(momentum), float(eps), _p(z), pix_ld(z, C),
+         act_id(act), float(alpha), float(drop_rate), ctypes.c_uint32(drop_seed & 0xFFFFFFFF),
+         ctypes.c_uint32(drop_seed_stride & 0xFFFFFFFF), _p(step_dev),
+         zp[0][0], zp[0][1], zp[0][2], zp[1][0], zp[1][1], zp[1][2], _p(buf), n, _stream())
     return z
 
 

@@ -232,33 +232,6 @@ int dg_bn_fwd_train_seg(int S, int M, int C, const float *y, int ldy, const floa
                         float drop_rate, uint32_t drop_seed, uint32_t drop_seed_stride, const int32_t *step_dev,
                         void *zp0, int zp0C, int zp0col, void *zp1, int zp1C, int zp1col,
                         void *ws, size_t ws_bytes, dg_stream_t stream);
-/* BatchNorm statistics from the producing conv (the BN sites
- * pix2pix.py:115+119 (downsample Conv2D -> BN), :130+135 (upsample Conv2DTranspose
- * -> BN), :207+211 (PatchGAN), srgan.py:129-185): the conv's GEMM epilogue, which
- * holds the output tile in registers, writes per row group g (one wave's rows of a
- * block tile) and output channel c the rows' count, mean and M2 (shifted sums,
- * combined across the lanes by Chan's formula in a fixed order) -- the BN forward
- * then skips its statistics pass over y (k_bn_stats_partial: one read of y) and
- * finalises from those partials in the same fixed order.
- * dg_conv_bnstats_groups: R > 0 groups when d's forward plan can write them for S
- * image segments (a one-split bf16x6 / fp16 tiled GEMM whose row groups stay inside
- * one segment), else 0 (use dg_bn_fwd_train_seg).  dg_conv_fwd_bnstats:
- * dg_conv_fwd_pl with beta 0 that also writes stats [3][Cout][R] (n, mean, M2 of the
- * stored output) and segs[R] (the group's segment, -1: no rows).
- * dg_bn_fwd_train_stats: dg_bn_fwd_train_seg from those partials (workspace:
- * 2 * S * C floats). */
-int dg_conv_bnstats_groups(dg_conv_t d, int S, int *R);
-int dg_conv_fwd_bnstats(dg_conv_t d, const float *x, int ldx, const float *w, const float *bias,
-                        float *y, int ldy, int act, float alpha, const dg_conv_planes_t *planes,
-                        int S, float *stats, int *segs, void *ws, size_t ws_bytes, dg_stream_t stream);
-int dg_bn_fwd_train_stats(int S, int M, int C, const float *stats, const int *segs, int R,
-                          const float *y, int ldy, const float *gamma, const float *beta,
-                          float *save_mean, float *save_invstd,
-                          float *moving_mean, float *moving_var, float momentum, float eps,
-                          float *z, int ldz, int act, float alpha,
-                          float drop_rate, uint32_t drop_seed, uint32_t drop_seed_stride, const int32_t *step_dev,
-                          void *zp0, int zp0C, int zp0col, void *zp1, int zp1C, int zp1col,
-                          void *ws, size_t ws_bytes, dg_stream_t stream);
 int dg_bn_bwd_seg(int S, int M, int C, const float *dz, int lddz, const float *z, int ldz,
                   const float *y, int ldy, const float *gamma,
                   const float *save_mean, const float *save_invstd,

@@ -107,16 +107,3 @@ def test_size_thresholds_cite_a_measurement():
             assert re.search(r"A/B|measured|sweep", text), (f, m.group(1))
             for ref in re.findall(r"profiles/[\w/.\-]+", text):
                 assert os.path.exists(os.path.join(REPO, ref.rstrip(".,)"))), (f, m.group(1), ref)
-
-
-def test_bn_epilogue_statistics_plans():
-    """Which BN producers write the statistics in their GEMM epilogue (dg_conv_bnstats_groups):
-    the big pix2pix layers (bs16 x 2 pass, two segments), the SR family's fp16 convs; split-K
-    plans and row groups that would straddle a segment boundary report 0."""
-    from dgan.ops import ConvDesc
-    assert ConvDesc(32, 128, 128, 64, 128, 4, 2, "same").bnstats_groups(2) == 2048        # G.down2 (128x256 tiles)
-    assert ConvDesc(32, 64, 64, 256, 64, 4, 2, "same", transpose=True).bnstats_groups(2) == 8192   # G.up7 phases
-    assert ConvDesc(32, 4, 4, 512, 512, 4, 2, "same").bnstats_groups(2) == 0             # G.down7: split-K
-    assert ConvDesc(32, 24, 24, 64, 64, 3, 1, "same", math="fp16").bnstats_groups(1) == 384   # SRGAN residual conv
-    d = ConvDesc(32, 30, 30, 64, 128, 4, 2, "same")   # 225-pixel images: 64-row groups straddle the halves
-    assert d.bnstats_groups(2) == 0 and d.bnstats_groups(1) > 0
