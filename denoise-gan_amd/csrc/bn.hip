@@ -225,7 +225,7 @@ __global__ void __launch_bounds__(256)
 k_bn_apply(const float *__restrict__ y, int ld, long M, int S, int C, const float *__restrict__ scale,
            const float *__restrict__ shift, float *__restrict__ z, int ldz, int act, float alpha, float drop_rate,
            uint32_t seed, uint32_t seed_stride, const int32_t *step_dev, unsigned short *zp0, int zp0C, int zp0col,
-           unsigned short *zp1, int zp1C, int zp1col) {
+           unsigned short *zp1, int zp1C, int zp1col, _Float16 *__restrict__ zh) {
     const uint32_t step = step_dev ? (uint32_t)*step_dev : 0u;
     const float keep_scale = drop_rate > 0.f ? 1.f / (1.f - drop_rate) : 1.f;
     const int CV = C / V;
@@ -248,6 +248,11 @@ k_bn_apply(const float *__restrict__ y, int ld, long M, int S, int C, const floa
             o[q] = act_fwd(t, act, alpha);
         }
         storev<V>(z + r * ldz + c, o);
+        // the consuming fp16 conv's operand copy of z ([rows][C])
+        if (zh) {
+            if constexpr (V == 4) store_f16x4(zh + r * C + c, f32x4{o[0], o[1], o[2], o[3]});
+            else zh[r * C + c] = (_Float16)o[0];
+        }
         // (V = 4) bf16x6 planes of z for up to two consuming convs, at channel
         // column col of their [rows][3 C] packed x planes (a concat's slice)
         if constexpr (V == 4) {
@@ -383,7 +388,8 @@ template <int V>
 __global__ void __launch_bounds__(256)
 k_bn_bwd_apply(const float *__restrict__ dz, int lddz, const float *__restrict__ z, int ldz,
                const float *__restrict__ y, int ldy, long M, int S, int C, int act, float alpha, float dscale,
-               const float *__restrict__ coef, float *__restrict__ dy, int lddy, unsigned short *__restrict__ dyp) {
+               const float *__restrict__ coef, float *__restrict__ dy, int lddy, unsigned short *__restrict__ dyp,
+               _Float16 *__restrict__ dyh) {
     // coef[s] = [A | B | D | mean] per channel:  dy = A * dbn + B * (y - mean) + D
     // dyp (V = 4, C % 16 == 0): dy's bf16x6 planes too, in the packed layout
     // the consuming conv reads (no split pass before its backward GEMMs)
@@ -408,6 +414,9 @@ k_bn_bwd_apply(const float *__restrict__ dz, int lddz, const float *__restrict__
         if (dy) storev<V>(dy + r * lddy + c, o);
         if constexpr (V == 4) {
             if (dyp) store_planes4(dyp, C, r, c, f32x4{o[0], o[1], o[2], o[3]});
+            if (dyh) store_f16x4(dyh + r * C + c, f32x4{o[0], o[1], o[2], o[3]});
+        } else {
+            if (dyh) dyh[r * C + c] = (_Float16)o[0];
         }
     }
 }
@@ -476,7 +485,19 @@ int dg_bn_fwd_train_seg(int S, int M, int C, const float *y, int ldy, const floa
                         float eps, float *z, int ldz, int act, float alpha, float drop_rate, uint32_t drop_seed,
                         uint32_t drop_seed_stride, const int32_t *step_dev, void *zp0, int zp0C, int zp0col,
                         void *zp1, int zp1C, int zp1col, void *ws, size_t ws_bytes, dg_stream_t stream) {
+    return dg_bn_fwd_train_seg_h(S, M, C, y, ldy, gamma, beta, save_mean, save_invstd, moving_mean, moving_var,
+                                 momentum, eps, z, ldz, act, alpha, drop_rate, drop_seed, drop_seed_stride, step_dev,
+                                 zp0, zp0C, zp0col, zp1, zp1C, zp1col, nullptr, ws, ws_bytes, stream);
+}
+
+int dg_bn_fwd_train_seg_h(int S, int M, int C, const float *y, int ldy, const float *gamma, const float *beta,
+                          float *save_mean, float *save_invstd, float *moving_mean, float *moving_var, float momentum,
+                          float eps, float *z, int ldz, int act, float alpha, float drop_rate, uint32_t drop_seed,
+                          uint32_t drop_seed_stride, const int32_t *step_dev, void *zp0, int zp0C, int zp0col,
+                          void *zp1, int zp1C, int zp1col, void *z_f16, void *ws, size_t ws_bytes,
+                          dg_stream_t stream) {
     DG_ARG(y && z && ws, "NULL tensor");
+    DG_ARG(!z_f16 || (((uintptr_t)z_f16) & 7) == 0, "fp16 copy must be 8-byte aligned");
     DG_ARG(S >= 1 && S <= 8 && M > 0 && C > 0 && ldy >= C && ldz >= C, "bad shape");
     DG_ARG(ws_bytes >= dg::bn_ws_floats(M, C, S) * sizeof(float), "workspace too small");
     DG_ARG(drop_rate >= 0.f && drop_rate < 1.f, "bad dropout rate");
@@ -511,11 +532,11 @@ int dg_bn_fwd_train_seg(int S, int M, int C, const float *y, int ldy, const floa
     if (av4)
         hipLaunchKernelGGL(dg::k_bn_apply<4>, dim3(dg::ew_grid(MT * C / 4)), dim3(256), 0, s, y, ldy, (long)M, S, C,
                            scale, shift, z, ldz, act, alpha, drop_rate, drop_seed, drop_seed_stride, step_dev, p0,
-                           zp0C, zp0col, p1, zp1C, zp1col);
+                           zp0C, zp0col, p1, zp1C, zp1col, (_Float16 *)z_f16);
     else
         hipLaunchKernelGGL(dg::k_bn_apply<1>, dim3(dg::ew_grid(MT * C)), dim3(256), 0, s, y, ldy, (long)M, S, C, scale,
                            shift, z, ldz, act, alpha, drop_rate, drop_seed, drop_seed_stride, step_dev, p0, zp0C,
-                           zp0col, p1, zp1C, zp1col);
+                           zp0col, p1, zp1C, zp1col, (_Float16 *)z_f16);
     DG_LAUNCHED("bn_apply");
     return DG_OK;
 }
@@ -551,6 +572,15 @@ int dg_bn_bwd_seg(int S, int M, int C, const float *dz, int lddz, const float *z
                   const float *gamma, const float *save_mean, const float *save_invstd, int act, float alpha,
                   float drop_rate, float *dy, int lddy, void *dy_planes, float *dgamma, float *dbeta, float beta,
                   void *ws, size_t ws_bytes, dg_stream_t stream) {
+    return dg_bn_bwd_seg_h(S, M, C, dz, lddz, z, ldz, y, ldy, gamma, save_mean, save_invstd, act, alpha, drop_rate, dy,
+                           lddy, dy_planes, nullptr, dgamma, dbeta, beta, ws, ws_bytes, stream);
+}
+
+int dg_bn_bwd_seg_h(int S, int M, int C, const float *dz, int lddz, const float *z, int ldz, const float *y, int ldy,
+                    const float *gamma, const float *save_mean, const float *save_invstd, int act, float alpha,
+                    float drop_rate, float *dy, int lddy, void *dy_planes, void *dy_f16, float *dgamma, float *dbeta,
+                    float beta, void *ws, size_t ws_bytes, dg_stream_t stream) {
+    DG_ARG(!dy_f16 || (((uintptr_t)dy_f16) & 7) == 0, "fp16 copy must be 8-byte aligned");
     // dy NULL: only its planes are written (every consumer reads dy_planes)
     DG_ARG(dz && z && y && save_mean && save_invstd && (dy || dy_planes) && ws, "NULL tensor");
     DG_ARG(S >= 1 && S <= 8 && M > 0 && C > 0 && lddz >= C && ldz >= C && ldy >= C && (!dy || lddy >= C), "bad shape");
@@ -586,10 +616,10 @@ int dg_bn_bwd_seg(int S, int M, int C, const float *dz, int lddz, const float *z
     const long MT = (long)S * M;
     if (av4)
         hipLaunchKernelGGL(dg::k_bn_bwd_apply<4>, dim3(dg::ew_grid(MT * C / 4)), dim3(256), 0, s, dz, lddz, z, ldz, y,
-                           ldy, (long)M, S, C, act, alpha, dscale, coef, dy, lddy, dyp);
+                           ldy, (long)M, S, C, act, alpha, dscale, coef, dy, lddy, dyp, (_Float16 *)dy_f16);
     else
         hipLaunchKernelGGL(dg::k_bn_bwd_apply<1>, dim3(dg::ew_grid(MT * C)), dim3(256), 0, s, dz, lddz, z, ldz, y,
-                           ldy, (long)M, S, C, act, alpha, dscale, coef, dy, lddy, dyp);
+                           ldy, (long)M, S, C, act, alpha, dscale, coef, dy, lddy, dyp, (_Float16 *)dy_f16);
     DG_LAUNCHED("bn_bwd_apply");
     return DG_OK;
 }

@@ -89,6 +89,12 @@ __device__ __forceinline__ void store_planes4(unsigned short *yp, int C, long pi
     *reinterpret_cast<u32x2_t *>(d + 32) = u32x2_t{l0, l1};
 }
 
+// fp16 operand copy of a DG_MATH_FP16 GEMM operand ([rows][C], round-to-nearest-even like the
+// conversion pass k_split_f16) of 4 consecutive elements / of one element
+typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store_f16x4(_Float16 *d, f32x4 v) {
+    *reinterpret_cast<f16x4_t *>(d) = f16x4_t{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
+}
 
 }  // namespace dg
 

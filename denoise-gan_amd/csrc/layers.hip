@@ -89,8 +89,10 @@ __device__ __forceinline__ long shuf_out_pix(long pix, int ch, const ShufGeom &g
     return (n * g.H * g.B + (long)h * g.B + i) * ((long)g.W * g.B) + (long)w * g.B + j;
 }
 
+// zh: the consuming fp16 conv's operand copy of z ([output pixels][C]), or NULL
 __global__ void __launch_bounds__(256) k_prelu_fwd(long npix, ShufGeom g, const float *__restrict__ y, int ldy,
-                                                  const float *__restrict__ alpha, float *__restrict__ z, int ldz) {
+                                                  const float *__restrict__ alpha, float *__restrict__ z, int ldz,
+                                                  _Float16 *__restrict__ zh) {
     const int CB = g.C * g.B * g.B;
     const long total = npix * CB;
     for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
@@ -99,7 +101,9 @@ __global__ void __launch_bounds__(256) k_prelu_fwd(long npix, ShufGeom g, const 
         int c;
         const long op = shuf_out_pix(pix, ch, g, c);
         const float v = y[pix * ldy + ch];
-        z[op * ldz + c] = v > 0.f ? v : alpha[c] * v;
+        const float o = v > 0.f ? v : alpha[c] * v;
+        z[op * ldz + c] = o;
+        if (zh) zh[op * g.C + c] = (_Float16)o;
     }
 }
 
@@ -107,7 +111,7 @@ __global__ void __launch_bounds__(256) k_prelu_fwd(long npix, ShufGeom g, const 
 __global__ void __launch_bounds__(256) k_prelu_bwd(long npix, ShufGeom g, const float *__restrict__ y, int ldy,
                                                   const float *__restrict__ alpha, const float *__restrict__ dz,
                                                   int lddz, float *__restrict__ dy, int lddy, float beta, long rows,
-                                                  float *__restrict__ part) {
+                                                  float *__restrict__ part, _Float16 *__restrict__ dyh) {
     const int CB = g.C * g.B * g.B;
     const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
     const int ch = blockIdx.x * 64 + cl;
@@ -122,7 +126,9 @@ __global__ void __launch_bounds__(256) k_prelu_bwd(long npix, ShufGeom g, const 
             const float gz = dz[op * lddz + c];
             const float d = v > 0.f ? gz : (v < 0.f ? alpha[c] * gz : 0.f);
             float *o = dy + pix * lddy + ch;
-            *o = beta != 0.f ? d + beta * *o : d;
+            const float r = beta != 0.f ? d + beta * *o : d;
+            *o = r;
+            if (dyh) dyh[pix * CB + ch] = (_Float16)r;   // the producing fp16 conv's dy copy
             acc += gz * fminf(v, 0.f);
         }
     }
@@ -169,12 +175,14 @@ __global__ void __launch_bounds__(256) k_prelu_alpha_final(const float *part, in
 // elementwise helpers
 // --------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_add(long npix, int C, const float *a, int lda, const float *b, int ldb,
-                                            float *out, int ldo) {
+                                            float *out, int ldo, _Float16 *__restrict__ outh) {
     const long total = npix * C;
     for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
         const long p = e / C;
         const int c = (int)(e - p * C);
-        out[p * ldo + c] = a[p * lda + c] + b[p * ldb + c];
+        const float o = a[p * lda + c] + b[p * ldb + c];
+        out[p * ldo + c] = o;
+        if (outh) outh[p * C + c] = (_Float16)o;   // the consuming fp16 conv's operand copy
     }
 }
 
@@ -750,13 +758,18 @@ int dg_prelu_workspace_size(int N, int H, int W, int C, int block, size_t *bytes
 
 int dg_prelu_fwd(int N, int H, int W, int C, int block, const float *y, int ldy, const float *alpha, float *z,
                  int ldz, dg_stream_t stream) {
+    return dg_prelu_fwd_h(N, H, W, C, block, y, ldy, alpha, z, ldz, nullptr, stream);
+}
+
+int dg_prelu_fwd_h(int N, int H, int W, int C, int block, const float *y, int ldy, const float *alpha, float *z,
+                   int ldz, void *z_f16, dg_stream_t stream) {
     DG_ARG(y && alpha && z, "NULL tensor");
     DG_ARG(N > 0 && H > 0 && W > 0 && C > 0 && (block == 1 || block == 2), "bad shape");
     DG_ARG(ldy >= C * block * block && ldz >= C, "bad strides");
     const long npix = (long)N * H * W;
     dg::ShufGeom g{H, W, C, block};
     hipLaunchKernelGGL(dg::k_prelu_fwd, dim3(dg::lgrid(npix * C * block * block)), dim3(256), 0, (hipStream_t)stream,
-                       npix, g, y, ldy, alpha, z, ldz);
+                       npix, g, y, ldy, alpha, z, ldz, (_Float16 *)z_f16);
     DG_LAUNCHED("prelu_fwd");
     return DG_OK;
 }
@@ -764,6 +777,13 @@ int dg_prelu_fwd(int N, int H, int W, int C, int block, const float *y, int ldy,
 int dg_prelu_bwd(int N, int H, int W, int C, int block, const float *y, int ldy, const float *alpha, const float *dz,
                  int lddz, float *dy, int lddy, float beta, float *dalpha, float alpha_beta, void *ws,
                  size_t ws_bytes, dg_stream_t stream) {
+    return dg_prelu_bwd_h(N, H, W, C, block, y, ldy, alpha, dz, lddz, dy, lddy, nullptr, beta, dalpha, alpha_beta, ws,
+                          ws_bytes, stream);
+}
+
+int dg_prelu_bwd_h(int N, int H, int W, int C, int block, const float *y, int ldy, const float *alpha,
+                   const float *dz, int lddz, float *dy, int lddy, void *dy_f16, float beta, float *dalpha,
+                   float alpha_beta, void *ws, size_t ws_bytes, dg_stream_t stream) {
     DG_ARG(y && alpha && dz && dy && ws, "NULL tensor");
     DG_ARG(N > 0 && H > 0 && W > 0 && C > 0 && (block == 1 || block == 2), "bad shape");
     DG_ARG(ldy >= C * block * block && lddy >= C * block * block && lddz >= C, "bad strides");
@@ -776,7 +796,7 @@ int dg_prelu_bwd(int N, int H, int W, int C, int block, const float *y, int ldy,
     dg::ShufGeom g{H, W, C, block};
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(dg::k_prelu_bwd, dim3(dg_cdiv(CB, 64), rp.R), dim3(256), 0, s, npix, g, y, ldy, alpha, dz, lddz,
-                       dy, lddy, beta, rp.rows, (float *)ws);
+                       dy, lddy, beta, rp.rows, (float *)ws, (_Float16 *)dy_f16);
     DG_LAUNCHED("prelu_bwd");
     if (dalpha) {
         hipLaunchKernelGGL(dg::k_prelu_alpha_final, dim3(dg_cdiv(C, 16)), dim3(256), 0, s, (const float *)ws, rp.R, C,
@@ -788,11 +808,16 @@ int dg_prelu_bwd(int N, int H, int W, int C, int block, const float *y, int ldy,
 
 int dg_add(int64_t npix, int C, const float *a, int lda, const float *b, int ldb, float *out, int ldo,
            dg_stream_t stream) {
+    return dg_add_h(npix, C, a, lda, b, ldb, out, ldo, nullptr, stream);
+}
+
+int dg_add_h(int64_t npix, int C, const float *a, int lda, const float *b, int ldb, float *out, int ldo,
+             void *out_f16, dg_stream_t stream) {
     DG_ARG(a && b && out, "NULL tensor");
     DG_ARG(C > 0 && lda >= C && ldb >= C && ldo >= C, "bad strides");
     if (npix == 0) return DG_OK;
     hipLaunchKernelGGL(dg::k_add, dim3(dg::lgrid(npix * C)), dim3(256), 0, (hipStream_t)stream, (long)npix, C, a, lda,
-                       b, ldb, out, ldo);
+                       b, ldb, out, ldo, (_Float16 *)out_f16);
     DG_LAUNCHED("add");
     return DG_OK;
 }

@@ -70,6 +70,15 @@ _SIGS = {
     "dg_prelu_bwd": (c_int, [c_int, c_int, c_int, c_int, c_int, _P, c_int, _P, _P, c_int, _P, c_int, c_float, _P,
                              c_float, _P, c_size_t, _P]),
     "dg_add": (c_int, [c_int64, c_int, _P, c_int, _P, c_int, _P, c_int, _P]),
+    "dg_add_h": (c_int, [c_int64, c_int, _P, c_int, _P, c_int, _P, c_int, _P, _P]),
+    "dg_prelu_fwd_h": (c_int, [c_int, c_int, c_int, c_int, c_int, _P, c_int, _P, _P, c_int, _P, _P]),
+    "dg_prelu_bwd_h": (c_int, [c_int, c_int, c_int, c_int, c_int, _P, c_int, _P, _P, c_int, _P, c_int, _P, c_float,
+                               _P, c_float, _P, c_size_t, _P]),
+    "dg_bn_fwd_train_seg_h": (c_int, [c_int, c_int, c_int, _P, c_int, _P, _P, _P, _P, _P, _P, c_float, c_float, _P,
+                                      c_int, c_int, c_float, c_float, c_uint32, c_uint32, _P, _P, c_int, c_int, _P,
+                                      c_int, c_int, _P, _P, c_size_t, _P]),
+    "dg_bn_bwd_seg_h": (c_int, [c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, _P, _P, _P, c_int, c_float,
+                                c_float, _P, c_int, _P, _P, _P, _P, c_float, _P, c_size_t, _P]),
     "dg_accumulate": (c_int, [c_int64, c_int, _P, c_int, _P, c_int, c_float, _P]),
     "dg_act_fwd": (c_int, [c_int64, c_int, _P, c_int, c_int, c_float, _P, c_int, _P]),
     "dg_maxpool2_fwd": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P]),

@@ -416,6 +416,30 @@ class GraphPlan:
                     pn.dy = ops.PlaneBuf(dn.plane_bytes(ops.TENSOR_DY), device)
                     self.cplanes[k][c.idx].bwd_out = pn.dy
                 self.fed_dy.add(n.idx)
+        # ---- fp16 operand copies written by their producers (mixed_float16) ----
+        # an fp16 conv reads fp16 copies of x and dy (its dg_conv_planes_t buffers, converted
+        # per call otherwise): the BN / PReLU / Add producing its input writes the x copy beside
+        # its fp32 output, and the BN / PReLU right after it, whose backward produces its output
+        # gradient, writes the dy copy -- no conversion launch before the GEMMs
+        self.h_x_out = {}    # producer node idx -> consuming conv node idx
+        self.h_dy_out = {}   # node idx -> the conv node whose dy its backward writes
+        f16 = lambda d: d.math == ops.MATH_FP16   # noqa: E731
+        for c in (conv_nodes if (train and feed and not os.environ.get("DG_NO_F16_FEED")) else []):
+            dc = self.desc[c.idx]
+            if not f16(dc):
+                continue
+            t, p = c.ins[0], c.ins[0].node
+            if (dc.plane_mask[ops.OP_FWD] & ops.TENSOR_X and p.kind in ("bn", "prelu", "add")
+                    and t.id not in self.slice_of and p.idx not in self.h_x_out
+                    and sum(1 for m in cons[t.id] if m.kind == "conv") == 1
+                    and all(self.cplanes[k][c.idx].x is not None for k in range(slots))):
+                self.h_x_out[p.idx] = c.idx
+            cs = cons[c.out.id]
+            if (len(cs) == 1 and cs[0].kind in ("bn", "prelu") and cs[0].idx == c.idx + 1
+                    and ops.act_id(c.attrs["act"]) == 0 and c.out.id not in self.slice_of
+                    and (dc.plane_mask[ops.OP_BWD_DATA] | dc.plane_mask[ops.OP_BWD_FILTER]) & ops.TENSOR_DY
+                    and self.cplanes[0][c.idx].dy is not None):
+                self.h_dy_out[cs[0].idx] = c.idx
         # ---- max pools fused into their conv's forward epilogue ----
         # a conv (ReLU / LeakyReLU / linear) whose output feeds only a 2x2 max
         # pool, on a plan that can run the pool in its epilogue, writes the
@@ -539,6 +563,18 @@ class GraphPlan:
             self._wver = A.version
         if out is not None:
             s[g.output.id] = out
+        fed_now = set()   # convs whose fp16 x copy a producer wrote in this pass
+
+        def x_copy(n):
+            c = self.h_x_out.get(n.idx)
+            return None if c is None else self.cplanes[slot][c].x
+
+        def x_copied(n):
+            c = self.h_x_out.get(n.idx)
+            if c is not None:
+                self.cplanes[slot][c].x.ready = True
+                fed_now.add(c)
+
         for n in g.nodes[1:]:
             xin = s[n.ins[0].id]
             y = s[n.out.id]
@@ -548,7 +584,8 @@ class GraphPlan:
                 bias = A.param(f"{n.name}/bias") if n.attrs["bias"] else None
                 P = self.cplanes[slot][n.idx]
                 # (a fed input's planes were written by its producer in this pass)
-                P.invalidate(wbit | (0 if n.idx in self.fed_x else ops.TENSOR_X))
+                fed = n.idx in self.fed_x or n.idx in fed_now
+                P.invalidate(wbit | (0 if fed else ops.TENSOR_X))
                 mp = self.fused_conv.get(n.idx)
                 if mp is not None:
                     d.fwd_pool(xin, A.param(f"{n.name}/kernel"), self.pool_idx[slot][mp.idx], bias=bias,
@@ -563,15 +600,18 @@ class GraphPlan:
                     ops.bn_fwd_train(xin, A.param(f"{n.name}/gamma"), A.param(f"{n.name}/beta"), mean, inv,
                                      self.bn.mean[n.name], self.bn.var[n.name], y, act=n.attrs["act"],
                                      alpha=n.attrs["alpha"], momentum=n.attrs["momentum"], eps=n.attrs["eps"],
-                                     ws=ws)
+                                     ws=ws, f16_out=x_copy(n))
+                    x_copied(n)
                 else:
                     ops.bn_fwd_infer(xin, A.param(f"{n.name}/gamma"), A.param(f"{n.name}/beta"),
                                      self.bn.mean[n.name], self.bn.var[n.name], y, act=n.attrs["act"],
                                      alpha=n.attrs["alpha"], eps=n.attrs["eps"])
             elif k == "prelu":
-                ops.prelu_fwd(xin, A.param(f"{n.name}/alpha"), y, block=n.attrs["block"])
+                ops.prelu_fwd(xin, A.param(f"{n.name}/alpha"), y, block=n.attrs["block"], f16_out=x_copy(n))
+                x_copied(n)
             elif k == "add":
-                ops.add(xin, s[n.ins[1].id], y)
+                ops.add(xin, s[n.ins[1].id], y, f16_out=x_copy(n))
+                x_copied(n)
             elif k == "concat":
                 off = 0
                 for t in n.ins:
@@ -627,6 +667,17 @@ class GraphPlan:
         def need(t):
             return t.id != gin or input_grad is not None
 
+        fed_dy_now = set()   # convs whose fp16 dy copy the node after them wrote just now
+
+        def dy_copy(n, b):
+            c = self.h_dy_out.get(n.idx)
+            return None if (c is None or b != 0.0) else self.cplanes[slot][c].dy
+
+        def dy_copied(n, buf):
+            if buf is not None:
+                buf.ready = True
+                fed_dy_now.add(self.h_dy_out[n.idx])
+
         for n in reversed(g.nodes[1:]):
             k = n.kind
             t_in = n.ins[0]
@@ -640,7 +691,8 @@ class GraphPlan:
                 else:
                     dy = dz   # (already multiplied by act'(z) by the consumer when premasked)
                 P = self.cplanes[slot][n.idx]
-                if n.idx not in self.fed_dy:  # (else written by the consumer's bwd_data just now)
+                # (else written just now: by the consumer's bwd_data, or as the fp16 copy)
+                if n.idx not in self.fed_dy and n.idx not in fed_dy_now:
                     P.invalidate(ops.TENSOR_DY)
                 if pg:
                     db = A.grad_of(f"{n.name}/bias") if n.attrs["bias"] else None
@@ -664,15 +716,20 @@ class GraphPlan:
                 mean, inv = self.saved[slot][n.name]
                 b = beta_of(n, t_in)
                 tgt = gr[t_in.id] if b == 0.0 else self._scratch(self.shape[t_in.id])
+                hc = dy_copy(n, b)
                 ops.bn_bwd(dz, s[n.out.id], s[t_in.id], A.param(f"{n.name}/gamma"), mean, inv, tgt,
                            A.grad_of(f"{n.name}/gamma") if pg else None, A.grad_of(f"{n.name}/beta") if pg else None,
-                           act=n.attrs["act"], alpha=n.attrs["alpha"], beta=param_beta, ws=ws)
+                           act=n.attrs["act"], alpha=n.attrs["alpha"], beta=param_beta, ws=ws, f16_out=hc)
+                dy_copied(n, hc)
                 if b != 0.0:
                     ops.accumulate(tgt, gr[t_in.id], b)
             elif k == "prelu":
+                b = beta_of(n, t_in)
+                hc = dy_copy(n, b)
                 ops.prelu_bwd(s[t_in.id], A.param(f"{n.name}/alpha"), dz, gr[t_in.id],
                               dalpha=A.grad_of(f"{n.name}/alpha") if pg else None, block=n.attrs["block"],
-                              beta=beta_of(n, t_in), alpha_beta=param_beta, ws=ws)
+                              beta=b, alpha_beta=param_beta, ws=ws, f16_out=hc)
+                dy_copied(n, hc)
             elif k == "add":
                 for t in n.ins:
                     if need(t):

@@ -477,11 +477,12 @@ def _rows(t):
 
 def bn_fwd_train(y, gamma, beta, save_mean, save_invstd, moving_mean, moving_var, z, act="none", alpha=0.3,
                  momentum=0.99, eps=1e-3, drop_rate=0.0, drop_seed=0, step_dev=None, ws=None, z_planes=(),
-                 segments=1, drop_seed_stride=0):
+                 segments=1, drop_seed_stride=0, f16_out=None):
     """z_planes: up to two (uint8 device tensor, planes C, column) -- packed x
     planes of consuming convs that also receive z.  segments: the rows are that
     many consecutive independent BN calls (dg_bn_fwd_train_seg; save_mean /
-    save_invstd [segments, C], dropout seed drop_seed + s * drop_seed_stride)."""
+    save_invstd [segments, C], dropout seed drop_seed + s * drop_seed_stride).
+    f16_out: the consuming fp16 conv's x PlaneBuf, which also receives z's fp16 copy."""
     C = y.shape[-1]
     M = _rows(y)
     if M % segments:
@@ -490,11 +491,11 @@ def bn_fwd_train(y, gamma, beta, save_mean, save_invstd, moving_mean, moving_var
     ws = ws or default_workspace()
     buf, n = ws.get(bn_workspace_bytes(M, C, segments))
     zp = [(t.data_ptr(), int(pc), int(col)) for t, pc, col in z_planes] + [(None, 0, 0)] * (2 - len(z_planes))
-    call("dg_bn_fwd_train_seg", segments, M, C, _p(y), pix_ld(y, C), _p(gamma), _p(beta), _p(save_mean),
+    call("dg_bn_fwd_train_seg_h", segments, M, C, _p(y), pix_ld(y, C), _p(gamma), _p(beta), _p(save_mean),
          _p(save_invstd), _p(moving_mean), _p(moving_var), float(momentum), float(eps), _p(z), pix_ld(z, C),
          act_id(act), float(alpha), float(drop_rate), ctypes.c_uint32(drop_seed & 0xFFFFFFFF),
          ctypes.c_uint32(drop_seed_stride & 0xFFFFFFFF), _p(step_dev),
-         zp[0][0], zp[0][1], zp[0][2], zp[1][0], zp[1][1], zp[1][2], _p(buf), n, _stream())
+         zp[0][0], zp[0][1], zp[0][2], zp[1][0], zp[1][1], zp[1][2], _f16(f16_out), _p(buf), n, _stream())
     return z
 
 
@@ -506,12 +507,12 @@ def bn_fwd_infer(y, gamma, beta, moving_mean, moving_var, z, act="none", alpha=0
 
 
 def bn_bwd(dz, z, y, gamma, save_mean, save_invstd, dy, dgamma, dbeta, act="none", alpha=0.3, drop_rate=0.0,
-           beta=0.0, ws=None, dy_planes=None, segments=1, dy_fp32=True):
+           beta=0.0, ws=None, dy_planes=None, segments=1, dy_fp32=True, f16_out=None):
     """dy_planes: a uint8 device tensor (e.g. a slice of a ConvPlanes' dy
     PlaneBuf) that also receives dy's bf16x6 planes; dy_fp32=False then skips
     the fp32 dy (its consumers read the planes; dy only gives the shape).
     segments: see bn_fwd_train (dg_bn_bwd_seg; dgamma / dbeta summed over the
-    segments)."""
+    segments).  f16_out: the producing fp16 conv's dy PlaneBuf (dy's fp16 copy)."""
     C = y.shape[-1]
     M = _rows(y)
     if M % segments:
@@ -519,10 +520,10 @@ def bn_bwd(dz, z, y, gamma, save_mean, save_invstd, dy, dgamma, dbeta, act="none
     M //= segments
     ws = ws or default_workspace()
     buf, n = ws.get(bn_workspace_bytes(M, C, segments))
-    call("dg_bn_bwd_seg", segments, M, C, _p(dz), pix_ld(dz, C), _p(z), pix_ld(z, C), _p(y), pix_ld(y, C), _p(gamma),
-         _p(save_mean), _p(save_invstd), act_id(act), float(alpha), float(drop_rate),
+    call("dg_bn_bwd_seg_h", segments, M, C, _p(dz), pix_ld(dz, C), _p(z), pix_ld(z, C), _p(y), pix_ld(y, C),
+         _p(gamma), _p(save_mean), _p(save_invstd), act_id(act), float(alpha), float(drop_rate),
          _p(dy) if (dy_fp32 or dy_planes is None) else None, pix_ld(dy, C),
-         None if dy_planes is None else dy_planes.data_ptr(),
+         None if dy_planes is None else dy_planes.data_ptr(), _f16(f16_out),
          _p(dgamma), _p(dbeta), float(beta), _p(buf), n, _stream())
     return dy
 
@@ -635,27 +636,40 @@ def prelu_workspace_bytes(N, H, W, C, block):
     return n.value
 
 
-def prelu_fwd(y, alpha, z, block=1):
-    """z = PReLU(depth_to_space(y, block)); y [N,H,W,C*block^2] -> z [N,H*block,W*block,C]."""
+def _f16(buf):
+    """Device pointer of an fp16 operand-copy destination (PlaneBuf or tensor), or None."""
+    if buf is None:
+        return None
+    t = buf.buf if isinstance(buf, PlaneBuf) else buf
+    return t.data_ptr()
+
+
+def prelu_fwd(y, alpha, z, block=1, f16_out=None):
+    """z = PReLU(depth_to_space(y, block)); y [N,H,W,C*block^2] -> z [N,H*block,W*block,C].
+    f16_out: the consuming fp16 conv's x PlaneBuf, which also receives z's fp16 copy."""
     N, H, W, CB = _nhwc(y)
     C = CB // (block * block)
-    call("dg_prelu_fwd", N, H, W, C, block, _p(y), pix_ld(y, CB), _p(alpha), _p(z), pix_ld(z, C), _stream())
+    call("dg_prelu_fwd_h", N, H, W, C, block, _p(y), pix_ld(y, CB), _p(alpha), _p(z), pix_ld(z, C), _f16(f16_out),
+         _stream())
     return z
 
 
-def prelu_bwd(y, alpha, dz, dy, dalpha=None, block=1, beta=0.0, alpha_beta=0.0, ws=None):
+def prelu_bwd(y, alpha, dz, dy, dalpha=None, block=1, beta=0.0, alpha_beta=0.0, ws=None, f16_out=None):
+    """f16_out: the producing fp16 conv's dy PlaneBuf, which also receives dy's fp16 copy."""
     N, H, W, CB = _nhwc(y)
     C = CB // (block * block)
     ws = ws or default_workspace()
     buf, n = ws.get(prelu_workspace_bytes(N, H, W, C, block))
-    call("dg_prelu_bwd", N, H, W, C, block, _p(y), pix_ld(y, CB), _p(alpha), _p(dz), pix_ld(dz, C), _p(dy),
-         pix_ld(dy, CB), float(beta), _p(dalpha), float(alpha_beta), _p(buf), n, _stream())
+    call("dg_prelu_bwd_h", N, H, W, C, block, _p(y), pix_ld(y, CB), _p(alpha), _p(dz), pix_ld(dz, C), _p(dy),
+         pix_ld(dy, CB), _f16(f16_out), float(beta), _p(dalpha), float(alpha_beta), _p(buf), n, _stream())
     return dy
 
 
-def add(a, b, out):
+def add(a, b, out, f16_out=None):
+    """f16_out: the consuming fp16 conv's x PlaneBuf, which also receives out's fp16 copy."""
     C = a.shape[-1]
-    call("dg_add", _rows(a), C, _p(a), pix_ld(a, C), _p(b), pix_ld(b, C), _p(out), pix_ld(out, C), _stream())
+    call("dg_add_h", _rows(a), C, _p(a), pix_ld(a, C), _p(b), pix_ld(b, C), _p(out), pix_ld(out, C), _f16(f16_out),
+         _stream())
     return out
 
 

@@ -238,6 +238,24 @@ int dg_bn_bwd_seg(int S, int M, int C, const float *dz, int lddz, const float *z
                   int act, float alpha, float drop_rate,
                   float *dy, int lddy, void *dy_planes, float *dgamma, float *dbeta, float beta,
                   void *ws, size_t ws_bytes, dg_stream_t stream);
+/* The same, also writing the consuming conv's DG_MATH_FP16 operand copy of z / dy
+ * (z_f16 / dy_f16: [S*M rows][C] fp16, round-to-nearest-even -- the bytes the conv's own
+ * conversion would write into its dg_conv_planes_t x / dy buffer, which the caller then
+ * passes as ready; 8-byte aligned; NULL = none).  The SR family's mixed_float16 convs
+ * (srgan.py:63-66) thus skip their per-call fp32 -> fp16 conversion of these operands. */
+int dg_bn_fwd_train_seg_h(int S, int M, int C, const float *y, int ldy, const float *gamma, const float *beta,
+                          float *save_mean, float *save_invstd,
+                          float *moving_mean, float *moving_var, float momentum, float eps,
+                          float *z, int ldz, int act, float alpha,
+                          float drop_rate, uint32_t drop_seed, uint32_t drop_seed_stride, const int32_t *step_dev,
+                          void *zp0, int zp0C, int zp0col, void *zp1, int zp1C, int zp1col, void *z_f16,
+                          void *ws, size_t ws_bytes, dg_stream_t stream);
+int dg_bn_bwd_seg_h(int S, int M, int C, const float *dz, int lddz, const float *z, int ldz,
+                    const float *y, int ldy, const float *gamma,
+                    const float *save_mean, const float *save_invstd,
+                    int act, float alpha, float drop_rate,
+                    float *dy, int lddy, void *dy_planes, void *dy_f16, float *dgamma, float *dbeta, float beta,
+                    void *ws, size_t ws_bytes, dg_stream_t stream);
 /* dy = dz * act'(z)  for blocks without BN (pix2pix.py:118-121 with apply_batchnorm=False) */
 int dg_act_bwd(int M, int C, const float *dz, int lddz, const float *z, int ldz,
                int act, float alpha, float *dy, int lddy, dg_stream_t stream);
@@ -329,6 +347,15 @@ int dg_prelu_bwd(int N, int H, int W, int C, int block, const float *y, int ldy,
 /* keras.layers.Add (srgan.py:165): out = a + b */
 int dg_add(int64_t npix, int C, const float *a, int lda, const float *b, int ldb, float *out, int ldo,
            dg_stream_t stream);
+/* _h forms: also the consuming / producing fp16 conv's operand copy (dg_bn_fwd_train_seg_h):
+ * z_f16 [N*H*block*W*block][C], dy_f16 [N*H*W][C*block^2] (after beta), out_f16 [npix][C] */
+int dg_prelu_fwd_h(int N, int H, int W, int C, int block, const float *y, int ldy, const float *alpha,
+                   float *z, int ldz, void *z_f16, dg_stream_t stream);
+int dg_prelu_bwd_h(int N, int H, int W, int C, int block, const float *y, int ldy, const float *alpha,
+                   const float *dz, int lddz, float *dy, int lddy, void *dy_f16, float beta,
+                   float *dalpha, float alpha_beta, void *ws, size_t ws_bytes, dg_stream_t stream);
+int dg_add_h(int64_t npix, int C, const float *a, int lda, const float *b, int ldb, float *out, int ldo,
+             void *out_f16, dg_stream_t stream);
 /* dst = src + beta*dst (gradient fan-in) */
 int dg_accumulate(int64_t npix, int C, const float *src, int lds, float *dst, int ldd, float beta,
                   dg_stream_t stream);

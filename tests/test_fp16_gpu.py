@@ -282,3 +282,62 @@ def test_srgan_fp16_resume_restores_loss_scale(tmp_path):
             assert torch.equal(getattr(na.arena, t), getattr(nb.arena, t)), t
     name = full.model_name
     assert name.endswith("_fp16") and (tmp_path / "b" / "models" / f"{name}.npz").exists()
+
+
+@gpu
+def test_producer_fp16_copies_equal_the_conversion():
+    """BN / PReLU / Add write the consuming (or producing) fp16 conv's operand copy beside
+    their fp32 output (dg_*_h): bit-identical to the conversion pass (fp16 RNE of the fp32
+    values), dense [rows][C] even when the fp32 tensor has a pixel stride."""
+    from dgan import ops
+    torch.manual_seed(5)
+    dev = torch.device(DEV)
+    N, H, W, C = 2, 12, 20, 64
+    big = torch.randn(N, H, W, C + 16, device=dev)
+    y = big[..., :C]                                  # strided input
+    z = torch.empty(N, H, W, C, device=dev)
+    zh = torch.full((N * H * W * C,), 7.0, dtype=torch.float16, device=dev)
+    g, b = 1 + 0.1 * torch.randn(C, device=dev), 0.1 * torch.randn(C, device=dev)
+    mean, inv = torch.empty(1, C, device=dev), torch.empty(1, C, device=dev)
+    mm, mv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    ops.bn_fwd_train(y, g, b, mean, inv, mm, mv, z, act="lrelu", alpha=0.2, f16_out=zh)
+    dz = torch.randn(N, H, W, C, device=dev)
+    dy = torch.empty(N, H, W, C, device=dev)
+    dyh = torch.empty(N * H * W * C, dtype=torch.float16, device=dev)
+    ops.bn_bwd(dz, z, y, g, mean, inv, dy, None, None, act="lrelu", alpha=0.2, f16_out=dyh)
+    a2 = torch.randn(N, H, W, C, device=dev)
+    out = torch.empty(N, H, W, C, device=dev)
+    outh = torch.empty(N * H * W * C, dtype=torch.float16, device=dev)
+    ops.add(y, a2, out, f16_out=outh)
+    # PReLU with depth_to_space(2): y2 [N,H,W,4C'] -> z2 [N,2H,2W,C']
+    Cp = 16
+    y2 = torch.randn(N, H, W, 4 * Cp, device=dev)
+    al = 0.25 * torch.rand(Cp, device=dev)
+    z2 = torch.empty(N, 2 * H, 2 * W, Cp, device=dev)
+    z2h = torch.empty(N * 4 * H * W * Cp, dtype=torch.float16, device=dev)
+    ops.prelu_fwd(y2, al, z2, block=2, f16_out=z2h)
+    dz2 = torch.randn(N, 2 * H, 2 * W, Cp, device=dev)
+    dy2 = torch.empty(N, H, W, 4 * Cp, device=dev)
+    dy2h = torch.empty(N * H * W * 4 * Cp, dtype=torch.float16, device=dev)
+    ops.prelu_bwd(y2, al, dz2, dy2, block=2, f16_out=dy2h)
+    torch.cuda.synchronize()
+    for f32, f16, what in ((z, zh, "bn fwd"), (dy, dyh, "bn bwd"), (out, outh, "add"), (z2, z2h, "prelu fwd"),
+                           (dy2, dy2h, "prelu bwd")):
+        want = f32.contiguous().reshape(-1).half()
+        assert torch.equal(f16.view(torch.int16), want.view(torch.int16)), f"{what}: fp16 copy differs"
+
+
+@gpu
+def test_srgan_fp16_producers_feed_their_convs():
+    """In SRGAN's mixed_float16 step the residual blocks' BN / PReLU / Add write the next
+    conv's fp16 x copy and the BN / PReLU after a conv write its fp16 dy copy
+    (dgan/graph.py h_x_out / h_dy_out), so only the weights are converted per conv."""
+    from srgan import SRGAN
+    m = SRGAN(Args(crop_size=32))
+    x, y = _synthetic(2, 32, 4, seed=63)
+    tr = m.trainer(x.shape, y.shape)
+    Gp = tr.Gp
+    kinds = {Gp.g.nodes[i].kind for i in Gp.h_x_out}
+    assert {"bn", "prelu", "add"} <= kinds, kinds
+    assert len(Gp.h_x_out) >= 30 and len(Gp.h_dy_out) >= 30, (len(Gp.h_x_out), len(Gp.h_dy_out))
+    assert len(tr.Dp.h_x_out) >= 5 and len(tr.Dp.h_dy_out) >= 5
