@@ -1,5 +1,6 @@
 // Error reporting, version, and the small data-movement / optimizer kernels.
 #include "common.h"
+#include "conv_impl.h"
 #include <cstdarg>
 #include <cstdio>
 #include <algorithm>
@@ -237,6 +238,17 @@ int dg_strided_copy(int64_t npix, int C, const float *src, int lds, float *dst, 
     hipLaunchKernelGGL(dg::k_strided_copy, dim3(dg::grid_for(total)), dim3(256), 0, (hipStream_t)stream, (long)npix, C,
                        src, lds, dst, ldd);
     DG_LAUNCHED("strided_copy");
+    return DG_OK;
+}
+
+int dg_to_f16(int64_t n, const float *src, void *dst, dg_stream_t stream) {
+    DG_ARG((src && dst) || n == 0, "NULL tensor");
+    DG_ARG(n % 8 == 0 && (((uintptr_t)src) & 15) == 0 && (((uintptr_t)dst) & 15) == 0,
+           "n %% 8 == 0 and 16-byte aligned buffers");
+    if (n == 0) return DG_OK;
+    // rows of 8 elements: the operand conversion pass of the fp16 GEMMs, RNE
+    dg::launch_split_f16(src, 8, (long)(n / 8), 8, dst, (hipStream_t)stream);
+    DG_LAUNCHED("to_f16");
     return DG_OK;
 }
 

@@ -339,13 +339,32 @@ class GraphPlan:
         conv_nodes = [n for n in nodes[1:] if n.kind == "conv"]
         descs = [self.desc[n.idx] for n in conv_nodes]
         keep_x = train and param_grads and alias is None
+        # fp16 weight copies of a trainable network: views into one fp16 shadow of the
+        # arena (arena.half), converted by ONE launch per forward (dg_to_f16) instead of
+        # one conversion per conv (the weights change with every Adam step)
+        half = (not getattr(arena, "frozen", False) and not os.environ.get("DG_NO_F16_WARENA")
+                and any(d.math == ops.MATH_FP16 and (d.plane_mask[0] | d.plane_mask[1]) & ops.TENSOR_W
+                        for d in descs))
+        if half and getattr(arena, "half", None) is None:
+            arena.half = torch.empty(arena.numel, dtype=torch.float16, device=device)
+        self.half_w = set()   # conv node idx whose fp16 weight copy is an arena.half view
         self.cplanes = []
         for k in range(slots):
             wb = []
             for n, d in zip(conv_nodes, descs):
                 if (d.plane_mask[0] | d.plane_mask[1]) & ops.TENSOR_W:
                     if n.name not in wplanes:
-                        wplanes[n.name] = ops.PlaneBuf(d.plane_bytes(ops.TENSOR_W), device)
+                        if half and d.math == ops.MATH_FP16:
+                            wname = f"{n.name}/kernel"
+                            o, cnt = arena.offsets[wname], int(np.prod(arena.shapes[wname]))
+                            assert 2 * cnt <= d.plane_bytes(ops.TENSOR_W)   # (sized for bf16x6 planes)
+                            v = ops.PlaneBuf.__new__(ops.PlaneBuf)
+                            v.buf, v.ready = arena.half[o:o + cnt].view(torch.uint8), False
+                            wplanes[n.name] = v
+                        else:
+                            wplanes[n.name] = ops.PlaneBuf(d.plane_bytes(ops.TENSOR_W), device)
+                    if half and d.math == ops.MATH_FP16:
+                        self.half_w.add(n.idx)
                     wb.append(wplanes[n.name])
                 else:
                     wb.append(None)
@@ -561,6 +580,9 @@ class GraphPlan:
             if self._wver == A.version:
                 wbit = 0
             self._wver = A.version
+        if self.half_w:
+            # every fp16 conv's weight copy of this network in one launch
+            ops.to_f16(A.data, A.half)
         if out is not None:
             s[g.output.id] = out
         fed_now = set()   # convs whose fp16 x copy a producer wrote in this pass
@@ -585,7 +607,11 @@ class GraphPlan:
                 P = self.cplanes[slot][n.idx]
                 # (a fed input's planes were written by its producer in this pass)
                 fed = n.idx in self.fed_x or n.idx in fed_now
-                P.invalidate(wbit | (0 if fed else ops.TENSOR_X))
+                if n.idx in self.half_w:
+                    P.invalidate(0 if fed else ops.TENSOR_X)
+                    P.w.ready = True
+                else:
+                    P.invalidate(wbit | (0 if fed else ops.TENSOR_X))
                 mp = self.fused_conv.get(n.idx)
                 if mp is not None:
                     d.fwd_pool(xin, A.param(f"{n.name}/kernel"), self.pool_idx[slot][mp.idx], bias=bias,

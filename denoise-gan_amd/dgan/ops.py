@@ -602,6 +602,14 @@ def channel_concat(a, b, out):
     return out
 
 
+def to_f16(src, dst):
+    """dst (float16, contiguous) = fp16(src) in one launch (dg_to_f16)."""
+    if not (src.is_contiguous() and dst.is_contiguous()) or dst.numel() < src.numel():
+        raise DGError("to_f16 needs contiguous tensors and room for every element")
+    call("dg_to_f16", src.numel(), _p(src), dst.data_ptr(), _stream())
+    return dst
+
+
 def fill(t, value):
     if not t.is_contiguous():
         raise DGError("fill needs a contiguous tensor")

@@ -326,6 +326,10 @@ int dg_adam_sched(float *p, const float *g, float *m, float *v, int64_t n,
 int dg_channel_concat(int64_t npix, const float *a, int lda, int ca, const float *b, int ldb, int cb,
                       float *out, int ldo, dg_stream_t stream);
 int dg_fill(float *p, int64_t n, float value, dg_stream_t stream);
+/* dst[0:n] = fp16(src[0:n]) (round to nearest even; n % 8 == 0, 16-byte aligned): one launch
+ * converting a whole parameter arena into the fp16 weight copies its DG_MATH_FP16 convs read
+ * (dg_conv_planes_t.w views into dst, passed ready) instead of one conversion per conv */
+int dg_to_f16(int64_t n, const float *src, void *dst, dg_stream_t stream);
 int dg_strided_copy(int64_t npix, int C, const float *src, int lds, float *dst, int ldd, dg_stream_t stream);
 
 /* ------------------------------------------------------------------------
