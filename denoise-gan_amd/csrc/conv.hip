@@ -1269,7 +1269,7 @@ static bool cfg_vec(const ConvGeom &g, int mode, int bk) {
 // + split-K slab traffic, where blocks per CU = min(resident limit, blocks / 256).
 // Plan features switched off for same-box A/B runs: DG_PLAN_DISABLE is a
 // comma-separated list of {shortk, small, co1, tlast, direct, halo, halo2, halo4, halo_f16, xcd_phase, narrow_px, ntile,
-// tile32, f16planes}
+// tile32, f16planes, halo32}
 // (read when a descriptor is planned; unset in production runs)
 static bool plan_off(const char *feature) {
     const char *list = getenv("DG_PLAN_DISABLE");
@@ -1484,7 +1484,9 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         pl.hty = (Hout + 7) / 8;
         // (4x4: BN 128 needs 93 KB of LDS -- one block per CU -- and measured 0.685 vs
         // 0.666 ms for BN 64, which keeps two)
-        pl.cfg = pl.N > 64 && !h44 ? 128 : 64;
+        // (32 output columns, 3x3: BN 32 -- the SR family's 32-channel layers; a 64-wide tile
+        // spends half its MFMAs on zero columns there)
+        pl.cfg = pl.N > 64 && !h44 ? 128 : (h33 && pl.N <= 32 && !plan_off("halo32") ? 32 : 64);
         pl.mtiles = g.N * pl.htx * pl.hty;
         pl.ntiles = (pl.N + pl.cfg - 1) / pl.cfg;
         // split-K over channel chunks (at least two per split) until ~2 blocks per CU
@@ -1701,7 +1703,8 @@ struct PoolOut {
 // whose derivative is a function of the output's sign
 static bool pool_fusable(const dg_conv_desc_s *d, int act) {
     const OpPlan &pl = d->plan[DG_OP_FWD];
-    return !d->transpose && pl.x6 == 1 && pl.halo == 1 && pl.splits == 1 && !d->rc[DG_OP_FWD].on && d->g.Ho % 8 == 0 &&
+    return !d->transpose && pl.x6 == 1 && pl.halo == 1 && pl.cfg != 32 && pl.splits == 1 && !d->rc[DG_OP_FWD].on &&
+           d->g.Ho % 8 == 0 &&
            d->g.Wo % 16 == 0 && d->g.Co % 16 == 0 &&
            (act == DG_ACT_NONE || act == DG_ACT_RELU || act == DG_ACT_LRELU);
 }

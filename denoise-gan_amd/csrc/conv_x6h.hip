@@ -291,7 +291,8 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         if constexpr (!B_KC) {
             const int r = pos / (2 * BN);
             const int pdw = (pos - r * 2 * BN) >> 2;
-            const int swz = BN >= 128 ? 8 * ((r & 3) | (((r >> 3) & 1) << 2)) : 8 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
+            const int swz = BN >= 128 ? 8 * ((r & 3) | (((r >> 3) & 1) << 2))
+                                      : (BN >= 64 ? 8 * (((r >> 1) & 1) | (((r >> 3) & 1) << 1)) : 8 * ((r >> 1) & 1));
             const int col = n0 + 2 * (pdw ^ swz);
             bok[j] = col < p.N;
             if constexpr (NI == 3) bbase[j] = (r * (3 * p.ldb) + (col >> 4) * 48 + 16 * plane + (col & 8)) * 2;
@@ -455,12 +456,16 @@ void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int
     const dim3 blk(256);
 #define DG_X6H(M_, B_, P_, K_) hipLaunchKernelGGL((k_conv_gemm_x6h<M_, B_, P_, K_>), grid, blk, 0, s, a, tiles_x, tiles_y)
 #define DG_F16H(M_, B_) hipLaunchKernelGGL((k_conv_gemm_x6h<M_, B_, false, 3, 2>), grid, blk, 0, s, a, tiles_x, tiles_y)
+    // (bn 32: the SR discriminators' / FastSRGAN's 32-channel 3x3 layers, stride 1; a
+    // 64-wide tile computes half zeros there)
     if (ni == 2) {   // fp16: 3x3 stride 1, forward or input gradient
         if (mode == MODE_FWD) {
             if (bn == 128) DG_F16H(MODE_FWD, 128);
+            else if (bn == 32) DG_F16H(MODE_FWD, 32);
             else DG_F16H(MODE_FWD, 64);
         } else {
             if (bn == 128) DG_F16H(MODE_DGRAD, 128);
+            else if (bn == 32) DG_F16H(MODE_DGRAD, 32);
             else DG_F16H(MODE_DGRAD, 64);
         }
     } else if (mode == MODE_FWD && a.pidx) {
@@ -468,6 +473,7 @@ void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int
         else DG_X6H(MODE_FWD, 64, true, 3);
     } else if (mode == MODE_FWD) {
         if (bn == 128) DG_X6H(MODE_FWD, 128, false, 3);
+        else if (bn == 32) DG_X6H(MODE_FWD, 32, false, 3);
         else DG_X6H(MODE_FWD, 64, false, 3);
     } else if (kt == 2) {
         if (bn == 128) DG_X6H(MODE_DGRAD, 128, false, 2);
@@ -476,6 +482,7 @@ void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int
         DG_X6H(MODE_DGRAD, 64, false, 4);
     } else {
         if (bn == 128) DG_X6H(MODE_DGRAD, 128, false, 3);
+        else if (bn == 32) DG_X6H(MODE_DGRAD, 32, false, 3);
         else DG_X6H(MODE_DGRAD, 64, false, 3);
     }
 #undef DG_X6H

@@ -132,6 +132,11 @@ HALO_CASES = [
     ("h.splitk", 2, 8, 8, 512, 512, 3, 1, "same", False, False),
     ("h.valid", 2, 20, 21, 64, 64, 3, 1, "valid", False, True),
     ("h.tfpad", 3, 13, 29, 32, 48, 3, 1, (1, 1, 1, 1), False, False),
+    # BN 32 (32 output columns: the SR family's 32-channel layers): ragged patches,
+    # 16 input channels (one chunk), split-K over chunks on a small grid
+    ("h32.ragged", 3, 21, 37, 32, 32, 3, 1, "same", False, True),
+    ("h32.c16", 2, 24, 24, 16, 32, 3, 1, "same", False, False),
+    ("h32.splitk", 2, 8, 8, 256, 32, 3, 1, "same", False, True),
     # stride-2 4x4 layers: the input gradient in 4 sub-pixel phases (Conv2D
     # bwd_data and Conv2DTranspose fwd; ragged patches, odd sizes whose phases
     # differ in size, BN 64 / 128, split-K)

@@ -41,6 +41,7 @@ F16_CONVS = [
     ("f16h.ragged", 2, 20, 37, 96, 64, 3, 1),
     ("f16h.splitk", 1, 6, 6, 512, 512, 3, 1),
     ("f16h.bn128", 2, 24, 24, 128, 160, 3, 1),
+    ("f16h.bn32", 2, 20, 37, 32, 32, 3, 1),
 ]
 
 
