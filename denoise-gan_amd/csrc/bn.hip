@@ -225,7 +225,8 @@ __global__ void __launch_bounds__(256)
 k_bn_apply(const float *__restrict__ y, int ld, long M, int S, int C, const float *__restrict__ scale,
            const float *__restrict__ shift, float *__restrict__ z, int ldz, int act, float alpha, float drop_rate,
            uint32_t seed, uint32_t seed_stride, const int32_t *step_dev, unsigned short *zp0, int zp0C, int zp0col,
-           unsigned short *zp1, int zp1C, int zp1col, _Float16 *__restrict__ zh) {
+           unsigned short *zp1, int zp1C, int zp1col, _Float16 *__restrict__ zh, const float *__restrict__ res,
+           int ldres) {
     const uint32_t step = step_dev ? (uint32_t)*step_dev : 0u;
     const float keep_scale = drop_rate > 0.f ? 1.f / (1.f - drop_rate) : 1.f;
     const int CV = C / V;
@@ -246,6 +247,12 @@ k_bn_apply(const float *__restrict__ y, int ld, long M, int S, int C, const floa
             if (drop_rate > 0.f)
                 t = dropout_keep(sd, step, (uint32_t)(rr * C + c + q), drop_rate) ? t * keep_scale : 0.f;
             o[q] = act_fwd(t, act, alpha);
+        }
+        if (res) {   // a residual Add fused after the block (srgan.py:165, fsrgan.py:176): z = act(BN(y)) + res
+            float rv[V];
+            loadv<V>(res + r * ldres + c, rv);
+#pragma unroll
+            for (int q = 0; q < V; ++q) o[q] += rv[q];
         }
         storev<V>(z + r * ldz + c, o);
         // the consuming fp16 conv's operand copy of z ([rows][C])
@@ -487,16 +494,17 @@ int dg_bn_fwd_train_seg(int S, int M, int C, const float *y, int ldy, const floa
                         void *zp1, int zp1C, int zp1col, void *ws, size_t ws_bytes, dg_stream_t stream) {
     return dg_bn_fwd_train_seg_h(S, M, C, y, ldy, gamma, beta, save_mean, save_invstd, moving_mean, moving_var,
                                  momentum, eps, z, ldz, act, alpha, drop_rate, drop_seed, drop_seed_stride, step_dev,
-                                 zp0, zp0C, zp0col, zp1, zp1C, zp1col, nullptr, ws, ws_bytes, stream);
+                                 zp0, zp0C, zp0col, zp1, zp1C, zp1col, nullptr, 0, nullptr, ws, ws_bytes, stream);
 }
 
 int dg_bn_fwd_train_seg_h(int S, int M, int C, const float *y, int ldy, const float *gamma, const float *beta,
                           float *save_mean, float *save_invstd, float *moving_mean, float *moving_var, float momentum,
                           float eps, float *z, int ldz, int act, float alpha, float drop_rate, uint32_t drop_seed,
                           uint32_t drop_seed_stride, const int32_t *step_dev, void *zp0, int zp0C, int zp0col,
-                          void *zp1, int zp1C, int zp1col, void *z_f16, void *ws, size_t ws_bytes,
-                          dg_stream_t stream) {
+                          void *zp1, int zp1C, int zp1col, const float *res, int ldres, void *z_f16, void *ws,
+                          size_t ws_bytes, dg_stream_t stream) {
     DG_ARG(y && z && ws, "NULL tensor");
+    DG_ARG(!res || ldres >= C, "residual pixel stride smaller than channels");
     DG_ARG(!z_f16 || (((uintptr_t)z_f16) & 7) == 0, "fp16 copy must be 8-byte aligned");
     DG_ARG(S >= 1 && S <= 8 && M > 0 && C > 0 && ldy >= C && ldz >= C, "bad shape");
     DG_ARG(ws_bytes >= dg::bn_ws_floats(M, C, S) * sizeof(float), "workspace too small");
@@ -521,7 +529,7 @@ int dg_bn_fwd_train_seg_h(int S, int M, int C, const float *y, int ldy, const fl
     hipLaunchKernelGGL(dg::k_bn_stats_final, dim3(dg_cdiv(C, dg::FIN_C)), dim3(256), 0, s, pn, pmean, pm2, bp.R, C, S,
                        gamma, beta, save_mean, save_invstd, moving_mean, moving_var, momentum, eps, scale, shift);
     DG_LAUNCHED("bn_stats_final");
-    const bool av4 = dg::vec4_ok(C, {{y, ldy}, {z, ldz}});
+    const bool av4 = dg::vec4_ok(C, {{y, ldy}, {z, ldz}, {res, ldres}});
     unsigned short *p0 = (unsigned short *)zp0, *p1 = (unsigned short *)zp1;
     auto pl_ok = [&](const unsigned short *p, int pc, int col) {
         return !p || (av4 && pc % 16 == 0 && col % 16 == 0 && C % 16 == 0 && col + C <= pc && (((uintptr_t)p) & 15) == 0);
@@ -532,11 +540,11 @@ int dg_bn_fwd_train_seg_h(int S, int M, int C, const float *y, int ldy, const fl
     if (av4)
         hipLaunchKernelGGL(dg::k_bn_apply<4>, dim3(dg::ew_grid(MT * C / 4)), dim3(256), 0, s, y, ldy, (long)M, S, C,
                            scale, shift, z, ldz, act, alpha, drop_rate, drop_seed, drop_seed_stride, step_dev, p0,
-                           zp0C, zp0col, p1, zp1C, zp1col, (_Float16 *)z_f16);
+                           zp0C, zp0col, p1, zp1C, zp1col, (_Float16 *)z_f16, res, ldres);
     else
         hipLaunchKernelGGL(dg::k_bn_apply<1>, dim3(dg::ew_grid(MT * C)), dim3(256), 0, s, y, ldy, (long)M, S, C, scale,
                            shift, z, ldz, act, alpha, drop_rate, drop_seed, drop_seed_stride, step_dev, p0, zp0C,
-                           zp0col, p1, zp1C, zp1col, (_Float16 *)z_f16);
+                           zp0col, p1, zp1C, zp1col, (_Float16 *)z_f16, res, ldres);
     DG_LAUNCHED("bn_apply");
     return DG_OK;
 }

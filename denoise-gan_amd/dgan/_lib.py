@@ -77,7 +77,7 @@ _SIGS = {
                                _P, c_float, _P, c_size_t, _P]),
     "dg_bn_fwd_train_seg_h": (c_int, [c_int, c_int, c_int, _P, c_int, _P, _P, _P, _P, _P, _P, c_float, c_float, _P,
                                       c_int, c_int, c_float, c_float, c_uint32, c_uint32, _P, _P, c_int, c_int, _P,
-                                      c_int, c_int, _P, _P, c_size_t, _P]),
+                                      c_int, c_int, _P, c_int, _P, _P, c_size_t, _P]),
     "dg_bn_bwd_seg_h": (c_int, [c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, _P, _P, _P, c_int, c_float,
                                 c_float, _P, c_int, _P, _P, _P, _P, c_float, _P, c_size_t, _P]),
     "dg_accumulate": (c_int, [c_int64, c_int, _P, c_int, _P, c_int, c_float, _P]),

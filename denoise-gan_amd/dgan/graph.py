@@ -304,6 +304,22 @@ class GraphPlan:
             c = cs[0]
             if c.kind in ("conv", "maxpool") or (c.kind == "upsample" and ops.act_id(n.attrs["act"]) == 2):
                 self.premask.add(n.out.id)
+        # ---- BatchNorm + residual Add ----
+        # a linear BN whose only consumer is an Add (the SR residual blocks, srgan.py:165 /
+        # :180, fsrgan.py:176 / :214) writes act(BN(y)) + skip straight into the Add's output
+        # in a training forward; backward, the BN reads the Add's output gradient (aliased:
+        # the Add passes it through unchanged) and the Add only routes it to the skip input
+        self.bn_add = {}   # bn node idx -> (add node, skip input tensor)
+        for a in (nodes[1:] if train and not os.environ.get("DG_NO_BN_ADD") else []):
+            if a.kind != "add" or a.out.id in self.slice_of or a.out.id == graph.output.id:
+                continue
+            for t, o in ((a.ins[0], a.ins[1]), (a.ins[1], a.ins[0])):
+                b = t.node
+                if (b.kind == "bn" and ops.act_id(b.attrs["act"]) == 0 and len(cons[t.id]) == 1
+                        and t.id not in self.slice_of and o.id != t.id and b.idx not in self.bn_add):
+                    self.bn_add[b.idx] = (a, o)
+                    break
+        self.add_of_bn = {a.idx: nodes[b] for b, (a, _) in self.bn_add.items()}   # add idx -> its BN
         # ---- activation buffers per slot ----
         self.slots = []
         for k in range(slots):
@@ -322,6 +338,7 @@ class GraphPlan:
         if train:
             self.grad = self._alloc_set(nodes, shp)
             self._schedule(nodes, cons)
+            self._alias_add_grads(nodes, cons)
             mx = 0
             for n in nodes[1:]:
                 if n.kind in ("conv", "bn", "act"):
@@ -539,6 +556,38 @@ class GraphPlan:
             bufs[tid] = bufs[cid][..., off:off + C]
         return bufs
 
+    def _alias_add_grads(self, nodes, cons):
+        """An Add passes its output gradient unchanged to both inputs: an input whose
+        gradient buffer can BE the Add's (no copy) shares it.  That is the fused BN's output
+        (bn_add), and a skip input the Add writes first in backward order (beta 0) whose other
+        consumers all run after every reader of the Add's gradient -- they then accumulate
+        (beta 1) into the shared buffer after the BN / Add backward has read it.  Down the
+        SR residual trunk (srgan.py:165-181) every block's input gradient thus lives in one
+        buffer that each block's first conv accumulates into."""
+        self.add_alias = {}   # add node idx -> ids of the inputs whose gradient is the Add's
+        gin, gout = self.g.input.id, self.g.output.id
+        shared = set()
+        for a in (reversed(nodes[1:]) if not os.environ.get("DG_NO_ADD_ALIAS") else ()):
+            if a.kind != "add" or a.out.id == gout:
+                continue
+            root = self.grad[a.out.id]
+            al = set()
+            bn = self.add_of_bn.get(a.idx)
+            if bn is not None:   # (read by the BN's backward, at its place in the order)
+                self.grad[bn.out.id] = root
+                al.add(bn.out.id)
+            lim = a.idx if bn is None else bn.idx
+            for o in a.ins:
+                if (o.id in al or o.id in (gin, gout) or o.id in self.slice_of or o.id in shared
+                        or a.ins[0].id == a.ins[1].id or self.beta[(a.idx, o.id)] != 0.0
+                        or not all(c.idx < lim for c in cons[o.id] if c is not a)):
+                    continue
+                self.grad[o.id] = root
+                al.add(o.id)
+                shared.add(o.id)
+                break
+            self.add_alias[a.idx] = al
+
     def _schedule(self, nodes, cons):
         """beta (0 = first writer, 1 = accumulate) of every input-gradient write, in backward order."""
         written = set()
@@ -586,6 +635,7 @@ class GraphPlan:
         if out is not None:
             s[g.output.id] = out
         fed_now = set()   # convs whose fp16 x copy a producer wrote in this pass
+        add_done = set()  # Adds their BN wrote in this pass
 
         def x_copy(n):
             c = self.h_x_out.get(n.idx)
@@ -623,11 +673,15 @@ class GraphPlan:
             elif k == "bn":
                 mean, inv = self.saved[slot][n.name]
                 if training:
+                    fa = self.bn_add.get(n.idx)
+                    w = n if fa is None else fa[0]   # (the node whose output this call writes)
                     ops.bn_fwd_train(xin, A.param(f"{n.name}/gamma"), A.param(f"{n.name}/beta"), mean, inv,
-                                     self.bn.mean[n.name], self.bn.var[n.name], y, act=n.attrs["act"],
+                                     self.bn.mean[n.name], self.bn.var[n.name], s[w.out.id], act=n.attrs["act"],
                                      alpha=n.attrs["alpha"], momentum=n.attrs["momentum"], eps=n.attrs["eps"],
-                                     ws=ws, f16_out=x_copy(n))
-                    x_copied(n)
+                                     ws=ws, f16_out=x_copy(w), res=None if fa is None else s[fa[1].id])
+                    x_copied(w)
+                    if fa is not None:
+                        add_done.add(w.idx)
                 else:
                     ops.bn_fwd_infer(xin, A.param(f"{n.name}/gamma"), A.param(f"{n.name}/beta"),
                                      self.bn.mean[n.name], self.bn.var[n.name], y, act=n.attrs["act"],
@@ -636,8 +690,9 @@ class GraphPlan:
                 ops.prelu_fwd(xin, A.param(f"{n.name}/alpha"), y, block=n.attrs["block"], f16_out=x_copy(n))
                 x_copied(n)
             elif k == "add":
-                ops.add(xin, s[n.ins[1].id], y, f16_out=x_copy(n))
-                x_copied(n)
+                if n.idx not in add_done:
+                    ops.add(xin, s[n.ins[1].id], y, f16_out=x_copy(n))
+                    x_copied(n)
             elif k == "concat":
                 off = 0
                 for t in n.ins:
@@ -758,7 +813,8 @@ class GraphPlan:
                 dy_copied(n, hc)
             elif k == "add":
                 for t in n.ins:
-                    if need(t):
+                    # (a fused BN's or a skip input's gradient may BE this one: _alias_add_grads)
+                    if need(t) and t.id not in self.add_alias.get(n.idx, ()):
                         ops.accumulate(dz, gr[t.id], beta_of(n, t))
             elif k == "concat":
                 off = 0

@@ -477,12 +477,13 @@ def _rows(t):
 
 def bn_fwd_train(y, gamma, beta, save_mean, save_invstd, moving_mean, moving_var, z, act="none", alpha=0.3,
                  momentum=0.99, eps=1e-3, drop_rate=0.0, drop_seed=0, step_dev=None, ws=None, z_planes=(),
-                 segments=1, drop_seed_stride=0, f16_out=None):
+                 segments=1, drop_seed_stride=0, f16_out=None, res=None):
     """z_planes: up to two (uint8 device tensor, planes C, column) -- packed x
     planes of consuming convs that also receive z.  segments: the rows are that
     many consecutive independent BN calls (dg_bn_fwd_train_seg; save_mean /
     save_invstd [segments, C], dropout seed drop_seed + s * drop_seed_stride).
-    f16_out: the consuming fp16 conv's x PlaneBuf, which also receives z's fp16 copy."""
+    f16_out: the consuming fp16 conv's x PlaneBuf, which also receives z's fp16 copy.
+    res: a residual Add fused after the block, z = act(BN(y)) + res (same shape as z)."""
     C = y.shape[-1]
     M = _rows(y)
     if M % segments:
@@ -495,7 +496,8 @@ def bn_fwd_train(y, gamma, beta, save_mean, save_invstd, moving_mean, moving_var
          _p(save_invstd), _p(moving_mean), _p(moving_var), float(momentum), float(eps), _p(z), pix_ld(z, C),
          act_id(act), float(alpha), float(drop_rate), ctypes.c_uint32(drop_seed & 0xFFFFFFFF),
          ctypes.c_uint32(drop_seed_stride & 0xFFFFFFFF), _p(step_dev),
-         zp[0][0], zp[0][1], zp[0][2], zp[1][0], zp[1][1], zp[1][2], _f16(f16_out), _p(buf), n, _stream())
+         zp[0][0], zp[0][1], zp[0][2], zp[1][0], zp[1][1], zp[1][2], _p(res), pix_ld(res, C) if res is not None else 0,
+         _f16(f16_out), _p(buf), n, _stream())
     return z
 
 

@@ -242,13 +242,17 @@ int dg_bn_bwd_seg(int S, int M, int C, const float *dz, int lddz, const float *z
  * (z_f16 / dy_f16: [S*M rows][C] fp16, round-to-nearest-even -- the bytes the conv's own
  * conversion would write into its dg_conv_planes_t x / dy buffer, which the caller then
  * passes as ready; 8-byte aligned; NULL = none).  The SR family's mixed_float16 convs
- * (srgan.py:63-66) thus skip their per-call fp32 -> fp16 conversion of these operands. */
+ * (srgan.py:63-66) thus skip their per-call fp32 -> fp16 conversion of these operands.
+ * res (may be NULL): a residual Add fused after the block, z = act(BN(y)) + res
+ * ([S*M rows][C], pixel stride ldres; the residual blocks' keras.layers.Add,
+ * srgan.py:165 / :180, fsrgan.py:176 / :214) -- the Add's own pass disappears. */
 int dg_bn_fwd_train_seg_h(int S, int M, int C, const float *y, int ldy, const float *gamma, const float *beta,
                           float *save_mean, float *save_invstd,
                           float *moving_mean, float *moving_var, float momentum, float eps,
                           float *z, int ldz, int act, float alpha,
                           float drop_rate, uint32_t drop_seed, uint32_t drop_seed_stride, const int32_t *step_dev,
-                          void *zp0, int zp0C, int zp0col, void *zp1, int zp1C, int zp1col, void *z_f16,
+                          void *zp0, int zp0C, int zp0col, void *zp1, int zp1C, int zp1col,
+                          const float *res, int ldres, void *z_f16,
                           void *ws, size_t ws_bytes, dg_stream_t stream);
 int dg_bn_bwd_seg_h(int S, int M, int C, const float *dz, int lddz, const float *z, int ldz,
                     const float *y, int ldy, const float *gamma,

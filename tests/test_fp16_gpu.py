@@ -342,3 +342,51 @@ def test_srgan_fp16_producers_feed_their_convs():
     assert {"bn", "prelu", "add"} <= kinds, kinds
     assert len(Gp.h_x_out) >= 30 and len(Gp.h_dy_out) >= 30, (len(Gp.h_x_out), len(Gp.h_dy_out))
     assert len(tr.Dp.h_x_out) >= 5 and len(tr.Dp.h_dy_out) >= 5
+
+
+def _two_steps(model_cls, PG, PD, PV, x, y, bn_add, monkeypatch):
+    for k in ("DG_NO_BN_ADD", "DG_NO_ADD_ALIAS"):
+        if bn_add:
+            monkeypatch.delenv(k, raising=False)
+        else:
+            monkeypatch.setenv(k, "1")
+    m = model_cls(Args(crop_size=32))
+    m.generator.arena.load(PG)
+    m.discriminator.arena.load(PD)
+    if PV is not None:
+        m.vgg.arena.load(PV)
+    tr = m.trainer(x.shape, y.shape)
+    for t in m.loss_scales:
+        t[0] = LS
+    xd, yd = torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV)
+    losses = [tr.step(xd, yd).clone() for _ in range(2)]
+    torch.cuda.synchronize()
+    return m, tr, losses
+
+
+@gpu
+@pytest.mark.parametrize("which", ["srgan", "fsrgan"])
+def test_bn_residual_add_fusion_is_bit_identical(which, monkeypatch):
+    """A linear BN feeding only a residual Add writes act(BN(y)) + skip into the Add's output,
+    and the Add's inputs share its gradient buffer where the order allows (dgan/graph.py
+    bn_add, _alias_add_grads): the same fp32 operations, so two training steps match the
+    unfused, copying graph bit for bit (losses, weights, Adam slots, G(x))."""
+    if which == "srgan":
+        from srgan import SRGAN as cls
+    else:
+        from fsrgan import FastSRGAN as cls
+    m0 = cls(Args(crop_size=32))
+    PG, PD = m0.generator.arena.export(), m0.discriminator.arena.export()
+    PV = m0.vgg.arena.export() if m0.vgg is not None else None
+    x, y = _synthetic(2, 32, 4, seed=71)
+    a, ta, la = _two_steps(cls, PG, PD, PV, x, y, True, monkeypatch)
+    b, tb, lb = _two_steps(cls, PG, PD, PV, x, y, False, monkeypatch)
+    assert len(ta.Gp.bn_add) >= (17 if which == "srgan" else 2) and not tb.Gp.bn_add
+    shared = sum(len(v) for v in ta.Gp.add_alias.values())
+    assert shared >= len(ta.Gp.bn_add) + 1 and not any(tb.Gp.add_alias.values()), shared
+    for u, v in zip(la, lb):
+        assert torch.equal(u, v), (u, v)
+    assert torch.equal(ta.gen_output, tb.gen_output)
+    for na, nb in ((a.generator, b.generator), (a.discriminator, b.discriminator)):
+        for t in ("data", "m", "v"):
+            assert torch.equal(getattr(na.arena, t), getattr(nb.arena, t)), t
