@@ -19,6 +19,8 @@
 // (dx = new + beta * dx) so a tensor with several consumers accumulates its
 // gradient in place.
 #include "common.h"
+#include <cstring>
+#include <initializer_list>
 #include <algorithm>
 
 namespace dg {
@@ -75,6 +77,15 @@ __global__ void __launch_bounds__(256) k_rows_final10(const float *part, int R, 
 // PReLU = relu(x) - alpha*relu(-x)  (Keras): x>0 ? x : alpha[c]*x; its
 // gradient is 1 / alpha / 0 for x >0 / <0 / ==0, d alpha = -relu(-x).
 // --------------------------------------------------------------------------
+// A/B switch: DG_PLAN_DISABLE containing "prelu4" keeps the one-channel kernels
+static bool plan_off_prelu4() {
+    static const bool off = [] {
+        const char *l = getenv("DG_PLAN_DISABLE");
+        return l && strstr(l, "prelu4");
+    }();
+    return off;
+}
+
 struct ShufGeom {
     int H, W, C, B;
 };
@@ -87,6 +98,14 @@ __device__ __forceinline__ long shuf_out_pix(long pix, int ch, const ShufGeom &g
     const int r = (int)(pix - n * hw);
     const int h = r / g.W, w = r - h * g.W;
     return (n * g.H * g.B + (long)h * g.B + i) * ((long)g.W * g.B) + (long)w * g.B + j;
+}
+
+// float4 path: C % 4 == 0, every row stride % 4 == 0 and every base 16-byte aligned
+static bool prelu_v4(int C, std::initializer_list<std::pair<const void *, int>> ts) {
+    if (C % 4) return false;
+    for (const auto &t : ts)
+        if ((t.second % 4) || (((uintptr_t)t.first) & 15)) return false;
+    return !plan_off_prelu4();
 }
 
 // zh: the consuming fp16 conv's operand copy of z ([output pixels][C]), or NULL
@@ -104,6 +123,28 @@ __global__ void __launch_bounds__(256) k_prelu_fwd(long npix, ShufGeom g, const 
         const float o = v > 0.f ? v : alpha[c] * v;
         z[op * ldz + c] = o;
         if (zh) zh[op * g.C + c] = (_Float16)o;
+    }
+}
+
+// four channels per thread (C % 4 == 0, float4-aligned rows): the four share one
+// depth_to_space sub-position, so their z elements are adjacent too
+__global__ void __launch_bounds__(256) k_prelu_fwd4(long npix, ShufGeom g, const float *__restrict__ y, int ldy,
+                                                   const float *__restrict__ alpha, float *__restrict__ z, int ldz,
+                                                   _Float16 *__restrict__ zh) {
+    const int CB4 = g.C * g.B * g.B / 4;
+    const long total = npix * CB4;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long pix = e / CB4;
+        const int ch = (int)(e - pix * CB4) * 4;
+        int c;
+        const long op = shuf_out_pix(pix, ch, g, c);
+        const f32x4 v = *reinterpret_cast<const f32x4 *>(y + pix * ldy + ch);
+        const f32x4 a = *reinterpret_cast<const f32x4 *>(alpha + c);
+        f32x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = v[q] > 0.f ? v[q] : a[q] * v[q];
+        *reinterpret_cast<f32x4 *>(z + op * ldz + c) = o;
+        if (zh) store_f16x4(zh + op * g.C + c, o);
     }
 }
 
@@ -138,6 +179,55 @@ __global__ void __launch_bounds__(256) k_prelu_bwd(long npix, ShufGeom g, const 
     if (rl == 0 && ch < CB) {
         float s = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
         part[(long)blockIdx.y * CB + ch] = s;  // per input channel; folded over the B*B sub-positions below
+    }
+}
+
+// four channels per thread, 64 channel quads x 4 row lanes per block: each channel's
+// rows and row lanes are summed in k_prelu_bwd's order (the same partials)
+__global__ void __launch_bounds__(256) k_prelu_bwd4(long npix, ShufGeom g, const float *__restrict__ y, int ldy,
+                                                   const float *__restrict__ alpha, const float *__restrict__ dz,
+                                                   int lddz, float *__restrict__ dy, int lddy, float beta, long rows,
+                                                   float *__restrict__ part, _Float16 *__restrict__ dyh) {
+    const int CB = g.C * g.B * g.B;
+    const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+    const int ch = (blockIdx.x * 64 + cl) * 4;
+    const long r0 = (long)blockIdx.y * rows;
+    const long r1 = std::min<long>(npix, r0 + rows);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (ch < CB) {
+        int c = 0;
+        shuf_out_pix(r0, ch, g, c);
+        const f32x4 a = *reinterpret_cast<const f32x4 *>(alpha + c);
+        auto row = [&](long pix) {
+            int cc;
+            const long op = shuf_out_pix(pix, ch, g, cc);
+            const f32x4 v = *reinterpret_cast<const f32x4 *>(y + pix * ldy + ch);
+            const f32x4 gz = *reinterpret_cast<const f32x4 *>(dz + op * lddz + c);
+            float *o = dy + pix * lddy + ch;
+            f32x4 r;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float d = v[q] > 0.f ? gz[q] : (v[q] < 0.f ? a[q] * gz[q] : 0.f);
+                r[q] = d;
+                acc[q] += gz[q] * fminf(v[q], 0.f);
+            }
+            if (beta != 0.f) r += beta * *reinterpret_cast<const f32x4 *>(o);
+            *reinterpret_cast<f32x4 *>(o) = r;
+            if (dyh) store_f16x4(dyh + pix * CB + ch, r);   // the producing fp16 conv's dy copy
+        };
+        long pix = r0 + rl;
+        for (; pix + 4 < r1; pix += 8) {
+            row(pix);
+            row(pix + 4);
+        }
+        for (; pix < r1; pix += 4) row(pix);
+    }
+    __shared__ f32x4 red[4][64];
+    red[rl][cl] = acc;
+    __syncthreads();
+    if (rl == 0 && ch < CB) {
+        const f32x4 sum = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+        *reinterpret_cast<f32x4 *>(part + (long)blockIdx.y * CB + ch) = sum;
     }
 }
 
@@ -768,8 +858,12 @@ int dg_prelu_fwd_h(int N, int H, int W, int C, int block, const float *y, int ld
     DG_ARG(ldy >= C * block * block && ldz >= C, "bad strides");
     const long npix = (long)N * H * W;
     dg::ShufGeom g{H, W, C, block};
-    hipLaunchKernelGGL(dg::k_prelu_fwd, dim3(dg::lgrid(npix * C * block * block)), dim3(256), 0, (hipStream_t)stream,
-                       npix, g, y, ldy, alpha, z, ldz, (_Float16 *)z_f16);
+    if (dg::prelu_v4(C, {{y, ldy}, {z, ldz}, {alpha, 4}}) && (((uintptr_t)z_f16) & 7) == 0)
+        hipLaunchKernelGGL(dg::k_prelu_fwd4, dim3(dg::lgrid(npix * C * block * block / 4)), dim3(256), 0,
+                           (hipStream_t)stream, npix, g, y, ldy, alpha, z, ldz, (_Float16 *)z_f16);
+    else
+        hipLaunchKernelGGL(dg::k_prelu_fwd, dim3(dg::lgrid(npix * C * block * block)), dim3(256), 0,
+                           (hipStream_t)stream, npix, g, y, ldy, alpha, z, ldz, (_Float16 *)z_f16);
     DG_LAUNCHED("prelu_fwd");
     return DG_OK;
 }
@@ -795,8 +889,12 @@ int dg_prelu_bwd_h(int N, int H, int W, int C, int block, const float *y, int ld
     dg::RedPlan rp = dg::red_plan(npix);
     dg::ShufGeom g{H, W, C, block};
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(dg::k_prelu_bwd, dim3(dg_cdiv(CB, 64), rp.R), dim3(256), 0, s, npix, g, y, ldy, alpha, dz, lddz,
-                       dy, lddy, beta, rp.rows, (float *)ws, (_Float16 *)dy_f16);
+    if (dg::prelu_v4(C, {{y, ldy}, {dz, lddz}, {dy, lddy}, {alpha, 4}, {ws, 4}}) && (((uintptr_t)dy_f16) & 7) == 0)
+        hipLaunchKernelGGL(dg::k_prelu_bwd4, dim3(dg_cdiv(CB, 256), rp.R), dim3(256), 0, s, npix, g, y, ldy, alpha, dz,
+                           lddz, dy, lddy, beta, rp.rows, (float *)ws, (_Float16 *)dy_f16);
+    else
+        hipLaunchKernelGGL(dg::k_prelu_bwd, dim3(dg_cdiv(CB, 64), rp.R), dim3(256), 0, s, npix, g, y, ldy, alpha, dz,
+                           lddz, dy, lddy, beta, rp.rows, (float *)ws, (_Float16 *)dy_f16);
     DG_LAUNCHED("prelu_bwd");
     if (dalpha) {
         hipLaunchKernelGGL(dg::k_prelu_alpha_final, dim3(dg_cdiv(C, 16)), dim3(256), 0, s, (const float *)ws, rp.R, C,

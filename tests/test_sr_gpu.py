@@ -51,11 +51,13 @@ def _padded(shape, C_ld=None):
 # layers
 # -------------------------------------------------------------------------
 @gpu
-@pytest.mark.parametrize("block", [1, 2])
-def test_prelu_depth_to_space(block):
+@pytest.mark.parametrize("block,N,H,W,C", [(1, 2, 5, 7, 12), (2, 2, 5, 7, 12), (2, 3, 13, 9, 64), (2, 2, 5, 7, 3),
+                                           (1, 2, 6, 5, 3)])
+def test_prelu_depth_to_space(block, N, H, W, C):
+    """float4 kernels (C % 4 == 0: k_prelu_fwd4 / k_prelu_bwd4, SRGAN's 64-channel shape with
+    ragged row chunks) and the one-channel kernels (C = 3)."""
     from dgan import ops
-    rng = np.random.default_rng(block)
-    N, H, W, C = 2, 5, 7, 12
+    rng = np.random.default_rng(block * 100 + C)
     y = rng.standard_normal((N, H, W, C * block * block))
     y[0, 0, 0, :3] = 0.0  # exact zeros: gradient 0 (relu' at 0)
     a = rng.standard_normal((1, 1, C)) * 0.3
