@@ -182,15 +182,15 @@ __global__ void __launch_bounds__(256) k_prelu_bwd(long npix, ShufGeom g, const 
     }
 }
 
-// four channels per thread, 64 channel quads x 4 row lanes per block: each channel's
-// rows and row lanes are summed in k_prelu_bwd's order (the same partials)
+// four channels per thread, 16 channel quads x 16 row lanes per block (sixteen rows'
+// loads in flight per channel quad); the row lanes' sums are added in lane order
 __global__ void __launch_bounds__(256) k_prelu_bwd4(long npix, ShufGeom g, const float *__restrict__ y, int ldy,
                                                    const float *__restrict__ alpha, const float *__restrict__ dz,
                                                    int lddz, float *__restrict__ dy, int lddy, float beta, long rows,
                                                    float *__restrict__ part, _Float16 *__restrict__ dyh) {
     const int CB = g.C * g.B * g.B;
-    const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
-    const int ch = (blockIdx.x * 64 + cl) * 4;
+    const int cl = threadIdx.x & 15, rl = threadIdx.x >> 4;
+    const int ch = (blockIdx.x * 16 + cl) * 4;
     const long r0 = (long)blockIdx.y * rows;
     const long r1 = std::min<long>(npix, r0 + rows);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(256) k_prelu_bwd4(long npix, ShufGeom g, const
         int c = 0;
         shuf_out_pix(r0, ch, g, c);
         const f32x4 a = *reinterpret_cast<const f32x4 *>(alpha + c);
-        auto row = [&](long pix) {
+        for (long pix = r0 + rl; pix < r1; pix += 16) {
             int cc;
             const long op = shuf_out_pix(pix, ch, g, cc);
             const f32x4 v = *reinterpret_cast<const f32x4 *>(y + pix * ldy + ch);
@@ -207,26 +207,20 @@ __global__ void __launch_bounds__(256) k_prelu_bwd4(long npix, ShufGeom g, const
             f32x4 r;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const float d = v[q] > 0.f ? gz[q] : (v[q] < 0.f ? a[q] * gz[q] : 0.f);
-                r[q] = d;
+                r[q] = v[q] > 0.f ? gz[q] : (v[q] < 0.f ? a[q] * gz[q] : 0.f);
                 acc[q] += gz[q] * fminf(v[q], 0.f);
             }
             if (beta != 0.f) r += beta * *reinterpret_cast<const f32x4 *>(o);
             *reinterpret_cast<f32x4 *>(o) = r;
             if (dyh) store_f16x4(dyh + pix * CB + ch, r);   // the producing fp16 conv's dy copy
-        };
-        long pix = r0 + rl;
-        for (; pix + 4 < r1; pix += 8) {
-            row(pix);
-            row(pix + 4);
         }
-        for (; pix < r1; pix += 4) row(pix);
     }
-    __shared__ f32x4 red[4][64];
+    __shared__ f32x4 red[16][16];
     red[rl][cl] = acc;
     __syncthreads();
     if (rl == 0 && ch < CB) {
-        const f32x4 sum = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+        f32x4 sum = red[0][cl];
+        for (int l = 1; l < 16; ++l) sum += red[l][cl];
         *reinterpret_cast<f32x4 *>(part + (long)blockIdx.y * CB + ch) = sum;
     }
 }
@@ -890,7 +884,7 @@ int dg_prelu_bwd_h(int N, int H, int W, int C, int block, const float *y, int ld
     dg::ShufGeom g{H, W, C, block};
     hipStream_t s = (hipStream_t)stream;
     if (dg::prelu_v4(C, {{y, ldy}, {dz, lddz}, {dy, lddy}, {alpha, 4}, {ws, 4}}) && (((uintptr_t)dy_f16) & 7) == 0)
-        hipLaunchKernelGGL(dg::k_prelu_bwd4, dim3(dg_cdiv(CB, 256), rp.R), dim3(256), 0, s, npix, g, y, ldy, alpha, dz,
+        hipLaunchKernelGGL(dg::k_prelu_bwd4, dim3(dg_cdiv(CB, 64), rp.R), dim3(256), 0, s, npix, g, y, ldy, alpha, dz,
                            lddz, dy, lddy, beta, rp.rows, (float *)ws, (_Float16 *)dy_f16);
     else
         hipLaunchKernelGGL(dg::k_prelu_bwd, dim3(dg_cdiv(CB, 64), rp.R), dim3(256), 0, s, npix, g, y, ldy, alpha, dz,
