@@ -126,6 +126,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(f"bench.py --gpus {args.gpus}: launch one process per GPU with "
+                 f"`python -m torch.distributed.run --nproc-per-node {args.gpus} ... bench.py --gpus {args.gpus}`")
+    if "WORLD_SIZE" in os.environ and world != args.gpus:
+        sys.exit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world} (torch.distributed.run --nproc-per-node "
+                 f"must equal --gpus)")
     if os.environ.get("DG_DIST_BACKEND", "nccl") != "nccl":
         local %= max(1, torch.cuda.device_count())  # rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
@@ -139,10 +145,16 @@ def main():
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
         backend = os.environ.get("DG_DIST_BACKEND", "nccl")  # gloo: rehearse N ranks on one GPU
+        # no fallback: a process group that cannot be built on RCCL ends the run
         if backend == "nccl":
+            if not dist.is_nccl_available():
+                sys.exit("bench.py: torch.distributed has no nccl (RCCL) backend in this build")
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+        if dist.get_backend() != backend or dist.get_world_size() != world:
+            sys.exit(f"bench.py: process group is {dist.get_backend()} x{dist.get_world_size()}, "
+                     f"expected {backend} x{world}")
 
     import dgan
     dgan.build()  # no-op when the in-tree library is current
@@ -264,6 +276,24 @@ def main():
                     "frac_of_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK, 4),
                     "conv_launch_ms_per_step": round(conv_ms, 3), "conv_gflop_per_step": round(conv_flops / 1e9, 1),
                     "step_frac": round(conv_flops / (ms_per_step * 1e-3) / peak, 4)}
+        # per network (conv descriptor labels "G.down1", "D.last", "vgg19.block1_conv1", ...);
+        # for pix2pix, `p2p_convs` = the G + D Conv2D / Conv2DTranspose kernels the north star's
+        # ">= 40 % of MFMA peak" names (pix2pix.py:110-142, 194-220), VGG19 excluded
+        nets = {}
+        for r in recs:
+            net = (r["label"] or "?").split(".", 1)[0]
+            a = nets.setdefault(net, [0.0, 0.0])
+            a[0] += r["flops"]
+            a[1] += r["ms"]
+
+        def frac_of(fl, ms):
+            return {"gflop_per_step": round(fl / 1e9, 1), "ms_per_step": round(ms, 3),
+                    "achieved": round(fl / (ms * 1e-3) / 1e12, 2), "frac": round(fl / (ms * 1e-3) / peak, 4)}
+        roofline["by_net"] = {n: frac_of(*v) for n, v in sorted(nets.items()) if v[1] > 0}
+        if args.model == "pix2pix" and "G" in nets and "D" in nets:
+            fl, ms = nets["G"][0] + nets["D"][0], nets["G"][1] + nets["D"][1]
+            roofline["p2p_convs"] = {**frac_of(fl, ms), "nets": "G + D (VGG19 excluded)",
+                                     "target_frac": 0.40}
         if rank == 0 and os.environ.get("DG_BENCH_DETAIL"):
             for r in sorted(recs, key=lambda r: -r["ms"])[:int(os.environ.get("DG_BENCH_DETAIL_N", "60"))]:
                 print(json.dumps({**r, "tflops": r["flops"] / (r["ms"] * 1e-3) / 1e12}), file=sys.stderr)
@@ -311,6 +341,7 @@ def main():
             "config": {"workload": workload, "model": wl["model"], "global_batch": world * batch,
                        "batch_per_gpu": batch, "image_size": wl["size"], "scale": wl["scale"],
                        "parallelism": f"dp{world}", "hip_graph": hip_graph,
+                       "process_group": dist.get_backend() if distributed else None,
                        "identity_pass": not args.no_identity if args.model == "pix2pix" else None,
                        "conv_gflop_per_image": round(step_flops / batch / 1e9, 2) if step_flops else None},
             "losses": [round(float(v), 6) for v in losses],
@@ -331,8 +362,10 @@ def traffic_of(args, wl, content, batch, rank, world):
         except Exception as e:  # report and fall back to the committed profile
             print(f"[bench] PMC leg failed ({e}); using the committed profile", file=sys.stderr)
     path = os.path.join(REPO, "profiles", wl["traffic"])
-    if not content or batch != wl["batch"] or not os.path.exists(path):
-        return None, None
+    default_fp16 = bool(wl.get("fp16", 0))
+    if (not content or batch != wl["batch"] or args.no_identity or not os.path.exists(path)
+            or (args.fp16 is not None and bool(args.fp16) != default_fp16)):
+        return None, None   # the committed profile is of the default workload only
     with open(path) as f:
         t = json.load(f)
     sys.path.insert(0, os.path.join(REPO, "scripts"))
@@ -352,8 +385,15 @@ def pmc_leg(args, batch):
     from pmc_traffic import summarise
     steps = 3
     out = tempfile.mkdtemp(prefix="dg_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    # the child measures THIS workload: every flag that changes the step is passed on
     child = [sys.executable, os.path.join(REPO, "bench.py"), "--profile-only", "--no-graph", "--steps", str(steps),
              "--warmup", "2", "--model", args.model, "--batch", str(batch)]
+    if args.fp16 is not None:
+        child += ["--fp16", str(int(args.fp16))]
+    if args.no_content:
+        child.append("--no-content")
+    if args.no_identity:
+        child.append("--no-identity")
     csvs = []
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         d = os.path.join(out, ctr)

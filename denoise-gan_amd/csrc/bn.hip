@@ -284,6 +284,18 @@ k_bn_apply_infer(const float *__restrict__ y, int ld, long M, int C, const float
     }
 }
 
+// the block output z, read only for act' (z NULL: a linear BN, act' = 1 -- the
+// fused BN + residual Add never writes its own z)
+template <int V>
+__device__ __forceinline__ void load_z(const float *__restrict__ z, long off, float (&zv)[V]) {
+    if (z) {
+        loadv<V>(z + off, zv);
+    } else {
+#pragma unroll
+        for (int q = 0; q < V; ++q) zv[q] = 0.f;
+    }
+}
+
 // backward: partial sums of dbn and dbn*xhat per (chunk, channel)
 template <int V>
 __global__ void __launch_bounds__(256)
@@ -296,7 +308,8 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
     const int c0 = (blockIdx.x * cpb + slot) * V;
     {   // segment blockIdx.z: its rows and its saved statistics
         const long ro = (long)blockIdx.z * M;
-        dz += ro * lddz; z += ro * ldz; y += ro * ldy;
+        dz += ro * lddz; y += ro * ldy;
+        if (z) z += ro * ldz;
         mean += (long)blockIdx.z * C; invstd += (long)blockIdx.z * C;
     }
     const long pbase = (long)blockIdx.z * gridDim.y;
@@ -325,7 +338,7 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 loadv<V>(dz + (r + u * RL) * lddz + c0, dv[u]);
-                loadv<V>(z + (r + u * RL) * ldz + c0, zv[u]);
+                load_z<V>(z, (r + u * RL) * ldz + c0, zv[u]);
                 loadv<V>(y + (r + u * RL) * ldy + c0, yv[u]);
             }
 #pragma unroll
@@ -334,7 +347,7 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
         for (; r < r1; r += RL) {
             float dv[V], zv[V], yv[V];
             loadv<V>(dz + r * lddz + c0, dv);
-            loadv<V>(z + r * ldz + c0, zv);
+            load_z<V>(z, r * ldz + c0, zv);
             loadv<V>(y + r * ldy + c0, yv);
             acc_row(dv, zv, yv);
         }
@@ -409,7 +422,7 @@ k_bn_bwd_apply(const float *__restrict__ dz, int lddz, const float *__restrict__
         const float *cf = coef + (long)seg_of(rr, M) * 4 * C;
         float dv[V], zv[V], yv[V], A[V], B[V], D[V], Mu[V], o[V];
         loadv<V>(dz + r * lddz + c, dv);
-        loadv<V>(z + r * ldz + c, zv);
+        load_z<V>(z, r * ldz + c, zv);
         loadv<V>(y + r * ldy + c, yv);
         loadv<V>(cf + c, A);
         loadv<V>(cf + C + c, B);
@@ -590,7 +603,10 @@ int dg_bn_bwd_seg_h(int S, int M, int C, const float *dz, int lddz, const float 
                     float beta, void *ws, size_t ws_bytes, dg_stream_t stream) {
     DG_ARG(!dy_f16 || (((uintptr_t)dy_f16) & 7) == 0, "fp16 copy must be 8-byte aligned");
     // dy NULL: only its planes are written (every consumer reads dy_planes)
-    DG_ARG(dz && z && y && save_mean && save_invstd && (dy || dy_planes) && ws, "NULL tensor");
+    // z NULL: allowed for a linear BN without dropout (act' = 1, z is not read)
+    DG_ARG(dz && (z || (act == DG_ACT_NONE && drop_rate == 0.f)) && y && save_mean && save_invstd &&
+           (dy || dy_planes) && ws, "NULL tensor");
+    if (!z) ldz = C;
     DG_ARG(S >= 1 && S <= 8 && M > 0 && C > 0 && lddz >= C && ldz >= C && ldy >= C && (!dy || lddy >= C), "bad shape");
     DG_ARG(ws_bytes >= dg::bn_ws_floats(M, C, S) * sizeof(float), "workspace too small");
     if (drop_rate > 0.f && act != DG_ACT_RELU) {

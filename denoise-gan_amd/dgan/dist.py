@@ -42,6 +42,10 @@ class GradSync:
         self.bucket = max(1, bucket_bytes // 4)
         self.works = []
         self.issued = 0
+        # all-reduces of the last step: issued before finish() (i.e. while the
+        # backward was still being enqueued) and in total (D arena included)
+        self.last_mid_backward = 0
+        self.last_total = 0
         # arena end offset of every layer's last variable, in layout order
         self.layer_end = {}
         for name in g_arena.layout:
@@ -62,8 +66,10 @@ class GradSync:
             self.issued = end
 
     def finish(self):
+        self.last_mid_backward = len(self.works)
         if self.issued < self.g.numel:
             self._reduce(self.g.grad[self.issued:])
+        self.last_total = len(self.works)
         for w in self.works:
             w.wait()
         self.works.clear()

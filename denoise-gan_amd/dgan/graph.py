@@ -315,8 +315,11 @@ class GraphPlan:
                 continue
             for t, o in ((a.ins[0], a.ins[1]), (a.ins[1], a.ins[0])):
                 b = t.node
+                # the skip must be final when the BN runs: produced by an earlier node
+                # (the graph input is node 0)
                 if (b.kind == "bn" and ops.act_id(b.attrs["act"]) == 0 and len(cons[t.id]) == 1
-                        and t.id not in self.slice_of and o.id != t.id and b.idx not in self.bn_add):
+                        and t.id not in self.slice_of and o.id != t.id and b.idx not in self.bn_add
+                        and o.node.idx < b.idx):
                     self.bn_add[b.idx] = (a, o)
                     break
         self.add_of_bn = {a.idx: nodes[b] for b, (a, _) in self.bn_add.items()}   # add idx -> its BN
@@ -795,6 +798,9 @@ class GraphPlan:
                                    planes=P)
             elif k == "bn":
                 mean, inv = self.saved[slot][n.name]
+                # a BN fused with its residual Add never wrote s[n.out.id]: only a linear BN
+                # may be fused, whose backward does not read z (ops.bn_bwd passes NULL)
+                assert n.idx not in self.bn_add or ops.act_id(n.attrs["act"]) == 0
                 b = beta_of(n, t_in)
                 tgt = gr[t_in.id] if b == 0.0 else self._scratch(self.shape[t_in.id])
                 hc = dy_copy(n, b)

@@ -522,7 +522,10 @@ def bn_bwd(dz, z, y, gamma, save_mean, save_invstd, dy, dgamma, dbeta, act="none
     M //= segments
     ws = ws or default_workspace()
     buf, n = ws.get(bn_workspace_bytes(M, C, segments))
-    call("dg_bn_bwd_seg_h", segments, M, C, _p(dz), pix_ld(dz, C), _p(z), pix_ld(z, C), _p(y), pix_ld(y, C),
+    if act_id(act) == 0 and drop_rate == 0.0:
+        z = None   # a linear BN's backward does not read z (dg_bn_bwd_seg_h)
+    call("dg_bn_bwd_seg_h", segments, M, C, _p(dz), pix_ld(dz, C), _p(z), pix_ld(z, C) if z is not None else C,
+         _p(y), pix_ld(y, C),
          _p(gamma), _p(save_mean), _p(save_invstd), act_id(act), float(alpha), float(drop_rate),
          _p(dy) if (dy_fp32 or dy_planes is None) else None, pix_ld(dy, C),
          None if dy_planes is None else dy_planes.data_ptr(), _f16(f16_out),

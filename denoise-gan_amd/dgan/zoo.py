@@ -67,13 +67,13 @@ def _make_divisible(v, divisor, min_value=None):
 
 
 def fsrgan_generator(gf=32, n_blocks=6, expansion=6):
-    """FastSRGAN.build_generator (fsrgan.py:99-214): MobileNetV2 inverted
+    """FastSRGAN.build_generator (fsrgan.py:99-220): MobileNetV2 inverted
     residual blocks, then two pixel-shuffle x2 upsamplers."""
     g = Graph("generator")
     x = g.input
-    c1 = g.conv(x, gf, 3, use_bias=True, name="conv2d")                                     # :202
-    c1 = g.bn(c1, name="batch_normalization")                                                 # :203
-    c1 = g.prelu(c1, name="p_re_lu")                                                          # :204
+    c1 = g.conv(x, gf, 3, use_bias=True, name="conv2d")                                     # :198
+    c1 = g.bn(c1, name="batch_normalization")                                                 # :199
+    c1 = g.prelu(c1, name="p_re_lu")                                                          # :200
 
     def residual_block(inputs, filters, block_id):                                            # :112-177
         in_ch = inputs.C
@@ -93,17 +93,17 @@ def fsrgan_generator(gf=32, n_blocks=6, expansion=6):
             return g.add(inputs, h, name=prefix + "add")
         return h
 
-    r = residual_block(c1, gf, 0)                                                             # :207
+    r = residual_block(c1, gf, 0)                                                             # :203-205
     for idx in range(1, n_blocks):
         r = residual_block(r, gf, idx)
-    c2 = g.conv(r, gf, 3, use_bias=True, name="conv2d_post")                                  # :212
-    c2 = g.bn(c2, name="batch_normalization_post")
-    c2 = g.add(c2, c1, name="add_long")                                                       # :214
+    c2 = g.conv(r, gf, 3, use_bias=True, name="conv2d_post")                                  # :208
+    c2 = g.bn(c2, name="batch_normalization_post")                                           # :209
+    c2 = g.add(c2, c1, name="add_long")                                                       # :210
     u = c2
-    for i in range(2):                                                                        # :217-218
+    for i in range(2):                                                                        # :213-214 (deconv2d :187-190)
         u = g.conv(u, gf * 4, 3, use_bias=True, name=f"deconv_{i}_conv")
         u = g.prelu(u, block=2, name=f"deconv_{i}_p_re_lu")
-    out = g.conv(u, 3, 3, use_bias=True, act="tanh", name="conv2d_out")                       # :221-222
+    out = g.conv(u, 3, 3, use_bias=True, act="tanh", name="conv2d_out")                       # :217-218
     return g.set_output(out)
 
 

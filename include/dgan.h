@@ -245,7 +245,9 @@ int dg_bn_bwd_seg(int S, int M, int C, const float *dz, int lddz, const float *z
  * (srgan.py:63-66) thus skip their per-call fp32 -> fp16 conversion of these operands.
  * res (may be NULL): a residual Add fused after the block, z = act(BN(y)) + res
  * ([S*M rows][C], pixel stride ldres; the residual blocks' keras.layers.Add,
- * srgan.py:165 / :180, fsrgan.py:176 / :214) -- the Add's own pass disappears. */
+ * srgan.py:165 / :180, fsrgan.py:176 / :214) -- the Add's own pass disappears.
+ * Backward: z (the block output) is read only for act'; a linear BN without dropout
+ * may pass z = NULL (the fused BN + Add above never writes its own z). */
 int dg_bn_fwd_train_seg_h(int S, int M, int C, const float *y, int ldy, const float *gamma, const float *beta,
                           float *save_mean, float *save_invstd,
                           float *moving_mean, float *moving_var, float momentum, float eps,

@@ -77,7 +77,27 @@ FP16 = None
 
 
 def _q16(t):
-    return t.to(torch.float16).to(t.dtype)
+    r = t.to(torch.float16)
+    tau = FP16.get("flip_tau") if FP16 is not None else None
+    if tau:
+        r = _flip_near_ties(t, r, tau)
+    return r.to(t.dtype)
+
+
+def _flip_near_ties(t, r, tau):
+    """Tie sensitivity (test diagnostics only): the elements of t whose fp64 value lies
+    within tau fp16 ulps of the midpoint between its two fp16 neighbours -- where an
+    fp32 value of the same quantity may round to the other neighbour -- take the OTHER
+    neighbour.  r: t rounded to fp16 (RNE)."""
+    mag = r.abs().view(torch.int16).to(torch.int32)      # fp16 magnitude bits
+    up = t.abs() > r.abs().to(t.dtype)                   # the other neighbour is further from 0
+    other_mag = torch.where(up, mag + 1, torch.clamp(mag - 1, min=0))
+    other = other_mag.to(torch.int16).view(torch.float16).to(t.dtype) * torch.where(t < 0, -1.0, 1.0).to(t.dtype)
+    rd = r.to(t.dtype)
+    mid = (rd + other) / 2
+    near = (t - mid).abs() < tau * (rd - other).abs()
+    near &= torch.isfinite(other) & (other_mag != mag)
+    return torch.where(near, other.to(torch.float16), r)
 
 
 def fp16_ops(ci, co):
@@ -372,17 +392,19 @@ class SRState:
         return autoencoder_generator(P, x, dec=dec)
 
 
-def train_step(st, x, y, apply=True, dec=None):
+def train_step(st, x, y, apply=True, dec=None, flip_tau=None):
     """One step of train_srgan.py:61-118 / train_fsrgan.py:61-120 /
     train_autoencoder.py:66-112 (all three share the gen-loss composition
     content + adv + 0*mse + mae; FSRGAN halves the disc loss).
     Returns dict(losses=(gen_total, adv, mae, mse, content, disc, var),
     gen, gG, gD).  dec: {"G", "Dr", "Df", "Vsr", "Vhr": oracle.decisions.Decisions}
     (any subset) -- the activation decisions of G(x), D(y), D(G(x)) and VGG19
-    on G(x) and on y (mask-conditioned parity)."""
+    on G(x) and on y (mask-conditioned parity).  flip_tau (fp16 only, test diagnostics):
+    every GEMM operand within flip_tau fp16 ulps of a rounding tie takes the other fp16
+    neighbour (_flip_near_ties) -- the tie sensitivity of the mixed_float16 step."""
     global FP16
     dec = dec or {}
-    FP16 = {"scale": st.ls["G"][0]} if st.fp16 else None
+    FP16 = {"scale": st.ls["G"][0], "flip_tau": flip_tau} if st.fp16 else None
     try:
         return _train_step(st, x, y, apply, dec)
     finally:
@@ -413,7 +435,7 @@ def _train_step(st, x, y, apply, dec):
     gs = torch.autograd.grad(gen_loss, [gen] + list(PG.values()), retain_graph=True)
     dgen, gG = gs[0], gs[1:]
     if st.fp16:
-        FP16 = {"scale": st.ls["D"][0]}
+        FP16 = {**FP16, "scale": st.ls["D"][0]}
     gD = torch.autograd.grad(disc, list(PD.values()))
     gG = {k: g.numpy() for k, g in zip(PG, gG)}
     gD = {k: g.numpy() for k, g in zip(PD, gD)}

@@ -6,9 +6,12 @@ the dynamic loss scale of both optimizers.
   * conv GEMMs vs torch fp64 on the same fp16-rounded operands: only the
     accumulation order differs (tolerance 2e-5 of the output scale);
   * the SRGAN / FastSRGAN training step vs oracle/sr_oracle.py's mixed_float16
-    emulation (S8: the same operand rounding, gradients at the loss scale):
-    losses to 1e-3 relative, G(x) max-abs 2e-3, each gradient within 2x the
-    emulation's own distance from the fp64 step (relative L2; see _run);
+    emulation (S8: the same operand rounding, gradients at the loss scale),
+    mask-conditioned on the HIP path's activation decisions (audited): losses
+    to 1e-3 relative, G(x) max-abs 2e-3, each gradient elementwise within
+    1e-4 + the larger of the emulation's own max-abs distance from the fp64 step
+    and its measured fp16 tie sensitivity, relative L2 within 2x its relative
+    distance (see _run);
   * against the plain fp64 oracle: |dPSNR| < 0.05 dB, losses to 1e-2;
   * loss scale: an overflowing scale skips the step (weights, Adam slots and
     the iteration count unchanged) and halves; finite steps keep it and count.
@@ -98,6 +101,10 @@ def _synthetic(N, H, scale, seed):
 
 
 LS = 2.0 ** 8
+# decision audits of the conditioned mixed_float16 comparisons (see _run)
+F16_TIE_TOL = 2e-3
+F16_REF_TIE_TOL = 5e-2
+TIE_TAU = 1.0 / 64
 
 
 def _run(model_cls, kind, N, H, ls=LS, **kw):
@@ -125,20 +132,44 @@ def _run(model_cls, kind, N, H, ls=LS, **kw):
     assert sg == sd == LS0 and float(m.loss_scales[0][2]) == 1.0 and float(m.loss_scales[1][2]) == 1.0
     gG = {n: m.generator.arena.grad_of(n).cpu().double().numpy() / sg for n, _ in m.generator.arena.var_list}
     gD = {n: m.discriminator.arena.grad_of(n).cpu().double().numpy() / sd for n, _ in m.discriminator.arena.var_list}
+    # Mask conditioning (as the fp32 step tests): the emulation and the fp64 step take the HIP
+    # path's ReLU / LeakyReLU / PReLU / max-pool decisions, each override audited as a near-tie.
+    # In mixed_float16 a pre-activation carries fp16 operand rounding, so the audit bars are
+    # fp16-sized: against the emulation (same fp16 rounding; only fp32-vs-fp64 arithmetic and
+    # operands whose fp32 / fp64 values round to different fp16 neighbours differ)
+    # F16_TIE_TOL; against the fp64 step (no fp16 rounding at all) F16_REF_TIE_TOL.  An
+    # indexing error flips decisions on values O(1) of the layer scale.
+    from gpu_decisions import audit_ok
+    from test_sr_gpu import _sr_decisions
+    dec_e, dec_r = _sr_decisions(tr), _sr_decisions(tr)
     st = S.SRState(kind, PG, PD, PV, scale=4, lr=1e-3, fp16=True)
     st.ls = {"G": [LS0, 0], "D": [LS0, 0]}
-    emu = S.train_step(st, x, y, apply=False)
-    ref = S.train_step(S.SRState(kind, PG, PD, PV, scale=4, lr=1e-3), x, y, apply=False)
+    emu = S.train_step(st, x, y, apply=False, dec=dec_e)
+    ref = S.train_step(S.SRState(kind, PG, PD, PV, scale=4, lr=1e-3), x, y, apply=False, dec=dec_r)
+    n_e = audit_ok(dec_e, F16_TIE_TOL, f"{kind} fp16 emulation")
+    n_r = audit_ok(dec_r, F16_REF_TIE_TOL, f"{kind} fp64")
     assert np.allclose(got, emu["losses"], rtol=1e-3, atol=1e-6), (got, emu["losses"])
     assert np.abs(gen - emu["gen"]).max() < 2e-3
     # Gradients: fp16 operand rounding is itself a perturbation of ~2^-12 per operand, which the
     # BN backward's mean subtractions amplify into the early layers (measured: the fp16 emulation
-    # differs from the fp64 oracle by 14% of scale on G conv2d/kernel), and fp32 (GPU) vs fp64
-    # (oracle) values round to different fp16 neighbours at rounding ties.  So each variable's
-    # GPU gradient must be as close to the emulation as the emulation is to the fp64 step
-    # (relative L2 within 2x that noise, or within 2e-2) -- a wrong GEMM is orders larger.
-    worst = 0.0
-    for grads, refg, fp64, label in ((gG, emu["gG"], ref["gG"], "G"), (gD, emu["gD"], ref["gD"], "D")):
+    # differs from the fp64 oracle by 14% of scale on G conv2d/kernel).  With the decisions shared,
+    # what is left between the GPU and the emulation is fp32 arithmetic and the operands that sit
+    # on an fp16 rounding tie (fp32 and fp64 values rounding to different neighbours: one fp16 ulp
+    # on one operand each).  At bs2 the discriminators' deepest BNs normalise over 8 pixels and
+    # amplify a few such flips to the size of the whole fp16 rounding noise (measured: flipping
+    # the operands within 1/64 ulp of a tie moves D d3_bn/beta by 5.8e-4 against 3.9e-4 of fp16
+    # noise), so the emulation's own tie sensitivity is measured (TIE_TAU) and the GPU gradient
+    # must be elementwise within 1e-4 + 1x max(fp16 noise, tie sensitivity), relative L2 within
+    # 2x the noise (or 2e-2); a wrong GEMM is orders larger.
+    # tie sensitivity: the emulation with every operand within TIE_TAU fp16 ulps of a rounding
+    # tie rounded the other way (sr_oracle._flip_near_ties) -- diagnostics
+    st_t = S.SRState(kind, PG, PD, PV, scale=4, lr=1e-3, fp16=True)
+    st_t.ls = {"G": [LS0, 0], "D": [LS0, 0]}
+    tie = S.train_step(st_t, x, y, apply=False, dec=_sr_decisions(tr), flip_tau=TIE_TAU)
+    worst = worst_e = 0.0
+    rows, bad = [], []
+    for grads, refg, fp64, tg, label in ((gG, emu["gG"], ref["gG"], tie["gG"], "G"),
+                                         (gD, emu["gD"], ref["gD"], tie["gD"], "D")):
         for n, g_ref in refg.items():
             den = float(np.linalg.norm(g_ref))
             if den < 1e-12:
@@ -146,16 +177,30 @@ def _run(model_cls, kind, N, H, ls=LS, **kw):
             err = float(np.linalg.norm(grads[n] - g_ref)) / den
             noise = float(np.linalg.norm(g_ref - fp64[n])) / den
             worst = max(worst, err / max(noise, 1e-2))
-            assert err <= max(2.0 * noise, 2e-2), f"{label} {n}: rel-L2 {err:.3e}, fp16 noise {noise:.3e}"
-            # elementwise: within 1e-4 + 2x the emulation's own max-abs distance from fp64
+            if err > max(2.0 * noise, 2e-2):
+                bad.append(f"{label} {n}: rel-L2 {err:.3e}, fp16 noise {noise:.3e}")
+            # elementwise: within 1e-4 + 1x the larger of the emulation's own max-abs distance
+            # from fp64 (fp16 rounding) and its tie sensitivity (the operands within TIE_TAU ulps
+            # of an fp16 rounding tie flipped)
             emax = float(np.abs(grads[n] - g_ref).max())
             nmax = float(np.abs(g_ref - fp64[n]).max())
-            assert emax <= 1e-4 + 2.0 * nmax, f"{label} {n}: max-abs {emax:.3e}, fp16 noise {nmax:.3e}"
+            tmax = float(np.abs(tg[n] - g_ref).max())
+            bar = 1e-4 + max(nmax, tmax)
+            worst_e = max(worst_e, emax / bar)
+            rows.append((emax / bar, f"{label} {n}: max-abs {emax:.3e}, fp16 noise {nmax:.3e}, "
+                                     f"tie sensitivity {tmax:.3e}, max|g| {np.abs(g_ref).max():.3e}"))
+            if emax > bar:
+                bad.append(rows[-1][1])
+    for r, txt in sorted(rows, reverse=True)[:12]:
+        print(f"  {r:.3f}  {txt}")
+    assert not bad, bad
     # mixed precision vs the fp64 step
     assert abs(psnr(gen, y) - psnr(ref["gen"], y)) < 0.05
     assert np.allclose(got, ref["losses"], rtol=1e-2, atol=1e-5), (got, ref["losses"])
-    print(f"{kind} fp16: worst grad error / max(fp16 noise, 1e-2) {worst:.2f}; dPSNR vs fp64 "
-          f"{abs(psnr(gen, y) - psnr(ref['gen'], y)):.2e} dB")
+    print(f"{kind} fp16: worst rel-L2 / max(fp16 noise, 1e-2) {worst:.2f}, worst max-abs / bar "
+          f"{worst_e:.2f}; dPSNR vs fp64 {abs(psnr(gen, y) - psnr(ref['gen'], y)):.2e} dB; overridden "
+          f"decisions {n_e} (emulation, worst {max(d.worst()[1] for d in dec_e.values()):.2e}) / {n_r} (fp64, "
+          f"worst {max(d.worst()[1] for d in dec_r.values()):.2e})")
     return m
 
 

@@ -56,8 +56,9 @@ VGG_TIE_REL = 2e-3
 # tests/test_sr_gpu.py (test_*_full_config_parity, test_fsrgan_full_size_parity).
 # Measured spread at r3 (thread-per-pixel narrow forward on the Co-3 output convs): ae_bs4 D
 # d5_bn/beta 2.51e-4 = 1e-4 + 1.003e-2 of its max, SRGAN D d1_conv/bias 1.25e-3, FastSRGAN bs8 G
-# conv2d/kernel 2.9e-3; the bar is 2x the largest relative spread.
-SR_TIE_REL = 2e-2
+# conv2d/kernel 2.9e-3.  Per case: the round-2 bar 1e-2 where the measured spread is well inside it
+# (SRGAN, FastSRGAN); 2x the measured spread for ae_bs4, whose D d5_bn/beta near-tie sits just past 1e-2.
+SR_TIE_REL = {"srgan_bs32": 1e-2, "fsrgan_bs8": 1e-2, "ae_bs4": 2e-2}
 
 
 class Args:
@@ -150,7 +151,7 @@ def test_pix2pix_bs16_matches_golden(case):
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("case", ["srgan_bs32", "ae_bs4", "fsrgan_bs8"])
 def test_sr_family_matches_golden(case):
-    """Drift pins of the SR-family BASELINE configs (unconditioned, SR_TIE_REL).  The strict
+    """Drift pins of the SR-family BASELINE configs (unconditioned, SR_TIE_REL per case).  The strict
     mask-conditioned max-abs 1e-4 check of each config is owned by a live test:
       srgan_bs32  tests/test_sr_gpu.py::test_srgan_full_config_parity
       ae_bs4      tests/test_sr_gpu.py::test_autoencoder_full_config_parity
@@ -174,7 +175,7 @@ def test_sr_family_matches_golden(case):
     loss = tr.step(torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV))
     torch.cuda.synchronize()
     r = _check_step1(d, loss, tr.gen_output, y, Ga, Da, m.generator.bn.export(), m.discriminator.bn.export(), 7,
-                     case, g_rel=SR_TIE_REL, d_rel=SR_TIE_REL)
+                     case, g_rel=SR_TIE_REL[case], d_rel=SR_TIE_REL[case])
     print(f"{case} vs golden: |dPSNR| {r[0]:.2e} dB, worst G grad {r[1]}, worst D grad {r[2]}")
     x2, y2 = batch(meta, meta["batch_seeds"][1])
     loss2 = tr.step(torch.from_numpy(x2).to(DEV), torch.from_numpy(y2).to(DEV))

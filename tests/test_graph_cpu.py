@@ -78,3 +78,23 @@ def test_bn_add_switches(cpu_models, monkeypatch):
     monkeypatch.setenv("DG_NO_ADD_ALIAS", "1")
     p = _generator_plan("srgan")
     assert not p.bn_add and not any(p.add_alias.values())
+
+
+def test_bn_add_not_fused_when_skip_is_produced_later(cpu_models):
+    """A linear BN feeding an Add whose other input is computed AFTER the BN (in node
+    order) must not be fused: the fused BN would read the skip before it is written."""
+    from dgan.graph import Graph, GraphNetwork
+    g = Graph("late_skip")
+    a = g.conv(g.input, 8, 3, name="a")
+    b = g.bn(a, name="b")                      # linear BN, only consumer: the Add
+    late = g.conv(g.input, 8, 3, name="late")  # the skip, produced after the BN
+    g.set_output(g.conv(g.add(b, late, name="add"), 3, 3, name="out"))
+    p = GraphNetwork(g, seed=1, device=torch.device("cpu")).plan(2, 8, 8, slots=1, train=True)
+    assert not p.bn_add
+
+    g2 = Graph("early_skip")
+    early = g2.conv(g2.input, 8, 3, name="early")
+    b2 = g2.bn(g2.conv(g2.input, 8, 3, name="a"), name="b")
+    g2.set_output(g2.conv(g2.add(b2, early, name="add"), 3, 3, name="out"))
+    p2 = GraphNetwork(g2, seed=1, device=torch.device("cpu")).plan(2, 8, 8, slots=1, train=True)
+    assert len(p2.bn_add) == 1
