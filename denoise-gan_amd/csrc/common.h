@@ -70,8 +70,34 @@ __device__ __forceinline__ void split3(float x0, float x1, unsigned &h, unsigned
 }
 
 typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
-// planes of one output element / of 4 consecutive elements (col % 4 == 0)
+typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+
+// fp16x3 operand planes (include/dgan.h DG_MATH_F16X3, the forward GEMMs of 3x3
+// stride-1 layers): a pre-scaled value s*x = h + l is held as two fp16 pieces,
+// h = fp16(s*x), l = fp16(s*x - h) (both RNE), |l| <= 2^-11 |s*x|; a product is
+// h.h' + h.l' + l.h' (the dropped l.l' and l's own rounding each < 2^-22 |x x'|).
+// Activation rows hold, per 32-channel group, h[32] l[32] (4 B per element);
+// weight rows, per 16-column group, h[16] l[16].  The scales keep both operands
+// inside fp16's normal range: activations x 2^-4 (|x| < 2^20), weights x 2^8; the
+// GEMM multiplies its accumulators by F16X3_OSCALE.  A plane tensor in this
+// format is passed to the device helpers below with a NEGATIVE channel count.
+constexpr float F16X3_XS = 0.0625f;
+constexpr float F16X3_WS = 256.f;
+constexpr float F16X3_OSCALE = 1.f / (F16X3_XS * F16X3_WS);
+__device__ __forceinline__ void split_x3(float x, float s, _Float16 &h, _Float16 &l) {
+    const float v = x * s;
+    h = (_Float16)v;
+    l = (_Float16)(v - (float)h);
+}
+
+// planes of one output element / of 4 consecutive elements (col % 4 == 0) for the
+// consuming conv: C > 0 bf16x6 planes, C < 0 fp16x3 activation planes (-C channels)
 __device__ __forceinline__ void store_planes1(unsigned short *yp, int C, long pix, int col, float x) {
+    if (C < 0) {
+        _Float16 *d = reinterpret_cast<_Float16 *>(yp) + pix * 2 * (-C) + (col >> 5) * 64 + (col & 31);
+        split_x3(x, F16X3_XS, d[0], d[32]);
+        return;
+    }
     unsigned h, m, l;
     split3(x, 0.f, h, m, l);
     unsigned short *d = yp + pix * 3 * C + (col >> 4) * 48 + (col & 15);
@@ -80,6 +106,20 @@ __device__ __forceinline__ void store_planes1(unsigned short *yp, int C, long pi
     d[32] = (unsigned short)l;
 }
 __device__ __forceinline__ void store_planes4(unsigned short *yp, int C, long pix, int col, f32x4 v) {
+    if (C < 0) {
+        _Float16 *d = reinterpret_cast<_Float16 *>(yp) + pix * 2 * (-C) + (col >> 5) * 64 + (col & 31);
+        f16x4_t h, l;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            _Float16 a, b;
+            split_x3(v[q], F16X3_XS, a, b);
+            h[q] = a;
+            l[q] = b;
+        }
+        *reinterpret_cast<f16x4_t *>(d) = h;
+        *reinterpret_cast<f16x4_t *>(d + 32) = l;
+        return;
+    }
     unsigned h0, m0, l0, h1, m1, l1;
     split3(v[0], v[1], h0, m0, l0);
     split3(v[2], v[3], h1, m1, l1);
@@ -91,7 +131,6 @@ __device__ __forceinline__ void store_planes4(unsigned short *yp, int C, long pi
 
 // fp16 operand copy of a DG_MATH_FP16 GEMM operand ([rows][C], round-to-nearest-even like the
 // conversion pass k_split_f16) of 4 consecutive elements / of one element
-typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void store_f16x4(_Float16 *d, f32x4 v) {
     *reinterpret_cast<f16x4_t *>(d) = f16x4_t{(_Float16)v[0], (_Float16)v[1], (_Float16)v[2], (_Float16)v[3]};
 }

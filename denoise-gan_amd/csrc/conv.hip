@@ -1197,7 +1197,8 @@ constexpr int kNumF16Cfgs = sizeof(kF16Cfgs) / sizeof(kF16Cfgs[0]);
 struct OpPlan {
     int narrow;      // 1 => VALU narrow kernel
     int direct;      // narrow DGRAD on k_direct_dgrad (dy halo staged in LDS)
-    int x6;          // 1 => bf16x6 split-precision kernel (kX6Cfgs), 2 => fp16 (kF16Cfgs), else fp32 MFMA (kCfgs)
+    int x6;          // 1 => bf16x6 split-precision kernel (kX6Cfgs), 2 => fp16 (kF16Cfgs), 3 => fp16x3 halo
+                     // forward (DG_MATH_F16X3), else fp32 MFMA (kCfgs)
     int cfg;         // tile config index
     int vec;
     int splits, kchunk;
@@ -1426,13 +1427,20 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         x6_ok = g.Ci % 16 == 0 && g.Co % 16 == 0;
         ra = (long)g.N * g.H * g.W; ca = g.Ci; rb = (long)g.N * g.Ho * g.Wo; cb = g.Co;
     }
-    // (the bf16x6 kernel keeps a per-row bitmask of valid taps: at most 32 taps)
-    x6_ok = x6_ok && math == DG_MATH_BF16X6 && 6.0 * ra * ca < 2.0e9 && 6.0 * rb * cb < 2.0e9 && g.kh * g.kw <= 32;
+    // (the bf16x6 kernel keeps a per-row bitmask of valid taps: at most 32 taps; DG_MATH_F16X3
+    // is bf16x6 wherever its fp16x3 forward does not apply)
+    x6_ok = x6_ok && (math == DG_MATH_BF16X6 || math == DG_MATH_F16X3) && 6.0 * ra * ca < 2.0e9 &&
+            6.0 * rb * cb < 2.0e9 && g.kh * g.kw <= 32;
+    // (an fp16x3-eligible forward -- DG_MATH_F16X3, 3x3 stride 1, Cin % 32 == 0, Cout % 16 == 0,
+    // Cout > 32 -- takes the split-precision path whatever the fp32 estimate: see hx3 below)
+    const bool x3_geom = math == DG_MATH_F16X3 && mode == MODE_FWD && g.kh == 3 && g.kw == 3 && g.sh == 1 &&
+                         g.sw == 1 && g.Ci % 32 == 0 && g.Co % 16 == 0 && g.Co > 32 && !plan_off("x3") &&
+                         !plan_off("halo");
     if (x6_ok) {
         OpPlan p6 = pl;
         double t6 = choose_tiles(p6, kX6Cfgs, kNumX6Cfgs, 2516.6e12 / 6.0, "DG_FORCE_X6CFG", nullptr);
         t6 += (double)(ra * ca + rb * cb) * 10.0 / 4.0e12 + 4e-6;  // split passes: read 4 B, write 6 B
-        if (t6 < t32 || getenv("DG_FORCE_X6CFG")) {
+        if (t6 < t32 || getenv("DG_FORCE_X6CFG") || x3_geom) {
             pl = p6;
             pl.x6 = 1;
             pl.x6_ra = ra; pl.x6_ca = (int)ca; pl.x6_rb = rb; pl.x6_cb = (int)cb;
@@ -1471,10 +1479,14 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
                      pl.K % 256 == 0 && !plan_off("halo4");
     // (fp16: 3x3 only, 32-channel chunks; the forward's pool epilogue stays bf16x6)
     const bool hf16 = pl.x6 == 2 && h33 && pl.K % 288 == 0 && pl.N % 16 == 0 && !plan_off("halo_f16");
+    // fp16x3 forward (DG_MATH_F16X3): 3x3 stride-1 layers with 32-channel chunks and at
+    // least 48 output columns (BN 64 / 128 tiles) -- VGG19's layers after block1_conv1
+    const bool hx3 = x3_geom && pl.x6 == 1 && h33 && pl.K % 288 == 0 && 4.0 * ra * ca < 2.0e9 &&
+                     4.0 * rb * cb < 2.0e9;
     if ((pl.x6 == 1 && (h33 || h22 || h44) || hf16) && !plan_off("halo")) {
         // each input pixel staged once per channel chunk instead of once per tap
         const int ntap = h33 ? 9 : (h44 ? 16 : 4);
-        const int bkc = pl.x6 == 2 ? 32 : 16;   // channels per chunk
+        const int bkc = (pl.x6 == 2 || hx3) ? 32 : 16;   // channels per chunk
         int Hout, Wout;
         if (mode == MODE_FWD) { Hout = g.Ho; Wout = g.Wo; }
         else if (h33 || h44) { Hout = g.H; Wout = g.W; }
@@ -1498,13 +1510,14 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         const long cps = (nch + splits - 1) / splits;
         pl.kchunk = (int)(cps * bkc * ntap);
         pl.splits = (int)((nch + cps - 1) / cps);
+        if (hx3) pl.x6 = 3;
     }
     pl.vec = pl.x6 ? 1 : cfg_vec(g, mode, kCfgs[pl.cfg].bk);
     pl.slab_bytes = pl.splits > 1 ? (size_t)pl.nphase * pl.splits * pl.M * pl.N * sizeof(float) : 0;
     pl.ws_bytes = pl.slab_bytes;
     if (pl.x6) {
-        // workspace: [split-K slabs][A planes][B planes] (6 B per element bf16x6, 2 B fp16)
-        const size_t eb = pl.x6 == 2 ? 2 : 6;
+        // workspace: [split-K slabs][A planes][B planes] (6 B per element bf16x6, 2 B fp16, 4 B fp16x3)
+        const size_t eb = pl.x6 == 2 ? 2 : (pl.x6 == 3 ? 4 : 6);
         pl.x6_a_off = (pl.ws_bytes + 255) & ~(size_t)255;
         pl.x6_b_off = (pl.x6_a_off + eb * ra * ca + 255) & ~(size_t)255;
         pl.ws_bytes = pl.x6_b_off + eb * rb * cb;
@@ -1512,12 +1525,14 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     pl.gemm_bytes = pl.ws_bytes;
     if (getenv("DG_PLAN_DEBUG"))
         fprintf(stderr, "[dg plan] mode %d M=%d N=%d K=%d -> %s cfg %d splits %d\n", mode, pl.M, pl.N, pl.K,
-                pl.halo == 2 ? "x6h2" : pl.halo == 4 ? "x6h4" : pl.halo ? (pl.x6 == 2 ? "f16h" : "x6h") : (pl.x6 == 2 ? "f16" : (pl.x6 ? "x6" : "fp32")),
+                pl.halo == 2 ? "x6h2" : pl.halo == 4 ? "x6h4" : pl.halo ? (pl.x6 == 2 ? "f16h" : (pl.x6 == 3 ? "x3h" : "x6h")) : (pl.x6 == 2 ? "f16" : (pl.x6 ? "x6" : "fp32")),
                 pl.cfg, pl.splits);
     return pl;
 }
 
 static size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
+// bytes of the fp16x3 weight planes of a forward plan (x6 3), 256-aligned
+static size_t x3_w_bytes(const OpPlan &pl) { return al256((size_t)4 * pl.x6_rb * pl.x6_cb); }
 
 static ConvGeom geom_1x1(long pixels, int ci, int co) {
     ConvGeom q{};
@@ -1583,7 +1598,9 @@ static size_t colsum_ws(long M, int C);
 // (re)plan the three ops of a descriptor for its math mode
 static void plan_all(dg_conv_desc_s *d) {
     for (int op = 0; op < 3; ++op) {
-        d->plan[op] = make_plan(d->g, engine_mode(d, op), d->math);
+        // (DG_MATH_F16X3: fp16x3 for the forward of a Conv2D only; every other op bf16x6)
+        const int m = d->math == DG_MATH_F16X3 && (op != DG_OP_FWD || d->transpose) ? DG_MATH_BF16X6 : d->math;
+        d->plan[op] = make_plan(d->g, engine_mode(d, op), m);
         plan_recast(d, op);
         if (d->rc[op].on) d->plan[op].ws_bytes = d->rc[op].bytes;
         if (op == DG_OP_BWD_FILTER) {
@@ -1600,6 +1617,7 @@ static int default_math() {
     const char *m = getenv("DG_CONV_MATH");
     if (m && (!strcmp(m, "fp32") || !strcmp(m, "0"))) return DG_MATH_FP32;
     if (m && (!strcmp(m, "fp16") || !strcmp(m, "2"))) return DG_MATH_FP16;
+    if (m && (!strcmp(m, "f16x3") || !strcmp(m, "3"))) return DG_MATH_F16X3;
     (void)m;
     return DG_MATH_BF16X6;
 }
@@ -1696,6 +1714,7 @@ struct PoolOut {
     float *y;
     int ldy;
     unsigned short *planes;
+    int planes_fmt;   // DG_PLANES_*: the consuming conv's x plane format
 };
 
 // the forward plan of d can run MaxPool2D(2) in its epilogue: the halo-tiled
@@ -1703,7 +1722,8 @@ struct PoolOut {
 // whose derivative is a function of the output's sign
 static bool pool_fusable(const dg_conv_desc_s *d, int act) {
     const OpPlan &pl = d->plan[DG_OP_FWD];
-    return !d->transpose && pl.x6 == 1 && pl.halo == 1 && pl.cfg != 32 && pl.splits == 1 && !d->rc[DG_OP_FWD].on &&
+    return !d->transpose && (pl.x6 == 1 || pl.x6 == 3) && pl.halo == 1 && pl.cfg != 32 && pl.splits == 1 &&
+           !d->rc[DG_OP_FWD].on &&
            d->g.Ho % 8 == 0 &&
            d->g.Wo % 16 == 0 && d->g.Co % 16 == 0 &&
            (act == DG_ACT_NONE || act == DG_ACT_RELU || act == DG_ACT_LRELU);
@@ -1714,7 +1734,7 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
                       void *ws, size_t ws_bytes, hipStream_t s, const float *mz = nullptr, int ldmz = 0,
                       int mact = DG_ACT_NONE, float malpha = 0.f, const PlaneRefs *pr = nullptr,
                       unsigned short *yp = nullptr, const PoolOut *po = nullptr,
-                      const unsigned short *mzp = nullptr) {
+                      const unsigned short *mzp = nullptr, int yp_fmt = DG_PLANES_BF16X6) {
     const int mode = engine_mode(d, op);
     const OpPlan &pl = d->plan[op];
     const size_t need = d->rc[op].on ? d->rc[op].bytes : pl.gemm_bytes;
@@ -1732,6 +1752,10 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
         DG_ARG(beta == 0.f, "the fused pool overwrites its output (beta must be 0)");
         a.pidx = po->idx; a.pool_y = po->y; a.ldpy = po->ldy;
         a.yp = po->planes; a.ypC = d->g.Co;
+        if (po->planes && po->planes_fmt == DG_PLANES_F16X3) {
+            DG_ARG(d->g.Co % 32 == 0, "fp16x3 output planes need channels %% 32 == 0");
+            a.ypC = -d->g.Co;
+        }
     }
     if (mzp) {
         // mask from the hi plane's sign: the small-Cin kernels read fp32 masks only
@@ -1739,6 +1763,8 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
         DG_ARG(mact == DG_ACT_NONE || mact == DG_ACT_RELU || mact == DG_ACT_LRELU,
                "plane mask needs a sign-determined activation (got %d)", mact);
         a.mzp = mzp; a.mzpC = mode == MODE_FWD ? d->g.Co : d->g.Ci;
+        // (the layer input's planes: fp16x3 when this descriptor's forward reads them so)
+        if (mode == MODE_DGRAD && d->plan[DG_OP_FWD].x6 == 3) a.mzpC = -a.mzpC;
     }
     if (!C && !po) {
         // planes-only output: the GEMM epilogues skip the fp32 store
@@ -1755,6 +1781,10 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
         DG_ARG(oc % 16 == 0 && !pl.narrow && !d->rc[op].on, "output planes need a GEMM path and channels %% 16 == 0");
         DG_ARG((((uintptr_t)yp) & 15) == 0, "plane buffers must be 16-byte aligned");
         a.yp = yp; a.ypC = oc;
+        if (yp_fmt == DG_PLANES_F16X3) {
+            DG_ARG(oc % 32 == 0, "fp16x3 output planes need channels %% 32 == 0");
+            a.ypC = -oc;
+        }
     }
     if (d->rc[op].on) {
         DG_ARG(lda % 4 == 0 && ((uintptr_t)A & 15) == 0, "recast path needs lda%%4==0 and 16B-aligned A");
@@ -1854,6 +1884,34 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
         DG_ARG(ab < (1L << 31) && bb < (1L << 31), "operand larger than 2 GiB (buffer-resource offsets are 32-bit)");
         a.a_bytes = (unsigned)ab;
         a.b_bytes = (unsigned)bb;
+    }
+    if (pl.x6 == 3) {
+        // fp16x3 forward: activations -> fp16x3 planes in 32-channel groups, weights in
+        // 16-column groups (common.h); a caller-held weight buffer also receives the
+        // weights' bf16x6 planes behind them (tensor_plane_bytes), read by bwd_data
+        char *ws = (char *)a.slab;
+        DG_ARG(ws != nullptr, "workspace pointer is NULL");
+        void *pa = ws + pl.x6_a_off, *pb = ws + pl.x6_b_off;
+        if (pr && pr->a) pa = pr->a;
+        if (pr && pr->b) pb = pr->b;
+        if (!(pr && pr->a && pr->a_ready)) {
+            launch_split_x3(A, lda, pl.x6_ra, pl.x6_ca, pa, 32, F16X3_XS, s);
+            DG_LAUNCHED("split_x3_a");
+        }
+        if (!(pr && pr->b && pr->b_ready)) {
+            launch_split_x3(B, ldb, pl.x6_rb, pl.x6_cb, pb, 16, F16X3_WS, s);
+            DG_LAUNCHED("split_x3_b");
+            if (pr && pr->b) {
+                launch_split3(B, ldb, pl.x6_rb, pl.x6_cb, (unsigned short *)((char *)pb + x3_w_bytes(pl)), s);
+                DG_LAUNCHED("split3_b");
+            }
+        }
+        a.A = (const float *)pa; a.lda = pl.x6_ca; a.a_bytes = (unsigned)(4 * pl.x6_ra * pl.x6_ca);
+        a.B = (const float *)pb; a.ldb = pl.x6_cb; a.b_bytes = (unsigned)(4 * pl.x6_rb * pl.x6_cb);
+        dim3 grid(pl.mtiles * pl.ntiles, pl.nphase * pl.splits);
+        launch_gemm_x6h(mode, pl.cfg, 3, grid, a, pl.htx, pl.hty, s, 4);
+        DG_LAUNCHED("conv_gemm_x3h");
+        return finish_splitk(mode, pl, a, s);
     }
     if (pl.x6 == 2) {
         // fp16: round the operands into one fp16 plane each -- the caller-held
@@ -1981,10 +2039,15 @@ static void op_tensors(const dg_conv_desc_s *d, int op, int &ta, int &tb) {
     else { ta = DG_TENSOR_DY; tb = DG_TENSOR_X; }  // conv view of a transposed layer: A = its output grad
 }
 
+// A descriptor whose forward runs fp16x3 (plan x6 3) keeps x as fp16x3 planes (4 B per
+// element, read by the forward only) and w as [fp16x3 (4 B) | bf16x6 (6 B)] planes: the
+// forward reads the first part, bwd_data the second; dy stays bf16x6.
+static bool fwd_x3(const dg_conv_desc_s *d) { return d->plan[DG_OP_FWD].x6 == 3; }
 static size_t tensor_plane_bytes(const dg_conv_desc_s *d, int t) {
-    if (t == DG_TENSOR_X) return (size_t)6 * d->N * d->H * d->W * d->Cin;
+    const size_t nw = (size_t)d->g.kh * d->g.kw * d->Cin * d->Cout;
+    if (t == DG_TENSOR_X) return (size_t)(fwd_x3(d) ? 4 : 6) * d->N * d->H * d->W * d->Cin;
     if (t == DG_TENSOR_DY) return (size_t)6 * d->N * d->Ho * d->Wo * d->Cout;
-    return (size_t)6 * d->g.kh * d->g.kw * d->Cin * d->Cout;
+    return fwd_x3(d) ? x3_w_bytes(d->plan[DG_OP_FWD]) + 6 * nw : 6 * nw;
 }
 
 // tensors op reads as operand planes: bf16x6 planes (x6 1) or the fp16 copy
@@ -1993,10 +2056,12 @@ static size_t tensor_plane_bytes(const dg_conv_desc_s *d, int t) {
 // the two formats (an fp16 descriptor's other ops run fp32).
 static int op_plane_mask(const dg_conv_desc_s *d, int op) {
     const OpPlan &pl = d->plan[op];
-    if ((pl.x6 != 1 && pl.x6 != 2) || pl.narrow || d->rc[op].on || pl.M == 0 || pl.N == 0) return 0;
+    if ((pl.x6 != 1 && pl.x6 != 2 && pl.x6 != 3) || pl.narrow || d->rc[op].on || pl.M == 0 || pl.N == 0) return 0;
     if (pl.x6 == 2 && plan_off("f16planes")) return 0;
     int ta, tb;
     op_tensors(d, op, ta, tb);
+    // (an fp16x3 forward's x planes are not the bf16x6 planes a filter gradient reads)
+    if (op == DG_OP_BWD_FILTER && fwd_x3(d)) return (ta | tb) & ~DG_TENSOR_X;
     return ta | tb;
 }
 
@@ -2008,8 +2073,11 @@ static int plane_refs(const dg_conv_desc_s *d, int op, const dg_conv_planes_t *p
     int ta, tb;
     op_tensors(d, op, ta, tb);
     auto buf = [&](int t) -> void * { return t == DG_TENSOR_X ? p->x : (t == DG_TENSOR_DY ? p->dy : p->w); };
-    r.a = buf(ta); r.b = buf(tb);
+    const int mask = op_plane_mask(d, op);
+    r.a = (mask & ta) ? buf(ta) : nullptr; r.b = (mask & tb) ? buf(tb) : nullptr;
     r.a_ready = (p->ready & ta) != 0; r.b_ready = (p->ready & tb) != 0;
+    // bwd_data of an fp16x3-forward descriptor: the weights' bf16x6 part of the buffer
+    if (op == DG_OP_BWD_DATA && fwd_x3(d) && r.b) r.b = (char *)r.b + x3_w_bytes(d->plan[DG_OP_FWD]);
     DG_ARG(((((uintptr_t)r.a) | ((uintptr_t)r.b)) & 15) == 0, "plane buffers must be 16-byte aligned");
     out = &r;
     return DG_OK;
@@ -2064,7 +2132,8 @@ int dg_conv_desc_create(dg_conv_t *out, int N, int H, int W, int Cin, int Cout, 
 
 int dg_conv_set_math(dg_conv_t d, int math) {
     DG_ARG(d != nullptr, "descriptor is NULL");
-    DG_ARG(math == DG_MATH_FP32 || math == DG_MATH_BF16X6 || math == DG_MATH_FP16, "unknown conv math mode %d", math);
+    DG_ARG(math == DG_MATH_FP32 || math == DG_MATH_BF16X6 || math == DG_MATH_FP16 || math == DG_MATH_F16X3,
+           "unknown conv math mode %d", math);
     d->math = math;
     dg::plan_all(d);
     return DG_OK;
@@ -2101,6 +2170,13 @@ int dg_conv_planes_size(dg_conv_t d, int tensor, size_t *bytes) {
     return DG_OK;
 }
 
+int dg_conv_planes_format(dg_conv_t d, int tensor, int *format) {
+    DG_ARG(d && format, "NULL argument");
+    DG_ARG(tensor == DG_TENSOR_X || tensor == DG_TENSOR_DY || tensor == DG_TENSOR_W, "bad tensor id %d", tensor);
+    *format = (tensor != DG_TENSOR_DY && dg::fwd_x3(d)) ? DG_PLANES_F16X3 : DG_PLANES_BF16X6;
+    return DG_OK;
+}
+
 int dg_conv_op_planes(dg_conv_t d, int op, int *tensors) {
     DG_ARG(d && tensors, "NULL argument");
     DG_ARG(op >= 0 && op < 3, "bad op %d", op);
@@ -2119,7 +2195,8 @@ int dg_conv_fwd_pl(dg_conv_t d, const float *x, int ldx, const float *w, const f
     if (e != DG_OK) return e;
     return dg::run_engine(d, DG_OP_FWD, x, ldx, w, d->transpose ? 0 : d->Cout, y, ldy, bias, beta, act, alpha, ws,
                           ws_bytes, (hipStream_t)stream, nullptr, 0, DG_ACT_NONE, 0.f, pr,
-                          planes ? (unsigned short *)planes->out : nullptr);
+                          planes ? (unsigned short *)planes->out : nullptr, nullptr, nullptr,
+                          planes ? planes->out_format : DG_PLANES_BF16X6);
 }
 
 int dg_conv_fwd_pool_ok(dg_conv_t d, int act, int *ok) {
@@ -2142,7 +2219,8 @@ int dg_conv_fwd_pool(dg_conv_t d, const float *x, int ldx, const float *w, const
     const dg::PlaneRefs *pr;
     int e = dg::plane_refs(d, DG_OP_FWD, planes, r, pr);
     if (e != DG_OK) return e;
-    dg::PoolOut po{pool_idx, pool_y, ldpy, planes ? (unsigned short *)planes->out : nullptr};
+    dg::PoolOut po{pool_idx, pool_y, ldpy, planes ? (unsigned short *)planes->out : nullptr,
+                   planes ? planes->out_format : DG_PLANES_BF16X6};
     return dg::run_engine(d, DG_OP_FWD, x, ldx, w, d->Cout, nullptr, d->Cout, bias, 0.f, act, alpha, ws, ws_bytes,
                           (hipStream_t)stream, nullptr, 0, DG_ACT_NONE, 0.f, pr, nullptr, &po);
 }
@@ -2165,7 +2243,8 @@ int dg_conv_bwd_data_pl(dg_conv_t d, const float *dy, int lddy, const float *w, 
     if (e != DG_OK) return e;
     return dg::run_engine(d, DG_OP_BWD_DATA, dy, lddy, w, d->transpose ? d->g.Co : 0, dx, lddx, nullptr, beta,
                           DG_ACT_NONE, 0.f, ws, ws_bytes, (hipStream_t)stream, z, z ? ldz : 0,
-                          z ? act : DG_ACT_NONE, alpha, pr, planes ? (unsigned short *)planes->out : nullptr);
+                          z ? act : DG_ACT_NONE, alpha, pr, planes ? (unsigned short *)planes->out : nullptr, nullptr,
+                          nullptr, planes ? planes->out_format : DG_PLANES_BF16X6);
 }
 
 int dg_conv_bwd_data_xmask(dg_conv_t d, const float *dy, int lddy, const float *w, float *dx, int lddx, float beta,
@@ -2182,7 +2261,8 @@ int dg_conv_bwd_data_xmask(dg_conv_t d, const float *dy, int lddy, const float *
     if (e != DG_OK) return e;
     return dg::run_engine(d, DG_OP_BWD_DATA, dy, lddy, w, d->transpose ? d->g.Co : 0, dx, lddx, nullptr, beta,
                           DG_ACT_NONE, 0.f, ws, ws_bytes, (hipStream_t)stream, nullptr, 0, act, alpha, pr,
-                          (unsigned short *)planes->out, nullptr, (const unsigned short *)planes->x);
+                          (unsigned short *)planes->out, nullptr, (const unsigned short *)planes->x,
+                          planes->out_format);
 }
 
 int dg_conv_bwd_data(dg_conv_t d, const float *dy, int lddy, const float *w, float *dx, int lddx, float beta,

@@ -33,8 +33,9 @@ struct GemmArgs {
     // optional gradient mask of the output (dg_conv_bwd_data_masked):
     // C = (result * act'(mz)) + beta*C, act' expressed through the activation's output mz
     const float *mz; int ldmz; int mact; float malpha;
-    // optional bf16x6 planes of the final output (dg_conv_planes_t.out):
-    // [pixel][3 * ypC] in the packed layout of k_split3, written beside C
+    // optional planes of the final output (dg_conv_planes_t.out), written beside C:
+    // ypC > 0 bf16x6 [pixel][3 * ypC] in the packed layout of k_split3; ypC < 0 the
+    // consumer's fp16x3 planes [pixel][2 * -ypC] (common.h store_planes4)
     unsigned short *yp; int ypC;
     // optional MaxPool2D(2) of the activated output, fused into the forward
     // epilogue of the halo kernel (dg_conv_fwd_pool): the pooled output's
@@ -43,20 +44,28 @@ struct GemmArgs {
     // of the first maximum (row-major), bit 2 set when the pooled value > 0.
     // C (the full-size output) is not written.
     unsigned char *pidx; float *pool_y; int ldpy;
-    // optional gradient mask from the bf16x6 planes of the activation output
-    // instead of its fp32 values (dg_conv_bwd_data_xmask): act' of a
-    // sign-determined activation from the sign of the hi plane, [pixel][3 mzpC]
+    // optional gradient mask from the planes of the activation output instead of
+    // its fp32 values (dg_conv_bwd_data_xmask): act' of a sign-determined
+    // activation from the sign of the hi plane, [pixel][3 mzpC] (mzpC < 0: fp16x3)
     const unsigned short *mzp; int mzpC;
     // 1: DGRAD phase blocks in the plain XCD order (A/B switch DG_PLAN_DISABLE=xcd_phase)
     int xcd_plain;
 };
 
-// hi plane of element (pix, col) of a packed plane tensor, as a float
+// hi plane of element (pix, col) of a packed plane tensor, as a float (its sign is
+// the element's; C < 0: fp16x3 planes of -C channels, the value times F16X3_XS)
 __device__ __forceinline__ float hi_plane(const unsigned short *zp, int C, long pix, int col) {
+    if (C < 0)
+        return (float)reinterpret_cast<const _Float16 *>(zp)[pix * 2 * (-C) + (col >> 5) * 64 + (col & 31)];
     return __uint_as_float((unsigned)zp[pix * 3 * C + (col >> 4) * 48 + (col & 15)] << 16);
 }
 // the same for columns col..col+3 (col % 4 == 0): one 8-byte load
 __device__ __forceinline__ f32x4 hi_plane4(const unsigned short *zp, int C, long pix, int col) {
+    if (C < 0) {
+        const f16x4_t h = *reinterpret_cast<const f16x4_t *>(reinterpret_cast<const _Float16 *>(zp) +
+                                                           pix * 2 * (-C) + (col >> 5) * 64 + (col & 31));
+        return f32x4{(float)h[0], (float)h[1], (float)h[2], (float)h[3]};
+    }
     const u32x2_t h = *reinterpret_cast<const u32x2_t *>(zp + pix * 3 * C + (col >> 4) * 48 + (col & 15));
     return f32x4{__uint_as_float(h[0] << 16), __uint_as_float(h[0] & 0xffff0000u), __uint_as_float(h[1] << 16),
                  __uint_as_float(h[1] & 0xffff0000u)};
@@ -286,11 +295,15 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
 void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s);
 // the halo-tiled bf16x6 kernel (conv_x6h.hip): kt 3 = stride-1 3x3 FWD / DGRAD, kt 2 = the
 // sub-pixel phases of a stride-2 4x4 DGRAD (grid y = phase * splits + split); bn = 64 | 128.
+// ni 3 bf16x6, 2 fp16 (DG_MATH_FP16), 4 fp16x3 (DG_MATH_F16X3 forward, kt 3, bn 64 | 128).
 // a.pidx != NULL selects the fused max-pool epilogue (FWD, one split, output Ho % 8 == 0, Wo % 16 == 0)
 void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int tiles_x, int tiles_y, hipStream_t s,
                      int ni = 3);
 // fp32 [rows][ld] (first C columns, C % 8 == 0) -> bf16 hi/mid/lo planes [rows][C]
 void launch_split3(const float *src, int ld, long rows, int C, unsigned short *dst, hipStream_t s);
+// fp32 [rows][ld] -> fp16x3 planes (common.h): per group of G columns (32: activations,
+// 16: weights) h[G] l[G] of scale * value; C % G == 0
+void launch_split_x3(const float *src, int ld, long rows, int C, void *dst, int group, float scale, hipStream_t s);
 // the fp16 conv math (DG_MATH_FP16): one fp16 plane [rows][C] and its GEMM (kF16Cfgs)
 void launch_split_f16(const float *src, int ld, long rows, int C, void *dst, hipStream_t s);
 void launch_split_f16_pair(const float *a, int lda, long ra, int ca, void *da, const float *b, int ldb, long rb,

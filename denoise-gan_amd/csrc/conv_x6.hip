@@ -524,6 +524,51 @@ void launch_split3(const float *src, int ld, long rows, int C, unsigned short *d
     hipLaunchKernelGGL(k_split3, dim3(blocks), dim3(256), 0, s, src, ld, rows, C, dst);
 }
 
+// Split pass of the fp16x3 forward operands (common.h): fp32 [rows][ld] (first C
+// columns) -> per group of G columns h[G] l[G] of scale * value, 8 columns per lane
+template <int G>
+__global__ void __launch_bounds__(256)
+k_split_x3(const float *__restrict__ src, int ld, long rows, int C, float scale, _Float16 *__restrict__ dst) {
+    const int C8 = C >> 3;
+    const long total = rows * C8;
+    const bool vec = ((ld & 3) == 0) && ((((uintptr_t)src) & 15) == 0);
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long r = e / C8;
+        const int c = (int)(e - r * C8) * 8;
+        const float *sp = src + r * ld + c;
+        f32x4 v0, v1;
+        if (vec) {
+            v0 = *reinterpret_cast<const f32x4 *>(sp);
+            v1 = *reinterpret_cast<const f32x4 *>(sp + 4);
+        } else {
+            v0 = f32x4{sp[0], sp[1], sp[2], sp[3]};
+            v1 = f32x4{sp[4], sp[5], sp[6], sp[7]};
+        }
+        f16x8 h, l;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            _Float16 a, b;
+            split_x3(v0[q], scale, a, b);
+            h[q] = a; l[q] = b;
+            split_x3(v1[q], scale, a, b);
+            h[4 + q] = a; l[4 + q] = b;
+        }
+        _Float16 *d = dst + r * 2 * C + (c / G) * (2 * G) + (c % G);
+        *reinterpret_cast<f16x8 *>(d) = h;
+        *reinterpret_cast<f16x8 *>(d + G) = l;
+    }
+}
+
+void launch_split_x3(const float *src, int ld, long rows, int C, void *dst, int group, float scale, hipStream_t s) {
+    const long total = rows * (C / 8);
+    if (total == 0) return;
+    const unsigned blocks = (unsigned)std::min<long>((total + 255) / 256, 8192);
+    if (group == 32)
+        hipLaunchKernelGGL(k_split_x3<32>, dim3(blocks), dim3(256), 0, s, src, ld, rows, C, scale, (_Float16 *)dst);
+    else
+        hipLaunchKernelGGL(k_split_x3<16>, dim3(blocks), dim3(256), 0, s, src, ld, rows, C, scale, (_Float16 *)dst);
+}
+
 // both operands of one fp16 GEMM in one launch (blocks [0, nba) convert A, the rest B):
 // the SR family's mixed_float16 steps run hundreds of small GEMMs, where each conversion
 // launch costs about its launch latency (SRGAN: 368 per step, 17% of the step)

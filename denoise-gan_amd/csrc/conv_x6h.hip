@@ -51,14 +51,20 @@ constexpr bool kTapsColMajor = false;
 #else
 constexpr bool kTapsColMajor = true;
 #endif
-template <int KT, int NPL = 3>
+// PACKED (fp16x3): the NPL plane images lie back to back (HPX * 32 bytes each) and
+// only the whole halo is rounded up to KiB DMAs -- 23 KiB instead of 24 for KT 3,
+// which keeps two fp16x3 blocks (two halo buffers, two weight buffers) per CU
+template <int KT, int NPL = 3, bool PACKED = false>
 struct HaloGeom {
     static constexpr int HH = HX_PH + KT - 1, HW = HX_PW + KT - 1;
     static constexpr int HPX = HH * HW;
-    static constexpr int HPL = (HPX * 32 + 1023) / 1024 * 1024;  // bytes per halo plane image
-    static constexpr int HDMA = NPL * HPL / 1024;                 // one-KiB DMAs per halo
+    static constexpr int HPL = PACKED ? HPX * 32 : (HPX * 32 + 1023) / 1024 * 1024;  // bytes per plane image
+    static constexpr int BYTES = (NPL * HPL + 1023) / 1024 * 1024;                   // bytes per halo buffer
+    static constexpr int HDMA = BYTES / 1024;                                         // one-KiB DMAs per halo
     static constexpr int NTAP = KT * KT;
 };
+
+
 
 // Forward epilogue fused with the 2x2 max pool that follows the conv (VGG19
 // blockN_conv{2,4} -> blockN_pool, pix2pix.py:53-67 content features): a
@@ -149,7 +155,12 @@ __device__ __forceinline__ void for_taps(F &&f, std::integer_sequence<int, T...>
 // NI = 3: bf16x6 (three bf16 plane images per 16-channel chunk, three MFMAs
 // per fragment pair); NI = 2: fp16 (mixed_float16 policy): a chunk is 32
 // channels, its two 16-channel halves are the two plane images and one
-// v_mfma_f32_16x16x32_f16 covers them
+// v_mfma_f32_16x16x32_f16 covers them; NI = 4: fp16x3 (DG_MATH_F16X3 forward):
+// a chunk is 32 channels as four plane images h0 h1 l0 l1 (h / l of channels
+// 0-15 / 16-31), and three fp16 MFMAs over the 32 channels cover its three
+// piece products: [h0|h1].[w_h0|w_h1] + [l0|l1].[w_h0|w_h1] + [h0|h1].[w_l0|w_l1]
+// (= h.w_h + l.w_h + h.w_l) -- two A and two B fragment reads per K-tile.  Two
+// weight buffers (one K-tile ahead) and packed halo images keep two blocks per CU.
 template <int MODE, int BN, bool POOL, int KT, int NI = 3>
 __global__ void __launch_bounds__(256, 2)
 k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
@@ -157,12 +168,16 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     static_assert(!POOL || MODE == MODE_FWD, "the pool epilogue is a forward epilogue");
     static_assert(KT == 3 || (KT != 3 && MODE == MODE_DGRAD),
                   "3x3 stride 1, or a stride-1 4x4 / stride-2 4x4-phase input gradient");
-    static_assert(NI == 3 || (NI == 2 && KT == 3 && !POOL), "fp16: 3x3 stride 1, no pool epilogue");
-    constexpr int NPL = NI == 3 ? 3 : 2;        // plane images per chunk
-    using HG = HaloGeom<KT, NPL>;
+    static_assert(NI == 3 || (NI == 2 && KT == 3 && !POOL) || (NI == 4 && KT == 3 && MODE == MODE_FWD),
+                  "fp16: 3x3 stride 1, no pool epilogue; fp16x3: 3x3 stride-1 forward");
+    constexpr bool X3 = NI == 4;
+    constexpr int NPL = NI == 3 ? 3 : (X3 ? 4 : 2);   // plane images per chunk
+    using HG = HaloGeom<KT, NPL, X3>;
     constexpr int NTAP = HG::NTAP;
-    constexpr int NB = NTAP % 3 == 0 ? 3 : 4;   // weight K-tile buffers: a tap position owns one
-    static_assert(NTAP % NB == 0, "tap positions line up with the weight buffers across chunks");
+    // weight K-tile buffers: a tap position owns one (bf16x6 / fp16: two tiles in
+    // flight); fp16x3: two buffers alternating by tap and chunk, one tile ahead
+    constexpr int NB = X3 ? 2 : (NTAP % 3 == 0 ? 3 : 4);
+    static_assert(X3 || NTAP % NB == 0, "tap positions line up with the weight buffers across chunks");
     constexpr int BK = NI == 3 ? 16 : 32, NW = 4;   // channels per chunk
     constexpr int WTM = 64, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
     constexpr bool B_KC = MODE == MODE_DGRAD;
@@ -172,10 +187,10 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     constexpr int PPT = (H_NJ + NTAP - 2) / (NTAP - 1);     // pieces per K-tile, none at the last tap
     static_assert((H_NJ - 1) / PPT < NTAP - 1, "the next chunk's halo lands by the chunk's last K-tile");
 
-    __shared__ __attribute__((aligned(16))) char hal[2][NPL * HG::HPL];
+    __shared__ __attribute__((aligned(16))) char hal[2][HG::BYTES];
     __shared__ __attribute__((aligned(16))) char bs0[BBUF];
     __shared__ __attribute__((aligned(16))) char bs1[BBUF];
-    __shared__ __attribute__((aligned(16))) char bs2[BBUF];
+    __shared__ __attribute__((aligned(16))) char bs2[NB >= 3 ? BBUF : 16];
     __shared__ __attribute__((aligned(16))) char bs3[NB == 4 ? BBUF : 16];
     char *const hal0 = hal[0], *const hal1 = hal[1];
 
@@ -258,21 +273,33 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
 #pragma unroll
     for (int s = 0; s < H_NJ; ++s) {
         const int d = (wid + NW * s) % HG::HDMA;
-        const int pl = d / PER, kk = d - pl * PER;
-        hdst[s] = pl * HG::HPL + kk * 1024;
+        int pl, q;
+        if constexpr (X3) {   // packed images: 16-byte unit q of the buffer -> (image, pixel, half)
+            hdst[s] = d * 1024;
+            const int u = d * 64 + lane;
+            pl = u / (2 * HG::HPX);
+            q = u - pl * 2 * HG::HPX;
+        } else {
+            pl = d / PER;
+            const int kk = d - pl * PER;
+            hdst[s] = pl * HG::HPL + kk * 1024;
+            q = kk * 64 + lane;
+        }
         hoff[s] = -1;
-        const int q = kk * 64 + lane, hp = q >> 1, hh = q & 1;
-        if (hp < HG::HPX) {
+        const int hp = q >> 1, hh = q & 1;
+        if (hp < HG::HPX && pl < NPL) {
             const int hr = hp / HG::HW, hc = hp - hr * HG::HW;
             const int iy = oy + hr, ix = ox + hc;
             // (bf16x6 pixel rows: per 16 channels 3 x 16 plane values; fp16: the
-            // channel row itself, plane image pl = channel half pl of the chunk)
+            // channel row itself, plane image pl = channel half pl of the chunk;
+            // fp16x3: per 32 channels h[32] l[32], image pl = 16 values at 16 pl)
             if ((unsigned)iy < (unsigned)Hin && (unsigned)ix < (unsigned)Win)
-                hoff[s] = ((((nimg * Hin + iy) * Win + ix) * (NI == 3 ? 3 * p.lda : p.lda)) + 16 * pl + 8 * hh) * 2;
+                hoff[s] = ((((nimg * Hin + iy) * Win + ix) * (NI == 3 ? 3 * p.lda : (X3 ? 2 * p.lda : p.lda))) +
+                           16 * pl + 8 * hh) * 2;
         }
     }
     auto issue_h = [&](int s, int chunk, char *hb) __attribute__((always_inline)) {
-        dma(rA, hb + hdst[s], hoff[s] >= 0 ? (unsigned)(hoff[s] + chunk * (NI == 3 ? 96 : 64)) : DG_OOB);
+        dma(rA, hb + hdst[s], hoff[s] >= 0 ? (unsigned)(hoff[s] + chunk * (NI == 3 ? 96 : (X3 ? 128 : 64))) : DG_OOB);
     };
 
     // ---- weight K-tile slots (as conv_x6.hip): FWD RC image [16 k][BN],
@@ -296,6 +323,8 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
             const int col = n0 + 2 * (pdw ^ swz);
             bok[j] = col < p.N;
             if constexpr (NI == 3) bbase[j] = (r * (3 * p.ldb) + (col >> 4) * 48 + 16 * plane + (col & 8)) * 2;
+            else if constexpr (X3)   // image = piece plane>>1 of k rows 16 (plane&1) ..
+                bbase[j] = ((r + 16 * (plane & 1)) * (2 * p.ldb) + (col >> 4) * 32 + 16 * (plane >> 1) + (col & 8)) * 2;
             else bbase[j] = ((16 * plane + r) * p.ldb + col) * 2;   // image = k rows 16 plane ..
         } else {
             const int r = pos >> 5, c = (pos >> 4) & 1;
@@ -308,7 +337,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     // DGRAD rows ci of w[i,j] at co-chunk c
     auto issue_b = [&](int T, int chunk, char *bs) __attribute__((always_inline)) {
         int delta;
-        constexpr int LW = NI == 3 ? 3 : 1;   // weight row stride in units of ldb
+        constexpr int LW = NI == 3 ? 3 : (X3 ? 2 : 1);   // weight row stride in units of ldb
         if constexpr (!B_KC) delta = ((tap_w[T] * g.Ci + chunk * BK) * (LW * p.ldb)) * 2;
         else delta = (tap_w[T] * g.Ci * (LW * p.ldb) + chunk * (NI == 3 ? 48 : 32)) * 2;
 #pragma unroll
@@ -319,6 +348,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     auto bbuf = [&](int i) __attribute__((always_inline)) -> char * {
         return i == 0 ? bs0 : (i == 1 ? bs1 : (i == 2 ? bs2 : bs3));
     };
+    constexpr int HIMG = HG::HPL;   // bytes between the plane images of a halo buffer
 
     f32x4 acc[TM][TN];
 #pragma unroll
@@ -332,22 +362,29 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     // weight tile (and, at the chunk's last tap, the whole next halo)
     // A fragments of patch rows wm*TM + r (r = a + da, 0 <= r < TM + KT - 1) of the
     // current filter column: {hi|mid} and {hi|lo} of 16 halo pixels
+    // (fp16x3: fm = [h0|h1], fl = [l0|l1])
     bf16x8 fm[TM + KT - 1], fl[TM + KT - 1];
-    auto ktile = [&](auto TT, int chunk, const char *hc, char *hn) __attribute__((always_inline)) {
+    auto ktile = [&](auto TT, auto PARc, int chunk, const char *hc, char *hn) __attribute__((always_inline)) {
         constexpr int T = decltype(TT)::value;
+        constexpr int PAR = decltype(PARc)::value;   // (fp16x3) parity of the chunk in this block's sequence
         constexpr int ta = kTapsColMajor ? T % KT : T / KT, tb = kTapsColMajor ? T / KT : T % KT;
         constexpr int da = MODE == MODE_FWD ? ta : KT - 1 - ta;
         constexpr int db = MODE == MODE_FWD ? tb : KT - 1 - tb;
         constexpr int H0P = T * PPT, H1P = (T + 1) * PPT < H_NJ ? (T + 1) * PPT : H_NJ;
         constexpr int NH = H1P > H0P ? H1P - H0P : 0;   // halo pieces issued in this K-tile
-        const char *bc = bbuf(T % NB);
-        char *bn = bbuf((T + 2) % NB);
+        const char *bc = X3 ? bbuf((T + PAR) & 1) : bbuf(T % NB);
+        char *bn = X3 ? bbuf((T + PAR + 1) & 1) : bbuf((T + 2) % NB);
         bf16x8 b1[TN], b2[TN], b3[TN];
-        const char *H0 = hc, *H1 = hc + HG::HPL, *H2 = hc + 2 * HG::HPL;
+        const char *H0 = hc, *H1 = hc + HIMG, *H2 = hc + 2 * HIMG, *H3 = hc + 3 * HIMG;
         auto load_row = [&](int r) __attribute__((always_inline)) {
             const int r0 = (wm * TM + r) * HG::HW + db;
-            fm[r] = x6_kc_frag(H0, H1, r0, lane);
-            if constexpr (NI == 3) fl[r] = x6_kc_frag(H0, H2, r0, lane);
+            if constexpr (X3) {
+                fm[r] = x6_kc_frag(H0, H1, r0, lane);   // [h0|h1]
+                fl[r] = x6_kc_frag(H2, H3, r0, lane);   // [l0|l1]
+            } else {
+                fm[r] = x6_kc_frag(H0, H1, r0, lane);
+                if constexpr (NI == 3) fl[r] = x6_kc_frag(H0, H2, r0, lane);
+            }
         };
         if constexpr (ta == 0 || !kTapsColMajor) {   // a new filter column: its first tap's TM rows
 #pragma unroll
@@ -355,11 +392,14 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         } else {                   // one row beyond the previous tap's window
             load_row(MODE == MODE_FWD ? da + TM - 1 : da);
         }
-        const char *B0 = bc, *B1 = bc + BPL, *B2 = bc + 2 * BPL;
+        const char *B0 = bc, *B1 = bc + BPL, *B2 = bc + 2 * BPL, *B3 = bc + 3 * BPL;
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
             const int c0 = wn * WTN + b * 16;
-            if constexpr (B_KC) {
+            if constexpr (X3) {
+                b1[b] = x6_rc_frag<BN>(B0, B1, c0, lane);   // [w_h0|w_h1]
+                b3[b] = x6_rc_frag<BN>(B2, B3, c0, lane);   // [w_l0|w_l1]
+            } else if constexpr (B_KC) {
                 b1[b] = x6_kc_frag(B0, B1, c0, lane);
                 if constexpr (NI == 3) {
                     b2[b] = x6_kc_frag(B1, B0, c0, lane);
@@ -373,11 +413,36 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
                 }
             }
         }
+        if constexpr (X3) {   // the next weight tile first: the wait below leaves only the halo pieces in flight
+            if constexpr (T + 1 < NTAP) issue_b(T + 1, chunk, bn);
+            else issue_b(0, chunk + 1, bn);
+        }
 #pragma unroll
         for (int s = H0P; s < H0P + NH; ++s) issue_h(s, chunk + 1, hn);
-        if constexpr (T + 2 < NTAP) issue_b(T + 2, chunk, bn);
-        else issue_b(T + 2 - NTAP, chunk + 1, bn);
-        if constexpr (NI == 2) {
+        if constexpr (!X3) {
+            if constexpr (T + 2 < NTAP) issue_b(T + 2, chunk, bn);
+            else issue_b(T + 2 - NTAP, chunk + 1, bn);
+        }
+        if constexpr (X3) {   // h.w_h, l.w_h, h.w_l
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fm[a + da]),
+                                                                      __builtin_bit_cast(f16x8, b1[b]), acc[a][b], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fl[a + da]),
+                                                                      __builtin_bit_cast(f16x8, b1[b]), acc[a][b], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, fm[a + da]),
+                                                                      __builtin_bit_cast(f16x8, b3[b]), acc[a][b], 0, 0, 0);
+        } else if constexpr (NI == 2) {
 #pragma unroll
             for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -403,34 +468,46 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         }
         // DMAs issued in this K-tile may stay in flight; everything older
         // (the next weight tile, and at the last tap the whole next halo) has landed
-        wait_dma_c<B_NJ + NH>();
+        // (fp16x3: the weight tile issued in THIS K-tile, before its halo pieces, too)
+        wait_dma_c<X3 ? NH : B_NJ + NH>();
         barrier();
     };
-    auto chunk_tiles = [&](int chunk, const char *hc, char *hn) __attribute__((always_inline)) {
-        for_taps([&](auto TT) __attribute__((always_inline)) { ktile(TT, chunk, hc, hn); },
+    auto chunk_tiles = [&](auto PARc, int chunk, const char *hc, char *hn) __attribute__((always_inline)) {
+        for_taps([&](auto TT) __attribute__((always_inline)) { ktile(TT, PARc, chunk, hc, hn); },
                  std::make_integer_sequence<int, NTAP>{});
     };
 
     // prologue: the whole halo of the first chunk and its first two weight tiles
+    // (fp16x3: its first one)
 #pragma unroll
     for (int s = 0; s < H_NJ; ++s) issue_h(s, cbeg, hal0);
     issue_b(0, cbeg, bs0);
-    issue_b(1, cbeg, bs1);
-    wait_dma_c<B_NJ>();
+    if constexpr (X3) {
+        wait_dma_c<0>();
+    } else {
+        issue_b(1, cbeg, bs1);
+        wait_dma_c<B_NJ>();
+    }
     barrier();
     int c = cbeg;
     for (; c + 1 < cend; c += 2) {
-        chunk_tiles(c, hal0, hal1);
-        chunk_tiles(c + 1, hal1, hal0);
+        chunk_tiles(std::integral_constant<int, 0>{}, c, hal0, hal1);
+        chunk_tiles(std::integral_constant<int, 1>{}, c + 1, hal1, hal0);
     }
-    if (c < cend) chunk_tiles(c, hal0, hal1);
+    if (c < cend) chunk_tiles(std::integral_constant<int, 0>{}, c, hal0, hal1);
     // every wave's DMAs (including the harmless ones past the last chunk)
     // have landed before the halo buffers become the epilogue's staging area
     wait_dma_c<0>();
     barrier();
 
     constexpr int STAGE = 16 * (WTN + 4);
-    static_assert(NW * STAGE * 4 <= 2 * NPL * HG::HPL, "epilogue staging fits in the halo buffers");
+    static_assert(NW * STAGE * 4 <= 2 * HG::BYTES, "epilogue staging fits in the halo buffers");
+    if constexpr (X3) {   // undo the operand scales (a power of two: exact)
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b) acc[a][b] *= F16X3_OSCALE;
+    }
     float *stage = reinterpret_cast<float *>(hal0) + wid * STAGE;
     // patch row -> output pixel; slab rows: FWD / stride-1 DGRAD pixels, a
     // phase's GEMM rows otherwise (as k_splitk_reduce maps them)
@@ -456,9 +533,18 @@ void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int
     const dim3 blk(256);
 #define DG_X6H(M_, B_, P_, K_) hipLaunchKernelGGL((k_conv_gemm_x6h<M_, B_, P_, K_>), grid, blk, 0, s, a, tiles_x, tiles_y)
 #define DG_F16H(M_, B_) hipLaunchKernelGGL((k_conv_gemm_x6h<M_, B_, false, 3, 2>), grid, blk, 0, s, a, tiles_x, tiles_y)
+#define DG_X3H(B_, P_) hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_FWD, B_, P_, 3, 4>), grid, blk, 0, s, a, tiles_x, tiles_y)
     // (bn 32: the SR discriminators' / FastSRGAN's 32-channel 3x3 layers, stride 1; a
     // 64-wide tile computes half zeros there)
-    if (ni == 2) {   // fp16: 3x3 stride 1, forward or input gradient
+    if (ni == 4) {   // fp16x3 forward (bn 64 | 128), optionally with the fused pool
+        if (a.pidx) {
+            if (bn == 128) DG_X3H(128, true);
+            else DG_X3H(64, true);
+        } else {
+            if (bn == 128) DG_X3H(128, false);
+            else DG_X3H(64, false);
+        }
+    } else if (ni == 2) {   // fp16: 3x3 stride 1, forward or input gradient
         if (mode == MODE_FWD) {
             if (bn == 128) DG_F16H(MODE_FWD, 128);
             else if (bn == 32) DG_F16H(MODE_FWD, 32);
@@ -487,6 +573,7 @@ void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int
     }
 #undef DG_X6H
 #undef DG_F16H
+#undef DG_X3H
 }
 
 }  // namespace dg

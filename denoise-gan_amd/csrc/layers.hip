@@ -352,8 +352,9 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd(int N, int H, int W, int C,
 // float4 over channels (C % 4 == 0, 16-byte rows): one thread per (window,
 // 4 channels).  yp / dxp: optional bf16x6 planes of the output / input
 // gradient (C % 16 == 0) for the conv that consumes it -- no split pass.
+// (ypC: the planes' channel argument of store_planes4 -- C, or -C for fp16x3 planes)
 __global__ void __launch_bounds__(256) k_maxpool_fwd4(int N, int H, int W, int C, const float *x, int ldx, float *y,
-                                                     int ldy, unsigned short *yp) {
+                                                     int ldy, unsigned short *yp, int ypC) {
     const int Ho = H / 2, Wo = W / 2, C4 = C >> 2;
     const int total = N * Ho * Wo * C4;
     for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
@@ -369,7 +370,7 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd4(int N, int H, int W, int C
 #pragma unroll
         for (int q = 0; q < 4; ++q) o[q] = fmaxf(fmaxf(a[q], b[q]), fmaxf(d[q], f[q]));
         *reinterpret_cast<f32x4 *>(y + (long)op * ldy + c) = o;
-        if (yp) store_planes4(yp, C, op, c, o);
+        if (yp) store_planes4(yp, ypC, op, c, o);
     }
 }
 
@@ -941,23 +942,31 @@ static bool pool_vec4(int C, const void *a, int lda, const void *b, int ldb, con
            ((((uintptr_t)a) | ((uintptr_t)b) | ((uintptr_t)c)) & 15) == 0;
 }
 
-int dg_maxpool2_fwd_pl(int N, int H, int W, int C, const float *x, int ldx, float *y, int ldy, void *y_planes,
-                       dg_stream_t stream) {
+int dg_maxpool2_fwd_plf(int N, int H, int W, int C, const float *x, int ldx, float *y, int ldy, void *y_planes,
+                        int y_planes_format, dg_stream_t stream) {
     DG_ARG(x && y, "NULL tensor");
     DG_ARG(N > 0 && H >= 2 && W >= 2 && C > 0 && ldx >= C && ldy >= C, "bad shape");
+    DG_ARG(y_planes_format == DG_PLANES_BF16X6 || y_planes_format == DG_PLANES_F16X3, "bad plane format %d",
+           y_planes_format);
     const long total = (long)N * (H / 2) * (W / 2) * C;
     DG_ARG(total < (1L << 31), "tensor too large");
     const bool v4 = pool_vec4(C, x, ldx, y, ldy, y, ldy);
-    DG_ARG(!y_planes || (v4 && C % 16 == 0 && (((uintptr_t)y_planes) & 15) == 0),
-           "output planes need C %% 16 == 0 and 16-byte aligned rows");
+    const int cm = y_planes_format == DG_PLANES_F16X3 ? 32 : 16;
+    DG_ARG(!y_planes || (v4 && C % cm == 0 && (((uintptr_t)y_planes) & 15) == 0),
+           "output planes need C %% %d == 0 and 16-byte aligned rows", cm);
     if (v4)
         hipLaunchKernelGGL(dg::k_maxpool_fwd4, dim3(dg::lgrid(total / 4)), dim3(256), 0, (hipStream_t)stream, N, H, W,
-                           C, x, ldx, y, ldy, (unsigned short *)y_planes);
+                           C, x, ldx, y, ldy, (unsigned short *)y_planes, y_planes_format == DG_PLANES_F16X3 ? -C : C);
     else
         hipLaunchKernelGGL(dg::k_maxpool_fwd, dim3(dg::lgrid(total)), dim3(256), 0, (hipStream_t)stream, N, H, W, C, x,
                            ldx, y, ldy);
     DG_LAUNCHED("maxpool_fwd");
     return DG_OK;
+}
+
+int dg_maxpool2_fwd_pl(int N, int H, int W, int C, const float *x, int ldx, float *y, int ldy, void *y_planes,
+                       dg_stream_t stream) {
+    return dg_maxpool2_fwd_plf(N, H, W, C, x, ldx, y, ldy, y_planes, DG_PLANES_BF16X6, stream);
 }
 
 int dg_maxpool2_fwd(int N, int H, int W, int C, const float *x, int ldx, float *y, int ldy, dg_stream_t stream) {

@@ -88,9 +88,11 @@ _SIGS = {
     "dg_conv_bwd_data_masked": (c_int, [c_void_p, _P, c_int, _P, _P, c_int, c_float, _P, c_int, c_int, c_float, _P,
                                         c_size_t, _P]),
     "dg_maxpool2_fwd_pl": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, _P]),
+    "dg_maxpool2_fwd_plf": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, _P]),
     "dg_maxpool2_bwd_pl": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, c_float, c_int,
                                    c_float, _P, _P]),
     "dg_conv_planes_size": (c_int, [c_void_p, c_int, ctypes.POINTER(c_size_t)]),
+    "dg_conv_planes_format": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int)]),
     "dg_conv_op_planes": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int)]),
     "dg_conv_fwd_pl": (c_int, [c_void_p, _P, c_int, _P, _P, _P, c_int, c_float, c_int, c_float, _P, _P, c_size_t,
                                _P]),

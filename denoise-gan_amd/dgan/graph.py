@@ -405,9 +405,10 @@ class GraphPlan:
         self.pool_out = [dict() for _ in range(slots)]    # maxpool node -> consumer conv's x planes
         self.pool_gout = [dict() for _ in range(slots)]   # maxpool node -> producer conv's dy planes
         feed = not os.environ.get("DG_NO_FEED")
-        # (producer-written planes are bf16x6 planes: an fp16 descriptor's planes are
-        # the fp16 copies its own ops convert, so neither end of a feed may be fp16)
-        x6 = lambda d: d.math == ops.MATH_BF16X6   # noqa: E731
+        # (producer-written planes are bf16x6 or, for a consumer whose forward runs fp16x3,
+        # fp16x3 planes -- the PlaneBuf's fmt tells the producer; an fp16 descriptor's
+        # planes are the fp16 copies its own ops convert, so neither end of a feed may be fp16)
+        x6 = lambda d: d.math in (ops.MATH_BF16X6, ops.MATH_F16X3)   # noqa: E731
         for m in (nodes[1:] if feed else []):
             # max pool between two convs: its output is the next conv's input,
             # its input gradient the previous conv's dy (premask: act' folded in)
@@ -421,7 +422,7 @@ class GraphPlan:
                     for k in range(slots):
                         pc = self.cplanes[k][c.idx]
                         if pc.x is None:
-                            pc.x = ops.PlaneBuf(dc.plane_bytes(ops.TENSOR_X), device)
+                            pc.x = ops.PlaneBuf(dc.plane_bytes(ops.TENSOR_X), device, dc.plane_format(ops.TENSOR_X))
                         self.pool_out[k][m.idx] = pc.x
                     self.fed_x.add(c.idx)
             t_in = m.ins[0]
@@ -446,7 +447,7 @@ class GraphPlan:
                 for k in range(slots):
                     pc = self.cplanes[k][c.idx]
                     if pc.x is None:
-                        pc.x = ops.PlaneBuf(dc.plane_bytes(ops.TENSOR_X), device)
+                        pc.x = ops.PlaneBuf(dc.plane_bytes(ops.TENSOR_X), device, dc.plane_format(ops.TENSOR_X))
                     self.cplanes[k][n.idx].fwd_out = pc.x
                 self.fed_x.add(c.idx)
             if train and (dn.plane_mask[ops.OP_BWD_DATA] | dn.plane_mask[ops.OP_BWD_FILTER]) & ops.TENSOR_DY:

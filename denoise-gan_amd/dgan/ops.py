@@ -97,8 +97,10 @@ def default_workspace():
 
 
 # conv GEMM arithmetic (include/dgan.h DG_MATH_*)
-MATH_FP32, MATH_BF16X6, MATH_FP16 = 0, 1, 2
-MATH_MODES = {"fp32": MATH_FP32, "bf16x6": MATH_BF16X6, "fp16": MATH_FP16}
+MATH_FP32, MATH_BF16X6, MATH_FP16, MATH_F16X3 = 0, 1, 2, 3
+MATH_MODES = {"fp32": MATH_FP32, "bf16x6": MATH_BF16X6, "fp16": MATH_FP16, "f16x3": MATH_F16X3}
+# plane buffer formats (include/dgan.h DG_PLANES_*)
+PLANES_BF16X6, PLANES_F16X3 = 0, 1
 
 # layer tensors of dg_conv_planes_t (include/dgan.h DG_TENSOR_*)
 TENSOR_X, TENSOR_DY, TENSOR_W = 1, 2, 4
@@ -106,25 +108,28 @@ TENSOR_X, TENSOR_DY, TENSOR_W = 1, 2, 4
 
 class _PlanesC(ctypes.Structure):
     _fields_ = [("x", ctypes.c_void_p), ("dy", ctypes.c_void_p), ("w", ctypes.c_void_p), ("out", ctypes.c_void_p),
-                ("ready", ctypes.c_int)]
+                ("ready", ctypes.c_int), ("out_format", ctypes.c_int)]
 
 
 class PlaneBuf:
-    """A device buffer of bf16x6 planes and whether it holds the split of the
+    """A device buffer of operand planes and whether it holds the split of the
     tensor it stands for.  One PlaneBuf may serve several ConvPlanes: the
     weight planes of a network read by several plans, or one output-gradient
-    scratch reused layer after layer."""
+    scratch reused layer after layer.  fmt: PLANES_BF16X6, or PLANES_F16X3 for
+    the x planes of a descriptor whose forward runs fp16x3 (a producer writing
+    them needs to know)."""
 
-    __slots__ = ("buf", "ready")
+    __slots__ = ("buf", "ready", "fmt")
 
-    def __init__(self, nbytes, device=None):
+    def __init__(self, nbytes, device=None, fmt=PLANES_BF16X6):
         self.buf = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device or "cuda")
         self.ready = False
+        self.fmt = fmt
 
     def view(self, nbytes):
         """A PlaneBuf sharing the first nbytes of this one (own ready flag)."""
         v = PlaneBuf.__new__(PlaneBuf)
-        v.buf, v.ready = self.buf[:max(int(nbytes), 16)], False
+        v.buf, v.ready, v.fmt = self.buf[:max(int(nbytes), 16)], False, self.fmt
         return v
 
 
@@ -151,7 +156,7 @@ class ConvPlanes:
         used = d.plane_mask[0] | d.plane_mask[1] | d.plane_mask[2]
 
         def buf(t, want):
-            return PlaneBuf(d.plane_bytes(t), device) if want and (used & t) else None
+            return PlaneBuf(d.plane_bytes(t), device, d.plane_format(t)) if want and (used & t) else None
 
         return cls(buf(TENSOR_X, x), buf(TENSOR_DY, dy), buf(TENSOR_W, w))
 
@@ -174,7 +179,8 @@ class ConvPlanes:
 
     def _c(self, out=None):
         ptr = lambda b: None if b is None else b.buf.data_ptr()
-        return _PlanesC(ptr(self.x), ptr(self.dy), ptr(self.w), ptr(out), self.ready)
+        return _PlanesC(ptr(self.x), ptr(self.dy), ptr(self.w), ptr(out), self.ready,
+                        out.fmt if out is not None else PLANES_BF16X6)
 
     def _have(self):
         return sum(t for t, b in self._bufs() if b is not None)
@@ -196,7 +202,8 @@ def plan_planes(descs, device=None, keep_x=True, wbufs=None):
     dy_buf = PlaneBuf(max(dy_need), device) if dy_need and max(dy_need) else None
     out = []
     for i, (d, m) in enumerate(zip(descs, masks)):
-        x = PlaneBuf(d.plane_bytes(TENSOR_X), device) if keep_x and (m[0] & m[2] & TENSOR_X) else None
+        x = PlaneBuf(d.plane_bytes(TENSOR_X), device, d.plane_format(TENSOR_X)) if keep_x and (m[0] & m[2] & TENSOR_X) \
+            else None
         w = None
         if (m[0] | m[1]) & TENSOR_W:
             w = wbufs[i] if wbufs is not None and wbufs[i] is not None else PlaneBuf(d.plane_bytes(TENSOR_W), device)
@@ -266,6 +273,12 @@ class ConvDesc:
         n = ctypes.c_size_t()
         call("dg_conv_planes_size", self._h, tensor, ctypes.byref(n))
         return n.value
+
+    def plane_format(self, tensor):
+        """PLANES_F16X3 for the x / w planes of a descriptor whose forward runs fp16x3."""
+        f = ctypes.c_int()
+        call("dg_conv_planes_format", self._h, tensor, ctypes.byref(f))
+        return f.value
 
     def _pl(self, op, planes):
         """(struct pointer, bits this op fills) for a ConvPlanes (None -> no planes)."""
@@ -351,7 +364,7 @@ class ConvDesc:
             saved, planes.fwd_out = planes.fwd_out, pool_planes
         pp, fills = self._pl(OP_FWD, planes)
         if planes is None and pool_planes is not None:
-            pp, fills = ctypes.byref(_PlanesC(None, None, None, pool_planes.buf.data_ptr(), 0)), 0
+            pp, fills = ctypes.byref(_PlanesC(None, None, None, pool_planes.buf.data_ptr(), 0, pool_planes.fmt)), 0
         ev = _prof_begin()
         call("dg_conv_fwd_pool", self._h, _p(x), ldx, _p(w), _p(bias), act_id(act), float(alpha), _p(pool_y), ldpy,
              _p(pool_idx), pp, wp, wn, _stream())
@@ -701,8 +714,9 @@ def act_fwd(x, z, act, alpha=0.3):
 def maxpool2_fwd(x, y, planes_out=None):
     """planes_out: PlaneBuf of the consuming conv's input planes, written beside y."""
     N, H, W, C = _nhwc(x)
-    call("dg_maxpool2_fwd_pl", N, H, W, C, _p(x), pix_ld(x, C), _p(y), pix_ld(y, C),
-         None if planes_out is None else _p(planes_out.buf), _stream())
+    call("dg_maxpool2_fwd_plf", N, H, W, C, _p(x), pix_ld(x, C), _p(y), pix_ld(y, C),
+         None if planes_out is None else _p(planes_out.buf), PLANES_BF16X6 if planes_out is None else planes_out.fmt,
+         _stream())
     if planes_out is not None:
         planes_out.ready = True
     return y

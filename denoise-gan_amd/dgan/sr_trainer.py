@@ -13,6 +13,8 @@ One call = the reference's traced `train_step`:
 All launches go to the current stream with pre-sized buffers, so a step can
 be captured in one HIP graph.
 """
+import os
+
 import torch
 
 from . import ops
@@ -67,6 +69,14 @@ class VGGNetwork(GraphNetwork):
 
     def __init__(self, weights=None, seed=4242, width=1, device=None):
         super().__init__(vgg19_features(width), seed=seed, device=device, kind="vgg19", trainable=False)
+        # the frozen network's forward GEMMs on fp16x3 (include/dgan.h DG_MATH_F16X3: three fp16
+        # piece products, half the bf16x6 MFMA count; its input gradients stay bf16x6) when the
+        # library default is bf16x6; DG_VGG_MATH overrides (e.g. "bf16x6" for A/B runs)
+        vm = os.environ.get("DG_VGG_MATH")
+        if vm:
+            self.conv_math = vm
+        elif ops.default_conv_math() == ops.MATH_BF16X6:
+            self.conv_math = "f16x3"
         self.pretrained = False
         if weights:
             self.load_weights(weights)

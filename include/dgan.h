@@ -79,9 +79,23 @@ int dg_conv_workspace_size(dg_conv_t d, int op, size_t *bytes);
  *                    Eligible GEMMs: FWD Cin % 32 == 0, DGRAD Cout % 32 == 0,
  *                    WGRAD Cin, Cout % 16 == 0 (others keep fp32); no
  *                    caller-held planes (dg_conv_op_planes reports none).
- * New descriptors take $DG_CONV_MATH ("fp32" | "bf16x6" | "fp16"; default bf16x6).
+ *   DG_MATH_F16X3  : bf16x6, except the forward GEMM of a stride-1 3x3 Conv2D with
+ *                    Cin % 32 == 0 and Cout % 16 == 0, Cout > 32 (the frozen VGG19 of the
+ *                    content loss, pix2pix.py:53-67): each fp32 operand, pre-scaled by a
+ *                    power of two (activations 2^-4, weights 2^8), is split into fp16
+ *                    h + l (RNE, |l| <= 2^-11 |x|) and a product is h.h' + h.l' + l.h' --
+ *                    three fp16 piece products (dropped terms < 2^-21 |ab|) on three
+ *                    v_mfma_f32_16x16x32_f16 per 32 channels, half the bf16x6 MFMA count.
+ *                    Range: |activation| < 2^20 (fp16 max 65504 after the 2^-4 scale),
+ *                    |weight| < 255; smaller values keep an absolute error < 2^-21.
+ *                    Such a descriptor's x planes are fp16x3 (4 B per element, its
+ *                    forward only; its filter gradient splits x itself) and its w planes
+ *                    [fp16x3 | bf16x6] (dg_conv_planes_size), split by the forward.
+ * New descriptors take $DG_CONV_MATH ("fp32" | "bf16x6" | "fp16" | "f16x3"; default bf16x6).
  * Changing the mode re-plans the descriptor: query workspace sizes after it. */
-enum { DG_MATH_FP32 = 0, DG_MATH_BF16X6 = 1, DG_MATH_FP16 = 2 };
+enum { DG_MATH_FP32 = 0, DG_MATH_BF16X6 = 1, DG_MATH_FP16 = 2, DG_MATH_F16X3 = 3 };
+/* plane formats of dg_conv_planes_t buffers (dg_conv_planes_format) */
+enum { DG_PLANES_BF16X6 = 0, DG_PLANES_F16X3 = 1 };
 int dg_conv_set_math(dg_conv_t d, int math);
 int dg_conv_get_math(dg_conv_t d, int *math);
 
@@ -126,8 +140,14 @@ typedef struct dg_conv_planes {
                           (fwd: y, bwd_data: dx; channels % 16 == 0) -- the
                           consumer's x / dy planes, with no split pass */
     int ready;         /* DG_TENSOR_* bits whose buffer already holds the split */
+    int out_format;    /* DG_PLANES_* of `out`: the consumer's x planes format (its
+                          dg_conv_planes_format(DG_TENSOR_X)); DG_PLANES_F16X3 needs
+                          channels % 32 == 0 (zero-initialised callers get bf16x6) */
 } dg_conv_planes_t;
 int dg_conv_planes_size(dg_conv_t d, int tensor, size_t *bytes);
+/* DG_PLANES_F16X3 for the x / w planes of a descriptor whose forward runs fp16x3
+ * (DG_MATH_F16X3), else DG_PLANES_BF16X6 */
+int dg_conv_planes_format(dg_conv_t d, int tensor, int *format);
 int dg_conv_op_planes(dg_conv_t d, int op, int *tensors);
 int dg_conv_fwd_pl(dg_conv_t d, const float *x, int ldx, const float *w, const float *bias,
                    float *y, int ldy, float beta, int act, float alpha,
@@ -382,6 +402,9 @@ int dg_maxpool2_bwd(int N, int H, int W, int C, const float *x, int ldx, const f
  * the conv that reads them (VGG19: pool -> conv input, pool gradient -> the previous conv's dy) */
 int dg_maxpool2_fwd_pl(int N, int H, int W, int C, const float *x, int ldx, float *y, int ldy, void *y_planes,
                        dg_stream_t stream);
+/* the same with the consumer's plane format (DG_PLANES_*; fp16x3: C % 32 == 0) */
+int dg_maxpool2_fwd_plf(int N, int H, int W, int C, const float *x, int ldx, float *y, int ldy, void *y_planes,
+                        int y_planes_format, dg_stream_t stream);
 int dg_maxpool2_bwd_pl(int N, int H, int W, int C, const float *x, int ldx, const float *dy, int lddy,
                        float *dx, int lddx, float beta, int act, float alpha, void *dx_planes, dg_stream_t stream);
 /* backward of a pool fused by dg_conv_fwd_pool, from its index bytes (the full-size

@@ -54,10 +54,15 @@ def fused_pool_decisions(idx):
 
 
 def plane_positive(pbuf, shape):
-    """x > 0 from the hi plane of a packed bf16x6 plane buffer ([pixel][C/16][3][16]
-    int16; a positive bf16 is a positive int16) for an NHWC shape."""
+    """x > 0 from the hi plane of a packed plane buffer for an NHWC shape: bf16x6
+    [pixel][C/16][3][16] or fp16x3 [pixel][C/32][2][32] (pbuf.fmt); a positive bf16 /
+    fp16 is a positive int16."""
+    from dgan import ops
     N, H, W, C = shape
-    hi = pbuf.buf[:N * H * W * C * 6].view(torch.int16).reshape(N * H * W, C // 16, 3, 16)[:, :, 0, :]
+    if getattr(pbuf, "fmt", ops.PLANES_BF16X6) == ops.PLANES_F16X3:
+        hi = pbuf.buf[:N * H * W * C * 4].view(torch.int16).reshape(N * H * W, C // 32, 2, 32)[:, :, 0, :]
+    else:
+        hi = pbuf.buf[:N * H * W * C * 6].view(torch.int16).reshape(N * H * W, C // 16, 3, 16)[:, :, 0, :]
     return (hi.reshape(N, H, W, C) > 0)
 
 

@@ -1,0 +1,184 @@
+"""The fp16x3 forward of the frozen VGG19 (include/dgan.h DG_MATH_F16X3): every
+3x3 stride-1 Conv2D with Cin % 32 == 0 and Cout > 32 (keras VGG19 blocks 1-5
+after block1_conv1, as built by pix2pix.py:53-67 / srgan.py:70-76) runs its
+forward GEMM as three fp16 piece products of pre-scaled operands
+(s x = h + l, h.h' + l.h' + h.l') on the halo kernel (conv_x6h.hip NI 4).
+
+  * the layer against a torch fp64 reference at the conv engine's fp32 bar
+    (test_conv_gpu.py _close: relative L2 < 2e-6, max-abs < 1e-5 of scale),
+    forward, and the bf16x6 input / filter gradients of the same descriptor
+    reading the bf16x6 half of the shared weight planes;
+  * the fp16x3 planes a producer writes beside its output (conv epilogue,
+    fused pool epilogue, unfused max pool) are the bytes the layer's own split
+    pass writes, so a fed forward is bit-identical to an unfed one;
+  * the input gradient masked by the sign of the fp16x3 hi plane equals the
+    one masked by the fp32 activation;
+  * a mixed 2-layer chain (fused pool) ends bit-identical whether planes are
+    fed or split."""
+import pytest
+import torch
+
+from dgan import ops
+from test_conv_gpu import _close, test_conv_layer
+
+gpu = pytest.mark.gpu
+
+# (name, N, H, W, Cin, Cout, k, s, padding, transpose, bias): VGG19-like layers on
+# the fp16x3 halo kernel -- BN 64 / 128, ragged 8x16 patches, split-K over the
+# 32-channel chunks (small image, many channels), 'valid' padding, Cout 48 (BN 64 tile
+# with a ragged column block)
+X3_CASES = [
+    ("x3.b2", 2, 32, 32, 64, 128, 3, 1, "same", False, True),
+    ("x3.bn64", 2, 16, 16, 128, 64, 3, 1, "same", False, False),
+    ("x3.ragged", 3, 21, 37, 64, 128, 3, 1, "same", False, True),
+    ("x3.splitk", 2, 8, 8, 512, 512, 3, 1, "same", False, True),
+    ("x3.valid", 2, 20, 22, 32, 64, 3, 1, "valid", False, False),
+    ("x3.c48", 2, 16, 24, 96, 48, 3, 1, "same", False, True),
+]
+
+
+def _rand(shape, seed, scale=1.0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(shape, generator=g) * scale).cuda()
+
+
+@gpu
+@pytest.mark.parametrize("case", X3_CASES, ids=[c[0] for c in X3_CASES])
+def test_x3_layer_matches_fp64(case, monkeypatch):
+    monkeypatch.delenv("DG_PLAN_DISABLE", raising=False)
+    name, N, H, W, Cin, Cout, k, s, padding, transpose, bias = case
+    d = ops.ConvDesc(N, H, W, Cin, Cout, k, s, padding, transpose, math="f16x3")
+    assert d.plane_format(ops.TENSOR_X) == ops.PLANES_F16X3, f"{name}: forward not planned on fp16x3"
+    test_conv_layer(case, "f16x3")
+
+
+@gpu
+def test_x3_shared_weight_planes_serve_bwd_data():
+    """One weight PlaneBuf: the fp16x3 forward splits both halves ([fp16x3 | bf16x6]); the
+    input gradient reading the bf16x6 half equals the one that splits w itself."""
+    N, H, W, Ci, Co = 2, 24, 32, 64, 128
+    d = ops.ConvDesc(N, H, W, Ci, Co, 3, 1, "same", math="f16x3")
+    x, w, dy = _rand((N, H, W, Ci), 1), _rand(d.weight_shape, 2, 0.05), _rand((N, H, W, Co), 3)
+    P = ops.ConvPlanes.for_desc(d, x=True, dy=True, w=True)
+    assert P.w is not None and P.w.buf.numel() >= 10 * 9 * Ci * Co
+    y0, y1 = torch.empty(N, H, W, Co, device="cuda"), torch.empty(N, H, W, Co, device="cuda")
+    d.fwd(x, w, y0)
+    d.fwd(x, w, y1, planes=P)
+    assert P.w.ready
+    dx0, dx1 = torch.empty_like(x), torch.empty_like(x)
+    d.bwd_data(dy, w, dx0)
+    d.bwd_data(dy, w, dx1, planes=P)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    assert torch.equal(dx0, dx1)
+
+
+@gpu
+@pytest.mark.parametrize("prod_math", ["bf16x6", "f16x3"])
+def test_x3_producer_planes_equal_the_split(prod_math):
+    """conv A (relu) -> conv B (fp16x3): A's epilogue writes B's x planes (out_format
+    fp16x3); B's forward on them is bit-identical to B splitting A's fp32 output."""
+    N, H, W, C0, C1, C2 = 2, 24, 40, 32, 64, 128
+    a = ops.ConvDesc(N, H, W, C0, C1, 3, 1, "same", math=prod_math)
+    b = ops.ConvDesc(N, H, W, C1, C2, 3, 1, "same", math="f16x3")
+    x = _rand((N, H, W, C0), 4)
+    wa, wb = _rand(a.weight_shape, 5, 0.08), _rand(b.weight_shape, 6, 0.05)
+    ba = _rand((C1,), 7, 0.1)
+    ya = torch.empty(N, H, W, C1, device="cuda")
+    Pb = ops.ConvPlanes.for_desc(b, x=True)
+    assert Pb.x.fmt == ops.PLANES_F16X3 and Pb.x.buf.numel() >= 4 * N * H * W * C1
+    Pa = ops.ConvPlanes()
+    Pa.fwd_out = Pb.x
+    a.fwd(x, wa, ya, bias=ba, act="relu", planes=Pa)
+    assert Pb.x.ready
+    y_fed, y_own = torch.empty(N, H, W, C2, device="cuda"), torch.empty(N, H, W, C2, device="cuda")
+    b.fwd(ya, wb, y_fed, planes=Pb)        # reads the producer's planes
+    b.fwd(ya, wb, y_own)                   # splits ya itself
+    torch.cuda.synchronize()
+    assert torch.equal(y_fed, y_own)
+
+
+@gpu
+def test_x3_fused_pool_planes_and_unfused_pool():
+    """An fp16x3 conv with its 2x2 max pool fused (pool_fusable) writes the next fp16x3
+    conv's x planes; so does the unfused pool (dg_maxpool2_fwd_plf).  Both equal the
+    consumer's own split, and the pooled values equal conv -> pool."""
+    N, H, W, Ci, Co, Cn = 4, 32, 32, 64, 128, 128
+    d = ops.ConvDesc(N, H, W, Ci, Co, 3, 1, "same", math="f16x3")
+    nxt = ops.ConvDesc(N, H // 2, W // 2, Co, Cn, 3, 1, "same", math="f16x3")
+    assert d.pool_fusable("relu")
+    x, w, b = _rand((N, H, W, Ci), 8), _rand(d.weight_shape, 9, 0.06), _rand((Co,), 10, 0.1)
+    wn = _rand(nxt.weight_shape, 11, 0.05)
+    y = torch.empty(N, H, W, Co, device="cuda")
+    d.fwd(x, w, y, bias=b, act="relu")
+    py0 = torch.empty(N, H // 2, W // 2, Co, device="cuda")
+    P0 = ops.ConvPlanes.for_desc(nxt, x=True)
+    ops.maxpool2_fwd(y, py0, planes_out=P0.x)
+    py1 = torch.empty_like(py0)
+    P1 = ops.ConvPlanes.for_desc(nxt, x=True)
+    idx = torch.empty((N, H // 2, W // 2, Co), dtype=torch.uint8, device="cuda")
+    d.fwd_pool(x, w, idx, bias=b, act="relu", pool_y=py1, pool_planes=P1.x)
+    P2 = ops.ConvPlanes.for_desc(nxt, x=True)
+    yo = [torch.empty(N, H // 2, W // 2, Cn, device="cuda") for _ in range(3)]
+    nxt.fwd(py0, wn, yo[0], planes=P0)
+    nxt.fwd(py1, wn, yo[1], planes=P1)
+    nxt.fwd(py0, wn, yo[2], planes=P2)      # (splits py0 into P2)
+    torch.cuda.synchronize()
+    assert torch.equal(py0, py1)
+    nb = 4 * N * (H // 2) * (W // 2) * Co
+    assert torch.equal(P0.x.buf[:nb], P1.x.buf[:nb]) and torch.equal(P0.x.buf[:nb], P2.x.buf[:nb])
+    assert torch.equal(yo[0], yo[1]) and torch.equal(yo[0], yo[2])
+
+
+@gpu
+def test_x3_xmask_from_hi_plane_sign():
+    """dg_conv_bwd_data_xmask on fp16x3 x planes: act' from the sign of the fp16 hi
+    piece equals act' from the fp32 activation (relu and leaky relu)."""
+    N, H, W, Ci, Co = 2, 16, 32, 64, 64
+    d = ops.ConvDesc(N, H, W, Ci, Co, 3, 1, "same", math="f16x3")
+    z = _rand((N, H, W, Ci), 12)
+    z = torch.where(z > 0, z, 0.3 * z)            # a leaky relu output (signs on both sides)
+    w, dy = _rand(d.weight_shape, 13, 0.05), _rand((N, H, W, Co), 14)
+    P = ops.ConvPlanes.for_desc(d, x=True, w=True)
+    y = torch.empty(N, H, W, Co, device="cuda")
+    d.fwd(z, w, y, planes=P)                      # splits z into P.x (fp16x3)
+    assert P.x.ready and P.x.fmt == ops.PLANES_F16X3
+    for act in ("lrelu", "relu"):
+        dx0, dx1 = torch.empty_like(z), torch.empty_like(z)
+        d.bwd_data_masked(dy, w, dx0, z, act, alpha=0.3)
+        d.bwd_data_xmask(dy, w, dx1, act, alpha=0.3, planes=P)
+        torch.cuda.synchronize()
+        assert torch.equal(dx0, dx1), act
+
+
+@gpu
+def test_vgg_content_loss_x3_vs_bf16x6():
+    """The VGG19 content loss with its forward on fp16x3 against the all-bf16x6 network on
+    the same weights and inputs: value to 1e-6 relative, input gradient to 1e-4 in relative
+    L2 and of its scale elementwise (measured 1.1e-5: unconditioned, a ReLU / pool near-tie
+    of the 16 layers may route differently -- a sanity bar against indexing errors; the
+    mask-conditioned fp64 bars are test_sr_gpu.py's and test_step_gpu.py's)."""
+    from dgan.sr_trainer import ContentLoss, VGGNetwork
+    N, H, W = 2, 64, 64
+    nets = []
+    for vm in ("f16x3", "bf16x6"):
+        v = VGGNetwork(seed=5, width=4, device=torch.device("cuda"))
+        v.conv_math = vm
+        nets.append(v)
+    g, t = _rand((N, H, W, 3), 15).clamp(-1, 1), _rand((N, H, W, 3), 16).clamp(-1, 1)
+    out = []
+    for v in nets:
+        cl = ContentLoss(v, N, H, W, torch.device("cuda"))
+        ws = ops.Workspace()
+        ws.get(cl.ws_bytes)
+        val = cl.forward(g, t, ws=ws)[0].clone()
+        dg = torch.zeros(N, H, W, 3, device="cuda")
+        cl.backward(dg, beta=0.0, ws=ws)
+        out.append((val, dg))
+        if v.conv_math == "f16x3":
+            assert any(d.plane_format(ops.TENSOR_X) == ops.PLANES_F16X3 for d in cl.fplan.desc.values())
+    torch.cuda.synchronize()
+    (v0, g0), (v1, g1) = out
+    assert abs(float(v0) - float(v1)) <= 1e-6 * abs(float(v1))
+    assert float((g0 - g1).norm()) <= 1e-4 * float(g1.norm())
+    assert float((g0 - g1).abs().max()) <= 1e-4 * float(g1.abs().max())
