@@ -93,6 +93,7 @@ _SIGS = {
                                    c_float, _P, _P]),
     "dg_conv_planes_size": (c_int, [c_void_p, c_int, ctypes.POINTER(c_size_t)]),
     "dg_conv_planes_format": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int)]),
+    "dg_mark": (c_int, [c_int, _P]),
     "dg_conv_op_planes": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int)]),
     "dg_conv_fwd_pl": (c_int, [c_void_p, _P, c_int, _P, _P, _P, c_int, c_float, c_int, c_float, _P, _P, c_size_t,
                                _P]),

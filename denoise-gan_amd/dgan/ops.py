@@ -438,10 +438,20 @@ _PROF = None
 
 
 class ConvProfile:
-    """Records (HIP start event, end event, desc, op) around every conv call."""
+    """Records (HIP start event, end event, desc, op) around every conv call.
+    markers: also put a dg_mark dispatch before and after every conv call (and
+    `mark()` wherever the caller wants one), so per-dispatch PMC counters can be
+    attributed to conv calls (scripts/pmc_layers.py); `marks` lists them in order."""
 
-    def __init__(self):
+    def __init__(self, markers=False):
         self.records = []
+        self.markers = markers
+        self.marks = []
+
+    def mark(self, what):
+        if self.markers:
+            call("dg_mark", len(self.marks), _stream())
+            self.marks.append(what)
 
     def __enter__(self):
         global _PROF
@@ -465,6 +475,7 @@ class ConvProfile:
 def _prof_begin():
     if _PROF is None:
         return None
+    _PROF.mark(("begin", len(_PROF.records)))
     e = torch.cuda.Event(enable_timing=True)
     e.record(torch.cuda.current_stream())
     return e
@@ -475,6 +486,7 @@ def _prof_end(e0, desc, op):
         return
     e1 = torch.cuda.Event(enable_timing=True)
     e1.record(torch.cuda.current_stream())
+    _PROF.mark(("end", len(_PROF.records)))
     _PROF.records.append((e0, e1, desc, op))
 
 

@@ -45,6 +45,9 @@ enum { DG_OP_FWD = 0, DG_OP_BWD_DATA = 1, DG_OP_BWD_FILTER = 2 };
 
 const char *dg_last_error_string(void);
 int dg_version(void);
+/* an empty kernel dispatch on `stream`: a mark in the dispatch sequence for profiling
+ * (per-dispatch rocprofv3 PMC counters attributed to the calls between marks) */
+int dg_mark(int id, dg_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * Convolution layers: Conv2D (pix2pix.py:115-116, :207-209, :217-218) and

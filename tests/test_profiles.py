@@ -21,3 +21,17 @@ def test_traffic_profiles_match_the_library_sources():
         assert t.get("csrc_sha") == sha, (f"{os.path.basename(p)} was measured on other library sources "
                                           f"({t.get('csrc_sha')} vs {sha}): re-measure (scripts/traffic_from_bench.py)")
         assert t["conv_engine_bytes_per_step"] > 0
+
+
+def test_per_call_traffic_table_matches_the_aggregate():
+    """The committed per-conv-call traffic table (profiles/pmc_layers.md, scripts/pmc_layers.py)
+    is of the same library sources as the aggregate profiles/pmc_traffic.json: both carry this
+    tree's csrc_sha."""
+    from pmc_traffic import csrc_sha
+    path = os.path.join(REPO, "profiles", "pmc_layers.md")
+    assert os.path.exists(path), "no committed per-call traffic table"
+    text = open(path).read()
+    agg = json.load(open(os.path.join(REPO, "profiles", "pmc_traffic.json")))
+    assert f"csrc_sha {csrc_sha()}" in text, "profiles/pmc_layers.md was measured on other library sources"
+    assert agg.get("csrc_sha") == csrc_sha()
+    assert "| net | layer | op |" in text
