@@ -89,13 +89,52 @@ __device__ __forceinline__ void split_x3(float x, float s, _Float16 &h, _Float16
     h = (_Float16)v;
     l = (_Float16)(v - (float)h);
 }
+// Gradient operands (DG_MATH_F16X3 input gradients) have no static range: their planes
+// are scaled by 2^(14 - e) with bound = m * g < 2^e read from device memory -- m a
+// measured max |value| (atomicMax by the producer of the previous gradient), g a weight
+// bound (max over input channels of sum |w|, NULL = 1) -- so the scaled values stay below
+// 2^14 (fp16 max 65504) while values down to 2^-28 of the bound keep 22 bits
+// A measured max is kept as X3_SHARDS floats (one per workgroup shard, so the atomics of a
+// grid spread over that many words: one word takes about one atomic per 11 ns,
+// MI355X_MICROARCH.md 'fanin'); its value is their max.
+constexpr int X3_SHARDS = 8;
+__device__ __forceinline__ float x3_grad_scale(const float *m, const float *g) {
+    float mm = m[0];
+#pragma unroll
+    for (int i = 1; i < X3_SHARDS; ++i) mm = fmaxf(mm, m[i]);
+    const float b = mm * (g ? *g : 1.f);
+    if (!(b > 0.f) || !(b <= 3.0e38f)) return 1.f;
+    int e;
+    (void)frexpf(b, &e);   // b < 2^e
+    return ldexpf(1.f, 14 - e);
+}
+// |v| into a sharded device max (non-negative floats order as their bit patterns): a
+// butterfly over each wave's lanes, the waves' maxima through LDS, then one lane reads the
+// workgroup's shard and adds one vector atomic only when its value is larger (most
+// workgroups of a grid then add none).  Every thread of the workgroup must call it.
+__device__ __forceinline__ void block_atomic_absmax(float *dst, float v) {
+    __shared__ float red[16];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int nw = (blockDim.x + 63) >> 6;
+        for (int i = 1; i < nw; ++i) v = fmaxf(v, red[i]);
+        unsigned *w = reinterpret_cast<unsigned *>(dst) + ((blockIdx.x + blockIdx.y * gridDim.x) & (X3_SHARDS - 1));
+        const unsigned u = __float_as_uint(v);
+        if (u > __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(w, u);
+    }
+}
 
 // planes of one output element / of 4 consecutive elements (col % 4 == 0) for the
 // consuming conv: C > 0 bf16x6 planes, C < 0 fp16x3 activation planes (-C channels)
-__device__ __forceinline__ void store_planes1(unsigned short *yp, int C, long pix, int col, float x) {
+// (xs: the fp16x3 scale -- F16X3_XS for activations, x3_grad_scale for gradients)
+__device__ __forceinline__ void store_planes1(unsigned short *yp, int C, long pix, int col, float x,
+                                              float xs = F16X3_XS) {
     if (C < 0) {
         _Float16 *d = reinterpret_cast<_Float16 *>(yp) + pix * 2 * (-C) + (col >> 5) * 64 + (col & 31);
-        split_x3(x, F16X3_XS, d[0], d[32]);
+        split_x3(x, xs, d[0], d[32]);
         return;
     }
     unsigned h, m, l;
@@ -105,14 +144,15 @@ __device__ __forceinline__ void store_planes1(unsigned short *yp, int C, long pi
     d[16] = (unsigned short)m;
     d[32] = (unsigned short)l;
 }
-__device__ __forceinline__ void store_planes4(unsigned short *yp, int C, long pix, int col, f32x4 v) {
+__device__ __forceinline__ void store_planes4(unsigned short *yp, int C, long pix, int col, f32x4 v,
+                                              float xs = F16X3_XS) {
     if (C < 0) {
         _Float16 *d = reinterpret_cast<_Float16 *>(yp) + pix * 2 * (-C) + (col >> 5) * 64 + (col & 31);
         f16x4_t h, l;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             _Float16 a, b;
-            split_x3(v[q], F16X3_XS, a, b);
+            split_x3(v[q], xs, a, b);
             h[q] = a;
             l[q] = b;
         }

@@ -408,6 +408,8 @@ k_splitk_reduce(const GemmArgs p, int V4) {
     }
     const long plane = (long)p.M * p.N;
     const float *base = p.slab + (long)phase * p.splits * plane;
+    const float ys = p.yp ? plane_scale(p) : 0.f;
+    float vmax = 0.f;   // max |output| of this lane (p.ymax)
     if (V4) {  // N % 4 == 0, ldc % 4 == 0, 16-byte aligned C: float4 outputs, V4 lanes per output
         const int tpo = V4;  // power of two <= 16: lane j sums slabs j, j+tpo, ...; fixed butterfly after
         const int lane = threadIdx.x & (tpo - 1);
@@ -445,8 +447,11 @@ k_splitk_reduce(const GemmArgs p, int V4) {
                 if (p.beta != 0.f) o += p.beta * (*dst);
                 *dst = o;
             }
-            if (p.yp) store_planes4(p.yp, p.ypC, pix, col, o);
+            if (p.yp) store_planes4(p.yp, p.ypC, pix, col, o, ys);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) vmax = fmaxf(vmax, fabsf(o[q]));
         }
+        if (p.ymax) block_atomic_absmax(p.ymax, vmax);
         return;
     }
     const long total = (long)Mrows * p.N;
@@ -469,8 +474,10 @@ k_splitk_reduce(const GemmArgs p, int V4) {
             if (p.beta != 0.f) v += p.beta * p.C[off + col];
             p.C[off + col] = v;
         }
-        if (p.yp) store_planes1(p.yp, p.ypC, pix, col, v);
+        if (p.yp) store_planes1(p.yp, p.ypC, pix, col, v, ys);
+        vmax = fmaxf(vmax, fabsf(v));
     }
+    if (p.ymax) block_atomic_absmax(p.ymax, vmax);
 }
 
 // -------------------------------------------------------------------------
@@ -1223,6 +1230,8 @@ struct OpPlan {
     int tlast;
     // narrow stride-1 filter gradient on row segments (k_narrow_wgrad_tile): partial blocks
     int ntile;
+    // fp16x3 input gradient: workspace offset of the max |dy| float (no scale source set)
+    size_t x3_max_off;
 };
 
 // A narrow op (GEMM N <= 8) recast as a 1x1-geometry MFMA GEMM plus a gather:
@@ -1244,6 +1253,10 @@ struct Recast {
 struct dg_conv_desc_s {
     int transpose;
     int math;                        // DG_MATH_*
+    // fp16x3 input gradient scale context (dg_conv_set_grad_scale): sources (m, g) of the dy
+    // and dx planes' scales, and where max |dx| goes (device pointers; NULL = unset)
+    const float *gs_dy_m, *gs_dy_g, *gs_dx_m, *gs_dx_g;
+    float *gs_dx_max;
     int N, H, W, Cin, Cout, Ho, Wo;  // layer view
     dg::ConvGeom g;                  // conv view
     dg::OpPlan plan[3];              // indexed by DG_OP_*
@@ -1433,9 +1446,13 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
             6.0 * rb * cb < 2.0e9 && g.kh * g.kw <= 32;
     // (an fp16x3-eligible forward -- DG_MATH_F16X3, 3x3 stride 1, Cin % 32 == 0, Cout % 16 == 0,
     // Cout > 32 -- takes the split-precision path whatever the fp32 estimate: see hx3 below)
-    const bool x3_geom = math == DG_MATH_F16X3 && mode == MODE_FWD && g.kh == 3 && g.kw == 3 && g.sh == 1 &&
-                         g.sw == 1 && g.Ci % 32 == 0 && g.Co % 16 == 0 && g.Co > 32 && !plan_off("x3") &&
-                         !plan_off("halo");
+    // (input gradient, plan_all: only where the forward runs fp16x3 -- Cout % 32 == 0 chunks the
+    // reduction over output channels, Cin % 16 == 0 and Cin > 32 the BN 64 / 128 tiles)
+    const bool x3_geom = math == DG_MATH_F16X3 && g.kh == 3 && g.kw == 3 && g.sh == 1 && g.sw == 1 &&
+                         !plan_off("x3") && !plan_off("halo") &&
+                         ((mode == MODE_FWD && g.Ci % 32 == 0 && g.Co % 16 == 0 && g.Co > 32) ||
+                          (mode == MODE_DGRAD && g.Co % 32 == 0 && g.Ci % 16 == 0 && g.Ci > 32 &&
+                           !plan_off("x3dgrad")));
     if (x6_ok) {
         OpPlan p6 = pl;
         double t6 = choose_tiles(p6, kX6Cfgs, kNumX6Cfgs, 2516.6e12 / 6.0, "DG_FORCE_X6CFG", nullptr);
@@ -1505,7 +1522,9 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         const long nch = pl.K / (bkc * ntap), blocks = (long)pl.mtiles * pl.ntiles * pl.nphase;
         long splits = 1;
         // (same-box A/B of the target: 256 -0.2%, 1024 -0.8% full step vs 512)
-        constexpr long target = 512;
+        long target = 512;
+        // (diagnostic: DG_X3_TARGET sets the fp16x3 plans' block target for same-box sweeps)
+        if (hx3 && getenv("DG_X3_TARGET")) target = atol(getenv("DG_X3_TARGET"));
         while (blocks * splits < target && splits * 4 <= nch) splits *= 2;
         const long cps = (nch + splits - 1) / splits;
         pl.kchunk = (int)(cps * bkc * ntap);
@@ -1517,10 +1536,15 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     pl.ws_bytes = pl.slab_bytes;
     if (pl.x6) {
         // workspace: [split-K slabs][A planes][B planes] (6 B per element bf16x6, 2 B fp16, 4 B fp16x3)
+        // (+ fp16x3 input gradient: a float for max |dy| when no scale source is set)
         const size_t eb = pl.x6 == 2 ? 2 : (pl.x6 == 3 ? 4 : 6);
         pl.x6_a_off = (pl.ws_bytes + 255) & ~(size_t)255;
         pl.x6_b_off = (pl.x6_a_off + eb * ra * ca + 255) & ~(size_t)255;
         pl.ws_bytes = pl.x6_b_off + eb * rb * cb;
+        if (pl.x6 == 3 && mode == MODE_DGRAD) {
+            pl.x3_max_off = (pl.ws_bytes + 255) & ~(size_t)255;
+            pl.ws_bytes = pl.x3_max_off + 256;
+        }
     }
     pl.gemm_bytes = pl.ws_bytes;
     if (getenv("DG_PLAN_DEBUG"))
@@ -1598,8 +1622,10 @@ static size_t colsum_ws(long M, int C);
 // (re)plan the three ops of a descriptor for its math mode
 static void plan_all(dg_conv_desc_s *d) {
     for (int op = 0; op < 3; ++op) {
-        // (DG_MATH_F16X3: fp16x3 for the forward of a Conv2D only; every other op bf16x6)
-        const int m = d->math == DG_MATH_F16X3 && (op != DG_OP_FWD || d->transpose) ? DG_MATH_BF16X6 : d->math;
+        // (DG_MATH_F16X3: fp16x3 for the forward of a Conv2D and, where that runs fp16x3, its
+        // input gradient; the filter gradient and transposed layers bf16x6)
+        const bool x3op = !d->transpose && (op == DG_OP_FWD || (op == DG_OP_BWD_DATA && d->plan[DG_OP_FWD].x6 == 3));
+        const int m = d->math == DG_MATH_F16X3 && !x3op ? DG_MATH_BF16X6 : d->math;
         d->plan[op] = make_plan(d->g, engine_mode(d, op), m);
         plan_recast(d, op);
         if (d->rc[op].on) d->plan[op].ws_bytes = d->rc[op].bytes;
@@ -1742,6 +1768,16 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
     DG_ARG(need == 0 || ws != nullptr, "workspace pointer is NULL");
     GemmArgs a = make_args(d->g, pl, A, lda, B, ldb, C, ldc, bias, beta, act, alpha, ws);
     a.mz = mz; a.ldmz = ldmz; a.mact = mact; a.malpha = malpha;
+    if (op == DG_OP_BWD_DATA) {
+        // the gradient scale context (dg_conv_set_grad_scale): dy planes' scale source (an
+        // fp16x3 input gradient), dx planes' scale source, max |dx|
+        if (pl.x6 == 3) { a.as_m = d->gs_dy_m; a.as_g = d->gs_dy_g; }
+        a.ys_m = d->gs_dx_m; a.ys_g = d->gs_dx_g; a.ymax = d->gs_dx_max;
+        DG_ARG(!a.ymax || pl.halo || pl.splits > 1,
+               "max |dx| is measured by the halo / split-K epilogues only (plan of this input gradient: neither)");
+        DG_ARG(yp_fmt != DG_PLANES_F16X3 || a.ys_m,
+               "fp16x3 gradient planes need a scale source (dg_conv_set_grad_scale)");
+    }
     if (po) {
         DG_ARG(op == DG_OP_FWD && pool_fusable(d, act), "this forward plan cannot fuse the max pool");
         DG_ARG(po->idx && (((uintptr_t)po->idx) & 3) == 0, "pool index buffer NULL or not 4-byte aligned");
@@ -1886,23 +1922,40 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
         a.b_bytes = (unsigned)bb;
     }
     if (pl.x6 == 3) {
-        // fp16x3 forward: activations -> fp16x3 planes in 32-channel groups, weights in
+        // fp16x3: activations / gradients -> fp16x3 planes in 32-channel groups, weights in
         // 16-column groups (common.h); a caller-held weight buffer also receives the
-        // weights' bf16x6 planes behind them (tensor_plane_bytes), read by bwd_data
+        // weights' bf16x6 planes behind them (tensor_plane_bytes).  An input gradient's dy
+        // is scaled from its bound (a.as_m / as_g: the caller's scale source, else max |dy|
+        // measured here into the workspace)
         char *ws = (char *)a.slab;
         DG_ARG(ws != nullptr, "workspace pointer is NULL");
         void *pa = ws + pl.x6_a_off, *pb = ws + pl.x6_b_off;
+        const int ldbw = (mode == MODE_DGRAD) ? a.g.Co : ldb;   // DGRAD B is the dense weight tensor
         if (pr && pr->a) pa = pr->a;
         if (pr && pr->b) pb = pr->b;
-        if (!(pr && pr->a && pr->a_ready)) {
-            launch_split_x3(A, lda, pl.x6_ra, pl.x6_ca, pa, 32, F16X3_XS, s);
+        const bool a_ready = pr && pr->a && pr->a_ready;
+        if (mode == MODE_DGRAD && !a.as_m) {
+            DG_ARG(!a_ready, "fp16x3 dy planes given without their scale source (dg_conv_set_grad_scale)");
+            float *mx = (float *)(ws + pl.x3_max_off);
+            if (hipMemsetAsync(mx, 0, X3_SHARDS * sizeof(float), s) != hipSuccess) {
+                dg::set_error("hipMemsetAsync failed");
+                return DG_ERR_HIP;
+            }
+            launch_absmax(A, pl.x6_ra, pl.x6_ca, lda, mx, s);
+            DG_LAUNCHED("absmax_dy");
+            a.as_m = mx;
+            a.as_g = nullptr;
+        }
+        if (!a_ready) {
+            if (mode == MODE_DGRAD) launch_split_x3(A, lda, pl.x6_ra, pl.x6_ca, pa, 32, 1.f, s, a.as_m, a.as_g);
+            else launch_split_x3(A, lda, pl.x6_ra, pl.x6_ca, pa, 32, F16X3_XS, s);
             DG_LAUNCHED("split_x3_a");
         }
         if (!(pr && pr->b && pr->b_ready)) {
-            launch_split_x3(B, ldb, pl.x6_rb, pl.x6_cb, pb, 16, F16X3_WS, s);
+            launch_split_x3(B, ldbw, pl.x6_rb, pl.x6_cb, pb, 16, F16X3_WS, s);
             DG_LAUNCHED("split_x3_b");
             if (pr && pr->b) {
-                launch_split3(B, ldb, pl.x6_rb, pl.x6_cb, (unsigned short *)((char *)pb + x3_w_bytes(pl)), s);
+                launch_split3(B, ldbw, pl.x6_rb, pl.x6_cb, (unsigned short *)((char *)pb + x3_w_bytes(pl)), s);
                 DG_LAUNCHED("split3_b");
             }
         }
@@ -2043,10 +2096,11 @@ static void op_tensors(const dg_conv_desc_s *d, int op, int &ta, int &tb) {
 // element, read by the forward only) and w as [fp16x3 (4 B) | bf16x6 (6 B)] planes: the
 // forward reads the first part, bwd_data the second; dy stays bf16x6.
 static bool fwd_x3(const dg_conv_desc_s *d) { return d->plan[DG_OP_FWD].x6 == 3; }
+static bool dgrad_x3(const dg_conv_desc_s *d) { return d->plan[DG_OP_BWD_DATA].x6 == 3; }
 static size_t tensor_plane_bytes(const dg_conv_desc_s *d, int t) {
     const size_t nw = (size_t)d->g.kh * d->g.kw * d->Cin * d->Cout;
     if (t == DG_TENSOR_X) return (size_t)(fwd_x3(d) ? 4 : 6) * d->N * d->H * d->W * d->Cin;
-    if (t == DG_TENSOR_DY) return (size_t)6 * d->N * d->Ho * d->Wo * d->Cout;
+    if (t == DG_TENSOR_DY) return (size_t)(dgrad_x3(d) ? 4 : 6) * d->N * d->Ho * d->Wo * d->Cout;
     return fwd_x3(d) ? x3_w_bytes(d->plan[DG_OP_FWD]) + 6 * nw : 6 * nw;
 }
 
@@ -2060,8 +2114,9 @@ static int op_plane_mask(const dg_conv_desc_s *d, int op) {
     if (pl.x6 == 2 && plan_off("f16planes")) return 0;
     int ta, tb;
     op_tensors(d, op, ta, tb);
-    // (an fp16x3 forward's x planes are not the bf16x6 planes a filter gradient reads)
-    if (op == DG_OP_BWD_FILTER && fwd_x3(d)) return (ta | tb) & ~DG_TENSOR_X;
+    // (an fp16x3 forward's x planes / an fp16x3 input gradient's dy planes are not the bf16x6
+    // planes a filter gradient reads)
+    if (op == DG_OP_BWD_FILTER) return (ta | tb) & ~(fwd_x3(d) ? DG_TENSOR_X : 0) & ~(dgrad_x3(d) ? DG_TENSOR_DY : 0);
     return ta | tb;
 }
 
@@ -2076,8 +2131,8 @@ static int plane_refs(const dg_conv_desc_s *d, int op, const dg_conv_planes_t *p
     const int mask = op_plane_mask(d, op);
     r.a = (mask & ta) ? buf(ta) : nullptr; r.b = (mask & tb) ? buf(tb) : nullptr;
     r.a_ready = (p->ready & ta) != 0; r.b_ready = (p->ready & tb) != 0;
-    // bwd_data of an fp16x3-forward descriptor: the weights' bf16x6 part of the buffer
-    if (op == DG_OP_BWD_DATA && fwd_x3(d) && r.b) r.b = (char *)r.b + x3_w_bytes(d->plan[DG_OP_FWD]);
+    // bf16x6 bwd_data of an fp16x3-forward descriptor: the weights' bf16x6 part of the buffer
+    if (op == DG_OP_BWD_DATA && fwd_x3(d) && !dgrad_x3(d) && r.b) r.b = (char *)r.b + x3_w_bytes(d->plan[DG_OP_FWD]);
     DG_ARG(((((uintptr_t)r.a) | ((uintptr_t)r.b)) & 15) == 0, "plane buffers must be 16-byte aligned");
     out = &r;
     return DG_OK;
@@ -2173,7 +2228,23 @@ int dg_conv_planes_size(dg_conv_t d, int tensor, size_t *bytes) {
 int dg_conv_planes_format(dg_conv_t d, int tensor, int *format) {
     DG_ARG(d && format, "NULL argument");
     DG_ARG(tensor == DG_TENSOR_X || tensor == DG_TENSOR_DY || tensor == DG_TENSOR_W, "bad tensor id %d", tensor);
-    *format = (tensor != DG_TENSOR_DY && dg::fwd_x3(d)) ? DG_PLANES_F16X3 : DG_PLANES_BF16X6;
+    const bool x3 = tensor == DG_TENSOR_DY ? dg::dgrad_x3(d) : dg::fwd_x3(d);
+    *format = x3 ? DG_PLANES_F16X3 : DG_PLANES_BF16X6;
+    return DG_OK;
+}
+
+int dg_absmax(const float *x, int64_t rows, int C, int ld, float *out, dg_stream_t stream) {
+    DG_ARG(x && out, "NULL tensor");
+    DG_ARG(rows >= 0 && C > 0 && ld >= C, "bad shape");
+    dg::launch_absmax(x, rows, C, ld, out, (hipStream_t)stream);
+    DG_LAUNCHED("absmax");
+    return DG_OK;
+}
+
+int dg_conv_set_grad_scale(dg_conv_t d, const float *dy_m, const float *dy_g, const float *dx_m, const float *dx_g,
+                           float *dx_max) {
+    DG_ARG(d != nullptr, "descriptor is NULL");
+    d->gs_dy_m = dy_m; d->gs_dy_g = dy_g; d->gs_dx_m = dx_m; d->gs_dx_g = dx_g; d->gs_dx_max = dx_max;
     return DG_OK;
 }
 

@@ -150,7 +150,7 @@ k_co1_dgrad(const GemmArgs p) {
                 for (int u = 0; u < 4; ++u) o[u] = dst[u] = p.beta != 0.f ? o[u] + p.beta * dst[u] : o[u];
             }
         }
-        if (p.yp) store_planes4(p.yp, p.ypC, pix, c, o);
+        if (p.yp) store_planes4(p.yp, p.ypC, pix, c, o, plane_scale(p));
     }
 }
 

@@ -44,6 +44,10 @@ struct GemmArgs {
     // of the first maximum (row-major), bit 2 set when the pooled value > 0.
     // C (the full-size output) is not written.
     unsigned char *pidx; float *pool_y; int ldpy;
+    // fp16x3 input gradients (DG_MATH_F16X3 bwd_data, x3_grad_scale): the scale sources
+    // (m, g) of the A (dy) planes and of the output (dx) planes; ymax receives max |output|
+    const float *as_m, *as_g, *ys_m, *ys_g;
+    float *ymax;
     // optional gradient mask from the planes of the activation output instead of
     // its fp32 values (dg_conv_bwd_data_xmask): act' of a sign-determined
     // activation from the sign of the hi plane, [pixel][3 mzpC] (mzpC < 0: fp16x3)
@@ -69,6 +73,11 @@ __device__ __forceinline__ f32x4 hi_plane4(const unsigned short *zp, int C, long
     const u32x2_t h = *reinterpret_cast<const u32x2_t *>(zp + pix * 3 * C + (col >> 4) * 48 + (col & 15));
     return f32x4{__uint_as_float(h[0] << 16), __uint_as_float(h[0] & 0xffff0000u), __uint_as_float(h[1] << 16),
                  __uint_as_float(h[1] & 0xffff0000u)};
+}
+
+// the fp16x3 scale of the output planes (static activation scale unless a gradient source is set)
+__device__ __forceinline__ float plane_scale(const GemmArgs &p) {
+    return p.ys_m ? x3_grad_scale(p.ys_m, p.ys_g) : F16X3_XS;
 }
 
 __device__ __forceinline__ float epi_mask(const GemmArgs &p, long pix, int col, float v) {
@@ -180,7 +189,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs &p, f32x16 (&acc)[T
                         if (p.beta != 0.f) v += p.beta * p.C[off + col];
                         p.C[off + col] = v;
                     }
-                    if (p.yp) store_planes1(p.yp, p.ypC, pix, col, v);
+                    if (p.yp) store_planes1(p.yp, p.ypC, pix, col, v, plane_scale(p));
                 }
             }
         }
@@ -214,6 +223,8 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
     const int c4 = lane % C4;
     const int col = cbase + c4 * 4;
     const bool full = col + 3 < p.N;
+    const float ys = p.yp ? plane_scale(p) : 0.f;
+    float vmax = 0.f;   // max |output| of this lane (p.ymax)
 #pragma clang loop unroll(full)
     for (int a = 0; a < TM; ++a) {
 #pragma unroll
@@ -280,15 +291,21 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
             }
             if (p.yp) {
                 if (full) {
-                    store_planes4(p.yp, p.ypC, pix, col, o);
+                    store_planes4(p.yp, p.ypC, pix, col, o, ys);
                 } else {
 #pragma unroll
                     for (int q = 0; q < 4; ++q)
-                        if (col + q < p.N) store_planes1(p.yp, p.ypC, pix, col + q, o[q]);
+                        if (col + q < p.N) store_planes1(p.yp, p.ypC, pix, col + q, o[q], ys);
                 }
+            }
+            if (p.ymax) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (col + q < p.N) vmax = fmaxf(vmax, fabsf(o[q]));
             }
         }
     }
+    if (p.ymax) block_atomic_absmax(p.ymax, vmax);
 }
 
 // launcher of the bf16x6 kernels (conv_x6.hip); cfg indexes kX6Cfgs
@@ -303,7 +320,11 @@ void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int
 void launch_split3(const float *src, int ld, long rows, int C, unsigned short *dst, hipStream_t s);
 // fp32 [rows][ld] -> fp16x3 planes (common.h): per group of G columns (32: activations,
 // 16: weights) h[G] l[G] of scale * value; C % G == 0
-void launch_split_x3(const float *src, int ld, long rows, int C, void *dst, int group, float scale, hipStream_t s);
+// (sm != NULL: a gradient operand, scale = x3_grad_scale(sm, sg) instead of `scale`)
+void launch_split_x3(const float *src, int ld, long rows, int C, void *dst, int group, float scale, hipStream_t s,
+                     const float *sm = nullptr, const float *sg = nullptr);
+// max |x| of [rows][ld] (first C columns) into *out by atomicMax (zeroed by the caller)
+void launch_absmax(const float *x, long rows, int C, int ld, float *out, hipStream_t s);
 // the fp16 conv math (DG_MATH_FP16): one fp16 plane [rows][C] and its GEMM (kF16Cfgs)
 void launch_split_f16(const float *src, int ld, long rows, int C, void *dst, hipStream_t s);
 void launch_split_f16_pair(const float *a, int lda, long ra, int ca, void *da, const float *b, int ldb, long rb,

@@ -151,7 +151,7 @@ __device__ __forceinline__ void small_fwd_epilogue(const GemmArgs &p, const f32x
 #pragma unroll
             for (int q = 0; q < 4; ++q) dst[q] = o[q];
         }
-        if (p.yp) store_planes4(p.yp, p.ypC, pix, col, o);
+        if (p.yp) store_planes4(p.yp, p.ypC, pix, col, o, plane_scale(p));
     }
 }
 

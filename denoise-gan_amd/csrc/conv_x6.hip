@@ -528,7 +528,9 @@ void launch_split3(const float *src, int ld, long rows, int C, unsigned short *d
 // columns) -> per group of G columns h[G] l[G] of scale * value, 8 columns per lane
 template <int G>
 __global__ void __launch_bounds__(256)
-k_split_x3(const float *__restrict__ src, int ld, long rows, int C, float scale, _Float16 *__restrict__ dst) {
+k_split_x3(const float *__restrict__ src, int ld, long rows, int C, float scale, const float *sm, const float *sg,
+           _Float16 *__restrict__ dst) {
+    if (sm) scale = x3_grad_scale(sm, sg);   // a gradient operand: scale from its bound
     const int C8 = C >> 3;
     const long total = rows * C8;
     const bool vec = ((ld & 3) == 0) && ((((uintptr_t)src) & 15) == 0);
@@ -559,14 +561,35 @@ k_split_x3(const float *__restrict__ src, int ld, long rows, int C, float scale,
     }
 }
 
-void launch_split_x3(const float *src, int ld, long rows, int C, void *dst, int group, float scale, hipStream_t s) {
+void launch_split_x3(const float *src, int ld, long rows, int C, void *dst, int group, float scale, hipStream_t s,
+                     const float *sm, const float *sg) {
     const long total = rows * (C / 8);
     if (total == 0) return;
     const unsigned blocks = (unsigned)std::min<long>((total + 255) / 256, 8192);
     if (group == 32)
-        hipLaunchKernelGGL(k_split_x3<32>, dim3(blocks), dim3(256), 0, s, src, ld, rows, C, scale, (_Float16 *)dst);
+        hipLaunchKernelGGL(k_split_x3<32>, dim3(blocks), dim3(256), 0, s, src, ld, rows, C, scale, sm, sg,
+                           (_Float16 *)dst);
     else
-        hipLaunchKernelGGL(k_split_x3<16>, dim3(blocks), dim3(256), 0, s, src, ld, rows, C, scale, (_Float16 *)dst);
+        hipLaunchKernelGGL(k_split_x3<16>, dim3(blocks), dim3(256), 0, s, src, ld, rows, C, scale, sm, sg,
+                           (_Float16 *)dst);
+}
+
+// max |x| over [rows][ld] (first C columns) into *out (atomicMax; the caller zeroes it)
+__global__ void __launch_bounds__(256) k_absmax(const float *__restrict__ x, long rows, int C, int ld, float *out) {
+    float m = 0.f;
+    const long total = rows * C;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+        const long r = e / C;
+        m = fmaxf(m, fabsf(x[r * ld + (e - r * C)]));
+    }
+    block_atomic_absmax(out, m);
+}
+
+void launch_absmax(const float *x, long rows, int C, int ld, float *out, hipStream_t s) {
+    const long total = rows * C;
+    if (total == 0) return;
+    const unsigned blocks = (unsigned)std::min<long>((total + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_absmax, dim3(blocks), dim3(256), 0, s, x, rows, C, ld, out);
 }
 
 // both operands of one fp16 GEMM in one launch (blocks [0, nba) convert A, the rest B):

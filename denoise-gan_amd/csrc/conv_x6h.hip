@@ -141,7 +141,7 @@ __device__ __forceinline__ void conv_epilogue16_pool(const GemmArgs &p, f32x4 (&
             const long pp = ((long)nimg * Ho2 + ho2) * Wo2 + wo2;
             *reinterpret_cast<unsigned *>(p.pidx + pp * p.N + col) = fi;
             if (p.pool_y) *reinterpret_cast<f32x4 *>(p.pool_y + pp * p.ldpy + col) = fv;
-            if (p.yp) store_planes4(p.yp, p.ypC, pp, col, fv);
+            if (p.yp) store_planes4(p.yp, p.ypC, pp, col, fv, plane_scale(p));
         }
     }
 }
@@ -168,8 +168,8 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     static_assert(!POOL || MODE == MODE_FWD, "the pool epilogue is a forward epilogue");
     static_assert(KT == 3 || (KT != 3 && MODE == MODE_DGRAD),
                   "3x3 stride 1, or a stride-1 4x4 / stride-2 4x4-phase input gradient");
-    static_assert(NI == 3 || (NI == 2 && KT == 3 && !POOL) || (NI == 4 && KT == 3 && MODE == MODE_FWD),
-                  "fp16: 3x3 stride 1, no pool epilogue; fp16x3: 3x3 stride-1 forward");
+    static_assert(NI == 3 || (NI == 2 && KT == 3 && !POOL) || (NI == 4 && KT == 3),
+                  "fp16: 3x3 stride 1, no pool epilogue; fp16x3: 3x3 stride 1");
     constexpr bool X3 = NI == 4;
     constexpr int NPL = NI == 3 ? 3 : (X3 ? 4 : 2);   // plane images per chunk
     using HG = HaloGeom<KT, NPL, X3>;
@@ -330,7 +330,9 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
             const int r = pos >> 5, c = (pos >> 4) & 1;
             const int ci = n0 + r;
             bok[j] = ci < p.N;
-            bbase[j] = (ci * (NI == 3 ? 3 * p.ldb : p.ldb) + 16 * plane + 8 * c) * 2;
+            if constexpr (X3)   // image = piece plane>>1 of co 16 (plane&1) .. of the chunk
+                bbase[j] = (ci * (2 * p.ldb) + 32 * (plane & 1) + 16 * (plane >> 1) + 8 * c) * 2;
+            else bbase[j] = (ci * (NI == 3 ? 3 * p.ldb : p.ldb) + 16 * plane + 8 * c) * 2;
         }
     }
     // tap position T of chunk c: FWD rows (tap*Ci + 16c) of w[(a,b,ci)][co];
@@ -339,7 +341,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         int delta;
         constexpr int LW = NI == 3 ? 3 : (X3 ? 2 : 1);   // weight row stride in units of ldb
         if constexpr (!B_KC) delta = ((tap_w[T] * g.Ci + chunk * BK) * (LW * p.ldb)) * 2;
-        else delta = (tap_w[T] * g.Ci * (LW * p.ldb) + chunk * (NI == 3 ? 48 : 32)) * 2;
+        else delta = (tap_w[T] * g.Ci * (LW * p.ldb) + chunk * (NI == 3 ? 48 : (X3 ? 64 : 32))) * 2;
 #pragma unroll
         for (int j = 0; j < B_NJ; ++j) {
             dma(rB, bs + bdst[j], bok[j] ? (unsigned)(bbase[j] + delta) : DG_OOB);
@@ -396,7 +398,10 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
             const int c0 = wn * WTN + b * 16;
-            if constexpr (X3) {
+            if constexpr (X3 && B_KC) {
+                b1[b] = x6_kc_frag(B0, B1, c0, lane);        // [w_h0|w_h1] (co halves of the chunk)
+                b3[b] = x6_kc_frag(B2, B3, c0, lane);        // [w_l0|w_l1]
+            } else if constexpr (X3) {
                 b1[b] = x6_rc_frag<BN>(B0, B1, c0, lane);   // [w_h0|w_h1]
                 b3[b] = x6_rc_frag<BN>(B2, B3, c0, lane);   // [w_l0|w_l1]
             } else if constexpr (B_KC) {
@@ -502,11 +507,13 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
 
     constexpr int STAGE = 16 * (WTN + 4);
     static_assert(NW * STAGE * 4 <= 2 * HG::BYTES, "epilogue staging fits in the halo buffers");
-    if constexpr (X3) {   // undo the operand scales (a power of two: exact)
+    if constexpr (X3) {   // undo the operand scales (powers of two: exact)
+        const float osc = MODE == MODE_FWD || !p.as_m ? F16X3_OSCALE
+                                                      : 1.f / (x3_grad_scale(p.as_m, p.as_g) * F16X3_WS);
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
-            for (int b = 0; b < TN; ++b) acc[a][b] *= F16X3_OSCALE;
+            for (int b = 0; b < TN; ++b) acc[a][b] *= osc;
     }
     float *stage = reinterpret_cast<float *>(hal0) + wid * STAGE;
     // patch row -> output pixel; slab rows: FWD / stride-1 DGRAD pixels, a
@@ -536,7 +543,10 @@ void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int
 #define DG_X3H(B_, P_) hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_FWD, B_, P_, 3, 4>), grid, blk, 0, s, a, tiles_x, tiles_y)
     // (bn 32: the SR discriminators' / FastSRGAN's 32-channel 3x3 layers, stride 1; a
     // 64-wide tile computes half zeros there)
-    if (ni == 4) {   // fp16x3 forward (bn 64 | 128), optionally with the fused pool
+    if (ni == 4 && mode == MODE_DGRAD) {   // fp16x3 input gradient (3x3 stride 1, bn 64 | 128)
+        if (bn == 128) hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_DGRAD, 128, false, 3, 4>), grid, blk, 0, s, a, tiles_x, tiles_y);
+        else hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_DGRAD, 64, false, 3, 4>), grid, blk, 0, s, a, tiles_x, tiles_y);
+    } else if (ni == 4) {   // fp16x3 forward (bn 64 | 128), optionally with the fused pool
         if (a.pidx) {
             if (bn == 128) DG_X3H(128, true);
             else DG_X3H(64, true);

@@ -414,9 +414,12 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd4(int N, int H, int W, int C
 // dy * act'(pooled) at the first maximum, 0 at the other three positions.
 // dx (fp32) may be NULL when only its planes are consumed (a conv's backward
 // on bf16x6 planes).
+// (dxpC: C, or -C for the fp16x3 dy planes of an fp16x3 input gradient, scaled from (sm, sg))
 __global__ void __launch_bounds__(256) k_maxpool_bwd_idx4(int N, int H, int W, int C, const unsigned char *idx,
                                                          const float *dy, int lddy, float *dx, int lddx, float beta,
-                                                         float neg, unsigned short *dxp) {
+                                                         float neg, unsigned short *dxp, int dxpC, const float *sm,
+                                                         const float *sg) {
+    const float xs = sm ? x3_grad_scale(sm, sg) : F16X3_XS;
     const int Ho = H / 2, Wo = W / 2, C4 = C >> 2;
     const int total = N * Ho * Wo * C4;
     for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
@@ -440,7 +443,7 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd_idx4(int N, int H, int W, i
                 if (beta != 0.f) g += beta * *o;
                 *o = g;
             }
-            if (dxp) store_planes4(dxp, C, pp[q], c, g);
+            if (dxp) store_planes4(dxp, dxpC, pp[q], c, g, xs);
         }
     }
 }
@@ -1006,7 +1009,15 @@ int dg_maxpool2_bwd(int N, int H, int W, int C, const float *x, int ldx, const f
 
 int dg_maxpool2_bwd_idx(int N, int H, int W, int C, const unsigned char *idx, const float *dy, int lddy,
                         float *dx, int lddx, float beta, int act, float alpha, void *dx_planes, dg_stream_t stream) {
+    return dg_maxpool2_bwd_idx_x3(N, H, W, C, idx, dy, lddy, dx, lddx, beta, act, alpha, dx_planes, nullptr, nullptr,
+                                  stream);
+}
+
+int dg_maxpool2_bwd_idx_x3(int N, int H, int W, int C, const unsigned char *idx, const float *dy, int lddy,
+                           float *dx, int lddx, float beta, int act, float alpha, void *dx_planes,
+                           const float *scale_m, const float *scale_g, dg_stream_t stream) {
     DG_ARG(idx && dy && (dx || dx_planes), "NULL tensor");
+    DG_ARG(!scale_m || C % 32 == 0, "fp16x3 gradient planes need C %% 32 == 0");
     DG_ARG(N > 0 && H >= 2 && W >= 2 && H % 2 == 0 && W % 2 == 0 && C > 0 && C % 16 == 0, "bad shape");
     DG_ARG(lddy >= C && lddy % 4 == 0 && (((uintptr_t)dy) & 15) == 0 && (((uintptr_t)idx) & 3) == 0,
            "dy needs a float4-aligned layout, idx 4-byte alignment");
@@ -1018,7 +1029,8 @@ int dg_maxpool2_bwd_idx(int N, int H, int W, int C, const unsigned char *idx, co
     const float neg = act == DG_ACT_RELU ? 0.f : (act == DG_ACT_LRELU ? alpha : 1.f);
     const long total = (long)N * (H / 2) * (W / 2) * C;
     hipLaunchKernelGGL(dg::k_maxpool_bwd_idx4, dim3(dg::lgrid(total / 4)), dim3(256), 0, (hipStream_t)stream, N, H, W,
-                       C, idx, dy, lddy, dx, lddx, beta, neg, (unsigned short *)dx_planes);
+                       C, idx, dy, lddy, dx, lddx, beta, neg, (unsigned short *)dx_planes, scale_m ? -C : C, scale_m,
+                       scale_g);
     DG_LAUNCHED("maxpool_bwd_idx");
     return DG_OK;
 }

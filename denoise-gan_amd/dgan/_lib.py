@@ -106,6 +106,10 @@ _SIGS = {
     "dg_conv_fwd_pool": (c_int, [c_void_p, _P, c_int, _P, _P, c_int, c_float, _P, c_int, _P, _P, _P, c_size_t, _P]),
     "dg_maxpool2_bwd_idx": (c_int, [c_int, c_int, c_int, c_int, _P, _P, c_int, _P, c_int, c_float, c_int, c_float, _P,
                                     _P]),
+    "dg_maxpool2_bwd_idx_x3": (c_int, [c_int, c_int, c_int, c_int, _P, _P, c_int, _P, c_int, c_float, c_int, c_float,
+                                       _P, _P, _P, _P]),
+    "dg_conv_set_grad_scale": (c_int, [c_void_p, _P, _P, _P, _P, _P]),
+    "dg_absmax": (c_int, [_P, ctypes.c_int64, c_int, c_int, _P, _P]),
     "dg_upsample2_relu_fwd": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P]),
     "dg_upsample2_relu_bwd": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, c_float, _P]),
     "dg_dwconv3_workspace_size": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_size_t)]),

@@ -432,7 +432,7 @@ class GraphPlan:
                 if (dn.plane_mask[ops.OP_BWD_DATA] | dn.plane_mask[ops.OP_BWD_FILTER]) & ops.TENSOR_DY and x6(dn):
                     for k in range(slots):
                         pn = self.cplanes[k][n.idx]
-                        pn.dy = ops.PlaneBuf(dn.plane_bytes(ops.TENSOR_DY), device)
+                        pn.dy = ops.PlaneBuf(dn.plane_bytes(ops.TENSOR_DY), device, dn.plane_format(ops.TENSOR_DY))
                         self.pool_gout[k][m.idx] = pn.dy
                     self.fed_dy.add(n.idx)
         for n in (conv_nodes if feed else []):
@@ -453,7 +453,7 @@ class GraphPlan:
             if train and (dn.plane_mask[ops.OP_BWD_DATA] | dn.plane_mask[ops.OP_BWD_FILTER]) & ops.TENSOR_DY:
                 for k in range(slots):
                     pn = self.cplanes[k][n.idx]
-                    pn.dy = ops.PlaneBuf(dn.plane_bytes(ops.TENSOR_DY), device)
+                    pn.dy = ops.PlaneBuf(dn.plane_bytes(ops.TENSOR_DY), device, dn.plane_format(ops.TENSOR_DY))
                     self.cplanes[k][c.idx].bwd_out = pn.dy
                 self.fed_dy.add(n.idx)
         # ---- fp16 operand copies written by their producers (mixed_float16) ----
@@ -533,6 +533,54 @@ class GraphPlan:
                 c = cons[t.id][0]
                 if c.kind == "conv" and all(self.cplanes[k][n.idx].fwd_out is not None for k in range(slots)):
                     self.nofp32.add(n.idx)
+        # ---- fp16x3 input gradients (DG_MATH_F16X3: VGG19's backward) ----
+        # a gradient has no static range: each fp16x3 dy is scaled from a bound of its max
+        # (include/dgan.h dg_conv_set_grad_scale).  Per conv a device max slot gmax (max |dy|
+        # of that conv, written by atomicMax by the op that produces it) and a weight bound
+        # gwb (max_ci sum |w|, recomputed when the frozen weights change).  A conv's dy planes
+        # written by its consumer conv c are scaled from (gmax[c], gwb[c]) (|dy| <= that
+        # product); written by a pool's backward or split from the fp32 graph-output gradient,
+        # from their measured max gmax[itself].
+        self.x3_top = None
+        x3g = [n for n in conv_nodes if train and self.desc[n.idx].plane_format(ops.TENSOR_DY) == ops.PLANES_F16X3]
+        if x3g:
+            slot_of = {n.idx: i for i, n in enumerate(conv_nodes)}
+            self.gmax = torch.zeros(len(conv_nodes), 8, dtype=torch.float32, device=device)   # 8 atomic shards
+            self.gwb = torch.zeros(len(conv_nodes), dtype=torch.float32, device=device)
+            self._gwb_ver = None
+            self.x3_convs = [n for n in x3g]
+            gm = lambda n: self.gmax[slot_of[n.idx]]                      # noqa: E731
+            gw = lambda n: self.gwb[slot_of[n.idx]:slot_of[n.idx] + 1]    # noqa: E731
+            self.pool_gscale = {}   # fused maxpool node idx -> scale source of the dy planes it writes
+
+            def producer_conv(t):
+                """The conv whose output is t, directly or through one 2x2 max pool."""
+                nd = t.node
+                if nd.kind == "maxpool":
+                    nd = nd.ins[0].node
+                return nd if nd.kind == "conv" else None
+
+            for n in x3g:
+                d = self.desc[n.idx]
+                cs = cons[n.out.id]
+                if n.out.id == graph.output.id:
+                    src = (gm(n), None)   # the caller's fp32 gradient: max measured in backward()
+                    self.x3_top = n
+                elif len(cs) == 1 and cs[0].kind == "conv" and n.idx in self.fed_dy:
+                    src = (gm(cs[0]), gw(cs[0]))
+                elif len(cs) == 1 and cs[0].kind == "maxpool":
+                    src = (gm(n), None)   # the pool's input gradient: max written by the pool's consumer
+                    if cs[0].idx in self.fused_pool:
+                        self.pool_gscale[cs[0].idx] = src
+                    else:   # (an unfused pool's backward writes fp32 only; the conv splits it)
+                        for k in range(slots):
+                            self.pool_gout[k].pop(cs[0].idx, None)
+                        self.fed_dy.discard(n.idx)
+                else:
+                    raise ValueError(f"{n.name}: fp16x3 input gradient without a scale source")
+                p = producer_conv(n.ins[0])
+                d.set_grad_scale(dy_m=src[0], dy_g=src[1], dx_m=gm(n), dx_g=gw(n),
+                                 dx_max=gm(p) if p is not None else None)
         # ---- workspace ----
         ws = [0]
         for n in nodes[1:]:
@@ -718,6 +766,13 @@ class GraphPlan:
         return s[g.output.id]
 
     # --------------------------------------------------------------- backward
+    def _update_weight_bounds(self):
+        """gwb[conv] = max over input channels of sum |w| over taps and output channels
+        (a bound of |dx| / max |dy| of the layer's input gradient)."""
+        for i, n in enumerate(m for m in self.g.nodes if m.kind == "conv"):
+            w = self.arena.param(f"{n.name}/kernel")   # HWIO
+            self.gwb[i:i + 1].copy_(w.abs().sum(dim=(0, 1, 3)).amax().reshape(1))
+
     def _scratch(self, shape):
         N, H, W, C = shape
         ld = _ld(C)
@@ -735,6 +790,16 @@ class GraphPlan:
         s = self.slots[slot]
         gr = dict(self.grad)
         gr[g.output.id] = dout
+        if getattr(self, "x3_convs", None):
+            # fp16x3 input gradients: weight bounds (frozen weights: once per version), the
+            # per-step max slots, and the measured max of the gradient entering the graph
+            if not getattr(A, "frozen", False) or self._gwb_ver != A.version:   # (trainable: every step)
+                self._update_weight_bounds()
+                self._gwb_ver = A.version
+            self.gmax.zero_()
+            if self.x3_top is not None:
+                i = [n.idx for n in g.nodes if n.kind == "conv"].index(self.x3_top.idx)
+                ops.absmax(dout, self.gmax[i])
         gin = g.input.id
         if input_grad is not None:
             gr[gin] = input_grad
@@ -840,7 +905,8 @@ class GraphPlan:
                     _, H, W, C = self.shape[t_in.id]
                     ops.maxpool2_bwd_idx(self.pool_idx[slot][n.idx], dz, gr[t_in.id] if keep else None, C, H, W,
                                          beta=b, act=pa["act"] if t_in.id in self.premask else "none",
-                                         alpha=pa["alpha"], planes_out=gout)
+                                         alpha=pa["alpha"], planes_out=gout,
+                                         scale=getattr(self, "pool_gscale", {}).get(n.idx))
             elif k == "maxpool":
                 if need(t_in):
                     pa = t_in.node.attrs if t_in.id in self.premask else {"act": "none", "alpha": 0.0}

@@ -274,6 +274,16 @@ class ConvDesc:
         call("dg_conv_planes_size", self._h, tensor, ctypes.byref(n))
         return n.value
 
+    def set_grad_scale(self, dy_m=None, dy_g=None, dx_m=None, dx_g=None, dx_max=None):
+        """The fp16x3 input-gradient scale context (include/dgan.h dg_conv_set_grad_scale):
+        device floats (views that stay alive with the plan; the measured maxima dy_m, dx_m and
+        dx_max 8 floats each), None = unset."""
+        for t in (dy_m, dx_m, dx_max):
+            if t is not None and t.numel() < 8:
+                raise DGError("a measured gradient max is 8 floats (per-workgroup shards)")
+        self._gs = (dy_m, dy_g, dx_m, dx_g, dx_max)   # (keeps the views referenced)
+        call("dg_conv_set_grad_scale", self._h, _p(dy_m), _p(dy_g), _p(dx_m), _p(dx_g), _p(dx_max))
+
     def plane_format(self, tensor):
         """PLANES_F16X3 for the x / w planes of a descriptor whose forward runs fp16x3."""
         f = ctypes.c_int()
@@ -745,16 +755,31 @@ def maxpool2_bwd(x, dy, dx, beta=0.0, act="none", alpha=0.3, planes_out=None):
     return dx
 
 
-def maxpool2_bwd_idx(idx, dy, dx, C, H, W, beta=0.0, act="none", alpha=0.3, planes_out=None):
+def maxpool2_bwd_idx(idx, dy, dx, C, H, W, beta=0.0, act="none", alpha=0.3, planes_out=None, scale=None):
     """Backward of a pool fused by ConvDesc.fwd_pool: dx [N,H,W,C] (may be None
-    when planes_out, the producing conv's dy PlaneBuf, is all that is read)."""
+    when planes_out, the producing conv's dy PlaneBuf, is all that is read).  scale:
+    (m, g) device scalars (g may be None) -- the scale source of fp16x3 dy planes
+    (include/dgan.h dg_conv_set_grad_scale); planes_out must then be an fp16x3 buffer."""
     N = dy.shape[0]
-    call("dg_maxpool2_bwd_idx", N, H, W, C, _p(idx), _p(dy), pix_ld(dy, C), _p(dx),
+    sm, sg = scale if scale is not None else (None, None)
+    if planes_out is not None and planes_out.fmt == PLANES_F16X3 and sm is None:
+        raise DGError("fp16x3 gradient planes need a scale source")
+    call("dg_maxpool2_bwd_idx_x3", N, H, W, C, _p(idx), _p(dy), pix_ld(dy, C), _p(dx),
          pix_ld(dx, C) if dx is not None else 0, float(beta), act_id(act), float(alpha),
-         None if planes_out is None else _p(planes_out.buf), _stream())
+         None if planes_out is None else _p(planes_out.buf), _p(sm), _p(sg), _stream())
     if planes_out is not None:
         planes_out.ready = True
     return dx
+
+
+def absmax(t, out):
+    """out (8 device floats, zeroed by the caller; the max is their max) = max(out, max |t|)
+    (dg_absmax)."""
+    if out.numel() < 8:
+        raise DGError("absmax needs 8 floats (per-workgroup shards)")
+    C = t.shape[-1]
+    call("dg_absmax", _p(t), _rows(t), C, pix_ld(t, C), _p(out), _stream())
+    return out
 
 
 def upsample2_relu_fwd(x, z):

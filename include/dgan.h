@@ -151,6 +151,23 @@ int dg_conv_planes_size(dg_conv_t d, int tensor, size_t *bytes);
 /* DG_PLANES_F16X3 for the x / w planes of a descriptor whose forward runs fp16x3
  * (DG_MATH_F16X3), else DG_PLANES_BF16X6 */
 int dg_conv_planes_format(dg_conv_t d, int tensor, int *format);
+/* fp16x3 input gradients (DG_MATH_F16X3 bwd_data of a layer whose forward runs fp16x3;
+ * VGG19's backward, pix2pix.py:45-51): a gradient has no static range, so its fp16x3 planes
+ * are scaled by 2^(14 - e), bound = m * *g < 2^e (g NULL = 1) -- m a measured max |value|
+ * kept as 8 floats (per-workgroup shards of the atomics; m = their max), g a weight bound
+ * max_ci sum_{taps, co} |w| -- which keeps every scaled value below 2^14.
+ * dy_m / dy_g: the source of the dy planes' scale (the producer's: dx_m / dx_g of the
+ * consuming layer, or dg_maxpool2_bwd_idx_x3's); NULL dy_m: bwd_data measures max |dy| of
+ * its fp32 dy itself (dy planes must then not be ready).  dx_m / dx_g: the source of the
+ * scale of the dx planes this op writes (planes->out with out_format DG_PLANES_F16X3),
+ * normally (max |dy| of this layer, its weight bound).  dx_max: 8 floats receiving max |dx|
+ * by atomicMax (the caller zeroes them per step).  All device pointers, kept by the descriptor. */
+int dg_conv_set_grad_scale(dg_conv_t d, const float *dy_m, const float *dy_g, const float *dx_m, const float *dx_g,
+                           float *dx_max);
+/* max |x| over [rows][ld] (first C columns) into out[0..7] by atomicMax (the caller zeroes
+ * them; the max is their max): the measured max of a gradient entering an fp16x3 input
+ * gradient from fp32 */
+int dg_absmax(const float *x, int64_t rows, int C, int ld, float *out, dg_stream_t stream);
 int dg_conv_op_planes(dg_conv_t d, int op, int *tensors);
 int dg_conv_fwd_pl(dg_conv_t d, const float *x, int ldx, const float *w, const float *bias,
                    float *y, int ldy, float beta, int act, float alpha,
@@ -416,6 +433,11 @@ int dg_maxpool2_bwd_pl(int N, int H, int W, int C, const float *x, int ldx, cons
  * bf16x6 planes (dx_planes) are consumed */
 int dg_maxpool2_bwd_idx(int N, int H, int W, int C, const unsigned char *idx, const float *dy, int lddy,
                         float *dx, int lddx, float beta, int act, float alpha, void *dx_planes, dg_stream_t stream);
+/* the same writing the fp16x3 dy planes of an fp16x3 input gradient (C % 32 == 0), scaled
+ * from (scale_m, scale_g) as dg_conv_set_grad_scale describes (NULL scale_m: bf16x6 planes) */
+int dg_maxpool2_bwd_idx_x3(int N, int H, int W, int C, const unsigned char *idx, const float *dy, int lddy,
+                           float *dx, int lddx, float beta, int act, float alpha, void *dx_planes,
+                           const float *scale_m, const float *scale_g, dg_stream_t stream);
 /* UpSampling2D(2, 'nearest') + relu (autoencoder.py:117-131): [N,H,W,C] -> [N,2H,2W,C] */
 int dg_upsample2_relu_fwd(int N, int H, int W, int C, const float *x, int ldx, float *z, int ldz,
                           dg_stream_t stream);

@@ -182,3 +182,48 @@ def test_vgg_content_loss_x3_vs_bf16x6():
     assert abs(float(v0) - float(v1)) <= 1e-6 * abs(float(v1))
     assert float((g0 - g1).norm()) <= 1e-4 * float(g1.norm())
     assert float((g0 - g1).abs().max()) <= 1e-4 * float(g1.abs().max())
+
+
+@gpu
+def test_x3_input_gradient_chain_with_scale_context():
+    """Two fp16x3 layers (A -> relu -> B): B's input gradient writes A's fp16x3 dy planes
+    scaled from (max |dy_B|, B's weight bound) and measures max |dy_A| by atomicMax; A's
+    input gradient reads them with the same scale source.  Against torch fp64 at the conv
+    engine's bar (two layers deep: K of both), and max |dy_A| equals the fp32 dy_A's."""
+    from torch_ref import conv2d_ref
+    N, H, W, C0, C1, C2 = 2, 16, 32, 64, 64, 128
+    a = ops.ConvDesc(N, H, W, C0, C1, 3, 1, "same", math="f16x3")
+    b = ops.ConvDesc(N, H, W, C1, C2, 3, 1, "same", math="f16x3")
+    for d in (a, b):
+        assert d.plane_format(ops.TENSOR_DY) == ops.PLANES_F16X3
+    x64 = torch.randn(N, H, W, C0, dtype=torch.float64)
+    wa64 = torch.randn(*a.weight_shape, dtype=torch.float64) * 0.05
+    wb64 = torch.randn(*b.weight_shape, dtype=torch.float64) * 0.05
+    dy64 = torch.randn(N, H, W, C2, dtype=torch.float64) * 1e-7   # a small gradient (no static range)
+    dev = torch.device("cuda")
+    x, wa, wb, dy = (t.float().to(dev) for t in (x64, wa64, wb64, dy64))
+    zA = torch.empty(N, H, W, C1, device=dev)
+    a.fwd(x, wa, zA, act="relu")
+    # the reference takes the GPU's relu decisions (an fp32 / fp64 near-tie would route differently)
+    mask = (zA > 0).double().cpu()
+    xr = x64.clone().requires_grad_()
+    za = conv2d_ref(xr, wa64, 1, a.pads, None) * mask
+    yb = conv2d_ref(za, wb64, 1, b.pads, None)
+    yb.backward(dy64)
+    gmax = torch.zeros(2, 8, device=dev)   # [A, B] x 8 atomic shards
+    gwb = torch.stack([wa.abs().sum(dim=(0, 1, 3)).amax(), wb.abs().sum(dim=(0, 1, 3)).amax()])
+    b.set_grad_scale(dy_m=gmax[1], dx_m=gmax[1], dx_g=gwb[1:2], dx_max=gmax[0])
+    a.set_grad_scale(dy_m=gmax[1], dy_g=gwb[1:2])
+    ops.absmax(dy, gmax[1])
+    Pb, Pa = ops.ConvPlanes(), ops.ConvPlanes.for_desc(a, dy=True)
+    assert Pa.dy.fmt == ops.PLANES_F16X3
+    Pb.bwd_out = Pa.dy
+    dzA = torch.empty(N, H, W, C1, device=dev)
+    b.bwd_data_masked(dy, wb, dzA, zA, "relu", planes=Pb)        # writes A's dy planes
+    assert Pa.dy.ready
+    dx = torch.empty(N, H, W, C0, device=dev)
+    a.bwd_data(dzA, wa, dx, planes=Pa)                            # reads them
+    torch.cuda.synchronize()
+    assert float(gmax[0].max()) == float(dzA.abs().max())
+    assert float(gmax[1].max()) == float(dy.abs().max())
+    _close(dx, xr.grad, 2 * 9 * max(C1, C2), "chain dx")
