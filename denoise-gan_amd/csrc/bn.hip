@@ -24,8 +24,8 @@ struct BnPlan {
 
 static BnPlan bn_plan(long M, int C) {
     // row chunks of >= 64 rows, at most 256 (measured: more, shorter chunks
-    // slow the partial passes down); the finalize kernels spread a channel's
-    // R partials over 32 lanes
+    // slow the partial passes down); the finalize kernels hold a channel's
+    // R partials in the registers of 16 lanes
     (void)C;
     BnPlan p;
     long r = std::min<long>(256, std::max<long>(1, (M + 63) / 64));
@@ -150,15 +150,19 @@ k_bn_stats_partial(const float *__restrict__ y, int ld, long M, int C, long rows
     }
 }
 
-// finalize: block = 8 channels x 32 lanes; two parallel passes over the R chunk
-// partials (Chan's combine as sums: mean = sum n_i mean_i / n, M2 = sum M2_i + n_i (mean_i - mean)^2);
-// the 32 lane sums of a channel are combined in a fixed order (deterministic)
-constexpr int FIN_C = 8, FIN_L = 32;
+// finalize: block = 16 channels x 16 lanes; lane l holds the chunk partials
+// l, l + 16, ... (R <= 256: at most 16 per lane, all loads issued at once, each
+// wave-load 16 consecutive channels of 4 chunk rows); Chan's combine as sums
+// (mean = sum n_i mean_i / n, M2 = sum M2_i + n_i (mean_i - mean)^2) over the
+// registers; the 16 lane sums of a channel added in a fixed order (deterministic)
+constexpr int FIN_C = 16, FIN_L = 16, FIN_K = 16;
+static_assert(FIN_L * FIN_K >= 256, "bn_plan's 256 chunks fit the finalize lanes");
 
-__device__ __forceinline__ float lane_sum32(float v, float *sh, int cl, int ln) {
+__device__ __forceinline__ float lane_sum16(float v, float *sh, int cl, int ln) {
     sh[ln * FIN_C + cl] = v;
     __syncthreads();
     float s = 0.f;
+#pragma unroll
     for (int l = 0; l < FIN_L; ++l) s += sh[l * FIN_C + cl];
     __syncthreads();
     return s;
@@ -174,31 +178,38 @@ k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, i
     __shared__ float sh[256];
     const int cl = threadIdx.x % FIN_C, ln = threadIdx.x / FIN_C;
     const int c = blockIdx.x * FIN_C + cl;
+    const bool cok = c < C;
     float mmc = 0.f, mvc = 0.f;
-    if (ln == 0 && c < C) {
+    if (ln == 0 && cok) {
         if (mm) mmc = mm[c];
         if (mv) mvc = mv[c];
     }
     for (int sg = 0; sg < S; ++sg) {
         const long o = (long)sg * R * C;
+        float vn[FIN_K], vm[FIN_K], vq[FIN_K];
+#pragma unroll
+        for (int k = 0; k < FIN_K; ++k) {
+            const int r = ln + k * FIN_L;
+            const bool ok = cok && r < R;
+            const long i = o + (long)(ok ? r : 0) * C + (cok ? c : 0);
+            vn[k] = ok ? pn[i] : 0.f;
+            vm[k] = ok ? pmean[i] : 0.f;
+            vq[k] = ok ? pm2[i] : 0.f;
+        }
         float sn = 0.f, sm = 0.f;
-        if (c < C)
-            for (int r = ln; r < R; r += FIN_L) {
-                const float n = pn[o + (long)r * C + c];
-                sn += n;
-                sm += n * pmean[o + (long)r * C + c];
-            }
-        const float n = lane_sum32(sn, sh, cl, ln);
-        const float msum = lane_sum32(sm, sh, cl, ln);
+#pragma unroll
+        for (int k = 0; k < FIN_K; ++k) { sn += vn[k]; sm += vn[k] * vm[k]; }
+        const float n = lane_sum16(sn, sh, cl, ln);
+        const float msum = lane_sum16(sm, sh, cl, ln);
         const float mu = n > 0.f ? msum / n : 0.f;
         float q = 0.f;
-        if (c < C)
-            for (int r = ln; r < R; r += FIN_L) {
-                const float d = pmean[o + (long)r * C + c] - mu;
-                q += pm2[o + (long)r * C + c] + pn[o + (long)r * C + c] * d * d;
-            }
-        const float m2 = lane_sum32(q, sh, cl, ln);
-        if (ln != 0 || c >= C) continue;
+#pragma unroll
+        for (int k = 0; k < FIN_K; ++k) {
+            const float d = vm[k] - mu;
+            q += vq[k] + vn[k] * d * d;
+        }
+        const float m2 = lane_sum16(q, sh, cl, ln);
+        if (ln != 0 || !cok) continue;
         const float var = n > 0.f ? m2 / n : 0.f;
         const float inv = 1.f / sqrtf(var + eps);
         const int sc = sg * C + c;
@@ -212,7 +223,7 @@ k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, i
         const float unb = n > 1.f ? m2 / (n - 1.f) : m2;
         mvc -= (mvc - unb) * (1.f - momentum);
     }
-    if (ln == 0 && c < C) {
+    if (ln == 0 && cok) {
         if (mm) mm[c] = mmc;
         if (mv) mv[c] = mvc;
     }
@@ -380,11 +391,20 @@ k_bn_bwd_final(const float *p1, const float *p2, int R, int C, int S, long M, co
     float t1 = 0.f, t2 = 0.f;
     for (int sg = 0; sg < S; ++sg) {
         const long o = (long)sg * R * C;
+        float v1[FIN_K], v2[FIN_K];
+#pragma unroll
+        for (int k = 0; k < FIN_K; ++k) {
+            const int r = ln + k * FIN_L;
+            const bool ok = c < C && r < R;
+            const long i = o + (long)(ok ? r : 0) * C + (c < C ? c : 0);
+            v1[k] = ok ? p1[i] : 0.f;
+            v2[k] = ok ? p2[i] : 0.f;
+        }
         float a1 = 0.f, a2 = 0.f;
-        if (c < C)
-            for (int r = ln; r < R; r += FIN_L) { a1 += p1[o + (long)r * C + c]; a2 += p2[o + (long)r * C + c]; }
-        a1 = lane_sum32(a1, sh, cl, ln);
-        a2 = lane_sum32(a2, sh, cl, ln);
+#pragma unroll
+        for (int k = 0; k < FIN_K; ++k) { a1 += v1[k]; a2 += v2[k]; }
+        a1 = lane_sum16(a1, sh, cl, ln);
+        a2 = lane_sum16(a2, sh, cl, ln);
         if (ln != 0 || c >= C) continue;
         t1 += a1;
         t2 += a2;

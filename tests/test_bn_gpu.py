@@ -24,6 +24,11 @@ CASES = [
     ("c96.strided", 1, 1000, 96, "lrelu", 4),
     ("c3.scalar", 1, 37, 3, "none", 0),
     ("seg2.c256", 2, 2048, 256, "relu", 0),
+    # a ragged last chunk, 4 and 1024 channels, two large segments (pix2pix down3)
+    ("ragged", 1, 9001, 64, "lrelu", 0),
+    ("c4", 1, 20000, 4, "relu", 0),
+    ("c1024", 1, 300, 1024, "none", 0),
+    ("seg2.down3", 2, 16384, 256, "lrelu", 0),
 ]
 
 
@@ -110,3 +115,17 @@ def test_bn_train_matches_fp64(case):
     _close(dy.view(R, C), dy_r, "dy", rel=5e-5)
     _close(dg, dg_r + 0.5, "dgamma (beta = 1 accumulation)", rel=5e-5)
     _close(db, db_r - 0.25, "dbeta (beta = 1 accumulation)", rel=5e-5)
+    # deterministic: the same call again gives the same bits (fixed chunks, fixed-order folds)
+    z2 = torch.empty_like(z)
+    mean2, inv2 = torch.empty_like(mean), torch.empty_like(inv)
+    mm2, mv2 = mm64.float().to(DEV), mv64.float().to(DEV)
+    ops.bn_fwd_train(y, g, b, mean2, inv2, mm2, mv2, z2, act=act, alpha=alpha, momentum=momentum, eps=eps,
+                     segments=S)
+    dy2 = torch.empty_like(dy)
+    dg2, db2 = torch.full((C,), 0.5, device=DEV), torch.full((C,), -0.25, device=DEV)
+    ops.bn_bwd(dz, z2, y, g, mean2, inv2, dy2, dg2, db2, act=act, alpha=alpha, beta=1.0, segments=S)
+    torch.cuda.synchronize()
+    for a, b_, what in ((z, z2, "z"), (mm, mm2, "moving mean"), (mv, mv2, "moving var"), (dy, dy2, "dy"),
+                        (dg, dg2, "dgamma"), (db, db2, "dbeta")):
+        assert torch.equal(a, b_), f"{what} differs between two identical calls"
+
