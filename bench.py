@@ -59,6 +59,9 @@ BF16_MFMA_PEAK = 2516.6e12  # gfx950 dense bf16 MFMA: 1024 FLOP/clk/SIMD x 1024 
 # bf16x6 conv math: six bf16 piece products per fp32 product, so its
 # fp32-equivalent ceiling is the bf16 peak / 6
 X6_PEAK = BF16_MFMA_PEAK / 6.0
+# fp16x3 conv math: three fp16 piece products (fp16 MFMA rate = bf16) per fp32 product
+X3_PEAK = BF16_MFMA_PEAK / 3.0
+ARITH_PEAK = {"fp32": FP32_MFMA_PEAK, "bf16x6": X6_PEAK, "fp16": BF16_MFMA_PEAK, "f16x3": X3_PEAK}
 
 WORKLOADS = {
     "pix2pix": dict(metric="training images/sec, pix2pix 256x256 bs16/GPU", batch=16, size=256, scale=1,
@@ -242,6 +245,9 @@ def main():
     model, trainer, graph, elapsed = measure(content)
     hip_graph = graph is not None
     conv_math = "fp16" if fp16 else ("bf16x6" if ops.default_conv_math() == ops.MATH_BF16X6 else "fp32")
+    if args.model == "pix2pix":
+        from dgan import nets as _nets
+        conv_math = f"G/D {_nets.P2P_MATH}, VGG19 {os.environ.get('DG_VGG_MATH', 'f16x3')}"
     losses = trainer.loss.cpu().numpy()
     ms_per_step = elapsed / args.steps * 1e3
     images = world * batch * args.steps
@@ -260,7 +266,13 @@ def main():
         conv_ms = sum(r["ms"] for r in recs)
         step_flops = conv_flops
         achieved = conv_flops / (conv_ms * 1e-3)
-        peak = {"bf16x6": X6_PEAK, "fp16": BF16_MFMA_PEAK}.get(conv_math, FP32_MFMA_PEAK)
+        # each op against the dense MFMA peak of the arithmetic its GEMM runs in (ops.op_arith):
+        # peak = total FLOPs / the time they take at those peaks, frac = that time / launch time
+        t_peak = sum(r["flops"] / ARITH_PEAK[r["arith"]] for r in recs)
+        peak = conv_flops / t_peak if t_peak > 0 else X6_PEAK
+        arith_mix = {}
+        for r in recs:
+            arith_mix[r["arith"]] = arith_mix.get(r["arith"], 0.0) + r["flops"] / 1e9
         traffic, source = traffic_of(args, wl, content, batch, rank, world)
         roofline = {"bound": "mfma", "achieved": round(achieved / 1e12, 2), "peak": round(peak / 1e12, 1),
                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
@@ -270,29 +282,35 @@ def main():
                     "traffic_source": source,
                     "kernel": "dg conv engine (k_conv_gemm_x6 / k_conv_gemm + split passes + narrow + split-K "
                               "reduce), all conv launches of one step",
-                    "peak_basis": {"bf16x6": "bf16 dense MFMA peak / 6 (six bf16 piece products per fp32 product)",
-                                   "fp16": "fp16 dense MFMA peak (mixed_float16: eligible GEMMs fp16, the rest "
-                                           "fp32-accurate)"}.get(conv_math, "fp32 dense MFMA peak"),
+                    "peak_basis": "per op, the dense MFMA peak of its GEMM's arithmetic: fp16x3 bf16-rate peak / 3 "
+                                  "(three fp16 piece products per fp32 product), bf16x6 / 6, fp16 / 1, fp32 MFMA; "
+                                  "peak = total FLOPs / their time at those peaks",
+                    "gflop_by_arith": {k: round(v, 1) for k, v in sorted(arith_mix.items())},
+                    "frac_of_bf16x6_basis": round(achieved / X6_PEAK, 4),
                     "frac_of_fp32_mfma_peak": round(achieved / FP32_MFMA_PEAK, 4),
                     "conv_launch_ms_per_step": round(conv_ms, 3), "conv_gflop_per_step": round(conv_flops / 1e9, 1),
                     "step_frac": round(conv_flops / (ms_per_step * 1e-3) / peak, 4)}
         # per network (conv descriptor labels "G.down1", "D.last", "vgg19.block1_conv1", ...);
         # for pix2pix, `p2p_convs` = the G + D Conv2D / Conv2DTranspose kernels the north star's
         # ">= 40 % of MFMA peak" names (pix2pix.py:110-142, 194-220), VGG19 excluded
+
         nets = {}
         for r in recs:
             net = (r["label"] or "?").split(".", 1)[0]
-            a = nets.setdefault(net, [0.0, 0.0])
+            a = nets.setdefault(net, [0.0, 0.0, 0.0])
             a[0] += r["flops"]
             a[1] += r["ms"]
+            a[2] += r["flops"] / ARITH_PEAK[r["arith"]]
 
-        def frac_of(fl, ms):
+        def frac_of(fl, ms, tp):
             return {"gflop_per_step": round(fl / 1e9, 1), "ms_per_step": round(ms, 3),
-                    "achieved": round(fl / (ms * 1e-3) / 1e12, 2), "frac": round(fl / (ms * 1e-3) / peak, 4)}
+                    "achieved": round(fl / (ms * 1e-3) / 1e12, 2), "frac": round(tp / (ms * 1e-3), 4),
+                    "frac_of_bf16x6_basis": round(fl / (ms * 1e-3) / X6_PEAK, 4)}
         roofline["by_net"] = {n: frac_of(*v) for n, v in sorted(nets.items()) if v[1] > 0}
         if args.model == "pix2pix" and "G" in nets and "D" in nets:
             fl, ms = nets["G"][0] + nets["D"][0], nets["G"][1] + nets["D"][1]
-            roofline["p2p_convs"] = {**frac_of(fl, ms), "nets": "G + D (VGG19 excluded)",
+            tp = nets["G"][2] + nets["D"][2]
+            roofline["p2p_convs"] = {**frac_of(fl, ms, tp), "nets": "G + D (VGG19 excluded)",
                                      "target_frac": 0.40}
         if rank == 0 and os.environ.get("DG_BENCH_DETAIL"):
             for r in sorted(recs, key=lambda r: -r["ms"])[:int(os.environ.get("DG_BENCH_DETAIL_N", "60"))]:

@@ -37,10 +37,11 @@ static BnPlan bn_plan(long M, int C) {
 // ws layout (floats) for S row segments of M rows each (independent
 // statistics per segment: e.g. the G(x) and G(y) halves of one batched
 // generator pass, pix2pix.py:44 / :90):
-//   [3*S*R*C partials] [4*S*C scale/shift or bwd coefs]
+//   forward  [3*S*R*C partials (n, mean, M2)] [S*R*C unused] [4*S*C scale / shift]
+//   backward [4*S*R*C partials (sums, maxima)] [4*S*C coefficients]
 static size_t bn_ws_floats(long M, int C, int S = 1) {
     BnPlan p = bn_plan(M, C);
-    return (size_t)3 * S * p.R * C + (size_t)4 * S * C + 64;
+    return (size_t)4 * S * p.R * C + (size_t)4 * S * C + 64;
 }
 
 // segment of global row r (S is 1 or 2 in practice: a loop, no 64-bit divide)
@@ -158,6 +159,15 @@ k_bn_stats_partial(const float *__restrict__ y, int ld, long M, int C, long rows
 constexpr int FIN_C = 16, FIN_L = 16, FIN_K = 16;
 static_assert(FIN_L * FIN_K >= 256, "bn_plan's 256 chunks fit the finalize lanes");
 
+__device__ __forceinline__ float lane_max16(float v, float *sh, int cl, int ln) {
+    sh[ln * FIN_C + cl] = v;
+    __syncthreads();
+    float s = 0.f;
+#pragma unroll
+    for (int l = 0; l < FIN_L; ++l) s = fmaxf(s, sh[l * FIN_C + cl]);
+    __syncthreads();
+    return s;
+}
 __device__ __forceinline__ float lane_sum16(float v, float *sh, int cl, int ln) {
     sh[ln * FIN_C + cl] = v;
     __syncthreads();
@@ -313,8 +323,13 @@ __global__ void __launch_bounds__(256)
 k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict__ z, int ldz,
                  const float *__restrict__ y, int ldy, long M, int C, long rows, int cpb,
                  const float *__restrict__ mean, const float *__restrict__ invstd, int act, float alpha, float dscale,
-                 float *__restrict__ p1, float *__restrict__ p2) {
-    __shared__ float a1s[256 * V], a2s[256 * V];
+                 float *__restrict__ p1, float *__restrict__ p2, float *__restrict__ pd, float *__restrict__ pv,
+                 float *__restrict__ bound) {
+    // pd / pv (may be NULL): per chunk max |dbn| and max |y - mean|, the terms of the bound
+    // on |dy| that scales its fp16x3 planes (k_bn_bwd_final); bound zeroed here for it
+    __shared__ float a1s[256 * V], a2s[256 * V], dms[256 * V], vms[256 * V];
+    if (bound && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x < X3_SHARDS)
+        bound[threadIdx.x] = 0.f;
     const int slot = threadIdx.x % cpb, rl = threadIdx.x / cpb, RL = 256 / cpb;
     const int c0 = (blockIdx.x * cpb + slot) * V;
     {   // segment blockIdx.z: its rows and its saved statistics
@@ -326,9 +341,9 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
     const long pbase = (long)blockIdx.z * gridDim.y;
     const long r0 = (long)blockIdx.y * rows;
     const long r1 = min(M, r0 + rows);
-    float a1[V], a2[V], mu[V], inv[V];
+    float a1[V], a2[V], dm[V], vm[V], mu[V], inv[V];
 #pragma unroll
-    for (int q = 0; q < V; ++q) a1[q] = a2[q] = 0.f;
+    for (int q = 0; q < V; ++q) a1[q] = a2[q] = dm[q] = vm[q] = 0.f;
     const bool cok = c0 < C;
     if (cok) {
         loadv<V>(mean + c0, mu);
@@ -339,6 +354,8 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
                 float dbn = dv[q] * act_grad_from_out(zv[q], act, alpha) * dscale;
                 a1[q] += dbn;
                 a2[q] += dbn * (yv[q] - mu[q]) * inv[q];
+                dm[q] = fmaxf(dm[q], fabsf(dbn));
+                vm[q] = fmaxf(vm[q], fabsf(yv[q] - mu[q]));
             }
         };
         // U rows' loads in flight per lane, summed in row order (deterministic)
@@ -364,31 +381,41 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
         }
     }
 #pragma unroll
-    for (int q = 0; q < V; ++q) { a1s[threadIdx.x * V + q] = a1[q]; a2s[threadIdx.x * V + q] = a2[q]; }
+    for (int q = 0; q < V; ++q) {
+        a1s[threadIdx.x * V + q] = a1[q]; a2s[threadIdx.x * V + q] = a2[q];
+        dms[threadIdx.x * V + q] = dm[q]; vms[threadIdx.x * V + q] = vm[q];
+    }
     __syncthreads();
     if (rl != 0 || !cok) return;
     for (int l = 1; l < RL; ++l) {
         const int t = threadIdx.x + l * cpb;
 #pragma unroll
-        for (int q = 0; q < V; ++q) { a1[q] += a1s[t * V + q]; a2[q] += a2s[t * V + q]; }
+        for (int q = 0; q < V; ++q) {
+            a1[q] += a1s[t * V + q]; a2[q] += a2s[t * V + q];
+            dm[q] = fmaxf(dm[q], dms[t * V + q]); vm[q] = fmaxf(vm[q], vms[t * V + q]);
+        }
     }
 #pragma unroll
     for (int q = 0; q < V; ++q) {
         const long o = (pbase + blockIdx.y) * C + c0 + q;
         p1[o] = a1[q];
         p2[o] = a2[q];
+        if (pd) { pd[o] = dm[q]; pv[o] = vm[q]; }
     }
 }
 
 // per segment s: coef[s] = [A | B | D | mean] ([S][4][C]); dgamma / dbeta = the
 // sum over the segments (the reference's calls share the BN variables)
 __global__ void __launch_bounds__(256)
-k_bn_bwd_final(const float *p1, const float *p2, int R, int C, int S, long M, const float *gamma, const float *mean,
-               const float *invstd, float *dgamma, float *dbeta, float beta, float *coef) {
+k_bn_bwd_final(const float *p1, const float *p2, const float *pd, const float *pv, int R, int C, int S, long M,
+               const float *gamma, const float *mean, const float *invstd, float *dgamma, float *dbeta, float beta,
+               float *coef, float *bound) {
+    // bound (pd, pv set): max over channels and segments of |A| max|dbn| + |B| max|y - mean| + |D|
+    // >= max |dy|, into one of X3_SHARDS floats (zeroed by the partial pass)
     __shared__ float sh[256];
     const int cl = threadIdx.x % FIN_C, ln = threadIdx.x / FIN_C;
     const int c = blockIdx.x * FIN_C + cl;
-    float t1 = 0.f, t2 = 0.f;
+    float t1 = 0.f, t2 = 0.f, bnd = 0.f;
     for (int sg = 0; sg < S; ++sg) {
         const long o = (long)sg * R * C;
         float v1[FIN_K], v2[FIN_K];
@@ -405,6 +432,19 @@ k_bn_bwd_final(const float *p1, const float *p2, int R, int C, int S, long M, co
         for (int k = 0; k < FIN_K; ++k) { a1 += v1[k]; a2 += v2[k]; }
         a1 = lane_sum16(a1, sh, cl, ln);
         a2 = lane_sum16(a2, sh, cl, ln);
+        float md = 0.f, mv = 0.f;
+        if (pd) {
+#pragma unroll
+            for (int k = 0; k < FIN_K; ++k) {
+                const int r = ln + k * FIN_L;
+                if (c < C && r < R) {
+                    md = fmaxf(md, pd[o + (long)r * C + c]);
+                    mv = fmaxf(mv, pv[o + (long)r * C + c]);
+                }
+            }
+            md = lane_max16(md, sh, cl, ln);
+            mv = lane_max16(mv, sh, cl, ln);
+        }
         if (ln != 0 || c >= C) continue;
         t1 += a1;
         t2 += a2;
@@ -418,10 +458,21 @@ k_bn_bwd_final(const float *p1, const float *p2, int R, int C, int S, long M, co
         cf[C + c] = -k1 * m2 * invstd[sc];
         cf[2 * C + c] = -k1 * m1;
         cf[3 * C + c] = mean[sc];
+        bnd = fmaxf(bnd, fabsf(k1) * md + fabsf(cf[C + c]) * mv + fabsf(cf[2 * C + c]));
     }
-    if (ln != 0 || c >= C) return;
-    if (dbeta) dbeta[c] = t1 + (beta != 0.f ? beta * dbeta[c] : 0.f);
-    if (dgamma) dgamma[c] = t2 + (beta != 0.f ? beta * dgamma[c] : 0.f);
+    if (ln == 0 && c < C) {
+        if (dbeta) dbeta[c] = t1 + (beta != 0.f ? beta * dbeta[c] : 0.f);
+        if (dgamma) dgamma[c] = t2 + (beta != 0.f ? beta * dgamma[c] : 0.f);
+    }
+    if (bound) {   // the block's 16 channels, one vector atomic (non-negative floats order as uints)
+        sh[threadIdx.x] = ln == 0 ? bnd : 0.f;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float b = 0.f;
+            for (int i = 0; i < FIN_C; ++i) b = fmaxf(b, sh[i]);
+            atomicMax(reinterpret_cast<unsigned *>(bound) + (blockIdx.x & (X3_SHARDS - 1)), __float_as_uint(b));
+        }
+    }
 }
 
 template <int V>
@@ -429,7 +480,11 @@ __global__ void __launch_bounds__(256)
 k_bn_bwd_apply(const float *__restrict__ dz, int lddz, const float *__restrict__ z, int ldz,
                const float *__restrict__ y, int ldy, long M, int S, int C, int act, float alpha, float dscale,
                const float *__restrict__ coef, float *__restrict__ dy, int lddy, unsigned short *__restrict__ dyp,
-               _Float16 *__restrict__ dyh) {
+               _Float16 *__restrict__ dyh, const float *__restrict__ dyb) {
+    // dyb (may be NULL): dy's bound -- its planes are then the consumer's fp16x3 planes,
+    // scaled by x3_grad_scale(dyb) (k_bn_bwd_final)
+    const float xs = dyb ? x3_grad_scale(dyb, nullptr) : 1.f;
+    const int pC = dyb ? -C : C;
     // coef[s] = [A | B | D | mean] per channel:  dy = A * dbn + B * (y - mean) + D
     // dyp (V = 4, C % 16 == 0): dy's bf16x6 planes too, in the packed layout
     // the consuming conv reads (no split pass before its backward GEMMs)
@@ -453,7 +508,7 @@ k_bn_bwd_apply(const float *__restrict__ dz, int lddz, const float *__restrict__
             o[q] = A[q] * (dv[q] * act_grad_from_out(zv[q], act, alpha) * dscale) + B[q] * (yv[q] - Mu[q]) + D[q];
         if (dy) storev<V>(dy + r * lddy + c, o);
         if constexpr (V == 4) {
-            if (dyp) store_planes4(dyp, C, r, c, f32x4{o[0], o[1], o[2], o[3]});
+            if (dyp) store_planes4(dyp, pC, r, c, f32x4{o[0], o[1], o[2], o[3]}, xs);
             if (dyh) store_f16x4(dyh + r * C + c, f32x4{o[0], o[1], o[2], o[3]});
         } else {
             if (dyh) dyh[r * C + c] = (_Float16)o[0];
@@ -564,11 +619,14 @@ int dg_bn_fwd_train_seg_h(int S, int M, int C, const float *y, int ldy, const fl
     DG_LAUNCHED("bn_stats_final");
     const bool av4 = dg::vec4_ok(C, {{y, ldy}, {z, ldz}, {res, ldres}});
     unsigned short *p0 = (unsigned short *)zp0, *p1 = (unsigned short *)zp1;
+    // (planes C < 0: the consumer's fp16x3 planes of -C channels, 32-channel groups)
     auto pl_ok = [&](const unsigned short *p, int pc, int col) {
-        return !p || (av4 && pc % 16 == 0 && col % 16 == 0 && C % 16 == 0 && col + C <= pc && (((uintptr_t)p) & 15) == 0);
+        const int g = pc < 0 ? 32 : 16, apc = pc < 0 ? -pc : pc;
+        return !p || (av4 && apc % g == 0 && col % g == 0 && C % g == 0 && col + C <= apc && (((uintptr_t)p) & 15) == 0);
     };
     DG_ARG(pl_ok(p0, zp0C, zp0col) && pl_ok(p1, zp1C, zp1col),
-           "z planes need float4-aligned tensors, C and the column %% 16 == 0, col + C <= planes C, 16-byte alignment");
+           "z planes need float4-aligned tensors, C and the column a multiple of 16 (fp16x3: 32), col + C <= planes C, "
+           "16-byte alignment");
     const long MT = (long)S * M;
     if (av4)
         hipLaunchKernelGGL(dg::k_bn_apply<4>, dim3(dg::ew_grid(MT * C / 4)), dim3(256), 0, s, y, ldy, (long)M, S, C,
@@ -621,11 +679,24 @@ int dg_bn_bwd_seg_h(int S, int M, int C, const float *dz, int lddz, const float 
                     const float *gamma, const float *save_mean, const float *save_invstd, int act, float alpha,
                     float drop_rate, float *dy, int lddy, void *dy_planes, void *dy_f16, float *dgamma, float *dbeta,
                     float beta, void *ws, size_t ws_bytes, dg_stream_t stream) {
+    return dg_bn_bwd_seg_x(S, M, C, dz, lddz, z, ldz, y, ldy, gamma, save_mean, save_invstd, act, alpha, drop_rate, dy,
+                           lddy, dy_planes, DG_PLANES_BF16X6, nullptr, dy_f16, dgamma, dbeta, beta, ws, ws_bytes,
+                           stream);
+}
+
+int dg_bn_bwd_seg_x(int S, int M, int C, const float *dz, int lddz, const float *z, int ldz, const float *y, int ldy,
+                    const float *gamma, const float *save_mean, const float *save_invstd, int act, float alpha,
+                    float drop_rate, float *dy, int lddy, void *dy_planes, int dy_planes_format, float *dy_bound,
+                    void *dy_f16, float *dgamma, float *dbeta, float beta, void *ws, size_t ws_bytes,
+                    dg_stream_t stream) {
     DG_ARG(!dy_f16 || (((uintptr_t)dy_f16) & 7) == 0, "fp16 copy must be 8-byte aligned");
     // dy NULL: only its planes are written (every consumer reads dy_planes)
     // z NULL: allowed for a linear BN without dropout (act' = 1, z is not read)
     DG_ARG(dz && (z || (act == DG_ACT_NONE && drop_rate == 0.f)) && y && save_mean && save_invstd &&
            (dy || dy_planes) && ws, "NULL tensor");
+    DG_ARG(dy_planes_format == DG_PLANES_BF16X6 || dy_planes_format == DG_PLANES_F16X3, "bad plane format");
+    const bool x3 = dy_planes && dy_planes_format == DG_PLANES_F16X3;
+    DG_ARG(!x3 || (dy_bound && C % 32 == 0), "fp16x3 dy planes need a bound buffer (8 floats) and C %% 32 == 0");
     if (!z) ldz = C;
     DG_ARG(S >= 1 && S <= 8 && M > 0 && C > 0 && lddz >= C && ldz >= C && ldy >= C && (!dy || lddy >= C), "bad shape");
     DG_ARG(ws_bytes >= dg::bn_ws_floats(M, C, S) * sizeof(float), "workspace too small");
@@ -638,20 +709,23 @@ int dg_bn_bwd_seg_h(int S, int M, int C, const float *dz, int lddz, const float 
     dg::BnPlan bp = dg::bn_plan(M, C);
     float *w = (float *)ws;
     const size_t RC = (size_t)S * bp.R * C;
-    float *p1 = w, *p2 = w + RC, *coef = w + 3 * RC;
+    float *p1 = w, *p2 = w + RC, *coef = w + 4 * RC;
+    float *pd = x3 ? w + 2 * RC : nullptr, *pv = x3 ? w + 3 * RC : nullptr, *bnd = x3 ? dy_bound : nullptr;
     const bool v4 = dg::vec4_ok(C, {{dz, lddz}, {z, ldz}, {y, ldy}, {save_mean, 4}, {save_invstd, 4}});
     if (v4) {
         dg::PartGeom pg = dg::part_geom(C, 4);
         hipLaunchKernelGGL(dg::k_bn_bwd_partial<4>, dim3(pg.cg, bp.R, S), dim3(256), 0, s, dz, lddz, z, ldz, y, ldy,
-                           (long)M, C, bp.rows, pg.cpb, save_mean, save_invstd, act, alpha, dscale, p1, p2);
+                           (long)M, C, bp.rows, pg.cpb, save_mean, save_invstd, act, alpha, dscale, p1, p2, pd, pv,
+                           bnd);
     } else {
         dg::PartGeom pg = dg::part_geom(C, 1);
         hipLaunchKernelGGL(dg::k_bn_bwd_partial<1>, dim3(pg.cg, bp.R, S), dim3(256), 0, s, dz, lddz, z, ldz, y, ldy,
-                           (long)M, C, bp.rows, pg.cpb, save_mean, save_invstd, act, alpha, dscale, p1, p2);
+                           (long)M, C, bp.rows, pg.cpb, save_mean, save_invstd, act, alpha, dscale, p1, p2, pd, pv,
+                           bnd);
     }
     DG_LAUNCHED("bn_bwd_partial");
-    hipLaunchKernelGGL(dg::k_bn_bwd_final, dim3(dg_cdiv(C, dg::FIN_C)), dim3(256), 0, s, p1, p2, bp.R, C, S, (long)M,
-                       gamma, save_mean, save_invstd, dgamma, dbeta, beta, coef);
+    hipLaunchKernelGGL(dg::k_bn_bwd_final, dim3(dg_cdiv(C, dg::FIN_C)), dim3(256), 0, s, p1, p2, pd, pv, bp.R, C, S,
+                       (long)M, gamma, save_mean, save_invstd, dgamma, dbeta, beta, coef, bnd);
     DG_LAUNCHED("bn_bwd_final");
     const bool av4 = dg::vec4_ok(C, {{dz, lddz}, {z, ldz}, {y, ldy}, {dy, lddy}});
     unsigned short *dyp = (unsigned short *)dy_planes;
@@ -660,10 +734,10 @@ int dg_bn_bwd_seg_h(int S, int M, int C, const float *dz, int lddz, const float 
     const long MT = (long)S * M;
     if (av4)
         hipLaunchKernelGGL(dg::k_bn_bwd_apply<4>, dim3(dg::ew_grid(MT * C / 4)), dim3(256), 0, s, dz, lddz, z, ldz, y,
-                           ldy, (long)M, S, C, act, alpha, dscale, coef, dy, lddy, dyp, (_Float16 *)dy_f16);
+                           ldy, (long)M, S, C, act, alpha, dscale, coef, dy, lddy, dyp, (_Float16 *)dy_f16, bnd);
     else
         hipLaunchKernelGGL(dg::k_bn_bwd_apply<1>, dim3(dg::ew_grid(MT * C)), dim3(256), 0, s, dz, lddz, z, ldz, y,
-                           ldy, (long)M, S, C, act, alpha, dscale, coef, dy, lddy, dyp, (_Float16 *)dy_f16);
+                           ldy, (long)M, S, C, act, alpha, dscale, coef, dy, lddy, dyp, (_Float16 *)dy_f16, bnd);
     DG_LAUNCHED("bn_bwd_apply");
     return DG_OK;
 }

@@ -1200,6 +1200,14 @@ static const TileCfg kF16Cfgs[] = {
     {128, 32, 4, 1, 32, 3, 4, 1.45},   // 32-wide (SR discriminators' 32-channel layers)
 };
 constexpr int kNumF16Cfgs = sizeof(kF16Cfgs) / sizeof(kF16Cfgs[0]);
+// fp16x3 kernel configs (conv_x6.hip launch_gemm_x3: four images per K-tile of 32, the
+// 128-wide tiles one K-tile ahead in two LDS buffers)
+static const TileCfg kX3Cfgs[] = {
+    {128, 128, 2, 2, 32, 2, 2, 1.00}, {128, 64, 2, 2, 32, 2, 3, 1.15}, {64, 128, 2, 2, 32, 2, 3, 1.15},
+    {64, 64, 2, 2, 32, 3, 3, 1.40},   {256, 128, 4, 2, 32, 2, 1, 1.00}, {128, 256, 2, 4, 32, 2, 1, 0.90},
+    {128, 32, 4, 1, 32, 3, 2, 1.45},
+};
+constexpr int kNumX3Cfgs = sizeof(kX3Cfgs) / sizeof(kX3Cfgs[0]);
 
 struct OpPlan {
     int narrow;      // 1 => VALU narrow kernel
@@ -1453,11 +1461,18 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
                          ((mode == MODE_FWD && g.Ci % 32 == 0 && g.Co % 16 == 0 && g.Co > 32) ||
                           (mode == MODE_DGRAD && g.Co % 32 == 0 && g.Ci % 16 == 0 && g.Ci > 32 &&
                            !plan_off("x3dgrad")));
+    // fp16x3 on the implicit-GEMM kernel (conv_x6.hip NI 4) for every other eligible op of a
+    // DG_MATH_F16X3 descriptor: 32-channel chunks of the activation / gradient operand,
+    // 16-column weight groups
+    const bool x3_gen = math == DG_MATH_F16X3 && !plan_off("x3") && !plan_off("x3gen") && g.kh * g.kw <= 32 &&
+                        ((mode == MODE_FWD && g.Ci % 32 == 0 && g.Co % 16 == 0) ||
+                         (mode == MODE_DGRAD && g.Co % 32 == 0 && g.Ci % 16 == 0) ||
+                         (mode == MODE_WGRAD && g.Ci % 32 == 0 && g.Co % 32 == 0));
     if (x6_ok) {
         OpPlan p6 = pl;
         double t6 = choose_tiles(p6, kX6Cfgs, kNumX6Cfgs, 2516.6e12 / 6.0, "DG_FORCE_X6CFG", nullptr);
         t6 += (double)(ra * ca + rb * cb) * 10.0 / 4.0e12 + 4e-6;  // split passes: read 4 B, write 6 B
-        if (t6 < t32 || getenv("DG_FORCE_X6CFG") || x3_geom) {
+        if (t6 < t32 || getenv("DG_FORCE_X6CFG") || x3_geom || x3_gen) {
             pl = p6;
             pl.x6 = 1;
             pl.x6_ra = ra; pl.x6_ca = (int)ca; pl.x6_rb = rb; pl.x6_cb = (int)cb;
@@ -1531,17 +1546,22 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         pl.splits = (int)((nch + cps - 1) / cps);
         if (hx3) pl.x6 = 3;
     }
+    if (x3_gen && pl.x6 == 1 && 4.0 * ra * ca < 2.0e9 && 4.0 * rb * cb < 2.0e9) {
+        pl.halo = 0; pl.htx = pl.hty = 0;
+        choose_tiles(pl, kX3Cfgs, kNumX3Cfgs, 2516.6e12 / 3.0, "DG_FORCE_X3CFG", nullptr);
+        pl.x6 = 3;
+    }
     pl.vec = pl.x6 ? 1 : cfg_vec(g, mode, kCfgs[pl.cfg].bk);
     pl.slab_bytes = pl.splits > 1 ? (size_t)pl.nphase * pl.splits * pl.M * pl.N * sizeof(float) : 0;
     pl.ws_bytes = pl.slab_bytes;
     if (pl.x6) {
         // workspace: [split-K slabs][A planes][B planes] (6 B per element bf16x6, 2 B fp16, 4 B fp16x3)
-        // (+ fp16x3 input gradient: a float for max |dy| when no scale source is set)
+        // (+ fp16x3: 8 floats for max |dy| when no scale source is set)
         const size_t eb = pl.x6 == 2 ? 2 : (pl.x6 == 3 ? 4 : 6);
         pl.x6_a_off = (pl.ws_bytes + 255) & ~(size_t)255;
         pl.x6_b_off = (pl.x6_a_off + eb * ra * ca + 255) & ~(size_t)255;
         pl.ws_bytes = pl.x6_b_off + eb * rb * cb;
-        if (pl.x6 == 3 && mode == MODE_DGRAD) {
+        if (pl.x6 == 3) {   // (max |dy| when no scale source is set: any mode may read dy)
             pl.x3_max_off = (pl.ws_bytes + 255) & ~(size_t)255;
             pl.ws_bytes = pl.x3_max_off + 256;
         }
@@ -1549,7 +1569,7 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     pl.gemm_bytes = pl.ws_bytes;
     if (getenv("DG_PLAN_DEBUG"))
         fprintf(stderr, "[dg plan] mode %d M=%d N=%d K=%d -> %s cfg %d splits %d\n", mode, pl.M, pl.N, pl.K,
-                pl.halo == 2 ? "x6h2" : pl.halo == 4 ? "x6h4" : pl.halo ? (pl.x6 == 2 ? "f16h" : (pl.x6 == 3 ? "x3h" : "x6h")) : (pl.x6 == 2 ? "f16" : (pl.x6 ? "x6" : "fp32")),
+                pl.halo == 2 ? "x6h2" : pl.halo == 4 ? "x6h4" : pl.halo ? (pl.x6 == 2 ? "f16h" : (pl.x6 == 3 ? "x3h" : "x6h")) : (pl.x6 == 2 ? "f16" : (pl.x6 == 3 ? "x3" : (pl.x6 ? "x6" : "fp32"))),
                 pl.cfg, pl.splits);
     return pl;
 }
@@ -1565,6 +1585,10 @@ static ConvGeom geom_1x1(long pixels, int ci, int co) {
     return q;
 }
 
+// (a recast GEMM's operands are gathered / transposed fp32 scratch, not a layer's tensors:
+// DG_MATH_F16X3 descriptors run them bf16x6)
+static int recast_math(const dg_conv_desc_s *d) { return d->math == DG_MATH_F16X3 ? DG_MATH_BF16X6 : d->math; }
+
 // decide whether a narrow op runs as a recast 1x1 MFMA GEMM (+ gather), and size its workspace
 static void plan_recast(dg_conv_desc_s *d, int op) {
     Recast &rc = d->rc[op];
@@ -1578,7 +1602,7 @@ static void plan_recast(dg_conv_desc_s *d, int op) {
         long P = (long)g.N * g.H * g.W;
         rc.nv = ntap; rc.nvp = ntap; rc.mode1 = MODE_FWD;
         rc.g1 = geom_1x1(P, g.Ci, ntap);
-        rc.p1 = make_plan(rc.g1, MODE_FWD, d->math);
+        rc.p1 = make_plan(rc.g1, MODE_FWD, recast_math(d));
         rc.wt_off = 0;
         rc.v_off = al256((size_t)g.Ci * ntap * 4);
         rc.slab_off = al256(rc.v_off + (size_t)P * ntap * 4);
@@ -1598,7 +1622,7 @@ static void plan_recast(dg_conv_desc_s *d, int op) {
         long P = (long)g.N * g.Ho * g.Wo;
         rc.nv = nv; rc.nvp = nvp; rc.mode1 = MODE_FWD;
         rc.g1 = geom_1x1(P, g.Co, nvp);
-        rc.p1 = make_plan(rc.g1, MODE_FWD, d->math);
+        rc.p1 = make_plan(rc.g1, MODE_FWD, recast_math(d));
         rc.wt_off = 0;
         rc.v_off = al256((size_t)g.Co * nvp * 4);
         rc.slab_off = al256(rc.v_off + (size_t)P * nvp * 4);
@@ -1607,7 +1631,7 @@ static void plan_recast(dg_conv_desc_s *d, int op) {
         long P = (long)g.N * g.H * g.W;
         rc.nv = ntap; rc.nvp = ntap; rc.mode1 = MODE_WGRAD;
         rc.g1 = geom_1x1(P, ntap, g.Ci);
-        rc.p1 = make_plan(rc.g1, MODE_WGRAD, d->math);
+        rc.p1 = make_plan(rc.g1, MODE_WGRAD, recast_math(d));
         rc.wt_off = 0;
         rc.v_off = 0;
         rc.slab_off = al256((size_t)P * ntap * 4);
@@ -1622,11 +1646,8 @@ static size_t colsum_ws(long M, int C);
 // (re)plan the three ops of a descriptor for its math mode
 static void plan_all(dg_conv_desc_s *d) {
     for (int op = 0; op < 3; ++op) {
-        // (DG_MATH_F16X3: fp16x3 for the forward of a Conv2D and, where that runs fp16x3, its
-        // input gradient; the filter gradient and transposed layers bf16x6)
-        const bool x3op = !d->transpose && (op == DG_OP_FWD || (op == DG_OP_BWD_DATA && d->plan[DG_OP_FWD].x6 == 3));
-        const int m = d->math == DG_MATH_F16X3 && !x3op ? DG_MATH_BF16X6 : d->math;
-        d->plan[op] = make_plan(d->g, engine_mode(d, op), m);
+        // (DG_MATH_F16X3: fp16x3 wherever make_plan finds the op eligible, bf16x6 elsewhere)
+        d->plan[op] = make_plan(d->g, engine_mode(d, op), d->math);
         plan_recast(d, op);
         if (d->rc[op].on) d->plan[op].ws_bytes = d->rc[op].bytes;
         if (op == DG_OP_BWD_FILTER) {
@@ -1687,9 +1708,11 @@ static GemmArgs make_args(const ConvGeom &g, const OpPlan &pl, const float *A, i
 struct PlaneRefs {
     void *a, *b;
     int a_ready, b_ready;
+    int b_x6;   // (fp16x3 op, B = w) the weight buffer also holds bf16x6 planes behind the fp16x3 part
 };
 
 static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a, hipStream_t s, const PlaneRefs *pr = nullptr);
+static bool tensor_x3(const dg_conv_desc_s *d, int t);
 static int finish_splitk(int mode, const OpPlan &pl, const GemmArgs &a, hipStream_t s);
 
 // narrow op through its recast (1x1 MFMA GEMM + gather)
@@ -1768,13 +1791,21 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
     DG_ARG(need == 0 || ws != nullptr, "workspace pointer is NULL");
     GemmArgs a = make_args(d->g, pl, A, lda, B, ldb, C, ldc, bias, beta, act, alpha, ws);
     a.mz = mz; a.ldmz = ldmz; a.mact = mact; a.malpha = malpha;
+    if (pl.x6 == 3) {
+        // fp16x3 operand roles (op_tensors): A is x or dy, B is w, or, in a filter gradient,
+        // dy or x; dy is scaled from its bound (dg_conv_set_grad_scale's dy source, else
+        // measured by run_gemm), x by F16X3_XS, w by F16X3_WS
+        a.x3_sa = F16X3_XS;
+        a.x3_sb = op == DG_OP_BWD_FILTER ? F16X3_XS : F16X3_WS;
+        a.x3_dyn = op == DG_OP_FWD ? 0 : ((op == DG_OP_BWD_DATA || d->transpose) ? 1 : 2);
+        if (a.x3_dyn) { a.as_m = d->gs_dy_m; a.as_g = d->gs_dy_g; }
+    }
     if (op == DG_OP_BWD_DATA) {
-        // the gradient scale context (dg_conv_set_grad_scale): dy planes' scale source (an
-        // fp16x3 input gradient), dx planes' scale source, max |dx|
-        if (pl.x6 == 3) { a.as_m = d->gs_dy_m; a.as_g = d->gs_dy_g; }
+        // the gradient scale context (dg_conv_set_grad_scale): dx planes' scale source, max |dx|
         a.ys_m = d->gs_dx_m; a.ys_g = d->gs_dx_g; a.ymax = d->gs_dx_max;
-        DG_ARG(!a.ymax || pl.halo || pl.splits > 1,
-               "max |dx| is measured by the halo / split-K epilogues only (plan of this input gradient: neither)");
+        DG_ARG(!a.ymax || pl.x6 || pl.splits > 1,
+               "max |dx| is measured by the 16x16-tile epilogues and the split-K reduce only (plan of this input "
+               "gradient: neither)");
         DG_ARG(yp_fmt != DG_PLANES_F16X3 || a.ys_m,
                "fp16x3 gradient planes need a scale source (dg_conv_set_grad_scale)");
     }
@@ -1799,8 +1830,8 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
         DG_ARG(mact == DG_ACT_NONE || mact == DG_ACT_RELU || mact == DG_ACT_LRELU,
                "plane mask needs a sign-determined activation (got %d)", mact);
         a.mzp = mzp; a.mzpC = mode == MODE_FWD ? d->g.Co : d->g.Ci;
-        // (the layer input's planes: fp16x3 when this descriptor's forward reads them so)
-        if (mode == MODE_DGRAD && d->plan[DG_OP_FWD].x6 == 3) a.mzpC = -a.mzpC;
+        // (the layer input's planes: fp16x3 when this descriptor's ops read them so)
+        if (tensor_x3(d, DG_TENSOR_X)) a.mzpC = -a.mzpC;
     }
     if (!C && !po) {
         // planes-only output: the GEMM epilogues skip the fp32 store
@@ -1924,46 +1955,64 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
     if (pl.x6 == 3) {
         // fp16x3: activations / gradients -> fp16x3 planes in 32-channel groups, weights in
         // 16-column groups (common.h); a caller-held weight buffer also receives the
-        // weights' bf16x6 planes behind them (tensor_plane_bytes).  An input gradient's dy
-        // is scaled from its bound (a.as_m / as_g: the caller's scale source, else max |dy|
-        // measured here into the workspace)
+        // weights' bf16x6 planes behind them when a bf16x6 op of the layer reads them
+        // (tensor_plane_bytes).  The gradient operand (a.x3_dyn) is scaled from its bound:
+        // a.as_m / as_g, the caller's scale source, else max |dy| measured here
         char *ws = (char *)a.slab;
         DG_ARG(ws != nullptr, "workspace pointer is NULL");
+        DG_ARG(a.x3_sa > 0.f && a.x3_sb > 0.f, "fp16x3 GEMM without its operand roles (run_engine)");
         void *pa = ws + pl.x6_a_off, *pb = ws + pl.x6_b_off;
+        const bool b_w = mode != MODE_WGRAD;                    // B is the weight tensor
         const int ldbw = (mode == MODE_DGRAD) ? a.g.Co : ldb;   // DGRAD B is the dense weight tensor
         if (pr && pr->a) pa = pr->a;
         if (pr && pr->b) pb = pr->b;
         const bool a_ready = pr && pr->a && pr->a_ready;
-        if (mode == MODE_DGRAD && !a.as_m) {
-            DG_ARG(!a_ready, "fp16x3 dy planes given without their scale source (dg_conv_set_grad_scale)");
+        const bool b_ready = pr && pr->b && pr->b_ready;
+        if (a.x3_dyn && !a.as_m) {
+            DG_ARG(!(a.x3_dyn == 1 ? a_ready : b_ready),
+                   "fp16x3 dy planes given without their scale source (dg_conv_set_grad_scale)");
             float *mx = (float *)(ws + pl.x3_max_off);
             if (hipMemsetAsync(mx, 0, X3_SHARDS * sizeof(float), s) != hipSuccess) {
                 dg::set_error("hipMemsetAsync failed");
                 return DG_ERR_HIP;
             }
-            launch_absmax(A, pl.x6_ra, pl.x6_ca, lda, mx, s);
+            if (a.x3_dyn == 1) launch_absmax(A, pl.x6_ra, pl.x6_ca, lda, mx, s);
+            else launch_absmax(B, pl.x6_rb, pl.x6_cb, ldb, mx, s);
             DG_LAUNCHED("absmax_dy");
             a.as_m = mx;
             a.as_g = nullptr;
         }
         if (!a_ready) {
-            if (mode == MODE_DGRAD) launch_split_x3(A, lda, pl.x6_ra, pl.x6_ca, pa, 32, 1.f, s, a.as_m, a.as_g);
-            else launch_split_x3(A, lda, pl.x6_ra, pl.x6_ca, pa, 32, F16X3_XS, s);
+            if (a.x3_dyn == 1) launch_split_x3(A, lda, pl.x6_ra, pl.x6_ca, pa, 32, 1.f, s, a.as_m, a.as_g);
+            else launch_split_x3(A, lda, pl.x6_ra, pl.x6_ca, pa, 32, a.x3_sa, s);
             DG_LAUNCHED("split_x3_a");
         }
-        if (!(pr && pr->b && pr->b_ready)) {
-            launch_split_x3(B, ldbw, pl.x6_rb, pl.x6_cb, pb, 16, F16X3_WS, s);
-            DG_LAUNCHED("split_x3_b");
-            if (pr && pr->b) {
-                launch_split3(B, ldbw, pl.x6_rb, pl.x6_cb, (unsigned short *)((char *)pb + x3_w_bytes(pl)), s);
-                DG_LAUNCHED("split3_b");
+        if (!b_ready) {
+            if (!b_w) {
+                if (a.x3_dyn == 2) launch_split_x3(B, ldb, pl.x6_rb, pl.x6_cb, pb, 32, 1.f, s, a.as_m, a.as_g);
+                else launch_split_x3(B, ldb, pl.x6_rb, pl.x6_cb, pb, 32, a.x3_sb, s);
+                DG_LAUNCHED("split_x3_b");
+            } else {
+                launch_split_x3(B, ldbw, pl.x6_rb, pl.x6_cb, pb, 16, F16X3_WS, s);
+                DG_LAUNCHED("split_x3_w");
+                if (pr && pr->b && pr->b_x6) {
+                    launch_split3(B, ldbw, pl.x6_rb, pl.x6_cb, (unsigned short *)((char *)pb + x3_w_bytes(pl)), s);
+                    DG_LAUNCHED("split3_w");
+                }
             }
         }
         a.A = (const float *)pa; a.lda = pl.x6_ca; a.a_bytes = (unsigned)(4 * pl.x6_ra * pl.x6_ca);
         a.B = (const float *)pb; a.ldb = pl.x6_cb; a.b_bytes = (unsigned)(4 * pl.x6_rb * pl.x6_cb);
         dim3 grid(pl.mtiles * pl.ntiles, pl.nphase * pl.splits);
-        launch_gemm_x6h(mode, pl.cfg, 3, grid, a, pl.htx, pl.hty, s, 4);
-        DG_LAUNCHED("conv_gemm_x3h");
+        if (pl.halo) {
+            launch_gemm_x6h(mode, pl.cfg, 3, grid, a, pl.htx, pl.hty, s, 4);
+            DG_LAUNCHED("conv_gemm_x3h");
+        } else {
+            fastdiv_magic((unsigned)a.g.Wo, a.mg_wo, a.sh_wo);
+            fastdiv_magic((unsigned)a.g.Ho, a.mg_ho, a.sh_ho);
+            launch_gemm_x3(mode, pl.cfg, grid, a, s);
+            DG_LAUNCHED("conv_gemm_x3");
+        }
         return finish_splitk(mode, pl, a, s);
     }
     if (pl.x6 == 2) {
@@ -2092,32 +2141,47 @@ static void op_tensors(const dg_conv_desc_s *d, int op, int &ta, int &tb) {
     else { ta = DG_TENSOR_DY; tb = DG_TENSOR_X; }  // conv view of a transposed layer: A = its output grad
 }
 
-// A descriptor whose forward runs fp16x3 (plan x6 3) keeps x as fp16x3 planes (4 B per
-// element, read by the forward only) and w as [fp16x3 (4 B) | bf16x6 (6 B)] planes: the
-// forward reads the first part, bwd_data the second; dy stays bf16x6.
-static bool fwd_x3(const dg_conv_desc_s *d) { return d->plan[DG_OP_FWD].x6 == 3; }
-static bool dgrad_x3(const dg_conv_desc_s *d) { return d->plan[DG_OP_BWD_DATA].x6 == 3; }
+// an op that reads operand planes at all: bf16x6 (x6 1), the fp16 copy (x6 2,
+// DG_MATH_FP16: [rows][C] fp16, the same for every op that reads the tensor) or fp16x3
+// (x6 3); fp32 / narrow / recast plans read fp32
+static bool op_reads_planes(const dg_conv_desc_s *d, int op) {
+    const OpPlan &pl = d->plan[op];
+    if ((pl.x6 != 1 && pl.x6 != 2 && pl.x6 != 3) || pl.narrow || d->rc[op].on || pl.M == 0 || pl.N == 0) return false;
+    return !(pl.x6 == 2 && plan_off("f16planes"));
+}
+// tensor t's planes are fp16x3 when an fp16x3 op reads them; a bf16x6 op of the same
+// layer then splits that tensor itself, except w, whose buffer holds [fp16x3 | bf16x6]
+static bool tensor_reader(const dg_conv_desc_s *d, int t, int x6) {
+    for (int op = 0; op < 3; ++op) {
+        int ta, tb;
+        op_tensors(d, op, ta, tb);
+        if (((ta | tb) & t) && op_reads_planes(d, op) && d->plan[op].x6 == x6) return true;
+    }
+    return false;
+}
+static bool tensor_x3(const dg_conv_desc_s *d, int t) { return tensor_reader(d, t, 3); }
+static size_t x3_wbytes(const dg_conv_desc_s *d) {
+    return al256((size_t)4 * d->g.kh * d->g.kw * d->Cin * d->Cout);
+}
 static size_t tensor_plane_bytes(const dg_conv_desc_s *d, int t) {
     const size_t nw = (size_t)d->g.kh * d->g.kw * d->Cin * d->Cout;
-    if (t == DG_TENSOR_X) return (size_t)(fwd_x3(d) ? 4 : 6) * d->N * d->H * d->W * d->Cin;
-    if (t == DG_TENSOR_DY) return (size_t)(dgrad_x3(d) ? 4 : 6) * d->N * d->Ho * d->Wo * d->Cout;
-    return fwd_x3(d) ? x3_w_bytes(d->plan[DG_OP_FWD]) + 6 * nw : 6 * nw;
+    if (t == DG_TENSOR_X) return (size_t)(tensor_x3(d, t) ? 4 : 6) * d->N * d->H * d->W * d->Cin;
+    if (t == DG_TENSOR_DY) return (size_t)(tensor_x3(d, t) ? 4 : 6) * d->N * d->Ho * d->Wo * d->Cout;
+    if (!tensor_x3(d, t)) return 6 * nw;
+    return x3_wbytes(d) + (tensor_reader(d, t, 1) ? 6 * nw : 0);
 }
 
-// tensors op reads as operand planes: bf16x6 planes (x6 1) or the fp16 copy
-// (x6 2, DG_MATH_FP16: [rows][C] fp16, the same for every op that reads the
-// tensor); 0 for fp32 / narrow / recast plans.  A descriptor's ops never mix
-// the two formats (an fp16 descriptor's other ops run fp32).
+// tensors op reads as operand planes (op_reads_planes); x and dy only in the format
+// tensor_x3 gives them
 static int op_plane_mask(const dg_conv_desc_s *d, int op) {
-    const OpPlan &pl = d->plan[op];
-    if ((pl.x6 != 1 && pl.x6 != 2 && pl.x6 != 3) || pl.narrow || d->rc[op].on || pl.M == 0 || pl.N == 0) return 0;
-    if (pl.x6 == 2 && plan_off("f16planes")) return 0;
+    if (!op_reads_planes(d, op)) return 0;
     int ta, tb;
     op_tensors(d, op, ta, tb);
-    // (an fp16x3 forward's x planes / an fp16x3 input gradient's dy planes are not the bf16x6
-    // planes a filter gradient reads)
-    if (op == DG_OP_BWD_FILTER) return (ta | tb) & ~(fwd_x3(d) ? DG_TENSOR_X : 0) & ~(dgrad_x3(d) ? DG_TENSOR_DY : 0);
-    return ta | tb;
+    const bool x3 = d->plan[op].x6 == 3;
+    int m = ta | tb;
+    for (int t : {DG_TENSOR_X, DG_TENSOR_DY})
+        if ((m & t) && tensor_x3(d, t) != x3) m &= ~t;
+    return m;
 }
 
 // dg_conv_planes_t -> the op's PlaneRefs (out = nullptr when the op takes no planes)
@@ -2131,8 +2195,11 @@ static int plane_refs(const dg_conv_desc_s *d, int op, const dg_conv_planes_t *p
     const int mask = op_plane_mask(d, op);
     r.a = (mask & ta) ? buf(ta) : nullptr; r.b = (mask & tb) ? buf(tb) : nullptr;
     r.a_ready = (p->ready & ta) != 0; r.b_ready = (p->ready & tb) != 0;
-    // bf16x6 bwd_data of an fp16x3-forward descriptor: the weights' bf16x6 part of the buffer
-    if (op == DG_OP_BWD_DATA && fwd_x3(d) && !dgrad_x3(d) && r.b) r.b = (char *)r.b + x3_w_bytes(d->plan[DG_OP_FWD]);
+    // a bf16x6 op of a layer with fp16x3 weight planes: the weights' bf16x6 part of the buffer
+    if (tb == DG_TENSOR_W && r.b) {
+        if (d->plan[op].x6 == 1 && tensor_x3(d, DG_TENSOR_W)) r.b = (char *)r.b + x3_wbytes(d);
+        r.b_x6 = d->plan[op].x6 == 3 && tensor_reader(d, DG_TENSOR_W, 1);
+    }
     DG_ARG(((((uintptr_t)r.a) | ((uintptr_t)r.b)) & 15) == 0, "plane buffers must be 16-byte aligned");
     out = &r;
     return DG_OK;
@@ -2228,8 +2295,7 @@ int dg_conv_planes_size(dg_conv_t d, int tensor, size_t *bytes) {
 int dg_conv_planes_format(dg_conv_t d, int tensor, int *format) {
     DG_ARG(d && format, "NULL argument");
     DG_ARG(tensor == DG_TENSOR_X || tensor == DG_TENSOR_DY || tensor == DG_TENSOR_W, "bad tensor id %d", tensor);
-    const bool x3 = tensor == DG_TENSOR_DY ? dg::dgrad_x3(d) : dg::fwd_x3(d);
-    *format = x3 ? DG_PLANES_F16X3 : DG_PLANES_BF16X6;
+    *format = dg::tensor_x3(d, tensor) ? DG_PLANES_F16X3 : DG_PLANES_BF16X6;
     return DG_OK;
 }
 
@@ -2245,6 +2311,14 @@ int dg_conv_set_grad_scale(dg_conv_t d, const float *dy_m, const float *dy_g, co
                            float *dx_max) {
     DG_ARG(d != nullptr, "descriptor is NULL");
     d->gs_dy_m = dy_m; d->gs_dy_g = dy_g; d->gs_dx_m = dx_m; d->gs_dx_g = dx_g; d->gs_dx_max = dx_max;
+    return DG_OK;
+}
+
+int dg_conv_op_arith(dg_conv_t d, int op, int *arith) {
+    DG_ARG(d && arith, "NULL argument");
+    DG_ARG(op >= 0 && op < 3, "bad op %d", op);
+    const dg::OpPlan &pl = d->rc[op].on ? d->rc[op].p1 : d->plan[op];
+    *arith = (pl.narrow || pl.co1 || pl.small || pl.ntile) ? DG_MATH_FP32 : pl.x6;
     return DG_OK;
 }
 

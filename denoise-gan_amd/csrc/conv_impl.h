@@ -48,6 +48,9 @@ struct GemmArgs {
     // (m, g) of the A (dy) planes and of the output (dx) planes; ymax receives max |output|
     const float *as_m, *as_g, *ys_m, *ys_g;
     float *ymax;
+    // fp16x3 GEMMs: which operand is the gradient scaled from (as_m, as_g) -- 0 none, 1 A,
+    // 2 B -- and the static scales of the others (F16X3_XS activations, F16X3_WS weights)
+    int x3_dyn; float x3_sa, x3_sb;
     // optional gradient mask from the planes of the activation output instead of
     // its fp32 values (dg_conv_bwd_data_xmask): act' of a sign-determined
     // activation from the sign of the hi plane, [pixel][3 mzpC] (mzpC < 0: fp16x3)
@@ -55,6 +58,13 @@ struct GemmArgs {
     // 1: DGRAD phase blocks in the plain XCD order (A/B switch DG_PLAN_DISABLE=xcd_phase)
     int xcd_plain;
 };
+
+// the factor that undoes an fp16x3 GEMM's operand scales (powers of two: exact)
+__device__ __forceinline__ float x3_out_scale(const GemmArgs &p) {
+    const float sa = p.x3_dyn == 1 ? x3_grad_scale(p.as_m, p.as_g) : p.x3_sa;
+    const float sb = p.x3_dyn == 2 ? x3_grad_scale(p.as_m, p.as_g) : p.x3_sb;
+    return 1.f / (sa * sb);
+}
 
 // hi plane of element (pix, col) of a packed plane tensor, as a float (its sign is
 // the element's; C < 0: fp16x3 planes of -C channels, the value times F16X3_XS)
@@ -330,6 +340,8 @@ void launch_split_f16(const float *src, int ld, long rows, int C, void *dst, hip
 void launch_split_f16_pair(const float *a, int lda, long ra, int ca, void *da, const float *b, int ldb, long rb,
                            int cb, void *db, hipStream_t s);
 void launch_gemm_f16(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s);
+// fp16x3 (DG_MATH_F16X3) generic GEMM: kX3Cfgs tiles, NI = 4 images per K-tile of 32
+void launch_gemm_x3(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s);
 // small-Cin 4x4 stride-2 FWD / WGRAD on fp32 MFMA (conv_small.hip)
 bool small_conv_ok(const ConvGeom &g, int mode, int lda);
 int small_wgrad_rows_per_block(const ConvGeom &g);

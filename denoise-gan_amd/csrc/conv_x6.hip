@@ -100,6 +100,12 @@ k_split_f16(const float *__restrict__ src, int ld, long rows, int C, _Float16 *_
 //     channels whose three plane images feed three MFMAs (six piece products);
 //   NI = 2 (DG_MATH_FP16): one fp16 plane, rows of C, a K-tile is 32 channels
 //     (pixels for WGRAD) staged as two 16-wide images of one MFMA.
+//   NI = 4 (DG_MATH_F16X3, common.h): fp16 h + l pieces of pre-scaled operands, a
+//     K-tile is 32 channels (pixels) staged as four 16-wide images -- h and l of
+//     k 0..15 and 16..31 -- feeding three MFMAs (h.h', l.h', h.l').  Activation /
+//     gradient rows hold per 32-channel group h[32] l[32] (images 0,1 = h, 2,3 = l);
+//     weight rows per 16-column group h[16] l[16]: as RC images (FWD) image i is
+//     piece i>>1 of k-rows 16 (i&1) .., as KC images (DGRAD) images 0,2 = h, 1,3 = l.
 // An operand row's K-chunk group holds 16 * NI elements in both layouts, so
 // the KC images (k contiguous in memory) address identically; RC images
 // (k-rows = GEMM rows of memory) take image i as plane i (NI = 3) or as the
@@ -107,12 +113,13 @@ k_split_f16(const float *__restrict__ src, int ld, long rows, int C, _Float16 *_
 template <int MODE, int BM, int BN, int WGM, int WGN, int MINW, int NBUF = 3, int NI = 3>
 __global__ void __launch_bounds__(64 * WGM * WGN, MINW)
 k_conv_gemm_x6(const GemmArgs p) {
-    static_assert(NBUF == 3 || NBUF == 4, "3 or 4 LDS buffers (2 or 3 K-tiles in flight)");
-    static_assert(NI == 3 || NI == 2, "bf16x6 (3 plane images) or fp16 (2 chunk images)");
+    static_assert(NBUF >= 2 && NBUF <= 4, "2 to 4 LDS buffers (1 to 3 K-tiles in flight)");
+    static_assert(NI == 3 || NI == 2 || NI == 4, "bf16x6 (3 plane images), fp16 (2 chunk images), fp16x3 (4)");
     constexpr bool X6 = NI == 3;
+    constexpr bool X3 = NI == 4;
     constexpr int BK = X6 ? 16 : 32;   // k per K-tile
     constexpr int GS = 16 * NI;        // elements of one K-chunk group in an operand row
-    constexpr int RM = X6 ? 3 : 1;     // operand row = RM * C elements
+    constexpr int RM = X6 ? 3 : (X3 ? 2 : 1);   // operand row = RM * C elements
     constexpr bool A_KC = (MODE != MODE_WGRAD);
     constexpr bool B_KC = (MODE == MODE_DGRAD);
     constexpr int NT = 64 * WGM * WGN;  // threads
@@ -136,7 +143,7 @@ k_conv_gemm_x6(const GemmArgs p) {
     constexpr int BUF0 = BUF > NW_ * STAGE * 4 ? BUF : NW_ * STAGE * 4;
     __shared__ __attribute__((aligned(16))) char smem0[BUF0];
     __shared__ __attribute__((aligned(16))) char smem1[BUF];
-    __shared__ __attribute__((aligned(16))) char smem2[BUF];
+    __shared__ __attribute__((aligned(16))) char smem2[NBUF >= 3 ? BUF : 16];
     __shared__ __attribute__((aligned(16))) char smem3[NBUF == 4 ? BUF : 16];
 
     const ConvGeom &g = p.g;
@@ -240,7 +247,9 @@ k_conv_gemm_x6(const GemmArgs p) {
             if (mc < p.M) {
                 arow_n[j] = 0;  // column valid
                 int tap = mc / g.Ci; int ci = mc - tap * g.Ci; wg_i[j] = tap / g.kw; wg_j[j] = tap - wg_i[j] * g.kw;
-                wg_ci[j] = X6 ? (ci >> 4) * 48 + 16 * asl[j].plane + (ci & 8) : ci;  // packed column offset
+                // packed column offset (fp16x3: piece plane>>1 of the 32-channel group)
+                wg_ci[j] = X6 ? (ci >> 4) * 48 + 16 * asl[j].plane + (ci & 8)
+                              : (X3 ? (ci >> 5) * 64 + 32 * (asl[j].plane >> 1) + (ci & 31) : ci);
             }
         }
     }
@@ -291,6 +300,8 @@ k_conv_gemm_x6(const GemmArgs p) {
                 const int col = n0 + bsl[j].c;
                 bok[j] = col < p.N;
                 bbase[j] = X6 ? (bsl[j].r * (3 * p.ldb) + (col >> 4) * 48 + 16 * bsl[j].plane + (col & 8)) * 2
+                         : X3 ? ((bsl[j].r + 16 * (bsl[j].plane & 1)) * (2 * p.ldb) + (col >> 4) * 32 +
+                                 16 * (bsl[j].plane >> 1) + (col & 8)) * 2
                               : ((bsl[j].r + 16 * bsl[j].plane) * p.ldb + col) * 2;
             } else {                           // KC weights: row ci
                 const int ci = n0 + bsl[j].r;
@@ -344,7 +355,7 @@ k_conv_gemm_x6(const GemmArgs p) {
                 ok = (amask[j] >> tap_bit) & 1;
                 off = (unsigned)(abase[j] + a_delta);
             } else {
-                const unsigned pix = (unsigned)(k0 + asl[j].r + (X6 ? 0 : 16 * asl[j].plane));
+                const unsigned pix = (unsigned)(k0 + asl[j].r + (X6 ? 0 : 16 * (X3 ? asl[j].plane & 1 : asl[j].plane)));
                 const unsigned t = fdiv(pix, p.mg_wo, p.sh_wo); const int wo = (int)(pix - t * g.Wo);
                 const unsigned n = fdiv(t, p.mg_ho, p.sh_ho); const int ho = (int)(t - n * g.Ho);
                 const int hi = ho * g.sh - g.pt + wg_i[j], wi = wo * g.sw - g.pl + wg_j[j];
@@ -367,9 +378,10 @@ k_conv_gemm_x6(const GemmArgs p) {
                 off = (unsigned)(bbase[j] + b_delta);
             } else {  // WGRAD: dy rows (pixels) contiguous along co
                 const int col = n0 + bsl[j].c;
-                const int pix = k0 + bsl[j].r + (X6 ? 0 : 16 * bsl[j].plane);
+                const int pix = k0 + bsl[j].r + (X6 ? 0 : 16 * (X3 ? bsl[j].plane & 1 : bsl[j].plane));
                 ok = col < p.N && pix < kend;
                 off = X6 ? ((unsigned)pix * (3 * p.ldb) + (col >> 4) * 48 + 16 * bsl[j].plane + (col & 8)) * 2u
+                    : X3 ? ((unsigned)pix * (2 * p.ldb) + (col >> 5) * 64 + 32 * (bsl[j].plane >> 1) + (col & 31)) * 2u
                          : ((unsigned)pix * p.ldb + col) * 2u;
             }
             dma(rB, dst, ok ? off : DG_OOB);
@@ -429,6 +441,44 @@ k_conv_gemm_x6(const GemmArgs p) {
     // fetch harmless data into idle buffers.
     constexpr int AHEAD = NBUF - 1;
     auto ktile = [&](int kt, const char *cur, char *nxt) __attribute__((always_inline)) {
+        if constexpr (X3) {
+            // fp16x3: A [h | h'] / [l | l'] of k 0..15 | 16..31; B the same pairs (KC
+            // weights of DGRAD: images 0,2 = h, 1,3 = l); h.h', l.h', h.l'
+            f16x8 ah[TM], al[TM], bh[TN], bl[TN];
+            const char *B0 = cur + 4 * APL;
+#pragma unroll
+            for (int a = 0; a < TM; ++a) {
+                const int r0 = wm * WTM + a * 16;
+                ah[a] = __builtin_bit_cast(f16x8, frag(cur, cur + APL, r0, A_KC, true));
+                al[a] = __builtin_bit_cast(f16x8, frag(cur + 2 * APL, cur + 3 * APL, r0, A_KC, true));
+            }
+            constexpr int BH1 = B_KC ? 2 : 1, BL0 = B_KC ? 1 : 2;
+#pragma unroll
+            for (int b = 0; b < TN; ++b) {
+                const int c0 = wn * WTN + b * 16;
+                bh[b] = __builtin_bit_cast(f16x8, frag(B0, B0 + BH1 * BPL, c0, B_KC, false));
+                bl[b] = __builtin_bit_cast(f16x8, frag(B0 + BL0 * BPL, B0 + 3 * BPL, c0, B_KC, false));
+            }
+            issue_tile(kbeg + (kt + AHEAD) * BK, nxt);
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[a], bh[b], acc[a][b], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[a], bh[b], acc[a][b], 0, 0, 0);
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[a], bl[b], acc[a][b], 0, 0, 0);
+            wait_dma_c<(AHEAD - 1) * NMINE>();
+            barrier();
+            return;
+        }
         bf16x8 ahm[TM], ahl[X6 ? TM : 1], b1[TN], b2[X6 ? TN : 1], b3[X6 ? TN : 1];
         if constexpr (X6) {
             read_frags(cur, ahm, ahl, b1, b2, b3);
@@ -467,12 +517,20 @@ k_conv_gemm_x6(const GemmArgs p) {
     };
     auto pipeline = [&](char *L0, char *L1, char *L2, char *L3) __attribute__((always_inline)) {
         issue_tile(kbeg, L0);
-        issue_tile(kbeg + BK, L1);
+        if constexpr (NBUF >= 3) issue_tile(kbeg + BK, L1);
         if constexpr (NBUF == 4) issue_tile(kbeg + 2 * BK, L2);
         wait_dma_c<(AHEAD - 1) * NMINE>();
         barrier();
         int kt = 0;
-        if constexpr (NBUF == 3) {
+        if constexpr (NBUF == 2) {
+            // one K-tile ahead: tile kt+1 lands in the buffer tile kt-1 used while
+            // the MFMAs of tile kt run
+            for (; kt + 1 < nk; kt += 2) {
+                ktile(kt, L0, L1);
+                ktile(kt + 1, L1, L0);
+            }
+            if (kt < nk) ktile(kt, L0, L1);
+        } else if constexpr (NBUF == 3) {
             for (; kt + 2 < nk; kt += 3) {
                 ktile(kt, L0, L2);
                 ktile(kt + 1, L1, L0);
@@ -498,6 +556,13 @@ k_conv_gemm_x6(const GemmArgs p) {
     // before smem0 becomes the epilogue's staging area
     wait_dma_c<0>();
     barrier();
+    if constexpr (X3) {   // undo the operand scales (powers of two: exact)
+        const float osc = x3_out_scale(p);
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b) acc[a][b] *= osc;
+    }
     static_assert(NW * STAGE * 4 <= BUF0, "epilogue staging fits in LDS buffer 0");
     // GEMM row -> output pixel (DGRAD: the phase's sub-grid; unit stride and
     // FWD / WGRAD rows are pixels / filter rows); slab rows are GEMM rows
@@ -673,6 +738,30 @@ void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t
 
 void launch_gemm_f16(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s) {
     launch_gemm_planes<2>(mode, cfg, grid, a, s);
+}
+
+// fp16x3 tile configs (index = kX3Cfgs in conv.hip): four 16-wide images per K-tile of
+// 32, so the 128-wide tiles keep one K-tile ahead in two LDS buffers (67 KB at 128 x 128:
+// two blocks per CU), the narrow ones two ahead in three
+void launch_gemm_x3(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s) {
+#define DG_X3(C, BM_, BN_, WM_, WN_, MW_, NB_)                                                                  \
+    case C: {                                                                                                   \
+        const dim3 blk(64 * WM_ * WN_);                                                                         \
+        if (mode == MODE_FWD) hipLaunchKernelGGL((k_conv_gemm_x6<MODE_FWD, BM_, BN_, WM_, WN_, MW_, NB_, 4>), grid, blk, 0, s, a); \
+        else if (mode == MODE_DGRAD) hipLaunchKernelGGL((k_conv_gemm_x6<MODE_DGRAD, BM_, BN_, WM_, WN_, MW_, NB_, 4>), grid, blk, 0, s, a); \
+        else hipLaunchKernelGGL((k_conv_gemm_x6<MODE_WGRAD, BM_, BN_, WM_, WN_, MW_, NB_, 4>), grid, blk, 0, s, a); \
+        break;                                                                                                  \
+    }
+    switch (cfg) {
+        DG_X3(0, 128, 128, 2, 2, 2, 2)
+        DG_X3(1, 128, 64, 2, 2, 2, 2)
+        DG_X3(2, 64, 128, 2, 2, 2, 2)
+        DG_X3(3, 64, 64, 2, 2, 3, 3)
+        DG_X3(4, 256, 128, 4, 2, 1, 2)
+        DG_X3(5, 128, 256, 2, 4, 1, 2)
+        DG_X3(6, 128, 32, 4, 1, 3, 3)
+    }
+#undef DG_X3
 }
 
 }  // namespace dg

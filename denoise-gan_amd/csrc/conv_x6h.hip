@@ -508,8 +508,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     constexpr int STAGE = 16 * (WTN + 4);
     static_assert(NW * STAGE * 4 <= 2 * HG::BYTES, "epilogue staging fits in the halo buffers");
     if constexpr (X3) {   // undo the operand scales (powers of two: exact)
-        const float osc = MODE == MODE_FWD || !p.as_m ? F16X3_OSCALE
-                                                      : 1.f / (x3_grad_scale(p.as_m, p.as_g) * F16X3_WS);
+        const float osc = x3_out_scale(p);
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll

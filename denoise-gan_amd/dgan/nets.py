@@ -34,18 +34,51 @@ FEED_X = not os.environ.get("DG_NO_FEED_X")    # BN forward writes the next conv
 DY_PLANES_ONLY = not os.environ.get("DG_DY_FP32")  # ... and then skips the fp32 dy (its readers take the planes)
 
 
+def _eb(buf):
+    """bytes per element of PlaneBuf buf's format (bf16x6 6, fp16x3 4)"""
+    return 4 if buf.fmt == ops.PLANES_F16X3 else 6
+
+
 def xrows(buf, row0, rows, C):
     """The bytes of PlaneBuf `buf` holding rows [row0, row0 + rows) of a
-    [rows, C]-channel tensor's bf16x6 planes."""
-    return buf.buf[row0 * 6 * C:(row0 + rows) * 6 * C]
+    [rows, C]-channel tensor's planes (bf16x6 or fp16x3, buf.fmt)."""
+    e = _eb(buf)
+    return buf.buf[row0 * e * C:(row0 + rows) * e * C]
 
 
 def plane_rows(buf, t, row0):
     """The bytes of PlaneBuf `buf` holding rows [row0, row0 + rows of t) of a
-    [rows, C] tensor's bf16x6 planes (6 bytes per element)."""
+    [rows, C] tensor's planes (6 bytes per element bf16x6, 4 fp16x3)."""
     C = t.shape[-1]
     rows = t[..., 0].numel()
-    return buf.buf[row0 * 6 * C:(row0 + rows) * 6 * C]
+    e = _eb(buf)
+    return buf.buf[row0 * e * C:(row0 + rows) * e * C]
+
+
+def zplanes(buf, rows, C, col):
+    """(bytes, planes C, column) of a BN forward's plane output into PlaneBuf buf: a
+    negative planes C names fp16x3 planes (dg_bn_fwd_train_seg_h)."""
+    return xrows(buf, 0, rows, C), (-C if buf.fmt == ops.PLANES_F16X3 else C), col
+
+
+# conv arithmetic of the pix2pix G / D GEMMs (include/dgan.h DG_MATH_*): fp16x3 -- three
+# fp16 piece products of pre-scaled operands, gradients scaled from their bound -- by
+# default; DG_P2P_MATH=bf16x6 for the six-piece bf16 form
+P2P_MATH = os.environ.get("DG_P2P_MATH", "f16x3")
+
+
+def grad_bounds(descs, planes, device):
+    """One 8-float dy bound per conv whose dy planes are fp16x3 (written by the BN backward
+    producing that dy, dg_bn_bwd_seg_x), set as the conv's dy scale source; None elsewhere
+    (the conv measures max |dy| itself where it splits dy)."""
+    out = []
+    for d, P in zip(descs, planes):
+        b = None
+        if FEED_DY and P is not None and P.dy is not None and P.dy.fmt == ops.PLANES_F16X3:
+            b = torch.zeros(8, dtype=torch.float32, device=device)
+            d.set_grad_scale(dy_m=b)
+        out.append(b)
+    return out
 
 
 # ---------------------------------------------------------------------------
@@ -211,8 +244,9 @@ class GeneratorPlan:
     (statistics, moving averages, dropout masks) is applied per half, exactly
     as the reference's two separate generator calls."""
 
-    def __init__(self, N, H, W, width, arena, bn_state, device, halves=1, train=True):
+    def __init__(self, N, H, W, width, arena, bn_state, device, halves=1, train=True, conv_math=None):
         self.N, self.H, self.W, self.width = N, H, W, width
+        math_ = conv_math or P2P_MATH
         self.halves = halves
         NT = N * halves
         self.NT = NT
@@ -228,15 +262,15 @@ class GeneratorPlan:
         h, w = H, W
         self.down_hw = []
         for name, ci, co, _ in self.downs:
-            d = ConvDesc(NT, h, w, ci, co, 4, 2, "same")
+            d = ConvDesc(NT, h, w, ci, co, 4, 2, "same", math=math_)
             self.ddesc.append(d)
             h, w = d.Ho, d.Wo
             self.down_hw.append((h, w))
         for name, ci, co, _ in self.ups:
-            d = ConvDesc(NT, h, w, ci, co, 4, 2, "same", transpose=True)
+            d = ConvDesc(NT, h, w, ci, co, 4, 2, "same", transpose=True, math=math_)
             self.udesc.append(d)
             h, w = d.Ho, d.Wo
-        self.ldesc = ConvDesc(NT, h, w, self.last[1], self.last[2], 4, 2, "same", transpose=True)
+        self.ldesc = ConvDesc(NT, h, w, self.last[1], self.last[2], 4, 2, "same", transpose=True, math=math_)
         for d, (name, *_) in zip(self.ddesc + self.udesc + [self.ldesc], self.downs + self.ups + [self.last]):
             d.label = f"G.{name}"
         self.out_shape = self.ldesc.out_shape
@@ -273,6 +307,7 @@ class GeneratorPlan:
         # down1 (conv + LeakyReLU, no BN) writes down2's x planes in its epilogue
         if train and FEED_X and self.planes[1].x is not None:
             self.planes[0].fwd_out = self.planes[1].x
+        self.gbound = grad_bounds(descs, self.planes, device) if train else [None] * len(descs)
         self.ws_bytes = max([d.max_ws() for d in self.ddesc + self.udesc + [self.ldesc]] + [self._bn_ws_max()])
 
     @property
@@ -381,7 +416,7 @@ class GeneratorPlan:
         A = self.arena
         if training:
             rows = z[..., 0].numel()
-            zp = [(xrows(self.planes[k].x, 0, rows, pc), pc, col) for k, pc, col in outs]
+            zp = [zplanes(self.planes[k].x, rows, pc, col) for k, pc, col in outs]
             seed0 = seed_of(0) if seed_of else 0
             stride = ((seed_of(1) - seed0) & 0xFFFFFFFF) if (seed_of and self.halves > 1) else 0
             ops.bn_fwd_train(y, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), s["mean"][name], s["inv"][name],
@@ -393,17 +428,18 @@ class GeneratorPlan:
             ops.bn_fwd_infer(self._half(y, hv), A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.bn.mean[name],
                              self.bn.var[name], self._half(z, hv), act=act, alpha=ALPHA, eps=BN_EPS)
 
-    def _bn_bwd(self, s, name, dz, z, y, dy, act, beta, ws, drop_rate=0.0, P=None):
+    def _bn_bwd(self, s, name, dz, z, y, dy, act, beta, ws, drop_rate=0.0, P=None, k=None):
         """BN backward per half; the gamma/beta gradients of the halves accumulate.
-        P: the consuming conv's ConvPlanes -- when it keeps dy planes, the BN
-        backward writes them beside dy (no split pass before the conv's
-        backward GEMMs) and marks them ready."""
+        P: the consuming conv's ConvPlanes (plane index k) -- when it keeps dy planes,
+        the BN backward writes them beside dy (no split pass before the conv's
+        backward GEMMs; fp16x3 planes with their bound into the conv's scale source)
+        and marks them ready."""
         A = self.arena
         feed = P is not None and P.dy is not None
         ops.bn_bwd(dz, z, y, A.param(f"{name}/gamma"), s["mean"][name], s["inv"][name], dy, A.grad_of(f"{name}/gamma"),
                    A.grad_of(f"{name}/beta"), act=act, alpha=ALPHA, drop_rate=drop_rate, beta=beta, ws=ws,
                    dy_planes=plane_rows(P.dy, dy, 0) if feed else None, segments=self.halves,
-                   dy_fp32=not (feed and DY_PLANES_ONLY))
+                   dy_fp32=not (feed and DY_PLANES_ONLY), dy_bound=self.gbound[k] if feed else None)
         if feed:
             P._filled(ops.TENSOR_DY)
 
@@ -430,7 +466,7 @@ class GeneratorPlan:
             dy = self._dy(d, co)
             P = self._bwd_planes(8 + u)
             self._bn_bwd(s, name, self.dcat[u][..., :co], s["cat"][u][..., :co], s["yu"][u], dy, "relu", beta, ws,
-                         drop_rate=drop_rate if drop else 0.0, P=P if FEED_DY else None)
+                         drop_rate=drop_rate if drop else 0.0, P=P if FEED_DY else None, k=8 + u)
             hin = s["z8"] if u == 0 else s["cat"][u - 1]
             dhin = self.dz8 if u == 0 else self.dcat[u - 1]
             d.bwd_filter(hin, dy, A.grad_of(f"{name}/kernel"), beta=beta, ws=ws, planes=P)
@@ -445,7 +481,7 @@ class GeneratorPlan:
             dy = self._dy(d, co)
             P = self._bwd_planes(l)
             if bn:
-                self._bn_bwd(s, name, dz, z, s["yd"][l], dy, "lrelu", beta, ws, P=P if FEED_DY else None)
+                self._bn_bwd(s, name, dz, z, s["yd"][l], dy, "lrelu", beta, ws, P=P if FEED_DY else None, k=l)
             else:
                 ops.act_bwd(dz, z, dy, "lrelu", ALPHA)
             hin = s["x"] if l == 0 else self.z_view(s, l - 1)
@@ -491,9 +527,10 @@ class DiscriminatorPlan:
     the fake half runs on N-image descriptors over views of the same
     buffers.  `inp` is the [halves*N, H, W, 6] input buffer."""
 
-    def __init__(self, N, H, W, width, arena, bn_state, device, halves=1, train=True):
+    def __init__(self, N, H, W, width, arena, bn_state, device, halves=1, train=True, conv_math=None):
         self.N, self.H, self.W = N, H, W
         self.halves = halves
+        math_ = conv_math or P2P_MATH
         NT = N * halves
         self.arena, self.bn = arena, bn_state
         self.specs = d_layer_specs(width)
@@ -503,9 +540,9 @@ class DiscriminatorPlan:
             h, w = H, W
             for name, ci, co, _ in self.specs:
                 if name.startswith("down"):
-                    d = ConvDesc(n, h, w, ci, co, 4, 2, "same")
+                    d = ConvDesc(n, h, w, ci, co, 4, 2, "same", math=math_)
                 else:  # ZeroPadding2D() + Conv2D(k4, s1, 'valid') == explicit pad 1
-                    d = ConvDesc(n, h, w, ci, co, 4, 1, (1, 1, 1, 1))
+                    d = ConvDesc(n, h, w, ci, co, 4, 1, (1, 1, 1, 1), math=math_)
                 d.label = f"D.{name}"
                 out.append(d)
                 h, w = d.Ho, d.Wo
@@ -534,6 +571,15 @@ class DiscriminatorPlan:
             self.planes_half = (ops.plan_planes(self.desc_half, device, keep_x=False,
                                                 wbufs=[p.w for p in self.planes])
                                 if self.desc_half is not self.desc else self.planes)
+            # one dy bound per layer, shared by the full and the half-batch backward (in
+            # stream order, each BN backward rewrites it before its conv reads it)
+            self.gbound = grad_bounds(self.desc, self.planes, device)
+            if self.desc_half is not self.desc:
+                for i, (d, P) in enumerate(zip(self.desc_half, self.planes_half)):
+                    if FEED_DY and P is not None and P.dy is not None and P.dy.fmt == ops.PLANES_F16X3:
+                        if self.gbound[i] is None:
+                            self.gbound[i] = torch.zeros(8, dtype=torch.float32, device=device)
+                        d.set_grad_scale(dy_m=self.gbound[i])
         else:
             self.planes = self.planes_half = [None] * len(self.desc)
         # G path (train_pix2pix.py:64): of dL/d D([inp, G(x)]) only the G(x) channels 3..5
@@ -586,7 +632,7 @@ class DiscriminatorPlan:
                     ops.bn_fwd_train(y, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.mean[name],
                                      self.inv[name], self.bn.mean[name], self.bn.var[name], z, act="lrelu",
                                      alpha=ALPHA, momentum=BN_MOMENTUM, eps=BN_EPS, ws=ws,
-                                     z_planes=[(xrows(xp, 0, rows, co), co, 0)] if xp is not None else (),
+                                     z_planes=[zplanes(xp, rows, co, 0)] if xp is not None else (),
                                      segments=self.halves)
                 else:
                     for hv in range(self.halves):
@@ -637,7 +683,8 @@ class DiscriminatorPlan:
                                A.grad_of(f"{name}/gamma") if param_grads else None,
                                A.grad_of(f"{name}/beta") if param_grads else None, act="lrelu", alpha=ALPHA,
                                beta=beta, ws=ws, dy_planes=plane_rows(P.dy, dy, 0) if feed else None,
-                               segments=len(hs), dy_fp32=not (feed and DY_PLANES_ONLY))
+                               segments=len(hs), dy_fp32=not (feed and DY_PLANES_ONLY),
+                               dy_bound=self.gbound[i] if feed else None)
                     if feed:
                         P._filled(ops.TENSOR_DY)
                 else:

@@ -116,8 +116,8 @@ class PlaneBuf:
     tensor it stands for.  One PlaneBuf may serve several ConvPlanes: the
     weight planes of a network read by several plans, or one output-gradient
     scratch reused layer after layer.  fmt: PLANES_BF16X6, or PLANES_F16X3 for
-    the x planes of a descriptor whose forward runs fp16x3 (a producer writing
-    them needs to know)."""
+    the planes of a tensor that fp16x3 ops read (dg_conv_planes_format; a producer
+    writing them needs to know)."""
 
     __slots__ = ("buf", "ready", "fmt")
 
@@ -206,8 +206,11 @@ def plan_planes(descs, device=None, keep_x=True, wbufs=None):
             else None
         w = None
         if (m[0] | m[1]) & TENSOR_W:
-            w = wbufs[i] if wbufs is not None and wbufs[i] is not None else PlaneBuf(d.plane_bytes(TENSOR_W), device)
+            w = (wbufs[i] if wbufs is not None and wbufs[i] is not None
+                 else PlaneBuf(d.plane_bytes(TENSOR_W), device, d.plane_format(TENSOR_W)))
         dy = dy_buf.view(dy_need[i]) if dy_need[i] else None
+        if dy is not None:
+            dy.fmt = d.plane_format(TENSOR_DY)
         out.append(ConvPlanes(x, dy, w))
     return out
 
@@ -283,6 +286,14 @@ class ConvDesc:
                 raise DGError("a measured gradient max is 8 floats (per-workgroup shards)")
         self._gs = (dy_m, dy_g, dx_m, dx_g, dx_max)   # (keeps the views referenced)
         call("dg_conv_set_grad_scale", self._h, _p(dy_m), _p(dy_g), _p(dx_m), _p(dx_g), _p(dx_max))
+
+    def op_arith(self, op):
+        """'fp32' | 'bf16x6' | 'fp16' | 'f16x3': the arithmetic of op's GEMM (dg_conv_op_arith)."""
+        if isinstance(op, str):
+            op = {"fwd": OP_FWD, "bwd_data": OP_BWD_DATA, "bwd_filter": OP_BWD_FILTER}[op]
+        a = ctypes.c_int()
+        call("dg_conv_op_arith", self._h, op, ctypes.byref(a))
+        return ("fp32", "bf16x6", "fp16", "f16x3")[a.value]
 
     def plane_format(self, tensor):
         """PLANES_F16X3 for the x / w planes of a descriptor whose forward runs fp16x3."""
@@ -477,7 +488,7 @@ class ConvProfile:
         out = []
         for e0, e1, d, op in self.records:
             out.append(dict(op=op, label=getattr(d, "label", None), transpose=d.transpose,
-                            shape=(d.N, d.H, d.W, d.Cin, d.Cout, d.kh, d.sh),
+                            shape=(d.N, d.H, d.W, d.Cin, d.Cout, d.kh, d.sh), arith=d.op_arith(op),
                             flops=d.flops, bytes=d.op_bytes(op), ms=e0.elapsed_time(e1)))
         return out
 
@@ -544,10 +555,12 @@ def bn_fwd_infer(y, gamma, beta, moving_mean, moving_var, z, act="none", alpha=0
 
 
 def bn_bwd(dz, z, y, gamma, save_mean, save_invstd, dy, dgamma, dbeta, act="none", alpha=0.3, drop_rate=0.0,
-           beta=0.0, ws=None, dy_planes=None, segments=1, dy_fp32=True, f16_out=None):
+           beta=0.0, ws=None, dy_planes=None, segments=1, dy_fp32=True, f16_out=None, dy_bound=None):
     """dy_planes: a uint8 device tensor (e.g. a slice of a ConvPlanes' dy
-    PlaneBuf) that also receives dy's bf16x6 planes; dy_fp32=False then skips
-    the fp32 dy (its consumers read the planes; dy only gives the shape).
+    PlaneBuf) that also receives dy's bf16x6 planes -- or, with dy_bound (8 device
+    floats, the consuming conv's dy scale source), its fp16x3 planes scaled from the
+    bound written there (dg_bn_bwd_seg_x); dy_fp32=False then skips the fp32 dy (its
+    consumers read the planes; dy only gives the shape).
     segments: see bn_fwd_train (dg_bn_bwd_seg; dgamma / dbeta summed over the
     segments).  f16_out: the producing fp16 conv's dy PlaneBuf (dy's fp16 copy)."""
     C = y.shape[-1]
@@ -559,11 +572,14 @@ def bn_bwd(dz, z, y, gamma, save_mean, save_invstd, dy, dgamma, dbeta, act="none
     buf, n = ws.get(bn_workspace_bytes(M, C, segments))
     if act_id(act) == 0 and drop_rate == 0.0:
         z = None   # a linear BN's backward does not read z (dg_bn_bwd_seg_h)
-    call("dg_bn_bwd_seg_h", segments, M, C, _p(dz), pix_ld(dz, C), _p(z), pix_ld(z, C) if z is not None else C,
+    if dy_bound is not None and dy_bound.numel() < 8:
+        raise DGError("a gradient bound is 8 floats (per-workgroup shards)")
+    call("dg_bn_bwd_seg_x", segments, M, C, _p(dz), pix_ld(dz, C), _p(z), pix_ld(z, C) if z is not None else C,
          _p(y), pix_ld(y, C),
          _p(gamma), _p(save_mean), _p(save_invstd), act_id(act), float(alpha), float(drop_rate),
          _p(dy) if (dy_fp32 or dy_planes is None) else None, pix_ld(dy, C),
-         None if dy_planes is None else dy_planes.data_ptr(), _f16(f16_out),
+         None if dy_planes is None else dy_planes.data_ptr(),
+         PLANES_F16X3 if dy_bound is not None else PLANES_BF16X6, _p(dy_bound), _f16(f16_out),
          _p(dgamma), _p(dbeta), float(beta), _p(buf), n, _stream())
     return dy
 

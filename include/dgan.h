@@ -168,6 +168,10 @@ int dg_conv_set_grad_scale(dg_conv_t d, const float *dy_m, const float *dy_g, co
  * them; the max is their max): the measured max of a gradient entering an fp16x3 input
  * gradient from fp32 */
 int dg_absmax(const float *x, int64_t rows, int C, int ld, float *out, dg_stream_t stream);
+/* the arithmetic op's GEMM runs in (DG_MATH_*: fp32 for the exact direct kernels -- Co 1,
+ * narrow, small-Cin -- and fp32 MFMA tiles; bf16x6, fp16 or fp16x3 for the split kernels):
+ * per-op peaks for a roofline */
+int dg_conv_op_arith(dg_conv_t d, int op, int *arith);
 int dg_conv_op_planes(dg_conv_t d, int op, int *tensors);
 int dg_conv_fwd_pl(dg_conv_t d, const float *x, int ldx, const float *w, const float *bias,
                    float *y, int ldy, float beta, int act, float alpha,
@@ -302,6 +306,20 @@ int dg_bn_bwd_seg_h(int S, int M, int C, const float *dz, int lddz, const float 
                     int act, float alpha, float drop_rate,
                     float *dy, int lddy, void *dy_planes, void *dy_f16, float *dgamma, float *dbeta, float beta,
                     void *ws, size_t ws_bytes, dg_stream_t stream);
+/* dg_bn_bwd_seg_h with the format of the dy planes: DG_PLANES_F16X3 writes the consuming
+ * DG_MATH_F16X3 conv's fp16x3 dy planes (C % 32 == 0), scaled by x3 scale 2^(14 - e) from
+ * dy's bound b < 2^e -- b = max over channels of |A| max|dbn| + |B| max|y - mean| + |D|
+ * >= max |dy| (dy = A dbn + B (y - mean) + D per channel), written into dy_bound (8 floats:
+ * the bound's per-workgroup shards, their max is b) -- the buffer to pass that conv as its dy
+ * scale source (dg_conv_set_grad_scale dy_m, dy_g NULL).  In the forward calls above a
+ * NEGATIVE zp*C names the consumer's fp16x3 x planes of -zp*C channels (column and C
+ * multiples of 32). */
+int dg_bn_bwd_seg_x(int S, int M, int C, const float *dz, int lddz, const float *z, int ldz,
+                    const float *y, int ldy, const float *gamma,
+                    const float *save_mean, const float *save_invstd,
+                    int act, float alpha, float drop_rate,
+                    float *dy, int lddy, void *dy_planes, int dy_planes_format, float *dy_bound, void *dy_f16,
+                    float *dgamma, float *dbeta, float beta, void *ws, size_t ws_bytes, dg_stream_t stream);
 /* dy = dz * act'(z)  for blocks without BN (pix2pix.py:118-121 with apply_batchnorm=False) */
 int dg_act_bwd(int M, int C, const float *dz, int lddz, const float *z, int ldz,
                int act, float alpha, float *dy, int lddy, dg_stream_t stream);

@@ -44,7 +44,9 @@ DEV = "cuda"
 # the same step conditioned on the GPU's decisions holds max-abs 1e-4
 # (tests/test_step_gpu.py::test_step_parity_with_vgg_content) and the
 # content-free bs16 fixture (p2p_bs16_core) holds max-abs 1e-4 unconditioned.
-VGG_TIE_REL = 2e-3
+# (the fp16x3 G / D of the default conv math resolve more of those near-ties differently: measured
+# 2.3e-3 of down1/kernel's 0.95 at r4; the bf16x6 G / D keep 2e-3)
+VGG_TIE_REL = {"bf16x6": 2e-3, "f16x3": 4e-3}
 # The SR-family generators decide ReLU / PReLU / max-pool branches themselves
 # (SRGAN's residual blocks, the autoencoder's 15 ReLU convs and 5 pools), and
 # their discriminators' LeakyReLU(0.2) inputs tie within fp32 rounding (see
@@ -119,6 +121,7 @@ def test_pix2pix_bs16_matches_golden(case):
     mask-conditioned max-abs 1e-4 check at full width is owned by
     tests/test_step_gpu.py::test_step_parity_with_vgg_content[full_width]."""
     from pix2pix import Pix2Pix
+    from dgan import nets
     meta, d = load(case)
     content = bool(meta["content"])
     m = Pix2Pix(Args(crop_size=meta["H"], width=1, seed=meta["seed"], dropout_seed=meta["drop_seed"],
@@ -138,7 +141,7 @@ def test_pix2pix_bs16_matches_golden(case):
     assert np.abs(zr - d["s1|logits_real"]).max() < 1e-4
     assert np.abs(zf - d["s1|logits_fake"]).max() < 1e-4
     r = _check_step1(d, loss, tr.gen_output, y, m.generator.arena, m.discriminator.arena, m.generator.bn.export(),
-                     m.discriminator.bn.export(), 8, case, g_rel=VGG_TIE_REL if content else 0.0)
+                     m.discriminator.bn.export(), 8, case, g_rel=VGG_TIE_REL[nets.P2P_MATH] if content else 0.0)
     print(f"{case} vs golden: |dPSNR| {r[0]:.2e} dB, worst G grad {r[1]}, worst D grad {r[2]}")
     x2, y2 = batch(meta, meta["batch_seeds"][1])
     loss2 = tr.step(torch.from_numpy(x2).to(DEV), torch.from_numpy(y2).to(DEV))

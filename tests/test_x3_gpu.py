@@ -1,13 +1,12 @@
-"""The fp16x3 forward of the frozen VGG19 (include/dgan.h DG_MATH_F16X3): every
-3x3 stride-1 Conv2D with Cin % 32 == 0 and Cout > 32 (keras VGG19 blocks 1-5
-after block1_conv1, as built by pix2pix.py:53-67 / srgan.py:70-76) runs its
-forward GEMM as three fp16 piece products of pre-scaled operands
-(s x = h + l, h.h' + l.h' + h.l') on the halo kernel (conv_x6h.hip NI 4).
+"""The fp16x3 conv math (include/dgan.h DG_MATH_F16X3): three fp16 piece products of
+pre-scaled operands (s x = h + l, h.h' + l.h' + h.l') -- the frozen VGG19's 3x3 stride-1
+layers on the halo kernel (conv_x6h.hip NI 4; keras VGG19 blocks 1-5 after block1_conv1,
+as built by pix2pix.py:53-67 / srgan.py:70-76) and the pix2pix G / D layers on the
+implicit-GEMM kernel (conv_x6.hip NI 4; pix2pix.py:110-142, :194-220).
 
   * the layer against a torch fp64 reference at the conv engine's fp32 bar
     (test_conv_gpu.py _close: relative L2 < 2e-6, max-abs < 1e-5 of scale),
-    forward, and the bf16x6 input / filter gradients of the same descriptor
-    reading the bf16x6 half of the shared weight planes;
+    forward, input and filter gradient (gradients scaled from their measured max);
   * the fp16x3 planes a producer writes beside its output (conv epilogue,
     fused pool epilogue, unfused max pool) are the bytes the layer's own split
     pass writes, so a fed forward is bit-identical to an unfed one;
@@ -34,6 +33,17 @@ X3_CASES = [
     ("x3.splitk", 2, 8, 8, 512, 512, 3, 1, "same", False, True),
     ("x3.valid", 2, 20, 22, 32, 64, 3, 1, "valid", False, False),
     ("x3.c48", 2, 16, 24, 96, 48, 3, 1, "same", False, True),
+    # the pix2pix G / D layers on the implicit-GEMM kernel (conv_x6.hip NI 4): 4x4 stride 2
+    # down / up (the input gradient's 4 sub-pixel phases, ConvT forward), ragged and odd
+    # sizes, the deep U-Net shapes (tiny M, split-K over 8192-16384 k), the PatchGAN's
+    # stride-1 4x4
+    ("x3.down", 2, 32, 32, 64, 128, 4, 2, "same", False, False),
+    ("x3.up", 2, 16, 16, 256, 64, 4, 2, "same", True, False),
+    ("x3.down.ragged", 3, 26, 40, 32, 64, 4, 2, "same", False, True),
+    ("x3.up.odd", 2, 9, 7, 64, 32, 4, 2, "same", True, True),
+    ("x3.deep", 4, 4, 4, 512, 512, 4, 2, "same", False, False),
+    ("x3.deep.up", 4, 2, 2, 1024, 512, 4, 2, "same", True, False),
+    ("x3.patch", 2, 18, 21, 64, 128, 4, 1, (1, 1, 1, 1), False, False),
 ]
 
 
@@ -54,13 +64,14 @@ def test_x3_layer_matches_fp64(case, monkeypatch):
 
 @gpu
 def test_x3_shared_weight_planes_serve_bwd_data():
-    """One weight PlaneBuf: the fp16x3 forward splits both halves ([fp16x3 | bf16x6]); the
-    input gradient reading the bf16x6 half equals the one that splits w itself."""
+    """One weight PlaneBuf: the fp16x3 forward splits it; the (fp16x3) input gradient reading
+    it equals the one that splits w itself.  Every reader of w runs fp16x3 here, so the buffer
+    holds no bf16x6 part (tensor_plane_bytes)."""
     N, H, W, Ci, Co = 2, 24, 32, 64, 128
     d = ops.ConvDesc(N, H, W, Ci, Co, 3, 1, "same", math="f16x3")
     x, w, dy = _rand((N, H, W, Ci), 1), _rand(d.weight_shape, 2, 0.05), _rand((N, H, W, Co), 3)
     P = ops.ConvPlanes.for_desc(d, x=True, dy=True, w=True)
-    assert P.w is not None and P.w.buf.numel() >= 10 * 9 * Ci * Co
+    assert P.w is not None and 4 * 9 * Ci * Co <= P.w.buf.numel() < 10 * 9 * Ci * Co
     y0, y1 = torch.empty(N, H, W, Co, device="cuda"), torch.empty(N, H, W, Co, device="cuda")
     d.fwd(x, w, y0)
     d.fwd(x, w, y1, planes=P)
