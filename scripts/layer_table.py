@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
 """Per-layer conv table of one pix2pix bs16 training step (HIP events per conv
 call, dgan.ops.ConvProfile), grouped by layer geometry and op, as a markdown
-table: GFLOP, ms, TF/s (fp32-equivalent) and the fraction of the bf16x6
-basis (bf16 dense peak / 6 = 419.4 TF/s), plus each op's own roofline: the
-larger of its MFMA time at the basis and its HBM time for the algorithmic fp32
-operand bytes (x, w, y once each) at 8 TB/s -- narrow layers (Cin 3/6, Cout
-1/3) and the deep U-Net layers (M = 32..512 rows) are HBM- or weight-bound,
-and `roof` is their fraction of that bound.
+table: GFLOP, ms, TF/s (fp32-equivalent), the arithmetic of the op's GEMM
+(ops.ConvDesc.op_arith) and the fraction of that arithmetic's dense MFMA peak
+(fp16x3: bf16 peak / 3 = 838.9 TF/s, bf16x6: / 6 = 419.4, fp16: / 1, fp32 MFMA
+157.3), plus each op's own roofline: the larger of its MFMA time at that peak
+and its HBM time for the algorithmic fp32 operand bytes (x, w, y once each) at
+8 TB/s -- narrow layers (Cin 3/6, Cout 1/3) and the deep U-Net layers (M = 32..512
+rows) are HBM- or weight-bound, and `roof` is their fraction of that bound.
 
     python scripts/layer_table.py [--content 0|1] [--steps 3] > profiles/...md
 """
@@ -22,6 +23,7 @@ import torch  # noqa: E402
 
 BASIS = 2516.6e12 / 6
 HBM = 8.0e12
+PEAK = {"fp32": 157.3e12, "bf16x6": 2516.6e12 / 6, "fp16": 2516.6e12, "f16x3": 2516.6e12 / 3}
 
 
 def main():
@@ -64,32 +66,35 @@ def main():
         for r in prof.summary():
             N, H, W, Ci, Co, k, s = r["shape"]
             net, layer = (r["label"] or "?.?").split(".", 1)
-            key = (net, layer + (" (T)" if r["transpose"] else ""), r["op"], N, H, W, Ci, Co, k, s)
+            key = (net, layer + (" (T)" if r["transpose"] else ""), r["op"], N, H, W, Ci, Co, k, s, r["arith"])
             agg[key][0] += 1
             agg[key][1] += r["flops"]
             agg[key][2] += r["ms"]
             agg[key][3] += r["bytes"]
     rows = sorted(agg.items(), key=lambda kv: -kv[1][2])
-    tot = defaultdict(lambda: [0.0, 0.0])
-    print(f"| net | layer | op | N | H x W | Cin -> Cout | k/s | calls/step | GFLOP/step | MB/step | ms/step | TF/s | "
-          f"frac | bound | roof |")
-    print("|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|")
-    for (net, kind, op, N, H, W, Ci, Co, k, s), (n, fl, ms, by) in rows:
+    tot = defaultdict(lambda: [0.0, 0.0, 0.0])
+    print(f"| net | layer | op | N | H x W | Cin -> Cout | k/s | arith | calls/step | GFLOP/step | MB/step | ms/step | "
+          f"TF/s | frac | bound | roof |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|")
+    for (net, kind, op, N, H, W, Ci, Co, k, s, ar), (n, fl, ms, by) in rows:
         fl /= a.steps; ms /= a.steps; by /= a.steps
-        tot[net][0] += fl; tot[net][1] += ms
+        peak = BASIS if ar == "fp16" and BASIS != PEAK["bf16x6"] else PEAK[ar]
+        tot[net][0] += fl; tot[net][1] += ms; tot[net][2] += fl / peak
         tf = fl / (ms * 1e-3) / 1e12
-        t_mfma, t_hbm = fl / BASIS, by / HBM
+        t_mfma, t_hbm = fl / peak, by / HBM
         bound = "mfma" if t_mfma >= t_hbm else "hbm"
         roof = max(t_mfma, t_hbm) / (ms * 1e-3)
-        print(f"| {net} | {kind} | {op} | {N} | {H}x{W} | {Ci}->{Co} | {k}/{s} | {n // a.steps} | {fl / 1e9:.1f} | "
-              f"{by / 1e6:.0f} | {ms:.3f} | {tf:.1f} | {tf * 1e12 / BASIS:.3f} | {bound} | {roof:.3f} |")
+        print(f"| {net} | {kind} | {op} | {N} | {H}x{W} | {Ci}->{Co} | {k}/{s} | {ar} | {n // a.steps} | "
+              f"{fl / 1e9:.1f} | {by / 1e6:.0f} | {ms:.3f} | {tf:.1f} | {tf * 1e12 / peak:.3f} | {bound} | {roof:.3f} |")
     print()
-    for net, (fl, ms) in sorted(tot.items()):
+    for net, (fl, ms, tp) in sorted(tot.items()):
         tf = fl / (ms * 1e-3) / 1e12
-        print(f"- {net}: {fl / 1e9:.1f} GFLOP in {ms:.3f} ms/step = {tf:.1f} TF/s = {tf * 1e12 / BASIS:.3f} of the basis")
-    fl = sum(v[0] for v in tot.values()); ms = sum(v[1] for v in tot.values())
+        print(f"- {net}: {fl / 1e9:.1f} GFLOP in {ms:.3f} ms/step = {tf:.1f} TF/s = {tp / (ms * 1e-3):.3f} of its "
+              f"ops' arithmetic peaks ({tf * 1e12 / PEAK['bf16x6']:.3f} of the bf16x6 basis)")
+    fl = sum(v[0] for v in tot.values()); ms = sum(v[1] for v in tot.values()); tp = sum(v[2] for v in tot.values())
     print(f"- all convs: {fl / 1e9:.1f} GFLOP in {ms:.3f} ms/step = {fl / (ms * 1e-3) / 1e12:.1f} TF/s = "
-          f"{fl / (ms * 1e-3) / BASIS:.3f} of the basis")
+          f"{tp / (ms * 1e-3):.3f} of the ops' arithmetic peaks ({fl / (ms * 1e-3) / PEAK['bf16x6']:.3f} of the bf16x6 "
+          f"basis)")
 
 
 if __name__ == "__main__":
