@@ -1452,10 +1452,9 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     // is bf16x6 wherever its fp16x3 forward does not apply)
     x6_ok = x6_ok && (math == DG_MATH_BF16X6 || math == DG_MATH_F16X3) && 6.0 * ra * ca < 2.0e9 &&
             6.0 * rb * cb < 2.0e9 && g.kh * g.kw <= 32;
-    // (an fp16x3-eligible forward -- DG_MATH_F16X3, 3x3 stride 1, Cin % 32 == 0, Cout % 16 == 0,
-    // Cout > 32 -- takes the split-precision path whatever the fp32 estimate: see hx3 below)
-    // (input gradient, plan_all: only where the forward runs fp16x3 -- Cout % 32 == 0 chunks the
-    // reduction over output channels, Cin % 16 == 0 and Cin > 32 the BN 64 / 128 tiles)
+    // (DG_MATH_F16X3: the halo kernel's fp16x3 form for 3x3 stride-1 forwards (Cin % 32 == 0,
+    // Cout % 16 == 0, Cout > 32) and input gradients (Cout % 32 == 0 chunks the reduction over
+    // output channels, Cin % 16 == 0 and Cin > 32 the BN 64 / 128 tiles), see hx3 below)
     const bool x3_geom = math == DG_MATH_F16X3 && g.kh == 3 && g.kw == 3 && g.sh == 1 && g.sw == 1 &&
                          !plan_off("x3") && !plan_off("halo") &&
                          ((mode == MODE_FWD && g.Ci % 32 == 0 && g.Co % 16 == 0 && g.Co > 32) ||
@@ -1472,7 +1471,12 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         OpPlan p6 = pl;
         double t6 = choose_tiles(p6, kX6Cfgs, kNumX6Cfgs, 2516.6e12 / 6.0, "DG_FORCE_X6CFG", nullptr);
         t6 += (double)(ra * ca + rb * cb) * 10.0 / 4.0e12 + 4e-6;  // split passes: read 4 B, write 6 B
-        if (t6 < t32 || getenv("DG_FORCE_X6CFG") || x3_geom || x3_gen) {
+        // (the implicit-GEMM fp16x3 ops where the split path beats the fp32 tiles at all: on
+        // pix2pix's deepest layers (M 32..128 rows) the fp32 tiles win; DG_FORCE_X3: every
+        // eligible op, for the kernel tests at small sizes.  The halo kernel's fp16x3 3x3 layers
+        // stay forced: a VGG19 whose ops mix arithmetics is not planned -- the network picks its
+        // math by image size instead, sr_trainer.VGGNetwork)
+        if (t6 < t32 || getenv("DG_FORCE_X6CFG") || x3_geom || (x3_gen && getenv("DG_FORCE_X3"))) {
             pl = p6;
             pl.x6 = 1;
             pl.x6_ra = ra; pl.x6_ca = (int)ca; pl.x6_rb = rb; pl.x6_cb = (int)cb;

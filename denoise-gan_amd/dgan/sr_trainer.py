@@ -67,20 +67,31 @@ class VGGNetwork(GraphNetwork):
     "imagenet")); offline they load from a local .npz with Keras layer names
     (`vgg_weights`), else seeded He-normal weights stand in."""
 
+    # fp16x3 from this many pixels per image: pix2pix's 256^2 and FastSRGAN's 512^2 gain, the
+    # autoencoder's 64^2 VGG19 loses (bs4: 1036-1056 img/s vs 1074-1106 on bf16x6 / fp32 tiles) and
+    # SRGAN's 96^2 is even (4172-4176 vs 4183-4185), profiles/r4/ab_x3_small_layers.txt
+    X3_MIN_PIXELS = 128 * 128
+
     def __init__(self, weights=None, seed=4242, width=1, device=None):
         super().__init__(vgg19_features(width), seed=seed, device=device, kind="vgg19", trainable=False)
-        # the frozen network's forward GEMMs on fp16x3 (include/dgan.h DG_MATH_F16X3: three fp16
-        # piece products, half the bf16x6 MFMA count; its input gradients stay bf16x6) when the
-        # library default is bf16x6; DG_VGG_MATH overrides (e.g. "bf16x6" for A/B runs)
+        # the frozen network's GEMMs on fp16x3 (include/dgan.h DG_MATH_F16X3: three fp16 piece
+        # products, half the bf16x6 MFMA count) for large images when the library default is
+        # bf16x6 (plan()); DG_VGG_MATH overrides (e.g. "bf16x6" for A/B runs)
         vm = os.environ.get("DG_VGG_MATH")
+        self._auto_math = not vm and ops.default_conv_math() == ops.MATH_BF16X6
         if vm:
             self.conv_math = vm
-        elif ops.default_conv_math() == ops.MATH_BF16X6:
-            self.conv_math = "f16x3"
         self.pretrained = False
         if weights:
             self.load_weights(weights)
             self.pretrained = True
+
+
+    def plan(self, N, H, W, **kw):
+        # (a math the owner set -- "fp16" under mixed_float16, sr_models -- stays)
+        if self._auto_math and self.conv_math in (None, "f16x3"):
+            self.conv_math = "f16x3" if H * W >= self.X3_MIN_PIXELS else None
+        return super().plan(N, H, W, **kw)
 
 
 class ContentLoss:

@@ -22,6 +22,13 @@ from test_conv_gpu import _close, test_conv_layer
 
 gpu = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _force_x3(monkeypatch):
+    """Every fp16x3-eligible op on fp16x3, also where the planner would keep a small GEMM on the
+    fp32 tiles (csrc/conv.hip make_plan): these cases exercise the kernels at small sizes."""
+    monkeypatch.setenv("DG_FORCE_X3", "1")
+
 # (name, N, H, W, Cin, Cout, k, s, padding, transpose, bias): VGG19-like layers on
 # the fp16x3 halo kernel -- BN 64 / 128, ragged 8x16 patches, split-K over the
 # 32-channel chunks (small image, many channels), 'valid' padding, Cout 48 (BN 64 tile
