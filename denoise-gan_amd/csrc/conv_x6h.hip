@@ -51,6 +51,14 @@ constexpr bool kTapsColMajor = false;
 #else
 constexpr bool kTapsColMajor = true;
 #endif
+// fp16x3 weight prefetch distance: 2 (default) issues K-tile T+2 into the buffer
+// K-tile T has just read into registers (a second barrier per K-tile marks it
+// free); DG_X3H_DIST1 builds the one-ahead pipeline for same-box A/B runs
+#ifdef DG_X3H_DIST1
+constexpr int kX3Dist = 1;
+#else
+constexpr int kX3Dist = 2;
+#endif
 // PACKED (fp16x3): the NPL plane images lie back to back (HPX * 32 bytes each) and
 // only the whole halo is rounded up to KiB DMAs -- 23 KiB instead of 24 for KT 3,
 // which keeps two fp16x3 blocks (two halo buffers, two weight buffers) per CU
@@ -418,9 +426,13 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
                 }
             }
         }
-        if constexpr (X3) {   // the next weight tile first: the wait below leaves only the halo pieces in flight
+        if constexpr (X3 && kX3Dist == 1) {   // the next weight tile first: the wait below leaves only the halo pieces in flight
             if constexpr (T + 1 < NTAP) issue_b(T + 1, chunk, bn);
             else issue_b(0, chunk + 1, bn);
+        } else if constexpr (X3) {   // every wave holds this tile's fragments: its buffer takes tile T+2
+            barrier();
+            if constexpr (T + 2 < NTAP) issue_b(T + 2, chunk, const_cast<char *>(bc));
+            else issue_b(T + 2 - NTAP, chunk + 1, const_cast<char *>(bc));
         }
 #pragma unroll
         for (int s = H0P; s < H0P + NH; ++s) issue_h(s, chunk + 1, hn);
@@ -474,7 +486,8 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         // DMAs issued in this K-tile may stay in flight; everything older
         // (the next weight tile, and at the last tap the whole next halo) has landed
         // (fp16x3: the weight tile issued in THIS K-tile, before its halo pieces, too)
-        wait_dma_c<X3 ? NH : B_NJ + NH>();
+        // (fp16x3 distance 2: tile T+2's weights, issued in this K-tile, may stay in flight)
+        wait_dma_c<X3 && kX3Dist == 1 ? NH : B_NJ + NH>();
         barrier();
     };
     auto chunk_tiles = [&](auto PARc, int chunk, const char *hc, char *hn) __attribute__((always_inline)) {
@@ -487,7 +500,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
 #pragma unroll
     for (int s = 0; s < H_NJ; ++s) issue_h(s, cbeg, hal0);
     issue_b(0, cbeg, bs0);
-    if constexpr (X3) {
+    if constexpr (X3 && kX3Dist == 1) {
         wait_dma_c<0>();
     } else {
         issue_b(1, cbeg, bs1);
