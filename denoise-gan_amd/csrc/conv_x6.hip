@@ -440,6 +440,14 @@ k_conv_gemm_x6(const GemmArgs p) {
     // kt+2 .. kt+AHEAD are outstanding and crosses the barrier.  DMAs past nk
     // fetch harmless data into idle buffers.
     constexpr int AHEAD = NBUF - 1;
+    // fp16x3 with two buffers: tile kt+2 goes into the buffer tile kt has just
+    // read into registers (a second barrier per K-tile marks it free), so a DMA
+    // has two K-tiles of MFMAs to land instead of one (DG_X3_DIST1: one ahead)
+#ifdef DG_X3_DIST1
+    constexpr bool D2 = false;
+#else
+    constexpr bool D2 = X3 && NBUF == 2;
+#endif
     auto ktile = [&](int kt, const char *cur, char *nxt) __attribute__((always_inline)) {
         if constexpr (X3) {
             // fp16x3: A [h | h'] / [l | l'] of k 0..15 | 16..31; B the same pairs (KC
@@ -459,7 +467,12 @@ k_conv_gemm_x6(const GemmArgs p) {
                 bh[b] = __builtin_bit_cast(f16x8, frag(B0, B0 + BH1 * BPL, c0, B_KC, false));
                 bl[b] = __builtin_bit_cast(f16x8, frag(B0 + BL0 * BPL, B0 + 3 * BPL, c0, B_KC, false));
             }
-            issue_tile(kbeg + (kt + AHEAD) * BK, nxt);
+            if constexpr (D2) {
+                barrier();
+                issue_tile(kbeg + (kt + 2) * BK, const_cast<char *>(cur));
+            } else {
+                issue_tile(kbeg + (kt + AHEAD) * BK, nxt);
+            }
 #pragma unroll
             for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -475,7 +488,7 @@ k_conv_gemm_x6(const GemmArgs p) {
 #pragma unroll
                 for (int b = 0; b < TN; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[a], bl[b], acc[a][b], 0, 0, 0);
-            wait_dma_c<(AHEAD - 1) * NMINE>();
+            wait_dma_c<D2 ? NMINE : (AHEAD - 1) * NMINE>();
             barrier();
             return;
         }
@@ -517,9 +530,9 @@ k_conv_gemm_x6(const GemmArgs p) {
     };
     auto pipeline = [&](char *L0, char *L1, char *L2, char *L3) __attribute__((always_inline)) {
         issue_tile(kbeg, L0);
-        if constexpr (NBUF >= 3) issue_tile(kbeg + BK, L1);
+        if constexpr (NBUF >= 3 || D2) issue_tile(kbeg + BK, L1);
         if constexpr (NBUF == 4) issue_tile(kbeg + 2 * BK, L2);
-        wait_dma_c<(AHEAD - 1) * NMINE>();
+        wait_dma_c<D2 ? NMINE : (AHEAD - 1) * NMINE>();
         barrier();
         int kt = 0;
         if constexpr (NBUF == 2) {

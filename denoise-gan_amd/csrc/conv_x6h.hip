@@ -168,7 +168,8 @@ __device__ __forceinline__ void for_taps(F &&f, std::integer_sequence<int, T...>
 // 0-15 / 16-31), and three fp16 MFMAs over the 32 channels cover its three
 // piece products: [h0|h1].[w_h0|w_h1] + [l0|l1].[w_h0|w_h1] + [h0|h1].[w_l0|w_l1]
 // (= h.w_h + l.w_h + h.w_l) -- two A and two B fragment reads per K-tile.  Two
-// weight buffers (one K-tile ahead) and packed halo images keep two blocks per CU.
+// weight buffers and packed halo images keep two blocks per CU; a K-tile's buffer
+// takes tile T+2 once every wave holds its fragments (kX3Dist).
 template <int MODE, int BN, bool POOL, int KT, int NI = 3>
 __global__ void __launch_bounds__(256, 2)
 k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
