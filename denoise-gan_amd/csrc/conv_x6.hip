@@ -440,14 +440,19 @@ k_conv_gemm_x6(const GemmArgs p) {
     // kt+2 .. kt+AHEAD are outstanding and crosses the barrier.  DMAs past nk
     // fetch harmless data into idle buffers.
     constexpr int AHEAD = NBUF - 1;
-    // fp16x3 with two buffers: tile kt+2 goes into the buffer tile kt has just
-    // read into registers (a second barrier per K-tile marks it free), so a DMA
-    // has two K-tiles of MFMAs to land instead of one (DG_X3_DIST1: one ahead)
-#ifdef DG_X3_DIST1
-    constexpr bool D2 = false;
+    // MIDB: tile kt+NBUF goes into the buffer tile kt has just read into
+    // registers (a second barrier per K-tile marks it free), so a DMA has NBUF
+    // K-tiles of MFMAs to land instead of NBUF-1 (fp16x3 two-buffer tiles: 870
+    // -> 919 img/s pix2pix; bf16x6 / fp16: SRGAN 4175 -> 4227).  DG_NO_MIDB
+    // builds the plain pipeline, DG_MIDB_X3 the fp16x3-only form, for A/B runs
+#if defined(DG_NO_MIDB)
+    constexpr bool MIDB = false;
+#elif defined(DG_MIDB_X3)
+    constexpr bool MIDB = X3;
 #else
-    constexpr bool D2 = X3 && NBUF == 2;
+    constexpr bool MIDB = true;
 #endif
+    constexpr int DIST = MIDB ? NBUF : AHEAD;
     auto ktile = [&](int kt, const char *cur, char *nxt) __attribute__((always_inline)) {
         if constexpr (X3) {
             // fp16x3: A [h | h'] / [l | l'] of k 0..15 | 16..31; B the same pairs (KC
@@ -467,9 +472,9 @@ k_conv_gemm_x6(const GemmArgs p) {
                 bh[b] = __builtin_bit_cast(f16x8, frag(B0, B0 + BH1 * BPL, c0, B_KC, false));
                 bl[b] = __builtin_bit_cast(f16x8, frag(B0 + BL0 * BPL, B0 + 3 * BPL, c0, B_KC, false));
             }
-            if constexpr (D2) {
+            if constexpr (MIDB) {
                 barrier();
-                issue_tile(kbeg + (kt + 2) * BK, const_cast<char *>(cur));
+                issue_tile(kbeg + (kt + DIST) * BK, const_cast<char *>(cur));
             } else {
                 issue_tile(kbeg + (kt + AHEAD) * BK, nxt);
             }
@@ -488,7 +493,7 @@ k_conv_gemm_x6(const GemmArgs p) {
 #pragma unroll
                 for (int b = 0; b < TN; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[a], bl[b], acc[a][b], 0, 0, 0);
-            wait_dma_c<D2 ? NMINE : (AHEAD - 1) * NMINE>();
+            wait_dma_c<(DIST - 1) * NMINE>();
             barrier();
             return;
         }
@@ -499,7 +504,12 @@ k_conv_gemm_x6(const GemmArgs p) {
             bf16x8 dA[TM], dB[TN];
             read_frags(cur, ahm, dA, b1, dB, dB);
         }
-        issue_tile(kbeg + (kt + AHEAD) * BK, nxt);
+        if constexpr (MIDB) {
+            barrier();
+            issue_tile(kbeg + (kt + DIST) * BK, const_cast<char *>(cur));
+        } else {
+            issue_tile(kbeg + (kt + AHEAD) * BK, nxt);
+        }
         if constexpr (X6) {
 #pragma unroll
             for (int a = 0; a < TM; ++a)
@@ -525,14 +535,16 @@ k_conv_gemm_x6(const GemmArgs p) {
                                                                        __builtin_bit_cast(f16x8, b1[b]), acc[a][b],
                                                                        0, 0, 0);
         }
-        wait_dma_c<(AHEAD - 1) * NMINE>();
+        wait_dma_c<(DIST - 1) * NMINE>();
         barrier();
     };
     auto pipeline = [&](char *L0, char *L1, char *L2, char *L3) __attribute__((always_inline)) {
+        // the first DIST tiles (MIDB: one per buffer)
         issue_tile(kbeg, L0);
-        if constexpr (NBUF >= 3 || D2) issue_tile(kbeg + BK, L1);
-        if constexpr (NBUF == 4) issue_tile(kbeg + 2 * BK, L2);
-        wait_dma_c<D2 ? NMINE : (AHEAD - 1) * NMINE>();
+        if constexpr (DIST >= 2) issue_tile(kbeg + BK, L1);
+        if constexpr (DIST >= 3) issue_tile(kbeg + 2 * BK, L2);
+        if constexpr (DIST >= 4) issue_tile(kbeg + 3 * BK, L3);
+        wait_dma_c<(DIST - 1) * NMINE>();
         barrier();
         int kt = 0;
         if constexpr (NBUF == 2) {
