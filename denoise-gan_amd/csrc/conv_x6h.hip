@@ -51,13 +51,16 @@ constexpr bool kTapsColMajor = false;
 #else
 constexpr bool kTapsColMajor = true;
 #endif
-// fp16x3 weight prefetch distance: 2 (default) issues K-tile T+2 into the buffer
-// K-tile T has just read into registers (a second barrier per K-tile marks it
-// free); DG_X3H_DIST1 builds the one-ahead pipeline for same-box A/B runs
-#ifdef DG_X3H_DIST1
-constexpr int kX3Dist = 1;
+// Weight prefetch through a mid-K-tile barrier (as conv_x6.hip): once every wave
+// holds K-tile T's fragments in registers, its buffer takes tile T+NB, so a DMA
+// has NB K-tiles of MFMAs to land instead of NB-1.  DG_NO_MIDB builds the plain
+// pipelines, DG_MIDB_X3 the fp16x3-only form, for same-box A/B runs.
+#if defined(DG_NO_MIDB)
+constexpr int kMidb = 0;
+#elif defined(DG_MIDB_X3)
+constexpr int kMidb = 1;
 #else
-constexpr int kX3Dist = 2;
+constexpr int kMidb = 2;
 #endif
 // PACKED (fp16x3): the NPL plane images lie back to back (HPX * 32 bytes each) and
 // only the whole halo is rounded up to KiB DMAs -- 23 KiB instead of 24 for KT 3,
@@ -169,7 +172,7 @@ __device__ __forceinline__ void for_taps(F &&f, std::integer_sequence<int, T...>
 // piece products: [h0|h1].[w_h0|w_h1] + [l0|l1].[w_h0|w_h1] + [h0|h1].[w_l0|w_l1]
 // (= h.w_h + l.w_h + h.w_l) -- two A and two B fragment reads per K-tile.  Two
 // weight buffers and packed halo images keep two blocks per CU; a K-tile's buffer
-// takes tile T+2 once every wave holds its fragments (kX3Dist).
+// takes tile T+2 once every wave holds its fragments (MIDB).
 template <int MODE, int BN, bool POOL, int KT, int NI = 3>
 __global__ void __launch_bounds__(256, 2)
 k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
@@ -195,6 +198,21 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     constexpr int H_NJ = (HG::HDMA + NW - 1) / NW;          // halo pieces per wave
     constexpr int PPT = (H_NJ + NTAP - 2) / (NTAP - 1);     // pieces per K-tile, none at the last tap
     static_assert((H_NJ - 1) / PPT < NTAP - 1, "the next chunk's halo lands by the chunk's last K-tile");
+    constexpr int TL = (H_NJ - 1) / PPT;                    // the last tap position issuing halo pieces
+    // mid-K-tile barrier form: needs the last NB-1 tap positions free of halo pieces
+    // (the wait counts below), so not the KT 2 phases (4 taps, 4 buffers)
+    constexpr bool MIDB = (kMidb == 2 || (kMidb == 1 && X3)) && TL <= NTAP - NB;
+    constexpr auto nh_of = [](int t) constexpr {   // halo pieces issued at tap position t (t < 0: t + NTAP)
+        t = t < 0 ? t + NTAP : t;
+        const int h0 = t * PPT, h1 = (t + 1) * PPT < H_NJ ? (t + 1) * PPT : H_NJ;
+        return h1 > h0 ? h1 - h0 : 0;
+    };
+    constexpr auto midb_wait_v = [nh_of](int T) constexpr {
+        int n = (NB - 1) * B_NJ;
+        for (int j = 0; j < NB; ++j) n += nh_of(T - j);
+        const int last = (NTAP - 1 - TL) * B_NJ;
+        return T == NTAP - 1 && last < n ? last : n;
+    };
 
     __shared__ __attribute__((aligned(16))) char hal[2][HG::BYTES];
     __shared__ __attribute__((aligned(16))) char bs0[BBUF];
@@ -427,17 +445,17 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
                 }
             }
         }
-        if constexpr (X3 && kX3Dist == 1) {   // the next weight tile first: the wait below leaves only the halo pieces in flight
+        if constexpr (MIDB) {   // every wave holds this tile's fragments: its buffer takes tile T+NB
+            barrier();
+            if constexpr (T + NB < NTAP) issue_b(T + NB, chunk, const_cast<char *>(bc));
+            else issue_b(T + NB - NTAP, chunk + 1, const_cast<char *>(bc));
+        } else if constexpr (X3) {   // the next weight tile first: the wait below leaves only the halo pieces in flight
             if constexpr (T + 1 < NTAP) issue_b(T + 1, chunk, bn);
             else issue_b(0, chunk + 1, bn);
-        } else if constexpr (X3) {   // every wave holds this tile's fragments: its buffer takes tile T+2
-            barrier();
-            if constexpr (T + 2 < NTAP) issue_b(T + 2, chunk, const_cast<char *>(bc));
-            else issue_b(T + 2 - NTAP, chunk + 1, const_cast<char *>(bc));
         }
 #pragma unroll
         for (int s = H0P; s < H0P + NH; ++s) issue_h(s, chunk + 1, hn);
-        if constexpr (!X3) {
+        if constexpr (!X3 && !MIDB) {
             if constexpr (T + 2 < NTAP) issue_b(T + 2, chunk, bn);
             else issue_b(T + 2 - NTAP, chunk + 1, bn);
         }
@@ -487,8 +505,10 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         // DMAs issued in this K-tile may stay in flight; everything older
         // (the next weight tile, and at the last tap the whole next halo) has landed
         // (fp16x3: the weight tile issued in THIS K-tile, before its halo pieces, too)
-        // (fp16x3 distance 2: tile T+2's weights, issued in this K-tile, may stay in flight)
-        wait_dma_c<X3 && kX3Dist == 1 ? NH : B_NJ + NH>();
+        // (MIDB: the DMAs issued after tile T+1's weights -- tiles T+2 .. T+NB and the
+        // halo pieces of K-tiles T+1-NB .. T -- may stay in flight; at the chunk's last
+        // tap none issued before the last halo piece)
+        wait_dma_c<MIDB ? midb_wait_v(T) : (X3 ? NH : B_NJ + NH)>();
         barrier();
     };
     auto chunk_tiles = [&](auto PARc, int chunk, const char *hc, char *hn) __attribute__((always_inline)) {
@@ -501,7 +521,12 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
 #pragma unroll
     for (int s = 0; s < H_NJ; ++s) issue_h(s, cbeg, hal0);
     issue_b(0, cbeg, bs0);
-    if constexpr (X3 && kX3Dist == 1) {
+    if constexpr (MIDB) {   // one weight tile per buffer
+        issue_b(1, cbeg, bs1);
+        if constexpr (NB >= 3) issue_b(2, cbeg, bs2);
+        if constexpr (NB >= 4) issue_b(3, cbeg, bs3);
+        wait_dma_c<(NB - 1) * B_NJ>();
+    } else if constexpr (X3) {
         wait_dma_c<0>();
     } else {
         issue_b(1, cbeg, bs1);
