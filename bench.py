@@ -207,6 +207,9 @@ def main():
                     trainer.step(x, y)
                 torch.cuda.current_stream().wait_stream(s)
                 torch.cuda.synchronize()
+                if distributed:
+                    from dgan.dist import settle_before_capture
+                    settle_before_capture()
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph):
                     trainer.step(x, y)

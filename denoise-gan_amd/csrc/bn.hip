@@ -159,15 +159,6 @@ k_bn_stats_partial(const float *__restrict__ y, int ld, long M, int C, long rows
 constexpr int FIN_C = 16, FIN_L = 16, FIN_K = 16;
 static_assert(FIN_L * FIN_K >= 256, "bn_plan's 256 chunks fit the finalize lanes");
 
-__device__ __forceinline__ float lane_max16(float v, float *sh, int cl, int ln) {
-    sh[ln * FIN_C + cl] = v;
-    __syncthreads();
-    float s = 0.f;
-#pragma unroll
-    for (int l = 0; l < FIN_L; ++l) s = fmaxf(s, sh[l * FIN_C + cl]);
-    __syncthreads();
-    return s;
-}
 __device__ __forceinline__ float lane_sum16(float v, float *sh, int cl, int ln) {
     sh[ln * FIN_C + cl] = v;
     __syncthreads();
@@ -178,6 +169,34 @@ __device__ __forceinline__ float lane_sum16(float v, float *sh, int cl, int ln) 
     return s;
 }
 
+// two (or four: sum, sum, max, max) 16-lane reductions through one LDS round, each
+// in lane_sum16's order (bit-identical to separate calls, fewer barriers)
+__device__ __forceinline__ void lane_sum16x2(float a, float b, float &sa, float &sb, float *sh, int cl, int ln) {
+    sh[ln * FIN_C + cl] = a;
+    sh[256 + ln * FIN_C + cl] = b;
+    __syncthreads();
+    sa = 0.f; sb = 0.f;
+#pragma unroll
+    for (int l = 0; l < FIN_L; ++l) { sa += sh[l * FIN_C + cl]; sb += sh[256 + l * FIN_C + cl]; }
+    __syncthreads();
+}
+__device__ __forceinline__ void lane_red16x4(float (&v)[4], float *sh, int cl, int ln) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sh[j * 256 + ln * FIN_C + cl] = v[j];
+    __syncthreads();
+    float r[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int l = 0; l < FIN_L; ++l) {
+        r[0] += sh[l * FIN_C + cl];
+        r[1] += sh[256 + l * FIN_C + cl];
+        r[2] = fmaxf(r[2], sh[512 + l * FIN_C + cl]);
+        r[3] = fmaxf(r[3], sh[768 + l * FIN_C + cl]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = r[j];
+}
+
 // segments in order: segment s's statistics normalise its rows, and the moving
 // averages take the segments' updates one after the other (the reference's
 // separate BN calls, e.g. G(x) then G(y))
@@ -185,7 +204,7 @@ __global__ void __launch_bounds__(256)
 k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, int C, int S, const float *gamma,
                  const float *beta, float *save_mean, float *save_invstd, float *mm, float *mv, float momentum,
                  float eps, float *scale, float *shift) {
-    __shared__ float sh[256];
+    __shared__ float sh[2 * 256];
     const int cl = threadIdx.x % FIN_C, ln = threadIdx.x / FIN_C;
     const int c = blockIdx.x * FIN_C + cl;
     const bool cok = c < C;
@@ -209,8 +228,8 @@ k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, i
         float sn = 0.f, sm = 0.f;
 #pragma unroll
         for (int k = 0; k < FIN_K; ++k) { sn += vn[k]; sm += vn[k] * vm[k]; }
-        const float n = lane_sum16(sn, sh, cl, ln);
-        const float msum = lane_sum16(sm, sh, cl, ln);
+        float n, msum;
+        lane_sum16x2(sn, sm, n, msum, sh, cl, ln);
         const float mu = n > 0.f ? msum / n : 0.f;
         float q = 0.f;
 #pragma unroll
@@ -412,13 +431,14 @@ k_bn_bwd_final(const float *p1, const float *p2, const float *pd, const float *p
                float *coef, float *bound) {
     // bound (pd, pv set): max over channels and segments of |A| max|dbn| + |B| max|y - mean| + |D|
     // >= max |dy|, into one of X3_SHARDS floats (zeroed by the partial pass)
-    __shared__ float sh[256];
+    // one load round and one LDS round per segment: p1 / p2 (and pd / pv) together
+    __shared__ float sh[4 * 256];
     const int cl = threadIdx.x % FIN_C, ln = threadIdx.x / FIN_C;
     const int c = blockIdx.x * FIN_C + cl;
     float t1 = 0.f, t2 = 0.f, bnd = 0.f;
     for (int sg = 0; sg < S; ++sg) {
         const long o = (long)sg * R * C;
-        float v1[FIN_K], v2[FIN_K];
+        float v1[FIN_K], v2[FIN_K], vd[FIN_K], vv[FIN_K];
 #pragma unroll
         for (int k = 0; k < FIN_K; ++k) {
             const int r = ln + k * FIN_L;
@@ -426,25 +446,19 @@ k_bn_bwd_final(const float *p1, const float *p2, const float *pd, const float *p
             const long i = o + (long)(ok ? r : 0) * C + (c < C ? c : 0);
             v1[k] = ok ? p1[i] : 0.f;
             v2[k] = ok ? p2[i] : 0.f;
+            vd[k] = ok && pd ? pd[i] : 0.f;
+            vv[k] = ok && pd ? pv[i] : 0.f;
         }
-        float a1 = 0.f, a2 = 0.f;
+        float red[4] = {0.f, 0.f, 0.f, 0.f};   // sum, sum, max, max (maxima of non-negative values)
 #pragma unroll
-        for (int k = 0; k < FIN_K; ++k) { a1 += v1[k]; a2 += v2[k]; }
-        a1 = lane_sum16(a1, sh, cl, ln);
-        a2 = lane_sum16(a2, sh, cl, ln);
-        float md = 0.f, mv = 0.f;
-        if (pd) {
-#pragma unroll
-            for (int k = 0; k < FIN_K; ++k) {
-                const int r = ln + k * FIN_L;
-                if (c < C && r < R) {
-                    md = fmaxf(md, pd[o + (long)r * C + c]);
-                    mv = fmaxf(mv, pv[o + (long)r * C + c]);
-                }
-            }
-            md = lane_max16(md, sh, cl, ln);
-            mv = lane_max16(mv, sh, cl, ln);
+        for (int k = 0; k < FIN_K; ++k) {
+            red[0] += v1[k];
+            red[1] += v2[k];
+            red[2] = fmaxf(red[2], vd[k]);
+            red[3] = fmaxf(red[3], vv[k]);
         }
+        lane_red16x4(red, sh, cl, ln);
+        const float a1 = red[0], a2 = red[1], md = red[2], mv = red[3];
         if (ln != 0 || c >= C) continue;
         t1 += a1;
         t2 += a2;

@@ -22,8 +22,23 @@ soon as the last layer inside it has its gradient enqueued.  The
 collectives run on RCCL's own stream; `finish()` makes the compute stream
 wait for them before Adam.
 """
+import time
+
 import torch
 import torch.distributed as dist
+
+
+def settle_before_capture(seconds=1.0):
+    """Call before capturing a step that issues RCCL collectives into a HIP graph.
+    The process group's watchdog thread polls the end events of earlier (eager)
+    collectives until it retires them; on ROCm that query fails with
+    hipErrorCapturedEvent once RCCL's stream has joined a capture, which aborts
+    the process (seen intermittently in test_bench_dist_world1_uses_rccl).  After
+    the device is idle the watchdog retires every finished collective within one
+    100 ms poll; waiting `seconds` leaves it none to query during the capture."""
+    torch.cuda.synchronize()
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
+        time.sleep(seconds)
 
 
 BUCKET_BYTES = 25 << 20   # SURVEY.md §8(e): ~25 MB buckets -> 9 G buckets + D for pix2pix

@@ -74,6 +74,9 @@ def _run(kind, dp, bucket_bytes):
         tr.step(x, y)                      # eager step (builds every lazily sized buffer)
     cur.wait_stream(s)
     torch.cuda.synchronize()
+    if dp:
+        from dgan.dist import settle_before_capture
+        settle_before_capture()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         tr.step(x, y)                      # captured once: RCCL all-reduces + bucket hooks inside
