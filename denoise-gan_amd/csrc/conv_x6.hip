@@ -345,6 +345,9 @@ k_conv_gemm_x6(const GemmArgs p) {
             tap_bit = wk_a * TB + wk_b;
         }
         (void)a_delta; (void)b_delta; (void)tap_bit; (void)b_tap_ok;
+        // a tile past this block's K range (the pipeline's tail) is issued out of range:
+        // same DMA count, zeros, no memory traffic (WGRAD tests pix < kend per row)
+        const bool live = MODE == MODE_WGRAD || k0 < kend;
 #pragma unroll
         for (int j = 0; j < A_NJ; ++j) {
             const int d = asl[j].live ? wid + NW * j : 0, per = BM / 32;
@@ -362,7 +365,7 @@ k_conv_gemm_x6(const GemmArgs p) {
                 ok = arow_n[j] >= 0 && (int)pix < kend && (unsigned)hi < (unsigned)g.H && (unsigned)wi < (unsigned)g.W;
                 off = ((unsigned)(((int)n * g.H + hi) * g.W + wi) * (RM * p.lda) + wg_ci[j]) * 2u;
             }
-            dma(rA, dst, ok ? off : DG_OOB);
+            dma(rA, dst, ok && live ? off : DG_OOB);
         }
 #pragma unroll
         for (int j = 0; j < B_NJ; ++j) {
@@ -384,7 +387,7 @@ k_conv_gemm_x6(const GemmArgs p) {
                     : X3 ? ((unsigned)pix * (2 * p.ldb) + (col >> 5) * 64 + 32 * (bsl[j].plane >> 1) + (col & 31)) * 2u
                          : ((unsigned)pix * p.ldb + col) * 2u;
             }
-            dma(rB, dst, ok ? off : DG_OOB);
+            dma(rB, dst, ok && live ? off : DG_OOB);
         }
         if constexpr (MODE != MODE_WGRAD) walk_next();
     };

@@ -326,7 +326,9 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         }
     }
     auto issue_h = [&](int s, int chunk, char *hb) __attribute__((always_inline)) {
-        dma(rA, hb + hdst[s], hoff[s] >= 0 ? (unsigned)(hoff[s] + chunk * (NI == 3 ? 96 : (X3 ? 128 : 64))) : DG_OOB);
+        // (chunks past the split's range -- the pipeline's tail -- out of range: no traffic)
+        dma(rA, hb + hdst[s],
+            hoff[s] >= 0 && chunk < cend ? (unsigned)(hoff[s] + chunk * (NI == 3 ? 96 : (X3 ? 128 : 64))) : DG_OOB);
     };
 
     // ---- weight K-tile slots (as conv_x6.hip): FWD RC image [16 k][BN],
@@ -371,7 +373,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         else delta = (tap_w[T] * g.Ci * (LW * p.ldb) + chunk * (NI == 3 ? 48 : (X3 ? 64 : 32))) * 2;
 #pragma unroll
         for (int j = 0; j < B_NJ; ++j) {
-            dma(rB, bs + bdst[j], bok[j] ? (unsigned)(bbase[j] + delta) : DG_OOB);
+            dma(rB, bs + bdst[j], bok[j] && chunk < cend ? (unsigned)(bbase[j] + delta) : DG_OOB);
         }
     };
     auto bbuf = [&](int i) __attribute__((always_inline)) -> char * {
