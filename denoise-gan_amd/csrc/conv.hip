@@ -1519,10 +1519,14 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     // least 48 output columns (BN 64 / 128 tiles) -- VGG19's layers after block1_conv1
     const bool hx3 = x3_geom && pl.x6 == 1 && h33 && pl.K % 288 == 0 && 4.0 * ra * ca < 2.0e9 &&
                      4.0 * rb * cb < 2.0e9;
+    // fp16x3 stride-2 4x4 input-gradient phases on the halo kernel (ConvT forwards, down-block
+    // input gradients of G / D) where the implicit-GEMM fp16x3 plan applies (32-channel chunks)
+    const bool hx3p = x3_gen && pl.x6 == 1 && h22 && pl.K % 128 == 0 && 4.0 * ra * ca < 2.0e9 &&
+                      4.0 * rb * cb < 2.0e9 && !plan_off("x3h2");
     if ((pl.x6 == 1 && (h33 || h22 || h44) || hf16) && !plan_off("halo")) {
         // each input pixel staged once per channel chunk instead of once per tap
         const int ntap = h33 ? 9 : (h44 ? 16 : 4);
-        const int bkc = (pl.x6 == 2 || hx3) ? 32 : 16;   // channels per chunk
+        const int bkc = (pl.x6 == 2 || hx3 || hx3p) ? 32 : 16;   // channels per chunk
         int Hout, Wout;
         if (mode == MODE_FWD) { Hout = g.Ho; Wout = g.Wo; }
         else if (h33 || h44) { Hout = g.H; Wout = g.W; }
@@ -1548,7 +1552,7 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         const long cps = (nch + splits - 1) / splits;
         pl.kchunk = (int)(cps * bkc * ntap);
         pl.splits = (int)((nch + cps - 1) / cps);
-        if (hx3) pl.x6 = 3;
+        if (hx3 || hx3p) pl.x6 = 3;
     }
     if (x3_gen && pl.x6 == 1 && 4.0 * ra * ca < 2.0e9 && 4.0 * rb * cb < 2.0e9) {
         pl.halo = 0; pl.htx = pl.hty = 0;
@@ -1573,7 +1577,7 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     pl.gemm_bytes = pl.ws_bytes;
     if (getenv("DG_PLAN_DEBUG"))
         fprintf(stderr, "[dg plan] mode %d M=%d N=%d K=%d -> %s cfg %d splits %d\n", mode, pl.M, pl.N, pl.K,
-                pl.halo == 2 ? "x6h2" : pl.halo == 4 ? "x6h4" : pl.halo ? (pl.x6 == 2 ? "f16h" : (pl.x6 == 3 ? "x3h" : "x6h")) : (pl.x6 == 2 ? "f16" : (pl.x6 == 3 ? "x3" : (pl.x6 ? "x6" : "fp32"))),
+                pl.halo == 2 ? (pl.x6 == 3 ? "x3h2" : "x6h2") : pl.halo == 4 ? "x6h4" : pl.halo ? (pl.x6 == 2 ? "f16h" : (pl.x6 == 3 ? "x3h" : "x6h")) : (pl.x6 == 2 ? "f16" : (pl.x6 == 3 ? "x3" : (pl.x6 ? "x6" : "fp32"))),
                 pl.cfg, pl.splits);
     return pl;
 }
@@ -2009,7 +2013,7 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
         a.B = (const float *)pb; a.ldb = pl.x6_cb; a.b_bytes = (unsigned)(4 * pl.x6_rb * pl.x6_cb);
         dim3 grid(pl.mtiles * pl.ntiles, pl.nphase * pl.splits);
         if (pl.halo) {
-            launch_gemm_x6h(mode, pl.cfg, 3, grid, a, pl.htx, pl.hty, s, 4);
+            launch_gemm_x6h(mode, pl.cfg, pl.halo == 2 ? 2 : 3, grid, a, pl.htx, pl.hty, s, 4);
             DG_LAUNCHED("conv_gemm_x3h");
         } else {
             fastdiv_magic((unsigned)a.g.Wo, a.mg_wo, a.sh_wo);

@@ -180,8 +180,8 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     static_assert(!POOL || MODE == MODE_FWD, "the pool epilogue is a forward epilogue");
     static_assert(KT == 3 || (KT != 3 && MODE == MODE_DGRAD),
                   "3x3 stride 1, or a stride-1 4x4 / stride-2 4x4-phase input gradient");
-    static_assert(NI == 3 || (NI == 2 && KT == 3 && !POOL) || (NI == 4 && KT == 3),
-                  "fp16: 3x3 stride 1, no pool epilogue; fp16x3: 3x3 stride 1");
+    static_assert(NI == 3 || (NI == 2 && KT == 3 && !POOL) || (NI == 4 && (KT == 3 || (KT == 2 && MODE == MODE_DGRAD))),
+                  "fp16: 3x3 stride 1, no pool epilogue; fp16x3: 3x3 stride 1, or the stride-2 4x4 input-gradient phases");
     constexpr bool X3 = NI == 4;
     constexpr int NPL = NI == 3 ? 3 : (X3 ? 4 : 2);   // plane images per chunk
     using HG = HaloGeom<KT, NPL, X3>;
@@ -397,7 +397,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     bf16x8 fm[TM + KT - 1], fl[TM + KT - 1];
     auto ktile = [&](auto TT, auto PARc, int chunk, const char *hc, char *hn) __attribute__((always_inline)) {
         constexpr int T = decltype(TT)::value;
-        constexpr int PAR = decltype(PARc)::value;   // (fp16x3) parity of the chunk in this block's sequence
+        constexpr int PAR = decltype(PARc)::value;   // (fp16x3) parity of the chunk's first K-tile in this block's sequence (NTAP even: 0)
         constexpr int ta = kTapsColMajor ? T % KT : T / KT, tb = kTapsColMajor ? T / KT : T % KT;
         constexpr int da = MODE == MODE_FWD ? ta : KT - 1 - ta;
         constexpr int db = MODE == MODE_FWD ? tb : KT - 1 - tb;
@@ -538,7 +538,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     int c = cbeg;
     for (; c + 1 < cend; c += 2) {
         chunk_tiles(std::integral_constant<int, 0>{}, c, hal0, hal1);
-        chunk_tiles(std::integral_constant<int, 1>{}, c + 1, hal1, hal0);
+        chunk_tiles(std::integral_constant<int, NTAP & 1>{}, c + 1, hal1, hal0);
     }
     if (c < cend) chunk_tiles(std::integral_constant<int, 0>{}, c, hal0, hal1);
     // every wave's DMAs (including the harmless ones past the last chunk)
@@ -583,7 +583,10 @@ void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int
 #define DG_X3H(B_, P_) hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_FWD, B_, P_, 3, 4>), grid, blk, 0, s, a, tiles_x, tiles_y)
     // (bn 32: the SR discriminators' / FastSRGAN's 32-channel 3x3 layers, stride 1; a
     // 64-wide tile computes half zeros there)
-    if (ni == 4 && mode == MODE_DGRAD) {   // fp16x3 input gradient (3x3 stride 1, bn 64 | 128)
+    if (ni == 4 && mode == MODE_DGRAD && kt == 2) {   // fp16x3 stride-2 4x4 input-gradient phases (bn 64 | 128)
+        if (bn == 128) hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_DGRAD, 128, false, 2, 4>), grid, blk, 0, s, a, tiles_x, tiles_y);
+        else hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_DGRAD, 64, false, 2, 4>), grid, blk, 0, s, a, tiles_x, tiles_y);
+    } else if (ni == 4 && mode == MODE_DGRAD) {   // fp16x3 input gradient (3x3 stride 1, bn 64 | 128)
         if (bn == 128) hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_DGRAD, 128, false, 3, 4>), grid, blk, 0, s, a, tiles_x, tiles_y);
         else hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_DGRAD, 64, false, 3, 4>), grid, blk, 0, s, a, tiles_x, tiles_y);
     } else if (ni == 4) {   // fp16x3 forward (bn 64 | 128), optionally with the fused pool
