@@ -41,6 +41,7 @@ Prints ONE JSON line (rank 0).  Extra fields:
                 bounded sample of the same workload
 """
 import argparse
+import contextlib
 import json
 import os
 import subprocess
@@ -207,12 +208,11 @@ def main():
                     trainer.step(x, y)
                 torch.cuda.current_stream().wait_stream(s)
                 torch.cuda.synchronize()
-                if distributed:
-                    from dgan.dist import settle_before_capture
-                    settle_before_capture()
                 graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(graph):
-                    trainer.step(x, y)
+                # (collectives inside the capture go to a capture-only process group, dist.capture_group)
+                with (model.grad_sync.capturing() if distributed else contextlib.nullcontext()):
+                    with torch.cuda.graph(graph):
+                        trainer.step(x, y)
                 torch.cuda.synchronize()
             except Exception as e:  # report, fall back to eager launches
                 print(f"[bench] graph capture failed ({e}); eager launches", file=sys.stderr)
@@ -365,6 +365,7 @@ def main():
                        "process_group": dist.get_backend() if distributed else None,
                        "identity_pass": not args.no_identity if args.model == "pix2pix" else None,
                        "conv_gflop_per_image": round(step_flops / batch / 1e9, 2) if step_flops else None},
+            "lib": _lib_build_info(),
             "losses": [round(float(v), 6) for v in losses],
             "core": core,
             "roofline": roofline,
@@ -373,6 +374,17 @@ def main():
         print(json.dumps(out), file=json_out, flush=True)
     if distributed:
         dist.destroy_process_group()
+
+
+def _lib_build_info():
+    """Provenance of the library this run loaded: the source hash compiled into it (dg_build_info)
+    next to the hash of this tree's sources."""
+    from dgan import _lib
+    from dgan.build import LIB_PATH, source_sha
+    info = _lib.build_info()
+    return {"path": os.path.relpath(LIB_PATH, REPO), "built_from_source_sha": info.get("source_sha"),
+            "tree_source_sha": source_sha(), "matches_tree": info.get("source_sha") == source_sha(),
+            "hip": info.get("hip")}
 
 
 def traffic_of(args, wl, content, batch, rank, world):

@@ -1474,8 +1474,9 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         // (the implicit-GEMM fp16x3 ops where the split path beats the fp32 tiles at all: on
         // pix2pix's deepest layers (M 32..128 rows) the fp32 tiles win; DG_FORCE_X3: every
         // eligible op, for the kernel tests at small sizes.  The halo kernel's fp16x3 3x3 layers
-        // stay forced: a VGG19 whose ops mix arithmetics is not planned -- the network picks its
-        // math by image size instead, sr_trainer.VGGNetwork)
+        // stay forced: the network picks its math by image size, sr_trainer.VGGNetwork.  Plans
+        // of one network in different arithmetics are safe: the host keeps weight planes per
+        // layout (dg_conv_planes_format / _size), dgan/graph.py, tests/test_mixed_math_gpu.py)
         if (t6 < t32 || getenv("DG_FORCE_X6CFG") || x3_geom || (x3_gen && getenv("DG_FORCE_X3"))) {
             pl = p6;
             pl.x6 = 1;

@@ -140,6 +140,15 @@ extern "C" {
 const char *dg_last_error_string(void) { return dg::g_err; }
 int dg_version(void) { return 1; }
 
+#ifndef DG_SOURCE_SHA
+#define DG_SOURCE_SHA "unknown"
+#endif
+// the sources this binary was built from (dgan/build.py passes source_sha(): sha256 over
+// csrc/* and include/dgan.h), the target and the compiler
+const char *dg_build_info(void) {
+    return "source_sha=" DG_SOURCE_SHA ";arch=gfx950;hip=" __VERSION__;
+}
+
 int dg_mark(int id, dg_stream_t stream) {
     hipLaunchKernelGGL(k_mark, dim3(1), dim3(64), 0, (hipStream_t)stream, id);
     DG_LAUNCHED("mark");

@@ -22,6 +22,7 @@ _P = c_void_p  # device pointer
 _SIGS = {
     "dg_last_error_string": (c_char_p, []),
     "dg_version": (c_int, []),
+    "dg_build_info": (c_char_p, []),
     "dg_conv_desc_create": (c_int, [ctypes.POINTER(c_void_p)] + [c_int] * 14),
     "dg_conv_desc_destroy": (c_int, [c_void_p]),
     "dg_conv_out_shape": (c_int, [c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
@@ -158,3 +159,9 @@ def check(rc, what=""):
 
 def call(name, *args):
     check(getattr(lib(), name)(*args), name)
+
+
+def build_info():
+    """dg_build_info() of the loaded library as a dict (source_sha, arch, hip)."""
+    raw = lib().dg_build_info().decode()
+    return dict(kv.split("=", 1) for kv in raw.split(";") if "=" in kv)

@@ -22,23 +22,36 @@ soon as the last layer inside it has its gradient enqueued.  The
 collectives run on RCCL's own stream; `finish()` makes the compute stream
 wait for them before Adam.
 """
-import time
+import contextlib
 
 import torch
 import torch.distributed as dist
 
 
-def settle_before_capture(seconds=1.0):
-    """Call before capturing a step that issues RCCL collectives into a HIP graph.
-    The process group's watchdog thread polls the end events of earlier (eager)
-    collectives until it retires them; on ROCm that query fails with
-    hipErrorCapturedEvent once RCCL's stream has joined a capture, which aborts
-    the process (seen intermittently in test_bench_dist_world1_uses_rccl).  After
-    the device is idle the watchdog retires every finished collective within one
-    100 ms poll; waiting `seconds` leaves it none to query during the capture."""
-    torch.cuda.synchronize()
-    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
-        time.sleep(seconds)
+_CAPTURE_GROUPS = {}
+
+
+def capture_group(device=None):
+    """The process group that carries only collectives issued inside HIP-graph capture.
+
+    The watchdog thread of a process group queries the end event of every eager collective
+    until it retires it; on ROCm that query fails with hipErrorCapturedEvent while the stream
+    the event was recorded on is part of a capture, which aborts the process (round 4:
+    WorkNCCL::isCompleted in test_bench_dist_world1_uses_rccl, after the eager warm-up's
+    all-reduces were still listed when the captured step's all-reduces pulled RCCL's stream
+    into the capture).  Collectives issued under capture are never listed (ProcessGroupNCCL
+    enqueues a work for the watchdog only outside capture), so a group that runs nothing
+    eagerly has nothing to query, whatever the timing: its RCCL stream is the only one that
+    joins a capture, and the default group's eagerly recorded events stay on a stream that
+    never does.  Created (collectively, by every rank) with its communicator connected eagerly
+    (device_id), so no communicator is set up inside a capture."""
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    key = (dist.get_world_size(), str(device))
+    if key not in _CAPTURE_GROUPS:
+        _CAPTURE_GROUPS[key] = dist.new_group(backend=dist.get_backend(), device_id=device,
+                                              group_desc="dgan_graph_capture")
+    return _CAPTURE_GROUPS[key]
 
 
 BUCKET_BYTES = 25 << 20   # SURVEY.md §8(e): ~25 MB buckets -> 9 G buckets + D for pix2pix
@@ -79,6 +92,20 @@ class GradSync:
         if end - self.issued >= self.bucket:
             self._reduce(self.g.grad[self.issued:end])
             self.issued = end
+
+    @contextlib.contextmanager
+    def capturing(self, device=None):
+        """Issue this sync's collectives on capture_group() for the duration (a HIP-graph capture
+        of the step); the graph replays them there.  Every eager collective of the sync must have
+        completed (finish()) -- they ran on the sync's own group."""
+        if self.works:
+            raise RuntimeError("GradSync.capturing: eager all-reduces still outstanding")
+        group, self.group = self.group, (capture_group(device) if dist.get_backend(self.group) == "nccl"
+                                         else self.group)
+        try:
+            yield self
+        finally:
+            self.group = group
 
     def finish(self):
         self.last_mid_backward = len(self.works)

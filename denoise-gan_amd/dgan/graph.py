@@ -232,7 +232,6 @@ class GraphPlan:
                  alias=None, math=None):
         self.g = graph
         self.arena, self.bn = arena, bn_state
-        self._wver = None  # arena.version at the last forward (frozen networks)
         self.device = device
         self.N = N
         self.train = train
@@ -349,10 +348,14 @@ class GraphPlan:
                     mx = max(mx, int(np.prod(s0[:3])) * _ld(s0[3]))
             self.scratch = torch.empty(max(mx, 4), dtype=torch.float32, device=device)
         # ---- bf16x6 operand planes shared between the ops of a conv ----
-        # w: one buffer per conv of the NETWORK (arena.wplanes), shared by all
-        # its plans (e.g. the VGG19 forward over 2N images and the backward over
-        # N); x: per slot, split by fwd and kept for bwd_filter (trainable plans
-        # that own their activations); dy: one scratch per plan.
+        # w: one buffer per conv of the NETWORK and weight-plane layout
+        # (arena.wplanes[(layer, format, bytes)]), shared by all its plans of that
+        # layout (e.g. the VGG19 forward over 2N images and the backward over N);
+        # plans whose GEMMs run another arithmetic (a VGG19 planned at 32^2 on
+        # bf16x6 and at 256^2 on fp16x3) get buffers of their own, each stamped
+        # with the weight version it was split from; x: per slot, split by fwd and
+        # kept for bwd_filter (trainable plans that own their activations); dy: one
+        # scratch per plan.
         wplanes = getattr(arena, "wplanes", None)
         if wplanes is None:
             wplanes = arena.wplanes = {}
@@ -373,19 +376,20 @@ class GraphPlan:
             wb = []
             for n, d in zip(conv_nodes, descs):
                 if (d.plane_mask[0] | d.plane_mask[1]) & ops.TENSOR_W:
-                    if n.name not in wplanes:
-                        if half and d.math == ops.MATH_FP16:
+                    h16 = half and d.math == ops.MATH_FP16
+                    lay = ops.weight_layout(d)
+                    key = (n.name, "f16") if h16 else (n.name,) + lay
+                    if key not in wplanes:
+                        if h16:
                             wname = f"{n.name}/kernel"
                             o, cnt = arena.offsets[wname], int(np.prod(arena.shapes[wname]))
                             assert 2 * cnt <= d.plane_bytes(ops.TENSOR_W)   # (sized for bf16x6 planes)
-                            v = ops.PlaneBuf.__new__(ops.PlaneBuf)
-                            v.buf, v.ready = arena.half[o:o + cnt].view(torch.uint8), False
-                            wplanes[n.name] = v
+                            wplanes[key] = ops.PlaneBuf.over(arena.half[o:o + cnt].view(torch.uint8), lay)
                         else:
-                            wplanes[n.name] = ops.PlaneBuf(d.plane_bytes(ops.TENSOR_W), device)
-                    if half and d.math == ops.MATH_FP16:
+                            wplanes[key] = ops.PlaneBuf(lay[1], device, lay[0])
+                    if h16:
                         self.half_w.add(n.idx)
-                    wb.append(wplanes[n.name])
+                    wb.append(wplanes[key])
                 else:
                     wb.append(None)
             ps = ops.plan_planes(descs, device, keep_x=keep_x, wbufs=wb)
@@ -675,12 +679,8 @@ class GraphPlan:
         s = self.slots[slot]
         s[g.input.id] = x
         # weight planes: re-split every forward, except for a frozen network
-        # (VGG19 content loss) whose weights did not change since the last one
-        wbit = ops.TENSOR_W
-        if getattr(A, "frozen", False):
-            if self._wver == A.version:
-                wbit = 0
-            self._wver = A.version
+        # (VGG19 content loss) whose buffer holds the planes of the current weights
+        frozen = getattr(A, "frozen", False)
         if self.half_w:
             # every fp16 conv's weight copy of this network in one launch
             ops.to_f16(A.data, A.half)
@@ -713,7 +713,7 @@ class GraphPlan:
                     P.invalidate(0 if fed else ops.TENSOR_X)
                     P.w.ready = True
                 else:
-                    P.invalidate(wbit | (0 if fed else ops.TENSOR_X))
+                    P.invalidate((self._stale_w(P, frozen)) | (0 if fed else ops.TENSOR_X))
                 mp = self.fused_conv.get(n.idx)
                 if mp is not None:
                     d.fwd_pool(xin, A.param(f"{n.name}/kernel"), self.pool_idx[slot][mp.idx], bias=bias,
@@ -765,6 +765,22 @@ class GraphPlan:
                 raise ValueError(k)
         return s[g.output.id]
 
+    def _stale_w(self, P, frozen):
+        """TENSOR_W when P's weight planes must be split again before use, else 0: always for a
+        trainable network (its weights change with every Adam step), for a frozen one when the
+        buffer was split from another weight version.  The buffer is stamped with the current
+        version (the op about to read it splits it when it is not ready)."""
+        w = P.w
+        if w is None:
+            return 0
+        if not frozen:
+            return ops.TENSOR_W
+        v = self.arena.version
+        if w.stamp == v:
+            return 0
+        w.stamp = v
+        return ops.TENSOR_W
+
     # --------------------------------------------------------------- backward
     def _update_weight_bounds(self):
         """gwb[conv] = max over input channels of sum |w| over taps and output channels
@@ -804,6 +820,7 @@ class GraphPlan:
         if input_grad is not None:
             gr[gin] = input_grad
         pg = self.param_grads if params is None else bool(params)
+        frozen = getattr(A, "frozen", False)
         in_seen = [False]
 
         def beta_of(n, t):
@@ -844,6 +861,10 @@ class GraphPlan:
                 # (else written just now: by the consumer's bwd_data, or as the fp16 copy)
                 if n.idx not in self.fed_dy and n.idx not in fed_dy_now:
                     P.invalidate(ops.TENSOR_DY)
+                if frozen:
+                    # (a backward-only plan -- VGG19's N-image backward over its 2N forward -- may
+                    # hold weight planes of a layout the forward plan does not share)
+                    P.invalidate(self._stale_w(P, True))
                 if pg:
                     db = A.grad_of(f"{n.name}/bias") if n.attrs["bias"] else None
                     d.bwd_filter(s[t_in.id], dy, A.grad_of(f"{n.name}/kernel"), dbias=db, beta=param_beta, ws=ws,

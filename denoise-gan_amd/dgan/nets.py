@@ -612,6 +612,12 @@ class DiscriminatorPlan:
         for p in self.planes:
             if p is not None:
                 p.invalidate(ops.TENSOR_X | ops.TENSOR_W)
+        if self.planes_half is not self.planes:
+            # (the half-batch backward shares a layer's weight planes only where its descriptor
+            # has the same plane layout; a buffer of its own is split by its bwd_data)
+            for p in self.planes_half:
+                if p is not None:
+                    p.invalidate(ops.TENSOR_W)
         for i, (name, ci, co, bn) in enumerate(self.specs):
             d = self.desc[i]
             P = self.planes[i]

@@ -117,20 +117,40 @@ class PlaneBuf:
     weight planes of a network read by several plans, or one output-gradient
     scratch reused layer after layer.  fmt: PLANES_BF16X6, or PLANES_F16X3 for
     the planes of a tensor that fp16x3 ops read (dg_conv_planes_format; a producer
-    writing them needs to know)."""
+    writing them needs to know).  layout: (format, bytes) of the descriptor that
+    sized it -- a weight buffer is shared only between descriptors of the same
+    layout (a bf16x6 [6 B], fp16x3 [4 B] and fp16x3 + bf16x6 [4 + 6 B] weight
+    buffer hold different bytes at the same offsets).  stamp: the weight version
+    its planes were split from (frozen networks keep them across forwards)."""
 
-    __slots__ = ("buf", "ready", "fmt")
+    __slots__ = ("buf", "ready", "fmt", "layout", "stamp")
 
     def __init__(self, nbytes, device=None, fmt=PLANES_BF16X6):
         self.buf = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device or "cuda")
         self.ready = False
         self.fmt = fmt
+        self.layout = (fmt, int(nbytes))
+        self.stamp = None
+
+    @classmethod
+    def over(cls, t, layout):
+        """A PlaneBuf over existing device bytes t (e.g. a view into a network's fp16 arena)."""
+        v = cls.__new__(cls)
+        v.buf, v.ready, v.fmt, v.layout, v.stamp = t, False, layout[0], layout, None
+        return v
 
     def view(self, nbytes):
         """A PlaneBuf sharing the first nbytes of this one (own ready flag)."""
         v = PlaneBuf.__new__(PlaneBuf)
         v.buf, v.ready, v.fmt = self.buf[:max(int(nbytes), 16)], False, self.fmt
+        v.layout, v.stamp = (self.fmt, int(nbytes)), None
         return v
+
+
+def weight_layout(d):
+    """(format, bytes) of descriptor d's weight planes: the key under which plans of one
+    network may share a weight-plane buffer."""
+    return (d.plane_format(TENSOR_W), d.plane_bytes(TENSOR_W))
 
 
 class ConvPlanes:
@@ -206,8 +226,11 @@ def plan_planes(descs, device=None, keep_x=True, wbufs=None):
             else None
         w = None
         if (m[0] | m[1]) & TENSOR_W:
-            w = (wbufs[i] if wbufs is not None and wbufs[i] is not None
-                 else PlaneBuf(d.plane_bytes(TENSOR_W), device, d.plane_format(TENSOR_W)))
+            # (a shared buffer only when its layout is this descriptor's: plans of one network
+            # at different batch / image sizes may run a layer in different arithmetics)
+            w = wbufs[i] if wbufs is not None else None
+            if w is None or w.layout != weight_layout(d):
+                w = PlaneBuf(d.plane_bytes(TENSOR_W), device, d.plane_format(TENSOR_W))
         dy = dy_buf.view(dy_need[i]) if dy_need[i] else None
         if dy is not None:
             dy.fmt = d.plane_format(TENSOR_DY)

@@ -69,7 +69,9 @@ class VGGNetwork(GraphNetwork):
 
     # fp16x3 from this many pixels per image: pix2pix's 256^2 and FastSRGAN's 512^2 gain, the
     # autoencoder's 64^2 VGG19 loses (bs4: 1036-1056 img/s vs 1074-1106 on bf16x6 / fp32 tiles) and
-    # SRGAN's 96^2 is even (4172-4176 vs 4183-4185), profiles/r4/ab_x3_small_layers.txt
+    # SRGAN's 96^2 is even (4172-4176 vs 4183-4185), profiles/r4/ab_x3_small_layers.txt.  A speed
+    # rule only: one network planned on both sides of it holds weight planes per layout
+    # (graph.GraphPlan, tests/test_mixed_math_gpu.py)
     X3_MIN_PIXELS = 128 * 128
 
     def __init__(self, weights=None, seed=4242, width=1, device=None):

@@ -45,6 +45,9 @@ enum { DG_OP_FWD = 0, DG_OP_BWD_DATA = 1, DG_OP_BWD_FILTER = 2 };
 
 const char *dg_last_error_string(void);
 int dg_version(void);
+/* "source_sha=<16 hex>;arch=gfx950;hip=<compiler>": the hash of the library sources
+ * (csrc/*, include/dgan.h) this binary was compiled from -- provenance of a shipped .so */
+const char *dg_build_info(void);
 /* an empty kernel dispatch on `stream`: a mark in the dispatch sequence for profiling
  * (per-dispatch rocprofv3 PMC counters attributed to the calls between marks) */
 int dg_mark(int id, dg_stream_t stream);

@@ -4,6 +4,7 @@ ctypes binding uses, and the host-side geometry helpers restate TF's rules."""
 import os
 import re
 import subprocess
+import sys
 
 import pytest
 
@@ -35,6 +36,19 @@ def test_library_builds_and_exports_every_declared_symbol():
     L = _lib.lib()
     for name in decl:
         assert hasattr(L, name)
+
+
+def test_loaded_binary_is_built_from_this_tree():
+    """Binary provenance: the library carries the hash of the sources it was compiled from
+    (dg_build_info, dgan/build.py), and it is this tree's -- the GPU suite and the bench load
+    this same in-tree file."""
+    from dgan import _lib
+    from dgan.build import source_sha
+    sys.path.insert(0, os.path.join(REPO, "scripts"))
+    from pmc_traffic import csrc_sha
+    info = _lib.build_info()
+    assert info["source_sha"] == source_sha() == csrc_sha(), info
+    assert info["arch"] == "gfx950"
 
 
 def test_ctypes_signatures_match_header_arity():

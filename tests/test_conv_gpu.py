@@ -83,15 +83,17 @@ MATHS = ["fp32", "bf16x6"]
 @gpu
 @pytest.mark.parametrize("math_mode", MATHS)
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-def test_conv_layer(case, math_mode):
+def test_conv_layer(case, math_mode, xscale=1.0, gscale=1.0):
+    """xscale / gscale: magnitude of the activations (and bias) / of the output gradient
+    (test_x3_gpu.py: fp16x3 operand ranges); the bars are relative to each result's scale."""
     from dgan.ops import ConvDesc
     name, N, H, W, Cin, Cout, k, s, padding, transpose, has_bias = case
     torch.manual_seed(zlib.crc32(name.encode()))
     d = ConvDesc(N, H, W, Cin, Cout, k, s, padding, transpose, math=math_mode)
-    x = torch.randn(N, H, W, Cin, dtype=torch.float64)
+    x = torch.randn(N, H, W, Cin, dtype=torch.float64) * xscale
     w = torch.randn(*d.weight_shape, dtype=torch.float64) * 0.05
-    b = torch.randn(Cout, dtype=torch.float64) if has_bias else None
-    dy = torch.randn(N, d.Ho, d.Wo, Cout, dtype=torch.float64)
+    b = torch.randn(Cout, dtype=torch.float64) * xscale if has_bias else None
+    dy = torch.randn(N, d.Ho, d.Wo, Cout, dtype=torch.float64) * gscale
 
     xr, wr = x.clone().requires_grad_(), w.clone().requires_grad_()
     br = b.clone().requires_grad_() if has_bias else None

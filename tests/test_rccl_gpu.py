@@ -13,6 +13,7 @@ What is checked: at world size 1 the all-reduce is the identity and Adam's
 1/world scale is 1, so every G / D parameter, gradient, Adam slot and BN
 moving statistic after the three steps is bit-identical to the same three
 steps without the process group."""
+import contextlib
 import json
 import os
 import socket
@@ -74,12 +75,11 @@ def _run(kind, dp, bucket_bytes):
         tr.step(x, y)                      # eager step (builds every lazily sized buffer)
     cur.wait_stream(s)
     torch.cuda.synchronize()
-    if dp:
-        from dgan.dist import settle_before_capture
-        settle_before_capture()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        tr.step(x, y)                      # captured once: RCCL all-reduces + bucket hooks inside
+    # (no settling delay: the captured all-reduces run on the capture-only group, dist.capture_group)
+    with (sync.capturing() if dp else contextlib.nullcontext()):
+        with torch.cuda.graph(g):
+            tr.step(x, y)                  # captured once: RCCL all-reduces + bucket hooks inside
     torch.cuda.synchronize()
     counts = (sync.last_mid_backward, sync.last_total) if sync else None
     for _ in range(2):

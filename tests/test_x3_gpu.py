@@ -69,6 +69,22 @@ def test_x3_layer_matches_fp64(case, monkeypatch):
     test_conv_layer(case, "f16x3")
 
 
+# operand magnitudes far from the unit-scale cases above: activations of
+# 1e-3 and 1e3, output gradients of 1e-8 and 1e4 -- on the 3x3 halo kernel (forward / input
+# gradient) and the implicit-GEMM kernel (4x4 stride-2 conv and ConvT, filter gradients
+# included), each against fp64 at the same relative bar as the unit-scale cases
+X3_SCALE_CASES = [(c, xs, gs) for c in (X3_CASES[0], X3_CASES[6], X3_CASES[7])
+                  for xs, gs in ((1e-3, 1.0), (1e3, 1.0), (1.0, 1e-8), (1.0, 1e4), (1e-3, 1e-8))]
+
+
+@gpu
+@pytest.mark.parametrize("case,xs,gs", X3_SCALE_CASES,
+                         ids=[f"{c[0]}-x{xs:g}-g{gs:g}" for c, xs, gs in X3_SCALE_CASES])
+def test_x3_layer_at_operand_scales(case, xs, gs, monkeypatch):
+    monkeypatch.delenv("DG_PLAN_DISABLE", raising=False)
+    test_conv_layer(case, "f16x3", xscale=xs, gscale=gs)
+
+
 @gpu
 def test_x3_shared_weight_planes_serve_bwd_data():
     """One weight PlaneBuf: the fp16x3 forward splits it; the (fp16x3) input gradient reading
