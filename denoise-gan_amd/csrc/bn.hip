@@ -91,17 +91,21 @@ __device__ __forceinline__ void storev(float *p, const float (&v)[V]) {
 template <int V>
 __global__ void __launch_bounds__(256)
 k_bn_stats_partial(const float *__restrict__ y, int ld, long M, int C, long rows, int cpb, float *__restrict__ pn,
-                   float *__restrict__ pmean, float *__restrict__ pm2) {
-    __shared__ float s1s[256 * V], s2s[256 * V];
+                   float *__restrict__ pmean, float *__restrict__ pm2, float *__restrict__ pbd, float *zbound) {
+    // pbd (may be NULL): per chunk max |y - K| + |chunk mean - K| >= max |y - chunk mean|, the
+    // term of the output bound that scales fp16x3 z planes (k_bn_stats_final); zbound zeroed here
+    __shared__ float s1s[256 * V], s2s[256 * V], dms[256 * V];
+    if (zbound && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x < X3_SHARDS)
+        zbound[threadIdx.x] = 0.f;
     const int slot = threadIdx.x % cpb, rl = threadIdx.x / cpb, RL = 256 / cpb;
     const int c0 = (blockIdx.x * cpb + slot) * V;
     y += (long)blockIdx.z * M * ld;
     const long pbase = (long)blockIdx.z * gridDim.y;
     const long r0 = (long)blockIdx.y * rows;
     const long r1 = min(M, r0 + rows);
-    float s1[V], s2[V], K[V];
+    float s1[V], s2[V], K[V], dm[V];
 #pragma unroll
-    for (int q = 0; q < V; ++q) s1[q] = s2[q] = 0.f;
+    for (int q = 0; q < V; ++q) s1[q] = s2[q] = dm[q] = 0.f;
     const bool cok = c0 < C;
     if (cok) {
         loadv<V>(y + r0 * ld + c0, K);
@@ -119,6 +123,7 @@ k_bn_stats_partial(const float *__restrict__ y, int ld, long M, int C, long rows
                     float d = v[u][q] - K[q];
                     s1[q] += d;
                     s2[q] += d * d;
+                    dm[q] = fmaxf(dm[q], fabsf(d));
                 }
         }
         for (; r < r1; r += RL) {
@@ -129,17 +134,22 @@ k_bn_stats_partial(const float *__restrict__ y, int ld, long M, int C, long rows
                 float d = v[q] - K[q];
                 s1[q] += d;
                 s2[q] += d * d;
+                dm[q] = fmaxf(dm[q], fabsf(d));
             }
         }
     }
 #pragma unroll
-    for (int q = 0; q < V; ++q) { s1s[threadIdx.x * V + q] = s1[q]; s2s[threadIdx.x * V + q] = s2[q]; }
+    for (int q = 0; q < V; ++q) {
+        s1s[threadIdx.x * V + q] = s1[q]; s2s[threadIdx.x * V + q] = s2[q]; dms[threadIdx.x * V + q] = dm[q];
+    }
     __syncthreads();
     if (rl != 0 || !cok) return;
     for (int l = 1; l < RL; ++l) {
         const int t = threadIdx.x + l * cpb;
 #pragma unroll
-        for (int q = 0; q < V; ++q) { s1[q] += s1s[t * V + q]; s2[q] += s2s[t * V + q]; }
+        for (int q = 0; q < V; ++q) {
+            s1[q] += s1s[t * V + q]; s2[q] += s2s[t * V + q]; dm[q] = fmaxf(dm[q], dms[t * V + q]);
+        }
     }
     const float n = (float)(r1 - r0);
 #pragma unroll
@@ -148,6 +158,7 @@ k_bn_stats_partial(const float *__restrict__ y, int ld, long M, int C, long rows
         pn[o] = n;
         pmean[o] = K[q] + s1[q] / n;
         pm2[o] = fmaxf(s2[q] - s1[q] * s1[q] / n, 0.f);
+        if (pbd) pbd[o] = dm[q] + fabsf(s1[q] / n);
     }
 }
 
@@ -203,12 +214,17 @@ __device__ __forceinline__ void lane_red16x4(float (&v)[4], float *sh, int cl, i
 __global__ void __launch_bounds__(256)
 k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, int C, int S, const float *gamma,
                  const float *beta, float *save_mean, float *save_invstd, float *mm, float *mv, float momentum,
-                 float eps, float *scale, float *shift) {
+                 float eps, float *scale, float *shift, const float *pbd, float keep_scale, float *zbound,
+                 const float *cp_bound) {
+    // zbound (pbd set): max over channels and segments of (|scale| max |y - mean| + |beta|) x the
+    // dropout keep scale >= max |z| (ReLU / LeakyReLU do not grow |t|), and the bound of the
+    // tensor copied beside z (cp_bound, 8 shards), into one of X3_SHARDS floats (zeroed by the
+    // partial pass): the scale of the z planes (k_bn_apply)
     __shared__ float sh[2 * 256];
     const int cl = threadIdx.x % FIN_C, ln = threadIdx.x / FIN_C;
     const int c = blockIdx.x * FIN_C + cl;
     const bool cok = c < C;
-    float mmc = 0.f, mvc = 0.f;
+    float mmc = 0.f, mvc = 0.f, zbn = 0.f;
     if (ln == 0 && cok) {
         if (mm) mmc = mm[c];
         if (mv) mvc = mv[c];
@@ -238,6 +254,19 @@ k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, i
             q += vq[k] + vn[k] * d * d;
         }
         const float m2 = lane_sum16(q, sh, cl, ln);
+        float dmax = 0.f;   // max |y - mu| over the segment's rows: chunk bound + |chunk mean - mu|
+        if (pbd) {
+#pragma unroll
+            for (int k = 0; k < FIN_K; ++k) {
+                const int r = ln + k * FIN_L;
+                if (cok && r < R) dmax = fmaxf(dmax, pbd[o + (long)r * C + c] + fabsf(vm[k] - mu));
+            }
+            sh[ln * FIN_C + cl] = dmax;
+            __syncthreads();
+#pragma unroll
+            for (int l = 0; l < FIN_L; ++l) dmax = fmaxf(dmax, sh[l * FIN_C + cl]);
+            __syncthreads();
+        }
         if (ln != 0 || !cok) continue;
         const float var = n > 0.f ? m2 / n : 0.f;
         const float inv = 1.f / sqrtf(var + eps);
@@ -248,6 +277,7 @@ k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, i
         const float b = beta ? beta[c] : 0.f;
         scale[sc] = g * inv;
         shift[sc] = b - mu * g * inv;
+        zbn = fmaxf(zbn, (fabsf(g * inv) * dmax + fabsf(b)) * keep_scale);
         mmc -= (mmc - mu) * (1.f - momentum);
         const float unb = n > 1.f ? m2 / (n - 1.f) : m2;
         mvc -= (mvc - unb) * (1.f - momentum);
@@ -255,6 +285,17 @@ k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, i
     if (ln == 0 && cok) {
         if (mm) mm[c] = mmc;
         if (mv) mv[c] = mvc;
+    }
+    if (zbound) {   // the block's 16 channels (and the copied tensor's bound), one vector atomic
+        sh[threadIdx.x] = ln == 0 ? zbn : 0.f;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float b = 0.f;
+            for (int i = 0; i < FIN_C; ++i) b = fmaxf(b, sh[i]);
+            if (cp_bound && blockIdx.x == 0)
+                for (int i = 0; i < X3_SHARDS; ++i) b = fmaxf(b, cp_bound[i]);
+            atomicMax(reinterpret_cast<unsigned *>(zbound) + (blockIdx.x & (X3_SHARDS - 1)), __float_as_uint(b));
+        }
     }
 }
 
@@ -266,7 +307,11 @@ k_bn_apply(const float *__restrict__ y, int ld, long M, int S, int C, const floa
            const float *__restrict__ shift, float *__restrict__ z, int ldz, int act, float alpha, float drop_rate,
            uint32_t seed, uint32_t seed_stride, const int32_t *step_dev, unsigned short *zp0, int zp0C, int zp0col,
            unsigned short *zp1, int zp1C, int zp1col, _Float16 *__restrict__ zh, const float *__restrict__ res,
-           int ldres) {
+           int ldres, const float *zbound, const float *__restrict__ cp, int ldcp, int cpC, int cpcol) {
+    // zbound: the planes' scale source (fp16x3 planes; NULL: F16X3_XS); cp: cpC channels of a
+    // second tensor (the U-Net skip half of the concat, pix2pix.py:188) whose planes go to zp0 at
+    // column cpcol with the same scale -- one scale for the whole consumer operand
+    const float xs = zbound ? x3_grad_scale(zbound, nullptr) : F16X3_XS;
     const uint32_t step = step_dev ? (uint32_t)*step_dev : 0u;
     const float keep_scale = drop_rate > 0.f ? 1.f / (1.f - drop_rate) : 1.f;
     const int CV = C / V;
@@ -303,8 +348,19 @@ k_bn_apply(const float *__restrict__ y, int ld, long M, int S, int C, const floa
         // (V = 4) bf16x6 planes of z for up to two consuming convs, at channel
         // column col of their [rows][3 C] packed x planes (a concat's slice)
         if constexpr (V == 4) {
-            if (zp0) store_planes4(zp0, zp0C, r, zp0col + c, f32x4{o[0], o[1], o[2], o[3]});
-            if (zp1) store_planes4(zp1, zp1C, r, zp1col + c, f32x4{o[0], o[1], o[2], o[3]});
+            if (zp0) store_planes4(zp0, zp0C, r, zp0col + c, f32x4{o[0], o[1], o[2], o[3]}, xs);
+            if (zp1) store_planes4(zp1, zp1C, r, zp1col + c, f32x4{o[0], o[1], o[2], o[3]}, xs);
+        }
+    }
+    if constexpr (V == 4) {
+        if (cp) {
+            const int CP4 = cpC / 4;
+            const long tc = (long)S * M * CP4;
+            for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < tc; e += (long)gridDim.x * blockDim.x) {
+                const long r = e / CP4;
+                const int c = (int)(e - r * CP4) * 4;
+                store_planes4(zp0, zp0C, r, cpcol + c, *reinterpret_cast<const f32x4 *>(cp + r * ldcp + c), xs);
+            }
         }
     }
 }
@@ -605,7 +661,24 @@ int dg_bn_fwd_train_seg_h(int S, int M, int C, const float *y, int ldy, const fl
                           uint32_t drop_seed_stride, const int32_t *step_dev, void *zp0, int zp0C, int zp0col,
                           void *zp1, int zp1C, int zp1col, const float *res, int ldres, void *z_f16, void *ws,
                           size_t ws_bytes, dg_stream_t stream) {
+    return dg_bn_fwd_train_seg_x(S, M, C, y, ldy, gamma, beta, save_mean, save_invstd, moving_mean, moving_var,
+                                 momentum, eps, z, ldz, act, alpha, drop_rate, drop_seed, drop_seed_stride, step_dev,
+                                 zp0, zp0C, zp0col, zp1, zp1C, zp1col, nullptr, nullptr, 0, 0, 0, nullptr, res, ldres,
+                                 z_f16, ws, ws_bytes, stream);
+}
+
+int dg_bn_fwd_train_seg_x(int S, int M, int C, const float *y, int ldy, const float *gamma, const float *beta,
+                          float *save_mean, float *save_invstd, float *moving_mean, float *moving_var, float momentum,
+                          float eps, float *z, int ldz, int act, float alpha, float drop_rate, uint32_t drop_seed,
+                          uint32_t drop_seed_stride, const int32_t *step_dev, void *zp0, int zp0C, int zp0col,
+                          void *zp1, int zp1C, int zp1col, float *z_bound, const float *cp, int ldcp, int cpC,
+                          int cpcol, const float *cp_bound, const float *res, int ldres, void *z_f16, void *ws,
+                          size_t ws_bytes, dg_stream_t stream) {
     DG_ARG(y && z && ws, "NULL tensor");
+    DG_ARG(!z_bound || !res, "bound-scaled planes of a BN fused with a residual Add are not supported");
+    DG_ARG(!cp || (z_bound && zp0 && zp0C < 0 && cpC > 0 && cpC % 32 == 0 && cpcol % 32 == 0 && ldcp % 4 == 0 &&
+                   cpcol + cpC <= -zp0C && (((uintptr_t)cp) & 15) == 0),
+           "copied planes: fp16x3 zp0 with a bound, cpC and cpcol multiples of 32 inside zp0, float4 rows");
     DG_ARG(!res || ldres >= C, "residual pixel stride smaller than channels");
     DG_ARG(!z_f16 || (((uintptr_t)z_f16) & 7) == 0, "fp16 copy must be 8-byte aligned");
     DG_ARG(S >= 1 && S <= 8 && M > 0 && C > 0 && ldy >= C && ldz >= C, "bad shape");
@@ -618,18 +691,24 @@ int dg_bn_fwd_train_seg_h(int S, int M, int C, const float *y, int ldy, const fl
     float *pn = w, *pmean = w + RC, *pm2 = w + 2 * RC;
     float *scale = w + 3 * RC, *shift = scale + (size_t)S * C;
     const bool v4y = dg::vec4_ok(C, {{y, ldy}});
+    // (z_bound: the chunk bounds go to the forward's unused partial slot)
+    float *pbd = z_bound ? w + 3 * RC : nullptr;
+    scale = w + 4 * RC;
+    shift = scale + (size_t)S * C;
     if (v4y) {
         dg::PartGeom pg = dg::part_geom(C, 4);
         hipLaunchKernelGGL(dg::k_bn_stats_partial<4>, dim3(pg.cg, bp.R, S), dim3(256), 0, s, y, ldy, (long)M, C,
-                           bp.rows, pg.cpb, pn, pmean, pm2);
+                           bp.rows, pg.cpb, pn, pmean, pm2, pbd, z_bound);
     } else {
         dg::PartGeom pg = dg::part_geom(C, 1);
         hipLaunchKernelGGL(dg::k_bn_stats_partial<1>, dim3(pg.cg, bp.R, S), dim3(256), 0, s, y, ldy, (long)M, C,
-                           bp.rows, pg.cpb, pn, pmean, pm2);
+                           bp.rows, pg.cpb, pn, pmean, pm2, pbd, z_bound);
     }
     DG_LAUNCHED("bn_stats_partial");
+    const float keep = drop_rate > 0.f ? 1.f / (1.f - drop_rate) : 1.f;
     hipLaunchKernelGGL(dg::k_bn_stats_final, dim3(dg_cdiv(C, dg::FIN_C)), dim3(256), 0, s, pn, pmean, pm2, bp.R, C, S,
-                       gamma, beta, save_mean, save_invstd, moving_mean, moving_var, momentum, eps, scale, shift);
+                       gamma, beta, save_mean, save_invstd, moving_mean, moving_var, momentum, eps, scale, shift, pbd,
+                       keep, z_bound, cp_bound);
     DG_LAUNCHED("bn_stats_final");
     const bool av4 = dg::vec4_ok(C, {{y, ldy}, {z, ldz}, {res, ldres}});
     unsigned short *p0 = (unsigned short *)zp0, *p1 = (unsigned short *)zp1;
@@ -642,14 +721,16 @@ int dg_bn_fwd_train_seg_h(int S, int M, int C, const float *y, int ldy, const fl
            "z planes need float4-aligned tensors, C and the column a multiple of 16 (fp16x3: 32), col + C <= planes C, "
            "16-byte alignment");
     const long MT = (long)S * M;
+    DG_ARG(!cp || av4, "copied planes need float4-aligned tensors");
     if (av4)
         hipLaunchKernelGGL(dg::k_bn_apply<4>, dim3(dg::ew_grid(MT * C / 4)), dim3(256), 0, s, y, ldy, (long)M, S, C,
                            scale, shift, z, ldz, act, alpha, drop_rate, drop_seed, drop_seed_stride, step_dev, p0,
-                           zp0C, zp0col, p1, zp1C, zp1col, (_Float16 *)z_f16, res, ldres);
+                           zp0C, zp0col, p1, zp1C, zp1col, (_Float16 *)z_f16, res, ldres, z_bound, cp, ldcp, cpC,
+                           cpcol);
     else
         hipLaunchKernelGGL(dg::k_bn_apply<1>, dim3(dg::ew_grid(MT * C)), dim3(256), 0, s, y, ldy, (long)M, S, C, scale,
                            shift, z, ldz, act, alpha, drop_rate, drop_seed, drop_seed_stride, step_dev, p0, zp0C,
-                           zp0col, p1, zp1C, zp1col, (_Float16 *)z_f16, res, ldres);
+                           zp0col, p1, zp1C, zp1col, (_Float16 *)z_f16, res, ldres, z_bound, nullptr, 0, 0, 0);
     DG_LAUNCHED("bn_apply");
     return DG_OK;
 }

@@ -98,11 +98,16 @@ __device__ __forceinline__ void split_x3(float x, float s, _Float16 &h, _Float16
 // grid spread over that many words: one word takes about one atomic per 11 ns,
 // MI355X_MICROARCH.md 'fanin'); its value is their max.
 constexpr int X3_SHARDS = 8;
-__device__ __forceinline__ float x3_grad_scale(const float *m, const float *g) {
+// Activations use the same form when a scale source is given (dg_conv_set_act_scale,
+// dg_bn_fwd_train_seg_x): a BN forward's bound of its output, a measured max, or a conv
+// output's bound m * g + c (m: measured max |input|, g: max over output channels of sum |w|,
+// c: max |bias|) -- a static 2^-4 would leave |x| < 2 with a subnormal low piece (an absolute
+// floor of 2^-21 instead of 22 bits)
+__device__ __forceinline__ float x3_grad_scale(const float *m, const float *g, const float *c = nullptr) {
     float mm = m[0];
 #pragma unroll
     for (int i = 1; i < X3_SHARDS; ++i) mm = fmaxf(mm, m[i]);
-    const float b = mm * (g ? *g : 1.f);
+    const float b = mm * (g ? *g : 1.f) + (c ? *c : 0.f);
     if (!(b > 0.f) || !(b <= 3.0e38f)) return 1.f;
     int e;
     (void)frexpf(b, &e);   // b < 2^e

@@ -1239,7 +1239,7 @@ struct OpPlan {
     // narrow stride-1 filter gradient on row segments (k_narrow_wgrad_tile): partial blocks
     int ntile;
     // fp16x3 input gradient: workspace offset of the max |dy| float (no scale source set)
-    size_t x3_max_off;
+    size_t x3_max_off;   // (+256: max |x| when the x operand has no scale source)
 };
 
 // A narrow op (GEMM N <= 8) recast as a 1x1-geometry MFMA GEMM plus a gather:
@@ -1265,6 +1265,10 @@ struct dg_conv_desc_s {
     // and dx planes' scales, and where max |dx| goes (device pointers; NULL = unset)
     const float *gs_dy_m, *gs_dy_g, *gs_dx_m, *gs_dx_g;
     float *gs_dx_max;
+    // fp16x3 activation scale context (dg_conv_set_act_scale): source (m, g, c) of the x planes'
+    // scale, of the forward's output planes' scale, and where max |y| of the forward goes
+    const float *as_x_m, *as_x_g, *as_x_c, *as_y_m, *as_y_g, *as_y_c;
+    float *as_y_max;
     int N, H, W, Cin, Cout, Ho, Wo;  // layer view
     dg::ConvGeom g;                  // conv view
     dg::OpPlan plan[3];              // indexed by DG_OP_*
@@ -1570,9 +1574,9 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         pl.x6_a_off = (pl.ws_bytes + 255) & ~(size_t)255;
         pl.x6_b_off = (pl.x6_a_off + eb * ra * ca + 255) & ~(size_t)255;
         pl.ws_bytes = pl.x6_b_off + eb * rb * cb;
-        if (pl.x6 == 3) {   // (max |dy| when no scale source is set: any mode may read dy)
+        if (pl.x6 == 3) {   // (max |dy| and max |x| when no scale source is set: any mode may read dy / x)
             pl.x3_max_off = (pl.ws_bytes + 255) & ~(size_t)255;
-            pl.ws_bytes = pl.x3_max_off + 256;
+            pl.ws_bytes = pl.x3_max_off + 512;
         }
     }
     pl.gemm_bytes = pl.ws_bytes;
@@ -1803,11 +1807,24 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
     if (pl.x6 == 3) {
         // fp16x3 operand roles (op_tensors): A is x or dy, B is w, or, in a filter gradient,
         // dy or x; dy is scaled from its bound (dg_conv_set_grad_scale's dy source, else
-        // measured by run_gemm), x by F16X3_XS, w by F16X3_WS
+        // measured by run_gemm), x from its source (dg_conv_set_act_scale; else measured by
+        // run_gemm when it splits x into the workspace), w by F16X3_WS
         a.x3_sa = F16X3_XS;
         a.x3_sb = op == DG_OP_BWD_FILTER ? F16X3_XS : F16X3_WS;
         a.x3_dyn = op == DG_OP_FWD ? 0 : ((op == DG_OP_BWD_DATA || d->transpose) ? 1 : 2);
-        if (a.x3_dyn) { a.as_m = d->gs_dy_m; a.as_g = d->gs_dy_g; }
+        const int xo = op == DG_OP_BWD_DATA ? 0 : ((op == DG_OP_FWD || !d->transpose) ? 1 : 2);   // x: A 1, B 2
+        if (a.x3_dyn == 1) { a.as_m = d->gs_dy_m; a.as_g = d->gs_dy_g; }
+        if (a.x3_dyn == 2) { a.bs_m = d->gs_dy_m; a.bs_g = d->gs_dy_g; }
+        if (xo == 1) { a.as_m = d->as_x_m; a.as_g = d->as_x_g; a.as_c = d->as_x_c; }
+        if (xo == 2) { a.bs_m = d->as_x_m; a.bs_g = d->as_x_g; a.bs_c = d->as_x_c; }
+    }
+    if (op == DG_OP_FWD) {
+        // the activation scale context: the output planes' source and max |y| (any arithmetic:
+        // a forward writes the planes of its consumer)
+        a.ys_m = d->as_y_m; a.ys_g = d->as_y_g; a.ys_c = d->as_y_c; a.ymax = d->as_y_max;
+        DG_ARG(!a.ymax || !(pl.narrow || pl.co1 || d->rc[op].on),
+               "max |y| is measured by the GEMM epilogues, the split-K reduce and the small-Cin kernels only (this "
+               "forward runs a narrow / Co-1 / recast kernel)");
     }
     if (op == DG_OP_BWD_DATA) {
         // the gradient scale context (dg_conv_set_grad_scale): dx planes' scale source, max |dx|
@@ -1977,29 +1994,44 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
         if (pr && pr->b) pb = pr->b;
         const bool a_ready = pr && pr->a && pr->a_ready;
         const bool b_ready = pr && pr->b && pr->b_ready;
-        if (a.x3_dyn && !a.as_m) {
-            DG_ARG(!(a.x3_dyn == 1 ? a_ready : b_ready),
-                   "fp16x3 dy planes given without their scale source (dg_conv_set_grad_scale)");
-            float *mx = (float *)(ws + pl.x3_max_off);
-            if (hipMemsetAsync(mx, 0, X3_SHARDS * sizeof(float), s) != hipSuccess) {
+        // an operand without a scale source is measured before its split: max |value| into the
+        // workspace -- a gradient always (its planes must not be ready), an activation whose
+        // planes live in the workspace (caller-held activation planes without a source keep the
+        // static F16X3_XS, the producers' default); an activation source that is a plain max
+        // slot (g, c unset) is measured into by the op that splits x
+        for (int o = 1; o <= 2; ++o) {
+            const bool is_a = o == 1;
+            if (!is_a && b_w) continue;
+            const float *&m = is_a ? a.as_m : a.bs_m;
+            const bool ready = is_a ? a_ready : b_ready;
+            const bool held = is_a ? (pr && pr->a) : (pr && pr->b);
+            const bool grad = a.x3_dyn == o;
+            float *meas = nullptr;
+            if (!m) {
+                DG_ARG(!grad || !ready, "fp16x3 dy planes given without their scale source (dg_conv_set_grad_scale)");
+                if (!grad && held) continue;
+                meas = (float *)(ws + pl.x3_max_off + (grad ? 0 : 256));
+            } else if (!ready && (is_a ? !a.as_g && !a.as_c : !a.bs_g && !a.bs_c) && !grad) {
+                meas = const_cast<float *>(m);   // an x source that is a plain max slot: measured by this split
+            }
+            if (!meas) continue;
+            if (hipMemsetAsync(meas, 0, X3_SHARDS * sizeof(float), s) != hipSuccess) {
                 dg::set_error("hipMemsetAsync failed");
                 return DG_ERR_HIP;
             }
-            if (a.x3_dyn == 1) launch_absmax(A, pl.x6_ra, pl.x6_ca, lda, mx, s);
-            else launch_absmax(B, pl.x6_rb, pl.x6_cb, ldb, mx, s);
-            DG_LAUNCHED("absmax_dy");
-            a.as_m = mx;
-            a.as_g = nullptr;
+            if (is_a) launch_absmax(A, pl.x6_ra, pl.x6_ca, lda, meas, s);
+            else launch_absmax(B, pl.x6_rb, pl.x6_cb, ldb, meas, s);
+            DG_LAUNCHED("absmax_operand");
+            if (is_a) { a.as_m = meas; a.as_g = nullptr; a.as_c = nullptr; }
+            else { a.bs_m = meas; a.bs_g = nullptr; a.bs_c = nullptr; }
         }
         if (!a_ready) {
-            if (a.x3_dyn == 1) launch_split_x3(A, lda, pl.x6_ra, pl.x6_ca, pa, 32, 1.f, s, a.as_m, a.as_g);
-            else launch_split_x3(A, lda, pl.x6_ra, pl.x6_ca, pa, 32, a.x3_sa, s);
+            launch_split_x3(A, lda, pl.x6_ra, pl.x6_ca, pa, 32, a.x3_sa, s, a.as_m, a.as_g, a.as_c);
             DG_LAUNCHED("split_x3_a");
         }
         if (!b_ready) {
             if (!b_w) {
-                if (a.x3_dyn == 2) launch_split_x3(B, ldb, pl.x6_rb, pl.x6_cb, pb, 32, 1.f, s, a.as_m, a.as_g);
-                else launch_split_x3(B, ldb, pl.x6_rb, pl.x6_cb, pb, 32, a.x3_sb, s);
+                launch_split_x3(B, ldb, pl.x6_rb, pl.x6_cb, pb, 32, a.x3_sb, s, a.bs_m, a.bs_g, a.bs_c);
                 DG_LAUNCHED("split_x3_b");
             } else {
                 launch_split_x3(B, ldbw, pl.x6_rb, pl.x6_cb, pb, 16, F16X3_WS, s);
@@ -2316,10 +2348,38 @@ int dg_absmax(const float *x, int64_t rows, int C, int ld, float *out, dg_stream
     return DG_OK;
 }
 
+int dg_absmax_set(const float *x, int64_t rows, int C, int ld, float *out, dg_stream_t stream) {
+    DG_ARG(out, "NULL tensor");
+    if (hipMemsetAsync(out, 0, dg::X3_SHARDS * sizeof(float), (hipStream_t)stream) != hipSuccess) {
+        dg::set_error("hipMemsetAsync failed");
+        return DG_ERR_HIP;
+    }
+    return dg_absmax(x, rows, C, ld, out, stream);
+}
+
+int dg_weight_bound(const float *w, int64_t K, int Co, const float *bias, float *g_out, float *c_out,
+                    dg_stream_t stream) {
+    DG_ARG(w && g_out, "NULL tensor");
+    DG_ARG(K > 0 && Co > 0, "bad shape");
+    dg::launch_weight_bound(w, K, Co, bias, g_out, c_out, (hipStream_t)stream);
+    DG_LAUNCHED("weight_bound");
+    return DG_OK;
+}
+
 int dg_conv_set_grad_scale(dg_conv_t d, const float *dy_m, const float *dy_g, const float *dx_m, const float *dx_g,
                            float *dx_max) {
     DG_ARG(d != nullptr, "descriptor is NULL");
     d->gs_dy_m = dy_m; d->gs_dy_g = dy_g; d->gs_dx_m = dx_m; d->gs_dx_g = dx_g; d->gs_dx_max = dx_max;
+    return DG_OK;
+}
+
+int dg_conv_set_act_scale(dg_conv_t d, const float *x_m, const float *x_g, const float *x_c, const float *y_m,
+                          const float *y_g, const float *y_c, float *y_max) {
+    DG_ARG(d != nullptr, "descriptor is NULL");
+    DG_ARG(x_m || (!x_g && !x_c), "x scale source: g / c without m");
+    DG_ARG(y_m || (!y_g && !y_c), "output scale source: g / c without m");
+    d->as_x_m = x_m; d->as_x_g = x_g; d->as_x_c = x_c;
+    d->as_y_m = y_m; d->as_y_g = y_g; d->as_y_c = y_c; d->as_y_max = y_max;
     return DG_OK;
 }
 

@@ -44,12 +44,13 @@ struct GemmArgs {
     // of the first maximum (row-major), bit 2 set when the pooled value > 0.
     // C (the full-size output) is not written.
     unsigned char *pidx; float *pool_y; int ldpy;
-    // fp16x3 input gradients (DG_MATH_F16X3 bwd_data, x3_grad_scale): the scale sources
-    // (m, g) of the A (dy) planes and of the output (dx) planes; ymax receives max |output|
-    const float *as_m, *as_g, *ys_m, *ys_g;
+    // fp16x3 scale sources (x3_grad_scale: bound = max(m) * g + c) of the A and B operand
+    // planes (m NULL: the static scale x3_sa / x3_sb -- F16X3_XS, F16X3_WS for weights) and of
+    // the output planes (ys_m NULL: F16X3_XS); ymax receives max |output|
+    const float *as_m, *as_g, *as_c, *bs_m, *bs_g, *bs_c, *ys_m, *ys_g, *ys_c;
     float *ymax;
-    // fp16x3 GEMMs: which operand is the gradient scaled from (as_m, as_g) -- 0 none, 1 A,
-    // 2 B -- and the static scales of the others (F16X3_XS activations, F16X3_WS weights)
+    // fp16x3 GEMMs: which operand is the gradient (0 none, 1 A, 2 B) -- measured here when it
+    // arrives without a scale source -- and the static scales
     int x3_dyn; float x3_sa, x3_sb;
     // optional gradient mask from the planes of the activation output instead of
     // its fp32 values (dg_conv_bwd_data_xmask): act' of a sign-determined
@@ -61,8 +62,8 @@ struct GemmArgs {
 
 // the factor that undoes an fp16x3 GEMM's operand scales (powers of two: exact)
 __device__ __forceinline__ float x3_out_scale(const GemmArgs &p) {
-    const float sa = p.x3_dyn == 1 ? x3_grad_scale(p.as_m, p.as_g) : p.x3_sa;
-    const float sb = p.x3_dyn == 2 ? x3_grad_scale(p.as_m, p.as_g) : p.x3_sb;
+    const float sa = p.as_m ? x3_grad_scale(p.as_m, p.as_g, p.as_c) : p.x3_sa;
+    const float sb = p.bs_m ? x3_grad_scale(p.bs_m, p.bs_g, p.bs_c) : p.x3_sb;
     return 1.f / (sa * sb);
 }
 
@@ -87,7 +88,7 @@ __device__ __forceinline__ f32x4 hi_plane4(const unsigned short *zp, int C, long
 
 // the fp16x3 scale of the output planes (static activation scale unless a gradient source is set)
 __device__ __forceinline__ float plane_scale(const GemmArgs &p) {
-    return p.ys_m ? x3_grad_scale(p.ys_m, p.ys_g) : F16X3_XS;
+    return p.ys_m ? x3_grad_scale(p.ys_m, p.ys_g, p.ys_c) : F16X3_XS;
 }
 
 __device__ __forceinline__ float epi_mask(const GemmArgs &p, long pix, int col, float v) {
@@ -170,6 +171,7 @@ template <int MODE, int TM, int TN>
 __device__ __forceinline__ void conv_epilogue(const GemmArgs &p, f32x16 (&acc)[TM][TN], int rbase, int cbase,
                                               int Mrows, const PhaseInfo &ph, int phase, int split, int l32, int h2) {
     const ConvGeom &g = p.g;
+    float vmax = 0.f;   // max |output| of this lane (p.ymax)
 #pragma clang loop unroll(full)
     for (int a = 0; a < TM; ++a) {
 #pragma clang loop unroll(full)
@@ -200,10 +202,12 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs &p, f32x16 (&acc)[T
                         p.C[off + col] = v;
                     }
                     if (p.yp) store_planes1(p.yp, p.ypC, pix, col, v, plane_scale(p));
+                    vmax = fmaxf(vmax, fabsf(v));
                 }
             }
         }
     }
+    if (p.ymax) block_atomic_absmax(p.ymax, vmax);
 }
 
 // Row of a GEMM tile -> (row of the split-K slab, output pixel); slab < 0
@@ -330,11 +334,13 @@ void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int
 void launch_split3(const float *src, int ld, long rows, int C, unsigned short *dst, hipStream_t s);
 // fp32 [rows][ld] -> fp16x3 planes (common.h): per group of G columns (32: activations,
 // 16: weights) h[G] l[G] of scale * value; C % G == 0
-// (sm != NULL: a gradient operand, scale = x3_grad_scale(sm, sg) instead of `scale`)
+// (sm != NULL: a bound-scaled operand, scale = x3_grad_scale(sm, sg, sc) instead of `scale`)
 void launch_split_x3(const float *src, int ld, long rows, int C, void *dst, int group, float scale, hipStream_t s,
-                     const float *sm = nullptr, const float *sg = nullptr);
+                     const float *sm = nullptr, const float *sg = nullptr, const float *sc = nullptr);
 // max |x| of [rows][ld] (first C columns) into *out by atomicMax (zeroed by the caller)
 void launch_absmax(const float *x, long rows, int C, int ld, float *out, hipStream_t s);
+// max over columns of sum_k |w[k][co]| into gout[0], max |bias| into cout[0] (dg_weight_bound)
+void launch_weight_bound(const float *w, long K, int Co, const float *bias, float *gout, float *cout, hipStream_t s);
 // the fp16 conv math (DG_MATH_FP16): one fp16 plane [rows][C] and its GEMM (kF16Cfgs)
 void launch_split_f16(const float *src, int ld, long rows, int C, void *dst, hipStream_t s);
 void launch_split_f16_pair(const float *a, int lda, long ra, int ca, void *da, const float *b, int ldb, long rb,

@@ -120,7 +120,7 @@ __device__ __forceinline__ void small_epi_load(const GemmArgs &p, int rbase, int
 }
 template <bool XL>
 __device__ __forceinline__ void small_fwd_epilogue(const GemmArgs &p, const f32x16 &acc, int rbase, int cbase,
-                                                   float *stage, int lane, const SmallEpi &e) {
+                                                   float *stage, int lane, const SmallEpi &e, float &vmax) {
     const int l32 = lane & 31, h2 = lane >> 5;
 #pragma unroll
     for (int r = 0; r < 16; ++r) stage[((r & 3) + 8 * (r >> 2) + 4 * h2) * 36 + l32] = acc[r];
@@ -152,6 +152,10 @@ __device__ __forceinline__ void small_fwd_epilogue(const GemmArgs &p, const f32x
             for (int q = 0; q < 4; ++q) dst[q] = o[q];
         }
         if (p.yp) store_planes4(p.yp, p.ypC, pix, col, o, plane_scale(p));
+        if (p.ymax) {   // (max |y|: the consumer's measured input, dg_conv_set_act_scale)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) vmax = fmaxf(vmax, fabsf(o[q]));
+        }
     }
 }
 
@@ -188,8 +192,9 @@ k_small_fwd(const GemmArgs p) {
     SmallEpi epi;
     if (p.bias) epi.bias = sc_ld4(p.bias + col0 + (lane & 7) * 4, false);
     float pre[NL];
+    float vmax = 0.f;   // max |y| of this lane's outputs (p.ymax)
     int t = blockIdx.x;
-    if (t >= ntiles) return;
+    if (t >= ntiles) return;   // (the whole block: block_atomic_absmax below stays uniform)
     {
         const int row = t / segs, n = row / g.Ho;
         strip_fetch<CI, P, NTHR, KW, ST>(p, n, row - n * g.Ho, (t - row * segs) * P, tid, pre);
@@ -227,9 +232,10 @@ k_small_fwd(const GemmArgs p) {
         // the prefetched strip goes to LDS before this tile's stores are issued: waiting for the
         // loads then never waits for the stores (one vmcnt counts both)
         strip_store<CI, P, NTHR, KW, ST>(strip[(it + 1) & 1], tid, pre);
-        small_fwd_epilogue<XL>(p, acc, rbase, col0, stage[wid], lane, epi);
+        small_fwd_epilogue<XL>(p, acc, rbase, col0, stage[wid], lane, epi, vmax);
         __syncthreads();
     }
+    if (p.ymax) block_atomic_absmax(p.ymax, vmax);
 }
 
 // WGRAD: dw[k][co] = sum over pixels of A[pix][k] dy[pix][co].  Block (split, column tile):

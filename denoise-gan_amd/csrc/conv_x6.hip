@@ -622,8 +622,8 @@ void launch_split3(const float *src, int ld, long rows, int C, unsigned short *d
 template <int G>
 __global__ void __launch_bounds__(256)
 k_split_x3(const float *__restrict__ src, int ld, long rows, int C, float scale, const float *sm, const float *sg,
-           _Float16 *__restrict__ dst) {
-    if (sm) scale = x3_grad_scale(sm, sg);   // a gradient operand: scale from its bound
+           const float *sc, _Float16 *__restrict__ dst) {
+    if (sm) scale = x3_grad_scale(sm, sg, sc);   // a bound-scaled operand: scale from its source
     const int C8 = C >> 3;
     const long total = rows * C8;
     const bool vec = ((ld & 3) == 0) && ((((uintptr_t)src) & 15) == 0);
@@ -655,15 +655,15 @@ k_split_x3(const float *__restrict__ src, int ld, long rows, int C, float scale,
 }
 
 void launch_split_x3(const float *src, int ld, long rows, int C, void *dst, int group, float scale, hipStream_t s,
-                     const float *sm, const float *sg) {
+                     const float *sm, const float *sg, const float *sc) {
     const long total = rows * (C / 8);
     if (total == 0) return;
     const unsigned blocks = (unsigned)std::min<long>((total + 255) / 256, 8192);
     if (group == 32)
-        hipLaunchKernelGGL(k_split_x3<32>, dim3(blocks), dim3(256), 0, s, src, ld, rows, C, scale, sm, sg,
+        hipLaunchKernelGGL(k_split_x3<32>, dim3(blocks), dim3(256), 0, s, src, ld, rows, C, scale, sm, sg, sc,
                            (_Float16 *)dst);
     else
-        hipLaunchKernelGGL(k_split_x3<16>, dim3(blocks), dim3(256), 0, s, src, ld, rows, C, scale, sm, sg,
+        hipLaunchKernelGGL(k_split_x3<16>, dim3(blocks), dim3(256), 0, s, src, ld, rows, C, scale, sm, sg, sc,
                            (_Float16 *)dst);
 }
 
@@ -676,6 +676,37 @@ __global__ void __launch_bounds__(256) k_absmax(const float *__restrict__ x, lon
         m = fmaxf(m, fabsf(x[r * ld + (e - r * C)]));
     }
     block_atomic_absmax(out, m);
+}
+
+// forward bound of a conv's output (dg_conv_set_act_scale y_g / y_c): gout[0] = max over the
+// Co columns of sum over the K rows of |w[k][co]| (HWIO kernels: K = kh*kw*Cin), cout[0] =
+// max |bias| (0 without one).  One workgroup: lanes own columns, rows summed in order (the
+// small-Cin layers per step -- K 48 / 96 -- and the frozen VGG19 once per weight version)
+__global__ void __launch_bounds__(256) k_weight_bound(const float *__restrict__ w, long K, int Co,
+                                                     const float *__restrict__ bias, float *gout, float *cout) {
+    __shared__ float red[2][256];
+    float g = 0.f, c = 0.f;
+    for (int co = threadIdx.x; co < Co; co += blockDim.x) {
+        float sum = 0.f;
+        for (long k = 0; k < K; ++k) sum += fabsf(w[k * Co + co]);
+        g = fmaxf(g, sum);
+        if (bias) c = fmaxf(c, fabsf(bias[co]));
+    }
+    red[0][threadIdx.x] = g;
+    red[1][threadIdx.x] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < (int)blockDim.x; ++i) {
+            g = fmaxf(g, red[0][i]);
+            c = fmaxf(c, red[1][i]);
+        }
+        gout[0] = g;
+        if (cout) cout[0] = c;
+    }
+}
+
+void launch_weight_bound(const float *w, long K, int Co, const float *bias, float *gout, float *cout, hipStream_t s) {
+    hipLaunchKernelGGL(k_weight_bound, dim3(1), dim3(256), 0, s, w, K, Co, bias, gout, cout);
 }
 
 void launch_absmax(const float *x, long rows, int C, int ld, float *out, hipStream_t s) {

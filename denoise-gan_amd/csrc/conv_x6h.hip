@@ -108,6 +108,7 @@ __device__ __forceinline__ void conv_epilogue16_pool(const GemmArgs &p, f32x4 (&
     if (p.bias && colok) bias = *reinterpret_cast<const f32x4 *>(p.bias + col);
     f32x4 hv[NP];
     unsigned hix[NP];
+    float vmax = 0.f;   // max |pooled value| of this lane (p.ymax: the consumer's measured input)
 #pragma unroll
     for (int a = 0; a < TM; ++a) {
 #pragma unroll
@@ -153,8 +154,11 @@ __device__ __forceinline__ void conv_epilogue16_pool(const GemmArgs &p, f32x4 (&
             *reinterpret_cast<unsigned *>(p.pidx + pp * p.N + col) = fi;
             if (p.pool_y) *reinterpret_cast<f32x4 *>(p.pool_y + pp * p.ldpy + col) = fv;
             if (p.yp) store_planes4(p.yp, p.ypC, pp, col, fv, plane_scale(p));
+#pragma unroll
+            for (int q = 0; q < 4; ++q) vmax = fmaxf(vmax, fabsf(fv[q]));
         }
     }
+    if (p.ymax) block_atomic_absmax(p.ymax, vmax);
 }
 
 // f(integral_constant<T>) for T = 0 .. NTAP-1, unrolled at compile time

@@ -353,8 +353,12 @@ __global__ void __launch_bounds__(256) k_maxpool_bwd(int N, int H, int W, int C,
 // 4 channels).  yp / dxp: optional bf16x6 planes of the output / input
 // gradient (C % 16 == 0) for the conv that consumes it -- no split pass.
 // (ypC: the planes' channel argument of store_planes4 -- C, or -C for fp16x3 planes)
+// (fp16x3 planes: scaled from the source (sm, sg, sc) when given -- the producing conv's output
+// source, a bound of the pooled values too -- else F16X3_XS)
 __global__ void __launch_bounds__(256) k_maxpool_fwd4(int N, int H, int W, int C, const float *x, int ldx, float *y,
-                                                     int ldy, unsigned short *yp, int ypC) {
+                                                     int ldy, unsigned short *yp, int ypC, const float *sm,
+                                                     const float *sg, const float *sc) {
+    const float xs = sm ? x3_grad_scale(sm, sg, sc) : F16X3_XS;
     const int Ho = H / 2, Wo = W / 2, C4 = C >> 2;
     const int total = N * Ho * Wo * C4;
     for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
@@ -370,7 +374,7 @@ __global__ void __launch_bounds__(256) k_maxpool_fwd4(int N, int H, int W, int C
 #pragma unroll
         for (int q = 0; q < 4; ++q) o[q] = fmaxf(fmaxf(a[q], b[q]), fmaxf(d[q], f[q]));
         *reinterpret_cast<f32x4 *>(y + (long)op * ldy + c) = o;
-        if (yp) store_planes4(yp, ypC, op, c, o);
+        if (yp) store_planes4(yp, ypC, op, c, o, xs);
     }
 }
 
@@ -947,7 +951,14 @@ static bool pool_vec4(int C, const void *a, int lda, const void *b, int ldb, con
 
 int dg_maxpool2_fwd_plf(int N, int H, int W, int C, const float *x, int ldx, float *y, int ldy, void *y_planes,
                         int y_planes_format, dg_stream_t stream) {
+    return dg_maxpool2_fwd_x3(N, H, W, C, x, ldx, y, ldy, y_planes, y_planes_format, nullptr, nullptr, nullptr, stream);
+}
+
+int dg_maxpool2_fwd_x3(int N, int H, int W, int C, const float *x, int ldx, float *y, int ldy, void *y_planes,
+                       int y_planes_format, const float *scale_m, const float *scale_g, const float *scale_c,
+                       dg_stream_t stream) {
     DG_ARG(x && y, "NULL tensor");
+    DG_ARG(scale_m || (!scale_g && !scale_c), "scale source: g / c without m");
     DG_ARG(N > 0 && H >= 2 && W >= 2 && C > 0 && ldx >= C && ldy >= C, "bad shape");
     DG_ARG(y_planes_format == DG_PLANES_BF16X6 || y_planes_format == DG_PLANES_F16X3, "bad plane format %d",
            y_planes_format);
@@ -959,7 +970,8 @@ int dg_maxpool2_fwd_plf(int N, int H, int W, int C, const float *x, int ldx, flo
            "output planes need C %% %d == 0 and 16-byte aligned rows", cm);
     if (v4)
         hipLaunchKernelGGL(dg::k_maxpool_fwd4, dim3(dg::lgrid(total / 4)), dim3(256), 0, (hipStream_t)stream, N, H, W,
-                           C, x, ldx, y, ldy, (unsigned short *)y_planes, y_planes_format == DG_PLANES_F16X3 ? -C : C);
+                           C, x, ldx, y, ldy, (unsigned short *)y_planes, y_planes_format == DG_PLANES_F16X3 ? -C : C,
+                           scale_m, scale_g, scale_c);
     else
         hipLaunchKernelGGL(dg::k_maxpool_fwd, dim3(dg::lgrid(total)), dim3(256), 0, (hipStream_t)stream, N, H, W, C, x,
                            ldx, y, ldy);

@@ -79,6 +79,10 @@ _SIGS = {
     "dg_bn_fwd_train_seg_h": (c_int, [c_int, c_int, c_int, _P, c_int, _P, _P, _P, _P, _P, _P, c_float, c_float, _P,
                                       c_int, c_int, c_float, c_float, c_uint32, c_uint32, _P, _P, c_int, c_int, _P,
                                       c_int, c_int, _P, c_int, _P, _P, c_size_t, _P]),
+    "dg_bn_fwd_train_seg_x": (c_int, [c_int, c_int, c_int, _P, c_int, _P, _P, _P, _P, _P, _P, c_float, c_float, _P,
+                                      c_int, c_int, c_float, c_float, c_uint32, c_uint32, _P, _P, c_int, c_int, _P,
+                                      c_int, c_int, _P, _P, c_int, c_int, c_int, _P, _P, c_int, _P, _P, c_size_t,
+                                      _P]),
     "dg_bn_bwd_seg_h": (c_int, [c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, _P, _P, _P, c_int, c_float,
                                 c_float, _P, c_int, _P, _P, _P, _P, c_float, _P, c_size_t, _P]),
     "dg_conv_op_arith": (c_int, [_P, c_int, _P]),
@@ -93,6 +97,7 @@ _SIGS = {
                                         c_size_t, _P]),
     "dg_maxpool2_fwd_pl": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, _P]),
     "dg_maxpool2_fwd_plf": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, _P]),
+    "dg_maxpool2_fwd_x3": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, _P, _P, _P, _P]),
     "dg_maxpool2_bwd_pl": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, c_float, c_int,
                                    c_float, _P, _P]),
     "dg_conv_planes_size": (c_int, [c_void_p, c_int, ctypes.POINTER(c_size_t)]),
@@ -114,6 +119,9 @@ _SIGS = {
                                        _P, _P, _P, _P]),
     "dg_conv_set_grad_scale": (c_int, [c_void_p, _P, _P, _P, _P, _P]),
     "dg_absmax": (c_int, [_P, ctypes.c_int64, c_int, c_int, _P, _P]),
+    "dg_absmax_set": (c_int, [_P, ctypes.c_int64, c_int, c_int, _P, _P]),
+    "dg_weight_bound": (c_int, [_P, ctypes.c_int64, c_int, _P, _P, _P, _P]),
+    "dg_conv_set_act_scale": (c_int, [c_void_p, _P, _P, _P, _P, _P, _P, _P]),
     "dg_upsample2_relu_fwd": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P]),
     "dg_upsample2_relu_bwd": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, c_float, _P]),
     "dg_dwconv3_workspace_size": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_size_t)]),

@@ -585,6 +585,67 @@ class GraphPlan:
                 p = producer_conv(n.ins[0])
                 d.set_grad_scale(dy_m=src[0], dy_g=src[1], dx_m=gm(n), dx_g=gw(n),
                                  dx_max=gm(p) if p is not None else None)
+        # ---- fp16x3 activation scales (include/dgan.h dg_conv_set_act_scale) ----
+        # a conv's fp16x3 x planes carry the scale their producer wrote them with.  A conv that
+        # writes its consumer's planes -- in its epilogue, its fused pool's, or through an unfused
+        # pool -- scales them from its output bound: (max |its input|, measured) x (max over output
+        # channels of sum |w|) + max |bias| (awb, per weight version), and measures max |its
+        # output| (the consumer's input) in the same epilogue.  Every other fp16x3 x operand is
+        # measured by the op that splits it (a plain max slot).  VGG19's activations (a
+        # preprocessed image of +-128 onwards) thus keep 22 bits down to 2^-17 of each bound.
+        self.act_feeds = {}      # producer conv idx -> (consumer conv node, unfused pool node or None)
+        self.act_measure = []    # convs whose input max is measured before them (input not a conv's output)
+        self.pool_scale = {}     # unfused maxpool node idx -> scale source of the planes it writes
+        self.amax = self.awb = None
+        self._awb_ver = None
+        if alias is None and any(self.desc[n.idx].plane_format(ops.TENSOR_X) == ops.PLANES_F16X3 for n in conv_nodes):
+            ci = {n.idx: i for i, n in enumerate(conv_nodes)}
+            self.amax = torch.zeros(len(conv_nodes), 8, dtype=torch.float32, device=device)
+            self.awb = torch.zeros(len(conv_nodes), 2, dtype=torch.float32, device=device)
+            feeds = {}   # producer conv idx -> (consumer conv, unfused pool or None, planes it writes or None)
+            for n in conv_nodes:
+                cs = cons[n.out.id]
+                if len(cs) != 1:
+                    continue
+                m, buf = None, None
+                if cs[0].kind == "conv":
+                    c, buf = cs[0], self.cplanes[0][n.idx].fwd_out
+                elif cs[0].kind == "maxpool" and len(cons[cs[0].out.id]) == 1 and cons[cs[0].out.id][0].kind == "conv":
+                    m, c = cs[0], cons[cs[0].out.id][0]
+                    buf = self.pool_out[0].get(m.idx)
+                else:
+                    continue
+                feeds[n.idx] = (c, m if (m is not None and n.idx not in self.fused_conv) else None, buf)
+            self.act_feeds = {i: (c, m) for i, (c, m, buf) in feeds.items()
+                              if buf is not None and buf.fmt == ops.PLANES_F16X3}
+            producer = {c.idx: i for i, (c, _, _) in feeds.items()}
+
+            def ysrc(n):
+                i = ci[n.idx]
+                return (self.amax[i], self.awb[i, 0:1], self.awb[i, 1:2] if n.attrs["bias"] else None)
+
+            ctx = {n.idx: [None, None, None] for n in conv_nodes}   # x source, y source, y_max
+            for i, (c, m) in self.act_feeds.items():
+                n = nodes[i]
+                ctx[i][1] = ysrc(n)
+                if m is not None:
+                    self.pool_scale[m.idx] = ysrc(n)
+                # the producer's output bound needs max |its input|: measured by the epilogue of the
+                # conv producing that input (any arithmetic), else by an absmax pass before it
+                if i in producer:
+                    ctx[producer[i]][2] = self.amax[ci[i]]
+                else:
+                    self.act_measure.append(i)
+            for n in conv_nodes:
+                if self.desc[n.idx].plane_format(ops.TENSOR_X) != ops.PLANES_F16X3:
+                    continue
+                p = producer.get(n.idx)
+                ctx[n.idx][0] = ysrc(nodes[p]) if p in self.act_feeds else (self.amax[ci[n.idx]],)
+            for n in conv_nodes:
+                x, y, ymax = ctx[n.idx]
+                if x is not None or y is not None or ymax is not None:
+                    self.desc[n.idx].set_act_scale(x=x, y=y, y_max=ymax)
+            self._act_ci = ci
         # ---- workspace ----
         ws = [0]
         for n in nodes[1:]:
@@ -681,6 +742,18 @@ class GraphPlan:
         # weight planes: re-split every forward, except for a frozen network
         # (VGG19 content loss) whose buffer holds the planes of the current weights
         frozen = getattr(A, "frozen", False)
+        if self.act_feeds:
+            # fp16x3 activation scales: the output bounds' weight terms (frozen weights: once per
+            # version) and this pass's measured maxima
+            if not frozen or self._awb_ver != A.version:
+                for i in self.act_feeds:
+                    n = g.nodes[i]
+                    j = self._act_ci[i]
+                    ops.weight_bound(A.param(f"{n.name}/kernel"), self.awb[j, 0:1],
+                                     bias=A.param(f"{n.name}/bias") if n.attrs["bias"] else None,
+                                     c_out=self.awb[j, 1:2])
+                self._awb_ver = A.version
+            self.amax.zero_()
         if self.half_w:
             # every fp16 conv's weight copy of this network in one launch
             ops.to_f16(A.data, A.half)
@@ -714,6 +787,8 @@ class GraphPlan:
                     P.w.ready = True
                 else:
                     P.invalidate((self._stale_w(P, frozen)) | (0 if fed else ops.TENSOR_X))
+                if n.idx in self.act_measure:
+                    ops.absmax(xin, self.amax[self._act_ci[n.idx]])   # (zeroed above)
                 mp = self.fused_conv.get(n.idx)
                 if mp is not None:
                     d.fwd_pool(xin, A.param(f"{n.name}/kernel"), self.pool_idx[slot][mp.idx], bias=bias,
@@ -753,7 +828,8 @@ class GraphPlan:
                     off += t.C
             elif k == "maxpool":
                 if n.idx not in self.fused_pool:   # (else done by its conv's epilogue)
-                    ops.maxpool2_fwd(xin, y, planes_out=self.pool_out[slot].get(n.idx))
+                    ops.maxpool2_fwd(xin, y, planes_out=self.pool_out[slot].get(n.idx),
+                                     scale=self.pool_scale.get(n.idx))
             elif k == "upsample":
                 ops.upsample2_relu_fwd(xin, y)
             elif k == "dwconv":

@@ -81,6 +81,35 @@ def grad_bounds(descs, planes, device):
     return out
 
 
+def x3_planes(P):
+    """P keeps fp16x3 x planes (an fp16x3 op of its layer reads x from them)."""
+    return P is not None and P.x is not None and P.x.fmt == ops.PLANES_F16X3
+
+
+class ActBounds:
+    """Scale sources of a network's fp16x3 activation planes (include/dgan.h
+    dg_conv_set_act_scale): `zb[i]` (8 floats) the bound of BN block i's output written by its
+    statistics (dg_bn_fwd_train_seg_x), `in_max` the measured max |input| and `w1[0]` the
+    forward weight bound of the first conv (no BN after it: its output planes are scaled from
+    in_max x w1).  Each conv whose x planes are fp16x3 reads the source its producer wrote
+    them with, so values down to 2^-17 of the tensor's bound keep 22 bits (a static 2^-4
+    scale left |x| < 2 -- most of a BN output -- with a subnormal low piece)."""
+
+    def __init__(self, n, device):
+        self.zb = torch.zeros(n, 8, dtype=torch.float32, device=device)
+        self.in_max = torch.zeros(8, dtype=torch.float32, device=device)
+        self.w1 = torch.zeros(2, dtype=torch.float32, device=device)
+
+    def first_conv(self, x, w):
+        """Per forward: max |x| of the network input and the first conv's weight bound."""
+        ops.absmax_set(x, self.in_max)
+        ops.weight_bound(w, self.w1[0:1])
+
+    @property
+    def first_src(self):
+        return (self.in_max, self.w1[0:1])
+
+
 # ---------------------------------------------------------------------------
 # layer specs (pix2pix.py:147-173, :200-218); `width` divides filter counts
 # (tiny variants for tests only; width=1 is the reference model)
@@ -308,6 +337,20 @@ class GeneratorPlan:
         if train and FEED_X and self.planes[1].x is not None:
             self.planes[0].fwd_out = self.planes[1].x
         self.gbound = grad_bounds(descs, self.planes, device) if train else [None] * len(descs)
+        # fp16x3 activation planes scaled from their producers' bounds (ActBounds): down l's BN
+        # output -> zb[l] (down l+1's x), up u's BN output with the skip half of its concat ->
+        # zb[8+u] (up u+1's x), down1's conv output -> (max |x|, down1's weight bound) (down2's x)
+        self.ab = None
+        if train and any(x3_planes(P) for P in self.planes):
+            self.ab = ActBounds(16, device)
+            for k, d in enumerate(descs):
+                if not x3_planes(self.planes[k]):
+                    continue
+                # (plane index k: 0-7 down1-down8, 8-14 up1-up7, 15 last; the x of k >= 2 is the BN
+                # output of block k-1, zb[k-1])
+                d.set_act_scale(x=self.ab.first_src if k == 1 else self.ab.zb[k - 1])
+            if x3_planes(self.planes[1]) and FEED_X:
+                self.ddesc[0].set_act_scale(y=self.ab.first_src)
         self.ws_bytes = max([d.max_ws() for d in self.ddesc + self.udesc + [self.ldesc]] + [self._bn_ws_max()])
 
     @property
@@ -353,6 +396,11 @@ class GeneratorPlan:
         def xplanes(k):  # plane index k's kept x planes (None: its ops split x themselves)
             return P[k].x if feed and P[k] is not None else None
 
+        ab = self.ab
+        if ab is not None:
+            # down2's x planes: (max |x|, down1's bound) -- also in a training plan's inference pass,
+            # whose down1 still writes them
+            ab.first_conv(x, A.param("down1/kernel"))
         h = x
         for l, (name, ci, co, bn) in enumerate(self.downs):
             d = self.ddesc[l]
@@ -364,12 +412,15 @@ class GeneratorPlan:
                 d.fwd(h, A.param(f"{name}/kernel"), y, ws=ws, planes=P[l])
                 # z feeds the next down conv (plane index l+1; down8's z8 feeds
                 # up1, index 8) and, as the skip half of cat[6-l], the up conv
-                # reading that concat (index 15-l, its columns after up 6-l's)
+                # reading that concat (index 15-l, its columns after up 6-l's) -- bf16x6
+                # planes there; fp16x3 concat planes are written by up 6-l's BN, one scale
+                # over both halves (below)
                 nxt = l + 1
                 outs = [(nxt, co, 0)] if xplanes(nxt) is not None else []
-                if 1 <= l <= 6 and xplanes(15 - l) is not None:
+                if 1 <= l <= 6 and xplanes(15 - l) is not None and not x3_planes(P[15 - l]):
                     outs.append((15 - l, self.ups[7 - l][1], self.ups[6 - l][2]))
-                self._bn_fwd(s, name, y, z, "lrelu", training, ws, outs=outs)
+                self._bn_fwd(s, name, y, z, "lrelu", training, ws, outs=outs,
+                             z_bound=ab.zb[l] if ab is not None else None)
                 if xplanes(nxt) is not None:
                     P[nxt]._filled(ops.TENSOR_X)
             h = z
@@ -384,10 +435,13 @@ class GeneratorPlan:
             # conv: cat[6]'s planes are split by its consumer as before)
             k = 9 + u
             outs = []
+            copy = None
             if u <= 5 and xplanes(k) is not None:
                 outs.append((k, self.ups[u + 1][1], 0))
+                if x3_planes(P[k]):   # (+ the skip half, down 6-u's output, under one bound)
+                    copy = (self.z_view(s, 6 - u), co, ab.zb[6 - u])
             self._bn_fwd(s, name, y, z, "relu", training, ws, rate, lambda hv: dropout_seed(drop_seed, u, hv),
-                         step_dev, outs=outs)
+                         step_dev, outs=outs, z_bound=ab.zb[8 + u] if ab is not None else None, copy=copy)
             if outs:
                 P[k]._filled(ops.TENSOR_X)
             h = s["cat"][u]
@@ -407,7 +461,8 @@ class GeneratorPlan:
             p.invalidate(ops.TENSOR_DY)
         return p
 
-    def _bn_fwd(self, s, name, y, z, act, training, ws, drop_rate=0.0, seed_of=None, step_dev=None, outs=()):
+    def _bn_fwd(self, s, name, y, z, act, training, ws, drop_rate=0.0, seed_of=None, step_dev=None, outs=(),
+                z_bound=None, copy=None):
         """outs: (plane index k, its x channel count, column) -- the BN output is
         also written into plane k's kept x planes at that column (training).
         Training: one segmented call, each half normalised by its own statistics
@@ -422,7 +477,7 @@ class GeneratorPlan:
             ops.bn_fwd_train(y, A.param(f"{name}/gamma"), A.param(f"{name}/beta"), s["mean"][name], s["inv"][name],
                              self.bn.mean[name], self.bn.var[name], z, act=act, alpha=ALPHA, momentum=BN_MOMENTUM,
                              eps=BN_EPS, drop_rate=drop_rate, drop_seed=seed0, step_dev=step_dev, ws=ws, z_planes=zp,
-                             segments=self.halves, drop_seed_stride=stride)
+                             segments=self.halves, drop_seed_stride=stride, z_bound=z_bound, copy=copy)
             return
         for hv in range(self.halves):
             ops.bn_fwd_infer(self._half(y, hv), A.param(f"{name}/gamma"), A.param(f"{name}/beta"), self.bn.mean[name],
@@ -574,6 +629,16 @@ class DiscriminatorPlan:
             # one dy bound per layer, shared by the full and the half-batch backward (in
             # stream order, each BN backward rewrites it before its conv reads it)
             self.gbound = grad_bounds(self.desc, self.planes, device)
+            # fp16x3 activation planes scaled from their producers' bounds (ActBounds): D.down1's
+            # conv output from (max |input pair|, down1's weight bound), BN block i's output zb[i]
+            self.ab = None
+            if any(x3_planes(P) for P in self.planes):
+                self.ab = ActBounds(len(self.desc), device)
+                for k, d in enumerate(self.desc):
+                    if x3_planes(self.planes[k]):
+                        d.set_act_scale(x=self.ab.first_src if k == 1 else self.ab.zb[k - 1])
+                if x3_planes(self.planes[1]) and FEED_X:
+                    self.desc[0].set_act_scale(y=self.ab.first_src)
             if self.desc_half is not self.desc:
                 for i, (d, P) in enumerate(zip(self.desc_half, self.planes_half)):
                     if FEED_DY and P is not None and P.dy is not None and P.dy.fmt == ops.PLANES_F16X3:
@@ -582,6 +647,7 @@ class DiscriminatorPlan:
                         d.set_grad_scale(dy_m=self.gbound[i])
         else:
             self.planes = self.planes_half = [None] * len(self.desc)
+            self.ab = None
         # G path (train_pix2pix.py:64): of dL/d D([inp, G(x)]) only the G(x) channels 3..5
         # are used, so that input gradient runs as a Cin-3 conv over down1's filter slice
         # w[:, :, 3:6, :] (copied per step) straight into dL/dG(x) (beta 1); per channel the
@@ -618,6 +684,9 @@ class DiscriminatorPlan:
             for p in self.planes_half:
                 if p is not None:
                     p.invalidate(ops.TENSOR_W)
+        ab = self.ab
+        if ab is not None:
+            ab.first_conv(self.inp, A.param("down1/kernel"))   # D.down2's x planes: (max |inp|, down1's bound)
         for i, (name, ci, co, bn) in enumerate(self.specs):
             d = self.desc[i]
             P = self.planes[i]
@@ -639,7 +708,7 @@ class DiscriminatorPlan:
                                      self.inv[name], self.bn.mean[name], self.bn.var[name], z, act="lrelu",
                                      alpha=ALPHA, momentum=BN_MOMENTUM, eps=BN_EPS, ws=ws,
                                      z_planes=[zplanes(xp, rows, co, 0)] if xp is not None else (),
-                                     segments=self.halves)
+                                     segments=self.halves, z_bound=ab.zb[i] if ab is not None else None)
                 else:
                     for hv in range(self.halves):
                         ops.bn_fwd_infer(self._half(y, hv), A.param(f"{name}/gamma"), A.param(f"{name}/beta"),

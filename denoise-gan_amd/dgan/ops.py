@@ -310,6 +310,20 @@ class ConvDesc:
         self._gs = (dy_m, dy_g, dx_m, dx_g, dx_max)   # (keeps the views referenced)
         call("dg_conv_set_grad_scale", self._h, _p(dy_m), _p(dy_g), _p(dx_m), _p(dx_g), _p(dx_max))
 
+    def set_act_scale(self, x=None, y=None, y_max=None):
+        """The fp16x3 activation scale context (include/dgan.h dg_conv_set_act_scale): x, y = (m, g, c)
+        scale sources of the input planes and of the output planes the forward writes (device
+        floats: m 8 shards, g and c one float or None), y_max 8 floats receiving max |y|."""
+        def src(v):   # a tensor alone = (m,): a plain 8-float slot
+            v = (v,) if isinstance(v, torch.Tensor) else tuple(v or ())
+            return v + (None,) * (3 - len(v))
+        xs, ys = src(x), src(y)
+        for t in (xs[0], ys[0], y_max):
+            if t is not None and t.numel() < 8:
+                raise DGError("a measured max / bound slot is 8 floats (per-workgroup shards)")
+        self._as = (xs, ys, y_max)   # (keeps the views referenced)
+        call("dg_conv_set_act_scale", self._h, *(_p(t) for t in xs), *(_p(t) for t in ys), _p(y_max))
+
     def op_arith(self, op):
         """'fp32' | 'bf16x6' | 'fp16' | 'f16x3': the arithmetic of op's GEMM (dg_conv_op_arith)."""
         if isinstance(op, str):
@@ -546,13 +560,21 @@ def _rows(t):
 
 def bn_fwd_train(y, gamma, beta, save_mean, save_invstd, moving_mean, moving_var, z, act="none", alpha=0.3,
                  momentum=0.99, eps=1e-3, drop_rate=0.0, drop_seed=0, step_dev=None, ws=None, z_planes=(),
-                 segments=1, drop_seed_stride=0, f16_out=None, res=None):
+                 segments=1, drop_seed_stride=0, f16_out=None, res=None, z_bound=None, copy=None):
     """z_planes: up to two (uint8 device tensor, planes C, column) -- packed x
     planes of consuming convs that also receive z.  segments: the rows are that
     many consecutive independent BN calls (dg_bn_fwd_train_seg; save_mean /
     save_invstd [segments, C], dropout seed drop_seed + s * drop_seed_stride).
     f16_out: the consuming fp16 conv's x PlaneBuf, which also receives z's fp16 copy.
-    res: a residual Add fused after the block, z = act(BN(y)) + res (same shape as z)."""
+    res: a residual Add fused after the block, z = act(BN(y)) + res (same shape as z).
+    z_bound: 8 device floats, the bound of z that scales fp16x3 z planes (written here,
+    dg_bn_fwd_train_seg_x; the consumers' x scale source).  copy: (tensor, column, its bound)
+    -- a second tensor's planes into z_planes[0] at that column with the same scale (the
+    U-Net skip half of a concatenation)."""
+    if z_bound is not None or copy is not None:
+        return _bn_fwd_train_x(y, gamma, beta, save_mean, save_invstd, moving_mean, moving_var, z, act, alpha,
+                               momentum, eps, drop_rate, drop_seed, step_dev, ws, z_planes, segments,
+                               drop_seed_stride, z_bound, copy)
     C = y.shape[-1]
     M = _rows(y)
     if M % segments:
@@ -567,6 +589,30 @@ def bn_fwd_train(y, gamma, beta, save_mean, save_invstd, moving_mean, moving_var
          ctypes.c_uint32(drop_seed_stride & 0xFFFFFFFF), _p(step_dev),
          zp[0][0], zp[0][1], zp[0][2], zp[1][0], zp[1][1], zp[1][2], _p(res), pix_ld(res, C) if res is not None else 0,
          _f16(f16_out), _p(buf), n, _stream())
+    return z
+
+
+def _bn_fwd_train_x(y, gamma, beta, save_mean, save_invstd, moving_mean, moving_var, z, act, alpha, momentum, eps,
+                    drop_rate, drop_seed, step_dev, ws, z_planes, segments, drop_seed_stride, z_bound, copy):
+    C = y.shape[-1]
+    M = _rows(y)
+    if M % segments:
+        raise DGError(f"{M} rows do not split into {segments} segments")
+    M //= segments
+    if z_bound is None or z_bound.numel() < 8:
+        raise DGError("a z bound is 8 device floats (per-workgroup shards)")
+    ws = ws or default_workspace()
+    buf, n = ws.get(bn_workspace_bytes(M, C, segments))
+    zp = [(t.data_ptr(), int(pc), int(col)) for t, pc, col in z_planes] + [(None, 0, 0)] * (2 - len(z_planes))
+    cp, cpcol, cpb = copy if copy is not None else (None, 0, None)
+    cpC = cp.shape[-1] if cp is not None else 0
+    call("dg_bn_fwd_train_seg_x", segments, M, C, _p(y), pix_ld(y, C), _p(gamma), _p(beta), _p(save_mean),
+         _p(save_invstd), _p(moving_mean), _p(moving_var), float(momentum), float(eps), _p(z), pix_ld(z, C),
+         act_id(act), float(alpha), float(drop_rate), ctypes.c_uint32(drop_seed & 0xFFFFFFFF),
+         ctypes.c_uint32(drop_seed_stride & 0xFFFFFFFF), _p(step_dev),
+         zp[0][0], zp[0][1], zp[0][2], zp[1][0], zp[1][1], zp[1][2], _p(z_bound),
+         _p(cp), pix_ld(cp, cpC) if cp is not None else 0, cpC, int(cpcol), _p(cpb), None, 0, None, _p(buf), n,
+         _stream())
     return z
 
 
@@ -772,12 +818,14 @@ def act_fwd(x, z, act, alpha=0.3):
     return z
 
 
-def maxpool2_fwd(x, y, planes_out=None):
-    """planes_out: PlaneBuf of the consuming conv's input planes, written beside y."""
+def maxpool2_fwd(x, y, planes_out=None, scale=None):
+    """planes_out: PlaneBuf of the consuming conv's input planes, written beside y; scale: the
+    (m, g, c) source of fp16x3 planes (the producing conv's output source, dg_maxpool2_fwd_x3)."""
     N, H, W, C = _nhwc(x)
-    call("dg_maxpool2_fwd_plf", N, H, W, C, _p(x), pix_ld(x, C), _p(y), pix_ld(y, C),
+    sm, sg, sc = scale if scale is not None else (None, None, None)
+    call("dg_maxpool2_fwd_x3", N, H, W, C, _p(x), pix_ld(x, C), _p(y), pix_ld(y, C),
          None if planes_out is None else _p(planes_out.buf), PLANES_BF16X6 if planes_out is None else planes_out.fmt,
-         _stream())
+         _p(sm), _p(sg), _p(sc), _stream())
     if planes_out is not None:
         planes_out.ready = True
     return y
@@ -819,6 +867,22 @@ def absmax(t, out):
     C = t.shape[-1]
     call("dg_absmax", _p(t), _rows(t), C, pix_ld(t, C), _p(out), _stream())
     return out
+
+
+def absmax_set(t, out):
+    """out (8 device floats) = max |t| (zeroed first, dg_absmax_set): a measured max."""
+    if out.numel() < 8:
+        raise DGError("absmax needs 8 floats (per-workgroup shards)")
+    C = t.shape[-1]
+    call("dg_absmax_set", _p(t), _rows(t), C, pix_ld(t, C), _p(out), _stream())
+    return out
+
+
+def weight_bound(w, g_out, bias=None, c_out=None):
+    """g_out[0] = max over output channels of sum |w| over the other axes (HWIO w), c_out[0] =
+    max |bias| (dg_weight_bound): a conv output's bound terms."""
+    Co = w.shape[-1]
+    call("dg_weight_bound", _p(w), w.numel() // Co, Co, _p(bias), _p(g_out), _p(c_out), _stream())
 
 
 def upsample2_relu_fwd(x, z):

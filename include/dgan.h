@@ -85,18 +85,20 @@ int dg_conv_workspace_size(dg_conv_t d, int op, size_t *bytes);
  *                    Eligible GEMMs: FWD Cin % 32 == 0, DGRAD Cout % 32 == 0,
  *                    WGRAD Cin, Cout % 16 == 0 (others keep fp32); no
  *                    caller-held planes (dg_conv_op_planes reports none).
- *   DG_MATH_F16X3  : bf16x6, except the forward GEMM of a stride-1 3x3 Conv2D with
- *                    Cin % 32 == 0 and Cout % 16 == 0, Cout > 32 (the frozen VGG19 of the
- *                    content loss, pix2pix.py:53-67): each fp32 operand, pre-scaled by a
- *                    power of two (activations 2^-4, weights 2^8), is split into fp16
- *                    h + l (RNE, |l| <= 2^-11 |x|) and a product is h.h' + h.l' + l.h' --
- *                    three fp16 piece products (dropped terms < 2^-21 |ab|) on three
- *                    v_mfma_f32_16x16x32_f16 per 32 channels, half the bf16x6 MFMA count.
- *                    Range: |activation| < 2^20 (fp16 max 65504 after the 2^-4 scale),
- *                    |weight| < 255; smaller values keep an absolute error < 2^-21.
- *                    Such a descriptor's x planes are fp16x3 (4 B per element, its
- *                    forward only; its filter gradient splits x itself) and its w planes
- *                    [fp16x3 | bf16x6] (dg_conv_planes_size), split by the forward.
+ *   DG_MATH_F16X3  : fp16x3 wherever its kernels apply (the 3x3 stride-1 halo layers of the
+ *                    frozen VGG19, pix2pix.py:53-67; every eligible pix2pix G / D GEMM,
+ *                    pix2pix.py:110-142, :194-220), bf16x6 / fp32 tiles elsewhere: each fp32
+ *                    operand, pre-scaled by a power of two s, is split into fp16 h + l (RNE,
+ *                    |l| <= 2^-11 |s x|) and a product is h.h' + h.l' + l.h' -- three fp16 piece
+ *                    products (dropped terms < 2^-21 |ab|) on three v_mfma_f32_16x16x32_f16 per
+ *                    32 channels, half the bf16x6 MFMA count.  Scales: weights 2^8 (|w| < 255,
+ *                    22 bits for |w| >= 2^-11); gradients and activations 2^(14 - e) from a
+ *                    bound b < 2^e of the tensor (dg_conv_set_grad_scale, dg_conv_set_act_scale:
+ *                    22 bits for every value >= 2^-17 b); an activation without a scale source
+ *                    is measured by the op that splits it, or, in caller-held planes, keeps the
+ *                    static 2^-4 (|x| < 2^20; 22 bits only for |x| >= 2).
+ *                    A descriptor's x / dy planes are fp16x3 (4 B per element) when an fp16x3
+ *                    op reads them, its w planes [fp16x3 | bf16x6] (dg_conv_planes_size).
  * New descriptors take $DG_CONV_MATH ("fp32" | "bf16x6" | "fp16" | "f16x3"; default bf16x6).
  * Changing the mode re-plans the descriptor: query workspace sizes after it. */
 enum { DG_MATH_FP32 = 0, DG_MATH_BF16X6 = 1, DG_MATH_FP16 = 2, DG_MATH_F16X3 = 3 };
@@ -167,10 +169,33 @@ int dg_conv_planes_format(dg_conv_t d, int tensor, int *format);
  * by atomicMax (the caller zeroes them per step).  All device pointers, kept by the descriptor. */
 int dg_conv_set_grad_scale(dg_conv_t d, const float *dy_m, const float *dy_g, const float *dx_m, const float *dx_g,
                            float *dx_max);
+/* fp16x3 activation scale context (round 5).  An activation's fp16x3 planes are scaled by
+ * 2^(14 - e) from a bound b = max(m[0..7]) * (g ? *g : 1) + (c ? *c : 0) < 2^e, like a gradient's,
+ * so every |x| >= 2^-17 b keeps 22 bits (a static 2^-4 leaves |x| < 2 with a subnormal low piece).
+ *   x_m / x_g / x_c: the source of the layer input's planes (the one their producer wrote them
+ *     with: a BN forward's bound -- dg_bn_fwd_train_seg_x -- or a producing conv's output source
+ *     below); a plain 8-float slot (x_g, x_c NULL) is also measured into (max |x|) by any op of
+ *     this descriptor that splits x itself.  NULL x_m: x planes in the workspace are measured per
+ *     op; caller-held x planes keep the static 2^-4.
+ *   y_m / y_g / y_c: the source of the output planes the forward writes for its consumer
+ *     (planes->out, any arithmetic): normally (max |x| measured, max over output channels of
+ *     sum |w| over taps and input channels, max |bias|) -- a bound of |y| after a ReLU /
+ *     LeakyReLU / linear activation.  y_max: 8 floats receiving max |y| of the forward (the
+ *     16x16-tile, split-K reduce and small-Cin epilogues), the caller zeroes them.
+ * All device pointers, kept by the descriptor. */
+int dg_conv_set_act_scale(dg_conv_t d, const float *x_m, const float *x_g, const float *x_c, const float *y_m,
+                          const float *y_g, const float *y_c, float *y_max);
 /* max |x| over [rows][ld] (first C columns) into out[0..7] by atomicMax (the caller zeroes
  * them; the max is their max): the measured max of a gradient entering an fp16x3 input
  * gradient from fp32 */
 int dg_absmax(const float *x, int64_t rows, int C, int ld, float *out, dg_stream_t stream);
+/* the same into freshly zeroed out[0..7] (a measured max of one tensor) */
+int dg_absmax_set(const float *x, int64_t rows, int C, int ld, float *out, dg_stream_t stream);
+/* g_out[0] = max over output channels co of sum over k of |w[k][co]| (w as [K][Co]: an HWIO
+ * kernel with K = kh*kw*Cin), c_out[0] (may be NULL) = max |bias| (0 for bias NULL): the
+ * terms of a conv output's bound for dg_conv_set_act_scale (y_g, y_c) */
+int dg_weight_bound(const float *w, int64_t K, int Co, const float *bias, float *g_out, float *c_out,
+                    dg_stream_t stream);
 /* the arithmetic op's GEMM runs in (DG_MATH_*: fp32 for the exact direct kernels -- Co 1,
  * narrow, small-Cin -- and fp32 MFMA tiles; bf16x6, fp16 or fp16x3 for the split kernels):
  * per-op peaks for a roofline */
@@ -301,6 +326,23 @@ int dg_bn_fwd_train_seg_h(int S, int M, int C, const float *y, int ldy, const fl
                           float *z, int ldz, int act, float alpha,
                           float drop_rate, uint32_t drop_seed, uint32_t drop_seed_stride, const int32_t *step_dev,
                           void *zp0, int zp0C, int zp0col, void *zp1, int zp1C, int zp1col,
+                          const float *res, int ldres, void *z_f16,
+                          void *ws, size_t ws_bytes, dg_stream_t stream);
+/* dg_bn_fwd_train_seg_h with bound-scaled fp16x3 z planes (round 5).  z_bound (8 floats,
+ * zeroed and filled here; NULL: the static 2^-4): max over channels of (|gamma| invstd
+ * max |y - mean| + |beta|) x the dropout keep scale >= max |z|, from per-chunk maxima of the
+ * statistics pass -- the planes' scale source the consuming conv reads
+ * (dg_conv_set_act_scale x_m = z_bound).  cp (may be NULL): cpC channels ([S*M rows], pixel
+ * stride ldcp) of a second tensor whose planes go to zp0 at column cpcol with the same scale,
+ * and cp_bound their bound (8 floats, merged into z_bound): the U-Net skip half of the
+ * concatenation the next ConvT reads (pix2pix.py:188), so one scale covers its whole operand. */
+int dg_bn_fwd_train_seg_x(int S, int M, int C, const float *y, int ldy, const float *gamma, const float *beta,
+                          float *save_mean, float *save_invstd,
+                          float *moving_mean, float *moving_var, float momentum, float eps,
+                          float *z, int ldz, int act, float alpha,
+                          float drop_rate, uint32_t drop_seed, uint32_t drop_seed_stride, const int32_t *step_dev,
+                          void *zp0, int zp0C, int zp0col, void *zp1, int zp1C, int zp1col,
+                          float *z_bound, const float *cp, int ldcp, int cpC, int cpcol, const float *cp_bound,
                           const float *res, int ldres, void *z_f16,
                           void *ws, size_t ws_bytes, dg_stream_t stream);
 int dg_bn_bwd_seg_h(int S, int M, int C, const float *dz, int lddz, const float *z, int ldz,
@@ -446,6 +488,12 @@ int dg_maxpool2_fwd_pl(int N, int H, int W, int C, const float *x, int ldx, floa
 /* the same with the consumer's plane format (DG_PLANES_*; fp16x3: C % 32 == 0) */
 int dg_maxpool2_fwd_plf(int N, int H, int W, int C, const float *x, int ldx, float *y, int ldy, void *y_planes,
                         int y_planes_format, dg_stream_t stream);
+/* the same with fp16x3 planes scaled from the source (scale_m, scale_g, scale_c) -- the
+ * producing conv's output source (dg_conv_set_act_scale y_m / y_g / y_c), a bound of the pooled
+ * values too; NULL scale_m: the static 2^-4 */
+int dg_maxpool2_fwd_x3(int N, int H, int W, int C, const float *x, int ldx, float *y, int ldy, void *y_planes,
+                       int y_planes_format, const float *scale_m, const float *scale_g, const float *scale_c,
+                       dg_stream_t stream);
 int dg_maxpool2_bwd_pl(int N, int H, int W, int C, const float *x, int ldx, const float *dy, int lddy,
                        float *dx, int lddx, float beta, int act, float alpha, void *dx_planes, dg_stream_t stream);
 /* backward of a pool fused by dg_conv_fwd_pool, from its index bytes (the full-size

@@ -41,12 +41,12 @@ DEV = "cuda"
 # of each G variable's scale (measured: down1/kernel 1.2e-3 of 0.95, last/bias
 # 4.5e-5 of 21.4; D gradients, losses, logits and PSNR are unaffected).  G
 # gradients there are held to 1e-4 + 2e-3 * max|g| elementwise and 1e-3 on L2;
-# the same step conditioned on the GPU's decisions holds max-abs 1e-4
-# (tests/test_step_gpu.py::test_step_parity_with_vgg_content) and the
-# content-free bs16 fixture (p2p_bs16_core) holds max-abs 1e-4 unconditioned.
-# (the fp16x3 G / D of the default conv math resolve more of those near-ties differently: measured
-# 2.3e-3 of down1/kernel's 0.95 at r4; the bf16x6 G / D keep 2e-3)
-VGG_TIE_REL = {"bf16x6": 2e-3, "f16x3": 4e-3}
+# the same step conditioned on the GPU's decisions holds max-abs 1e-4 + 1e-4 * max|g| (the fp32
+# noise floor of the full-width content gradient, tests/test_step_gpu.py FLOOR_REL; measured r5:
+# G down1/kernel 9.5e-5 fp16x3, 1.4e-4 bf16x6) and the content-free bs16 fixture (p2p_bs16_core)
+# holds max-abs 1e-4 unconditioned.  (Round 4's static fp16x3 activation scale needed 4e-3 here;
+# with bound-scaled activation planes both conv arithmetics are held to the same 2e-3.)
+VGG_TIE_REL = {"bf16x6": 2e-3, "f16x3": 2e-3}
 # The SR-family generators decide ReLU / PReLU / max-pool branches themselves
 # (SRGAN's residual blocks, the autoencoder's 15 ReLU convs and 5 pools), and
 # their discriminators' LeakyReLU(0.2) inputs tie within fp32 rounding (see
@@ -147,11 +147,8 @@ def test_pix2pix_bs16_matches_golden(case):
     x2, y2 = batch(meta, meta["batch_seeds"][1])
     loss2 = tr.step(torch.from_numpy(x2).to(DEV), torch.from_numpy(y2).to(DEV))
     torch.cuda.synchronize()
-    # (the content-on fixture under the fp16x3 G / D: more step-1 sign differences among the
-    # content-spread G gradients, measured median 5.02% of a step on down8/gamma at r4 -> 10%)
     _check_step2(d, loss2, m.generator.arena, m.discriminator.arena, 2e-4, 2e-4, 8, case,
-                 steps_apart=4.2 if content else 2.0,
-                 median_frac=0.1 if content and nets.P2P_MATH == "f16x3" else 0.05)
+                 steps_apart=4.2 if content else 2.0, median_frac=0.05)
 
 
 @gpu

@@ -4,8 +4,10 @@ same seeded weights and synthetic noisy/clean 256x256 pairs.
 
 Tolerances (BASELINE.json north_star): |dPSNR| < 0.01 dB on the generator
 output, max-abs gradient difference < 1e-4 for every G and D variable (on the
-HIP path's own activation decisions, near-ties audited); loss values to 1e-5
-relative; BN moving statistics to 1e-5.
+HIP path's own activation decisions, near-ties audited) -- plus, for the
+full-width step with the VGG19 content term, the measured fp32 noise floor
+1e-4 x max|g| (FLOOR_REL below); loss values to 1e-5 relative; BN moving
+statistics to 1e-5.
 """
 import math
 
@@ -193,12 +195,13 @@ def test_generator_inference_uses_moving_stats():
 # D still meet 1e-4 on the fp32 CPU restatement itself).
 FP32_FLOOR_REL = 1e-4
 # The G / D GEMMs in their default fp16x3 arithmetic (include/dgan.h DG_MATH_F16X3: operands to
-# 2^-22, products to ~3 x 2^-22 -- eight times fp32's 2^-24, a thousand times below the TF32 that
-# TensorFlow runs fp32 convs in on NVIDIA GPUs by default): the content gradient crosses G's whole
-# fp16x3 backward to down1, whose kernel gradient then misses fp64 by 2.9e-4 x max|g| (r4: 8.1e-4 of
-# 2.85; the fp32 CPU restatement 1.1e-4 of it) -- held to 1e-4 + 4e-4 x max|g|; the bf16x6 G / D
-# (DG_P2P_MATH=bf16x6) keeps the fp32 floor
-FLOOR_REL = {"bf16x6": FP32_FLOOR_REL, "f16x3": 4e-4}
+# 2^-22, products to ~3 x 2^-22) are held to the same floor as fp32 / bf16x6.  Round 4 scaled
+# activation planes by a static 2^-4, so a BN output |x| < 2 carried an absolute 2^-21 instead of
+# 22 bits, and G down1/kernel missed fp64 by 2.9e-4 x max|g| (8.1e-4 of 2.85; it needed 4e-4 here);
+# with the planes scaled from their producers' bounds (dg_conv_set_act_scale,
+# dg_bn_fwd_train_seg_x) it misses by 3.4e-5 x max|g| (9.5e-5 absolute, r5) -- closer than the
+# bf16x6 G / D (5.0e-5 x, 1.4e-4) and the fp32 CPU restatement (1.1e-4 x)
+FLOOR_REL = {"bf16x6": FP32_FLOOR_REL, "f16x3": FP32_FLOOR_REL}
 
 VGG_PARITY_CASES = [
     # (id, G/D width divisor, VGG19 width divisor, dropout rate, G / D conv math)

@@ -92,6 +92,7 @@ def test_x3_shared_weight_planes_serve_bwd_data():
     holds no bf16x6 part (tensor_plane_bytes)."""
     N, H, W, Ci, Co = 2, 24, 32, 64, 128
     d = ops.ConvDesc(N, H, W, Ci, Co, 3, 1, "same", math="f16x3")
+    d.set_act_scale(x=(torch.zeros(8, device="cuda"),))   # held x planes: a plain max slot, measured
     x, w, dy = _rand((N, H, W, Ci), 1), _rand(d.weight_shape, 2, 0.05), _rand((N, H, W, Co), 3)
     P = ops.ConvPlanes.for_desc(d, x=True, dy=True, w=True)
     assert P.w is not None and 4 * 9 * Ci * Co <= P.w.buf.numel() < 10 * 9 * Ci * Co
@@ -111,13 +112,21 @@ def test_x3_shared_weight_planes_serve_bwd_data():
 @pytest.mark.parametrize("prod_math", ["bf16x6", "f16x3"])
 def test_x3_producer_planes_equal_the_split(prod_math):
     """conv A (relu) -> conv B (fp16x3): A's epilogue writes B's x planes (out_format
-    fp16x3); B's forward on them is bit-identical to B splitting A's fp32 output."""
+    fp16x3) scaled from A's output bound (dg_conv_set_act_scale: max |x| measured, A's weight
+    bound, max |bias|); B's forward on them is bit-identical to B splitting A's fp32 output
+    with the same scale source, and A's epilogue measures max |y_A| (B's input)."""
     N, H, W, C0, C1, C2 = 2, 24, 40, 32, 64, 128
     a = ops.ConvDesc(N, H, W, C0, C1, 3, 1, "same", math=prod_math)
     b = ops.ConvDesc(N, H, W, C1, C2, 3, 1, "same", math="f16x3")
     x = _rand((N, H, W, C0), 4)
     wa, wb = _rand(a.weight_shape, 5, 0.08), _rand(b.weight_shape, 6, 0.05)
     ba = _rand((C1,), 7, 0.1)
+    mx, wbd, ymx = torch.zeros(8, device="cuda"), torch.zeros(2, device="cuda"), torch.zeros(8, device="cuda")
+    ops.absmax_set(x, mx)
+    ops.weight_bound(wa, wbd[0:1], bias=ba, c_out=wbd[1:2])
+    src = (mx, wbd[0:1], wbd[1:2])
+    a.set_act_scale(y=src, y_max=ymx)
+    b.set_act_scale(x=src)
     ya = torch.empty(N, H, W, C1, device="cuda")
     Pb = ops.ConvPlanes.for_desc(b, x=True)
     assert Pb.x.fmt == ops.PLANES_F16X3 and Pb.x.buf.numel() >= 4 * N * H * W * C1
@@ -127,9 +136,13 @@ def test_x3_producer_planes_equal_the_split(prod_math):
     assert Pb.x.ready
     y_fed, y_own = torch.empty(N, H, W, C2, device="cuda"), torch.empty(N, H, W, C2, device="cuda")
     b.fwd(ya, wb, y_fed, planes=Pb)        # reads the producer's planes
-    b.fwd(ya, wb, y_own)                   # splits ya itself
+    Po = ops.ConvPlanes.for_desc(b, x=True)
+    b.fwd(ya, wb, y_own, planes=Po)        # splits ya itself (same source)
     torch.cuda.synchronize()
     assert torch.equal(y_fed, y_own)
+    assert float(ymx.max()) == float(ya.abs().max())
+    bound = float(mx.max()) * float(wbd[0]) + float(wbd[1])
+    assert float(ya.abs().max()) <= bound
 
 
 @gpu
@@ -143,11 +156,18 @@ def test_x3_fused_pool_planes_and_unfused_pool():
     assert d.pool_fusable("relu")
     x, w, b = _rand((N, H, W, Ci), 8), _rand(d.weight_shape, 9, 0.06), _rand((Co,), 10, 0.1)
     wn = _rand(nxt.weight_shape, 11, 0.05)
+    # the pooled planes' scale source: d's output bound (max |x|, d's weight bound, max |b|)
+    mx, wbd, pmx = torch.zeros(8, device="cuda"), torch.zeros(2, device="cuda"), torch.zeros(8, device="cuda")
+    ops.absmax_set(x, mx)
+    ops.weight_bound(w, wbd[0:1], bias=b, c_out=wbd[1:2])
+    src = (mx, wbd[0:1], wbd[1:2])
+    d.set_act_scale(x=(torch.zeros(8, device="cuda"),), y=src, y_max=pmx)
+    nxt.set_act_scale(x=src)
     y = torch.empty(N, H, W, Co, device="cuda")
     d.fwd(x, w, y, bias=b, act="relu")
     py0 = torch.empty(N, H // 2, W // 2, Co, device="cuda")
     P0 = ops.ConvPlanes.for_desc(nxt, x=True)
-    ops.maxpool2_fwd(y, py0, planes_out=P0.x)
+    ops.maxpool2_fwd(y, py0, planes_out=P0.x, scale=src)
     py1 = torch.empty_like(py0)
     P1 = ops.ConvPlanes.for_desc(nxt, x=True)
     idx = torch.empty((N, H // 2, W // 2, Co), dtype=torch.uint8, device="cuda")
@@ -162,6 +182,7 @@ def test_x3_fused_pool_planes_and_unfused_pool():
     nb = 4 * N * (H // 2) * (W // 2) * Co
     assert torch.equal(P0.x.buf[:nb], P1.x.buf[:nb]) and torch.equal(P0.x.buf[:nb], P2.x.buf[:nb])
     assert torch.equal(yo[0], yo[1]) and torch.equal(yo[0], yo[2])
+    assert float(pmx.max()) == float(py1.abs().max())   # the fused pool measured its output
 
 
 @gpu
