@@ -117,6 +117,9 @@ def main():
                          "reference driver's (train_srgan.py fp16=1, the others 0)")
     ap.add_argument("--dist", action="store_true",
                     help="data-parallel path (process group + gradient all-reduce) even at world size 1")
+    ap.add_argument("--no-twin", action="store_true",
+                    help="pix2pix: skip the bf16x6 twin measurement (fp32_exact: every conv GEMM on six bf16 "
+                         "piece products instead of fp16x3)")
     args = ap.parse_args()
     wl = WORKLOADS[args.model]
     batch = args.batch or wl["batch"]
@@ -193,7 +196,20 @@ def main():
     def trainer_of(model):
         return model.trainer(x.shape) if args.model == "pix2pix" else model.trainer(x.shape, y.shape)
 
-    def measure(content):
+    def measure(content, twin=False):
+        if twin:   # every pix2pix / VGG19 GEMM in bf16x6 (fp32-accurate operands) instead of fp16x3
+            from dgan import nets as _nets_t
+            saved = (_nets_t.P2P_MATH, os.environ.get("DG_VGG_MATH"))
+            _nets_t.P2P_MATH = "bf16x6"
+            os.environ["DG_VGG_MATH"] = "bf16x6"
+            try:
+                return measure(content)
+            finally:
+                _nets_t.P2P_MATH = saved[0]
+                if saved[1] is None:
+                    os.environ.pop("DG_VGG_MATH", None)
+                else:
+                    os.environ["DG_VGG_MATH"] = saved[1]
         model = build(content)
         trainer = trainer_of(model)
         for _ in range(max(1, args.warmup // 2)):
@@ -248,6 +264,10 @@ def main():
     model, trainer, graph, elapsed = measure(content)
     hip_graph = graph is not None
     conv_math = "fp16" if fp16 else ("bf16x6" if ops.default_conv_math() == ops.MATH_BF16X6 else "fp32")
+    if not fp16 and args.model != "pix2pix" and content:
+        from dgan.sr_trainer import VGGNetwork
+        if wl["size"] ** 2 >= VGGNetwork.X3_MIN_PIXELS and not os.environ.get("DG_VGG_MATH"):
+            conv_math = f"G/D {conv_math}, VGG19 f16x3"
     if args.model == "pix2pix":
         from dgan import nets as _nets
         conv_math = f"G/D {_nets.P2P_MATH}, VGG19 {os.environ.get('DG_VGG_MATH', 'f16x3')}"
@@ -327,6 +347,16 @@ def main():
         core = {"value": round(images / el_core, 2), "ms_per_step": round(el_core / args.steps * 1e3, 3),
                 "workload": "the same step without the VGG19 content term (pix2pix.py:87 weight 0)"}
 
+    twin = None
+    if (args.model == "pix2pix" and world == 1 and not args.no_twin and not args.profile_only
+            and os.environ.get("DG_P2P_MATH", "f16x3") == "f16x3"):
+        torch.cuda.empty_cache()
+        _, _, _, el_twin = measure(content, twin=True)
+        twin = {"value": round(images / el_twin, 2), "ms_per_step": round(el_twin / args.steps * 1e3, 3),
+                "conv_math": "bf16x6 (G / D and VGG19: six bf16 piece products per fp32 product, dropped terms "
+                             "< 2^-26)",
+                "workload": "the same step (same flags) with every fp16x3 GEMM on bf16x6"}
+
     # ---- CPU baseline: torch fp32 restatement, rank 0, N=1 only -------------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile_only:
@@ -355,7 +385,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp16 GEMM operands, fp32 accumulation (mixed_float16)" if fp16 else "fp32",
+            "dtype": ("fp16 GEMM operands, fp32 accumulation (mixed_float16)" if fp16 else
+                      "fp32 (GEMMs fp16x3, operands 2^-22)" if "f16x3" in conv_math else "fp32"),
             "conv_math": conv_math,
             "data": f"synthetic (seeded noisy/clean {wl['size']}x{wl['size']} pairs resident in HBM; "
                     "random-init weights)",
@@ -368,6 +399,7 @@ def main():
             "lib": _lib_build_info(),
             "losses": [round(float(v), 6) for v in losses],
             "core": core,
+            "fp32_exact": twin,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

@@ -231,7 +231,7 @@ k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, i
     }
     for (int sg = 0; sg < S; ++sg) {
         const long o = (long)sg * R * C;
-        float vn[FIN_K], vm[FIN_K], vq[FIN_K];
+        float vn[FIN_K], vm[FIN_K], vq[FIN_K], vb[FIN_K];
 #pragma unroll
         for (int k = 0; k < FIN_K; ++k) {
             const int r = ln + k * FIN_L;
@@ -240,6 +240,7 @@ k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, i
             vn[k] = ok ? pn[i] : 0.f;
             vm[k] = ok ? pmean[i] : 0.f;
             vq[k] = ok ? pm2[i] : 0.f;
+            vb[k] = ok && pbd ? pbd[i] : 0.f;   // (in the same load round: the chunk bounds)
         }
         float sn = 0.f, sm = 0.f;
 #pragma unroll
@@ -259,7 +260,7 @@ k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, i
 #pragma unroll
             for (int k = 0; k < FIN_K; ++k) {
                 const int r = ln + k * FIN_L;
-                if (cok && r < R) dmax = fmaxf(dmax, pbd[o + (long)r * C + c] + fabsf(vm[k] - mu));
+                if (cok && r < R) dmax = fmaxf(dmax, vb[k] + fabsf(vm[k] - mu));
             }
             sh[ln * FIN_C + cl] = dmax;
             __syncthreads();

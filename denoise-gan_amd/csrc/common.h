@@ -103,15 +103,40 @@ constexpr int X3_SHARDS = 8;
 // output's bound m * g + c (m: measured max |input|, g: max over output channels of sum |w|,
 // c: max |bias|) -- a static 2^-4 would leave |x| < 2 with a subnormal low piece (an absolute
 // floor of 2^-21 instead of 22 bits)
-__device__ __forceinline__ float x3_grad_scale(const float *m, const float *g, const float *c = nullptr) {
-    float mm = m[0];
-#pragma unroll
-    for (int i = 1; i < X3_SHARDS; ++i) mm = fmaxf(mm, m[i]);
-    const float b = mm * (g ? *g : 1.f) + (c ? *c : 0.f);
+__device__ __forceinline__ float x3_bound_scale(float b) {
     if (!(b > 0.f) || !(b <= 3.0e38f)) return 1.f;
     int e;
     (void)frexpf(b, &e);   // b < 2^e
     return ldexpf(1.f, 14 - e);
+}
+__device__ __forceinline__ float x3_grad_scale(const float *m, const float *g, const float *c = nullptr) {
+    float mm = m[0];
+#pragma unroll
+    for (int i = 1; i < X3_SHARDS; ++i) mm = fmaxf(mm, m[i]);
+    return x3_bound_scale(mm * (g ? *g : 1.f) + (c ? *c : 0.f));
+}
+// the raw terms of a scale source, loaded at kernel entry and combined in the epilogue (the
+// GEMM kernels: the loads then complete under the main loop instead of stalling each block's tail)
+struct X3Raw {
+    float m[X3_SHARDS];
+    float g, c;
+    bool on;
+};
+__device__ __forceinline__ X3Raw x3_raw(const float *m, const float *g, const float *c) {
+    X3Raw r;
+    r.on = m != nullptr;
+#pragma unroll
+    for (int i = 0; i < X3_SHARDS; ++i) r.m[i] = m ? m[i] : 0.f;
+    r.g = g ? *g : 1.f;
+    r.c = c ? *c : 0.f;
+    return r;
+}
+__device__ __forceinline__ float x3_raw_scale(const X3Raw &r, float dflt) {
+    if (!r.on) return dflt;
+    float mm = r.m[0];
+#pragma unroll
+    for (int i = 1; i < X3_SHARDS; ++i) mm = fmaxf(mm, r.m[i]);
+    return x3_bound_scale(mm * r.g + r.c);
 }
 // |v| into a sharded device max (non-negative floats order as their bit patterns): a
 // butterfly over each wave's lanes, the waves' maxima through LDS, then one lane reads the

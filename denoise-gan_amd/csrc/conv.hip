@@ -2358,10 +2358,10 @@ int dg_absmax_set(const float *x, int64_t rows, int C, int ld, float *out, dg_st
 }
 
 int dg_weight_bound(const float *w, int64_t K, int Co, const float *bias, float *g_out, float *c_out,
-                    dg_stream_t stream) {
+                    float *zero8, dg_stream_t stream) {
     DG_ARG(w && g_out, "NULL tensor");
     DG_ARG(K > 0 && Co > 0, "bad shape");
-    dg::launch_weight_bound(w, K, Co, bias, g_out, c_out, (hipStream_t)stream);
+    dg::launch_weight_bound(w, K, Co, bias, g_out, c_out, (hipStream_t)stream, zero8);
     DG_LAUNCHED("weight_bound");
     return DG_OK;
 }

@@ -67,6 +67,17 @@ __device__ __forceinline__ float x3_out_scale(const GemmArgs &p) {
     return 1.f / (sa * sb);
 }
 
+// the scale sources of an fp16x3 GEMM (operands A, B and the output planes), loaded at kernel entry
+struct X3Pre {
+    X3Raw a, b, y;
+};
+__device__ __forceinline__ X3Pre x3_pre(const GemmArgs &p) {
+    return X3Pre{x3_raw(p.as_m, p.as_g, p.as_c), x3_raw(p.bs_m, p.bs_g, p.bs_c), x3_raw(p.ys_m, p.ys_g, p.ys_c)};
+}
+__device__ __forceinline__ float x3_out_scale(const GemmArgs &p, const X3Pre &r) {
+    return 1.f / (x3_raw_scale(r.a, p.x3_sa) * x3_raw_scale(r.b, p.x3_sb));
+}
+
 // hi plane of element (pix, col) of a packed plane tensor, as a float (its sign is
 // the element's; C < 0: fp16x3 planes of -C channels, the value times F16X3_XS)
 __device__ __forceinline__ float hi_plane(const unsigned short *zp, int C, long pix, int col) {
@@ -172,6 +183,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs &p, f32x16 (&acc)[T
                                               int Mrows, const PhaseInfo &ph, int phase, int split, int l32, int h2) {
     const ConvGeom &g = p.g;
     float vmax = 0.f;   // max |output| of this lane (p.ymax)
+    const float ys = p.yp ? plane_scale(p) : 0.f;
 #pragma clang loop unroll(full)
     for (int a = 0; a < TM; ++a) {
 #pragma clang loop unroll(full)
@@ -201,7 +213,7 @@ __device__ __forceinline__ void conv_epilogue(const GemmArgs &p, f32x16 (&acc)[T
                         if (p.beta != 0.f) v += p.beta * p.C[off + col];
                         p.C[off + col] = v;
                     }
-                    if (p.yp) store_planes1(p.yp, p.ypC, pix, col, v, plane_scale(p));
+                    if (p.yp) store_planes1(p.yp, p.ypC, pix, col, v, ys);
                     vmax = fmaxf(vmax, fabsf(v));
                 }
             }
@@ -225,7 +237,9 @@ struct RowPix {
 // once per row per lane.
 template <int MODE, int TM, int TN, class RowMap>
 __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[TM][TN], int rbase, int cbase,
-                                                RowMap rowmap, int phase, int split, int lane, float *stage) {
+                                                RowMap rowmap, int phase, int split, int lane, float *stage,
+                                                float ys_pre = 0.f) {
+    // (ys_pre > 0: the output planes' scale, computed by the caller from loads issued at entry)
     constexpr int WTN = 16 * TN;
     constexpr int LD = WTN + 4;   // padded staging row (floats): conflict-free writes
     constexpr int C4 = WTN / 4;   // float4 per row
@@ -237,7 +251,7 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
     const int c4 = lane % C4;
     const int col = cbase + c4 * 4;
     const bool full = col + 3 < p.N;
-    const float ys = p.yp ? plane_scale(p) : 0.f;
+    const float ys = p.yp ? (ys_pre > 0.f ? ys_pre : plane_scale(p)) : 0.f;
     float vmax = 0.f;   // max |output| of this lane (p.ymax)
 #pragma clang loop unroll(full)
     for (int a = 0; a < TM; ++a) {
@@ -340,7 +354,8 @@ void launch_split_x3(const float *src, int ld, long rows, int C, void *dst, int 
 // max |x| of [rows][ld] (first C columns) into *out by atomicMax (zeroed by the caller)
 void launch_absmax(const float *x, long rows, int C, int ld, float *out, hipStream_t s);
 // max over columns of sum_k |w[k][co]| into gout[0], max |bias| into cout[0] (dg_weight_bound)
-void launch_weight_bound(const float *w, long K, int Co, const float *bias, float *gout, float *cout, hipStream_t s);
+void launch_weight_bound(const float *w, long K, int Co, const float *bias, float *gout, float *cout, hipStream_t s,
+                         float *zero8 = nullptr);
 // the fp16 conv math (DG_MATH_FP16): one fp16 plane [rows][C] and its GEMM (kF16Cfgs)
 void launch_split_f16(const float *src, int ld, long rows, int C, void *dst, hipStream_t s);
 void launch_split_f16_pair(const float *a, int lda, long ra, int ca, void *da, const float *b, int ldb, long rb,

@@ -120,7 +120,7 @@ __device__ __forceinline__ void small_epi_load(const GemmArgs &p, int rbase, int
 }
 template <bool XL>
 __device__ __forceinline__ void small_fwd_epilogue(const GemmArgs &p, const f32x16 &acc, int rbase, int cbase,
-                                                   float *stage, int lane, const SmallEpi &e, float &vmax) {
+                                                   float *stage, int lane, const SmallEpi &e, float &vmax, float ys) {
     const int l32 = lane & 31, h2 = lane >> 5;
 #pragma unroll
     for (int r = 0; r < 16; ++r) stage[((r & 3) + 8 * (r >> 2) + 4 * h2) * 36 + l32] = acc[r];
@@ -151,7 +151,7 @@ __device__ __forceinline__ void small_fwd_epilogue(const GemmArgs &p, const f32x
 #pragma unroll
             for (int q = 0; q < 4; ++q) dst[q] = o[q];
         }
-        if (p.yp) store_planes4(p.yp, p.ypC, pix, col, o, plane_scale(p));
+        if (p.yp) store_planes4(p.yp, p.ypC, pix, col, o, ys);
         if (p.ymax) {   // (max |y|: the consumer's measured input, dg_conv_set_act_scale)
 #pragma unroll
             for (int q = 0; q < 4; ++q) vmax = fmaxf(vmax, fabsf(o[q]));
@@ -193,6 +193,7 @@ k_small_fwd(const GemmArgs p) {
     if (p.bias) epi.bias = sc_ld4(p.bias + col0 + (lane & 7) * 4, false);
     float pre[NL];
     float vmax = 0.f;   // max |y| of this lane's outputs (p.ymax)
+    const X3Raw ysr = x3_raw(p.ys_m, p.ys_g, p.ys_c);   // (the output planes' scale source)
     int t = blockIdx.x;
     if (t >= ntiles) return;   // (the whole block: block_atomic_absmax below stays uniform)
     {
@@ -232,7 +233,7 @@ k_small_fwd(const GemmArgs p) {
         // the prefetched strip goes to LDS before this tile's stores are issued: waiting for the
         // loads then never waits for the stores (one vmcnt counts both)
         strip_store<CI, P, NTHR, KW, ST>(strip[(it + 1) & 1], tid, pre);
-        small_fwd_epilogue<XL>(p, acc, rbase, col0, stage[wid], lane, epi, vmax);
+        small_fwd_epilogue<XL>(p, acc, rbase, col0, stage[wid], lane, epi, vmax, x3_raw_scale(ysr, F16X3_XS));
         __syncthreads();
     }
     if (p.ymax) block_atomic_absmax(p.ymax, vmax);

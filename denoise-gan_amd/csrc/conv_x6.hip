@@ -152,6 +152,8 @@ k_conv_gemm_x6(const GemmArgs p) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid / WGN, wn = wid % WGN;
     const int l32 = lane & 31, h2 = lane >> 5;
+    X3Pre x3s;   // (fp16x3: the scale sources, loaded here, combined in the epilogue)
+    if constexpr (X3) x3s = x3_pre(p);
 
     int zz, tile;
     xcd_remap(zz, tile);
@@ -584,8 +586,10 @@ k_conv_gemm_x6(const GemmArgs p) {
     // before smem0 becomes the epilogue's staging area
     wait_dma_c<0>();
     barrier();
+    float ys_pre = 0.f;
     if constexpr (X3) {   // undo the operand scales (powers of two: exact)
-        const float osc = x3_out_scale(p);
+        const float osc = x3_out_scale(p, x3s);
+        ys_pre = p.yp ? x3_raw_scale(x3s.y, F16X3_XS) : 0.f;
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -607,7 +611,7 @@ k_conv_gemm_x6(const GemmArgs p) {
         return RowPix{row, pix};
     };
     conv_epilogue16<MODE, TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, rowmap, phase, split, lane,
-                                  reinterpret_cast<float *>(smem0) + wid * STAGE);
+                                  reinterpret_cast<float *>(smem0) + wid * STAGE, ys_pre);
 }
 
 void launch_split3(const float *src, int ld, long rows, int C, unsigned short *dst, hipStream_t s) {
@@ -667,46 +671,79 @@ void launch_split_x3(const float *src, int ld, long rows, int C, void *dst, int 
                            (_Float16 *)dst);
 }
 
-// max |x| over [rows][ld] (first C columns) into *out (atomicMax; the caller zeroes it)
+// max |x| over [rows][ld] (first C columns) into *out (atomicMax; the caller zeroes it); a dense
+// tensor (ld == C, 16-byte aligned) is read as one flat float4 array
 __global__ void __launch_bounds__(256) k_absmax(const float *__restrict__ x, long rows, int C, int ld, float *out) {
     float m = 0.f;
     const long total = rows * C;
-    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
-        const long r = e / C;
-        m = fmaxf(m, fabsf(x[r * ld + (e - r * C)]));
+    if (ld == C && ((((uintptr_t)x) & 15) == 0)) {
+        const long t4 = total >> 2;
+        for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < t4; e += (long)gridDim.x * blockDim.x) {
+            const f32x4 v = reinterpret_cast<const f32x4 *>(x)[e];
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+        }
+        for (long e = (t4 << 2) + (long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+             e += (long)gridDim.x * blockDim.x)
+            m = fmaxf(m, fabsf(x[e]));
+    } else {
+        for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
+            const long r = e / C;
+            m = fmaxf(m, fabsf(x[r * ld + (e - r * C)]));
+        }
     }
     block_atomic_absmax(out, m);
 }
 
 // forward bound of a conv's output (dg_conv_set_act_scale y_g / y_c): gout[0] = max over the
 // Co columns of sum over the K rows of |w[k][co]| (HWIO kernels: K = kh*kw*Cin), cout[0] =
-// max |bias| (0 without one).  One workgroup: lanes own columns, rows summed in order (the
-// small-Cin layers per step -- K 48 / 96 -- and the frozen VGG19 once per weight version)
+// max |bias| (0 without one); zero8 (may be NULL): 8 floats zeroed for a following absmax.
+// One workgroup: 64 columns at a time, 4 row lanes per column, rows summed 8 loads at a time
+// (the small-Cin layers per step -- K 48 / 96 -- and the frozen VGG19 once per weight version)
 __global__ void __launch_bounds__(256) k_weight_bound(const float *__restrict__ w, long K, int Co,
-                                                     const float *__restrict__ bias, float *gout, float *cout) {
-    __shared__ float red[2][256];
+                                                     const float *__restrict__ bias, float *gout, float *cout,
+                                                     float *zero8) {
+    __shared__ float red[256];
+    if (zero8 && threadIdx.x < X3_SHARDS) zero8[threadIdx.x] = 0.f;
+    const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
     float g = 0.f, c = 0.f;
-    for (int co = threadIdx.x; co < Co; co += blockDim.x) {
+    for (int c0 = 0; c0 < Co; c0 += 64) {
+        const int co = c0 + cl;
         float sum = 0.f;
-        for (long k = 0; k < K; ++k) sum += fabsf(w[k * Co + co]);
-        g = fmaxf(g, sum);
-        if (bias) c = fmaxf(c, fabsf(bias[co]));
+        if (co < Co) {
+            long k = rl;
+            for (; k + 28 < K; k += 32) {
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = w[(k + 4 * u) * Co + co];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) sum += fabsf(v[u]);
+            }
+            for (; k < K; k += 4) sum += fabsf(w[k * Co + co]);
+            if (bias && rl == 0) c = fmaxf(c, fabsf(bias[co]));
+        }
+        red[threadIdx.x] = sum;
+        __syncthreads();
+        if (rl == 0) g = fmaxf(g, red[cl] + red[64 + cl] + red[128 + cl] + red[192 + cl]);
+        __syncthreads();
     }
-    red[0][threadIdx.x] = g;
-    red[1][threadIdx.x] = c;
+    red[threadIdx.x] = g;
     __syncthreads();
     if (threadIdx.x == 0) {
-        for (int i = 1; i < (int)blockDim.x; ++i) {
-            g = fmaxf(g, red[0][i]);
-            c = fmaxf(c, red[1][i]);
-        }
+        for (int i = 1; i < 64; ++i) g = fmaxf(g, red[i]);
         gout[0] = g;
-        if (cout) cout[0] = c;
+    }
+    __syncthreads();
+    red[threadIdx.x] = c;
+    __syncthreads();
+    if (threadIdx.x == 0 && cout) {
+        for (int i = 1; i < 64; ++i) c = fmaxf(c, red[i]);
+        cout[0] = c;
     }
 }
 
-void launch_weight_bound(const float *w, long K, int Co, const float *bias, float *gout, float *cout, hipStream_t s) {
-    hipLaunchKernelGGL(k_weight_bound, dim3(1), dim3(256), 0, s, w, K, Co, bias, gout, cout);
+void launch_weight_bound(const float *w, long K, int Co, const float *bias, float *gout, float *cout, hipStream_t s,
+                         float *zero8) {
+    hipLaunchKernelGGL(k_weight_bound, dim3(1), dim3(256), 0, s, w, K, Co, bias, gout, cout, zero8);
 }
 
 void launch_absmax(const float *x, long rows, int C, int ld, float *out, hipStream_t s) {

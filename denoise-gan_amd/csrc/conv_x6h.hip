@@ -91,7 +91,8 @@ struct HaloGeom {
 // full-size activation is never written.
 template <int TM, int TN>
 __device__ __forceinline__ void conv_epilogue16_pool(const GemmArgs &p, f32x4 (&acc)[TM][TN], int prow0, int cbase,
-                                                     int ty, int tx, int nimg, int lane, float *stage) {
+                                                     int ty, int tx, int nimg, int lane, float *stage,
+                                                     float ys_pre = 0.f) {
     constexpr int WTN = 16 * TN;
     constexpr int LD = WTN + 4;
     constexpr int C4 = WTN / 4;
@@ -109,6 +110,7 @@ __device__ __forceinline__ void conv_epilogue16_pool(const GemmArgs &p, f32x4 (&
     f32x4 hv[NP];
     unsigned hix[NP];
     float vmax = 0.f;   // max |pooled value| of this lane (p.ymax: the consumer's measured input)
+    const float ys = p.yp ? (ys_pre > 0.f ? ys_pre : plane_scale(p)) : 0.f;
 #pragma unroll
     for (int a = 0; a < TM; ++a) {
 #pragma unroll
@@ -153,7 +155,7 @@ __device__ __forceinline__ void conv_epilogue16_pool(const GemmArgs &p, f32x4 (&
             const long pp = ((long)nimg * Ho2 + ho2) * Wo2 + wo2;
             *reinterpret_cast<unsigned *>(p.pidx + pp * p.N + col) = fi;
             if (p.pool_y) *reinterpret_cast<f32x4 *>(p.pool_y + pp * p.ldpy + col) = fv;
-            if (p.yp) store_planes4(p.yp, p.ypC, pp, col, fv, plane_scale(p));
+            if (p.yp) store_planes4(p.yp, p.ypC, pp, col, fv, ys);
 #pragma unroll
             for (int q = 0; q < 4; ++q) vmax = fmaxf(vmax, fabsf(fv[q]));
         }
@@ -230,6 +232,8 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     const int lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid >> 1, wn = wid & 1;
+    X3Pre x3s;   // (fp16x3: the scale sources, loaded here, combined in the epilogue)
+    if constexpr (X3) x3s = x3_pre(p);
 
     int zz, tile;
     // (the 4 phases of a patch back to back on one XCD: down2 input gradient
@@ -552,8 +556,10 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
 
     constexpr int STAGE = 16 * (WTN + 4);
     static_assert(NW * STAGE * 4 <= 2 * HG::BYTES, "epilogue staging fits in the halo buffers");
+    float ys_pre = 0.f;
     if constexpr (X3) {   // undo the operand scales (powers of two: exact)
-        const float osc = x3_out_scale(p);
+        const float osc = x3_out_scale(p, x3s);
+        ys_pre = p.yp ? x3_raw_scale(x3s.y, F16X3_XS) : 0.f;
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -574,9 +580,9 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         }
     };
     if constexpr (POOL)
-        conv_epilogue16_pool<TM, TN>(p, acc, wm * TM, n0 + wn * WTN, ty, tx, nimg, lane, stage);
+        conv_epilogue16_pool<TM, TN>(p, acc, wm * TM, n0 + wn * WTN, ty, tx, nimg, lane, stage, ys_pre);
     else
-        conv_epilogue16<MODE, TM, TN>(p, acc, wm * WTM, n0 + wn * WTN, rowmap, phase, split, lane, stage);
+        conv_epilogue16<MODE, TM, TN>(p, acc, wm * WTM, n0 + wn * WTN, rowmap, phase, split, lane, stage, ys_pre);
 }
 
 void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int tiles_x, int tiles_y, hipStream_t s,

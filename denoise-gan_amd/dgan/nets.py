@@ -32,6 +32,9 @@ DROP_RATE = 0.5   # pix2pix.py:138
 FEED_DY = not os.environ.get("DG_NO_FEED_DY")  # BN backward writes the conv's dy planes
 FEED_X = not os.environ.get("DG_NO_FEED_X")    # BN forward writes the next convs' x planes
 DY_PLANES_ONLY = not os.environ.get("DG_DY_FP32")  # ... and then skips the fp32 dy (its readers take the planes)
+# fp16x3 activation planes scaled from their producers' bounds (ActBounds); DG_NO_ACT_BOUND: the
+# round-4 static 2^-4 (same-box A/B only: |x| < 2 then loses bits)
+ACT_BOUNDS = not os.environ.get("DG_NO_ACT_BOUND")
 
 
 def _eb(buf):
@@ -102,8 +105,8 @@ class ActBounds:
 
     def first_conv(self, x, w):
         """Per forward: max |x| of the network input and the first conv's weight bound."""
-        ops.absmax_set(x, self.in_max)
-        ops.weight_bound(w, self.w1[0:1])
+        ops.weight_bound(w, self.w1[0:1], zero=self.in_max)   # (zeroes in_max for the absmax)
+        ops.absmax(x, self.in_max)
 
     @property
     def first_src(self):
@@ -341,7 +344,7 @@ class GeneratorPlan:
         # output -> zb[l] (down l+1's x), up u's BN output with the skip half of its concat ->
         # zb[8+u] (up u+1's x), down1's conv output -> (max |x|, down1's weight bound) (down2's x)
         self.ab = None
-        if train and any(x3_planes(P) for P in self.planes):
+        if train and ACT_BOUNDS and any(x3_planes(P) for P in self.planes):
             self.ab = ActBounds(16, device)
             for k, d in enumerate(descs):
                 if not x3_planes(self.planes[k]):
@@ -417,7 +420,7 @@ class GeneratorPlan:
                 # over both halves (below)
                 nxt = l + 1
                 outs = [(nxt, co, 0)] if xplanes(nxt) is not None else []
-                if 1 <= l <= 6 and xplanes(15 - l) is not None and not x3_planes(P[15 - l]):
+                if 1 <= l <= 6 and xplanes(15 - l) is not None and not (ab is not None and x3_planes(P[15 - l])):
                     outs.append((15 - l, self.ups[7 - l][1], self.ups[6 - l][2]))
                 self._bn_fwd(s, name, y, z, "lrelu", training, ws, outs=outs,
                              z_bound=ab.zb[l] if ab is not None else None)
@@ -438,7 +441,7 @@ class GeneratorPlan:
             copy = None
             if u <= 5 and xplanes(k) is not None:
                 outs.append((k, self.ups[u + 1][1], 0))
-                if x3_planes(P[k]):   # (+ the skip half, down 6-u's output, under one bound)
+                if ab is not None and x3_planes(P[k]):   # (+ the skip half, down 6-u's output, under one bound)
                     copy = (self.z_view(s, 6 - u), co, ab.zb[6 - u])
             self._bn_fwd(s, name, y, z, "relu", training, ws, rate, lambda hv: dropout_seed(drop_seed, u, hv),
                          step_dev, outs=outs, z_bound=ab.zb[8 + u] if ab is not None else None, copy=copy)
@@ -632,7 +635,7 @@ class DiscriminatorPlan:
             # fp16x3 activation planes scaled from their producers' bounds (ActBounds): D.down1's
             # conv output from (max |input pair|, down1's weight bound), BN block i's output zb[i]
             self.ab = None
-            if any(x3_planes(P) for P in self.planes):
+            if ACT_BOUNDS and any(x3_planes(P) for P in self.planes):
                 self.ab = ActBounds(len(self.desc), device)
                 for k, d in enumerate(self.desc):
                     if x3_planes(self.planes[k]):

@@ -878,11 +878,11 @@ def absmax_set(t, out):
     return out
 
 
-def weight_bound(w, g_out, bias=None, c_out=None):
+def weight_bound(w, g_out, bias=None, c_out=None, zero=None):
     """g_out[0] = max over output channels of sum |w| over the other axes (HWIO w), c_out[0] =
-    max |bias| (dg_weight_bound): a conv output's bound terms."""
+    max |bias| (dg_weight_bound): a conv output's bound terms; zero: 8 floats zeroed on the way."""
     Co = w.shape[-1]
-    call("dg_weight_bound", _p(w), w.numel() // Co, Co, _p(bias), _p(g_out), _p(c_out), _stream())
+    call("dg_weight_bound", _p(w), w.numel() // Co, Co, _p(bias), _p(g_out), _p(c_out), _p(zero), _stream())
 
 
 def upsample2_relu_fwd(x, z):

@@ -193,9 +193,10 @@ int dg_absmax(const float *x, int64_t rows, int C, int ld, float *out, dg_stream
 int dg_absmax_set(const float *x, int64_t rows, int C, int ld, float *out, dg_stream_t stream);
 /* g_out[0] = max over output channels co of sum over k of |w[k][co]| (w as [K][Co]: an HWIO
  * kernel with K = kh*kw*Cin), c_out[0] (may be NULL) = max |bias| (0 for bias NULL): the
- * terms of a conv output's bound for dg_conv_set_act_scale (y_g, y_c) */
+ * terms of a conv output's bound for dg_conv_set_act_scale (y_g, y_c).  zero8 (may be NULL):
+ * 8 floats zeroed on the way (the measured-max slot a following dg_absmax fills). */
 int dg_weight_bound(const float *w, int64_t K, int Co, const float *bias, float *g_out, float *c_out,
-                    dg_stream_t stream);
+                    float *zero8, dg_stream_t stream);
 /* the arithmetic op's GEMM runs in (DG_MATH_*: fp32 for the exact direct kernels -- Co 1,
  * narrow, small-Cin -- and fp32 MFMA tiles; bf16x6, fp16 or fp16x3 for the split kernels):
  * per-op peaks for a roofline */

@@ -257,3 +257,35 @@ def test_step_parity_with_vgg_content(case, monkeypatch):
     wg = _compare_grads(m.generator.arena, gG, "G", rtol=FLOOR_REL[gd_math])
     wd = _compare_grads(m.discriminator.arena, gD, "D", rtol=FLOOR_REL[gd_math])
     print(f"pix2pix+VGG parity ({case[0]}): worst G {wg}, worst D {wd}, overridden decisions {n_over}")
+
+
+@gpu
+@pytest.mark.timeout(900)
+def test_twenty_step_loss_trajectory_f16x3_bf16x6_oracle(monkeypatch):
+    """20 training steps with Keras-Adam (width 4, bs2, dropout and identity on, fresh synthetic
+    pairs each step) in the default fp16x3 G / D arithmetic, in bf16x6, and in the fp64 oracle
+    (no test followed fp16x3 past step 2).  Adam's sign-like normalisation
+    amplifies ulp-level gradient differences, so the HIP trajectories drift from fp64 step by step;
+    the bar: fp16x3 stays within 2x bf16x6's distance from the oracle (+1e-5), and both within
+    1e-3 relative of every oracle loss."""
+    from dgan import nets
+    from pix2pix import Pix2Pix
+    width, seed, steps = 4, 31, 20
+    st = O.P2PState(width=width, seed=seed, drop_rate=0.5, drop_seed=6)
+    pairs = [O.synthetic_pair(2, 256, seed=500 + k) for k in range(steps)]
+    ref = np.array([O.train_step(st, x, y)["losses"] for x, y in pairs], np.float64)
+    traj = {}
+    for math_ in ("f16x3", "bf16x6"):
+        monkeypatch.setattr(nets, "P2P_MATH", math_)
+        m = Pix2Pix(Args(width=width, seed=seed, dropout_seed=6))
+        out = []
+        for x, y in pairs:
+            loss = m.trainer(x.shape).step(torch.from_numpy(x).cuda(), torch.from_numpy(y).cuda())
+            out.append(loss.cpu().double().numpy())
+        traj[math_] = np.array(out)
+    dev = {k: np.abs(v - ref) / (np.abs(ref) + 1e-6) for k, v in traj.items()}
+    worst = {k: float(v.max()) for k, v in dev.items()}
+    print(f"20-step loss trajectories: max relative deviation from fp64 {worst}; per step f16x3 "
+          f"{np.round(dev['f16x3'].max(axis=1), 7).tolist()}")
+    assert worst["f16x3"] <= 2 * worst["bf16x6"] + 1e-5, worst
+    assert max(worst.values()) < 1e-3, worst
