@@ -546,9 +546,11 @@ class GraphPlan:
         # product); written by a pool's backward or split from the fp32 graph-output gradient,
         # from their measured max gmax[itself].
         self.x3_top = None
+        self.x3_measure_dy = set()   # convs whose fp32 dy is measured (absmax) before their backward ops
         x3g = [n for n in conv_nodes if train and self.desc[n.idx].plane_format(ops.TENSOR_DY) == ops.PLANES_F16X3]
         if x3g:
             slot_of = {n.idx: i for i, n in enumerate(conv_nodes)}
+            self._x3_slot = slot_of
             self.gmax = torch.zeros(len(conv_nodes), 8, dtype=torch.float32, device=device)   # 8 atomic shards
             self.gwb = torch.zeros(len(conv_nodes), dtype=torch.float32, device=device)
             self._gwb_ver = None
@@ -581,7 +583,10 @@ class GraphPlan:
                             self.pool_gout[k].pop(cs[0].idx, None)
                         self.fed_dy.discard(n.idx)
                 else:
-                    raise ValueError(f"{n.name}: fp16x3 input gradient without a scale source")
+                    # a gradient arriving from a BN / PReLU / Add / concat (the SR family under
+                    # DG_CONV_MATH=f16x3): its max is measured in backward() before the conv's ops
+                    src = (gm(n), None)
+                    self.x3_measure_dy.add(n.idx)
                 p = producer_conv(n.ins[0])
                 d.set_grad_scale(dy_m=src[0], dy_g=src[1], dx_m=gm(n), dx_g=gw(n),
                                  dx_max=gm(p) if p is not None else None)
@@ -941,6 +946,8 @@ class GraphPlan:
                     # (a backward-only plan -- VGG19's N-image backward over its 2N forward -- may
                     # hold weight planes of a layout the forward plan does not share)
                     P.invalidate(self._stale_w(P, True))
+                if n.idx in self.x3_measure_dy:
+                    ops.absmax(dy, self.gmax[self._x3_slot[n.idx]])   # (gmax zeroed above)
                 if pg:
                     db = A.grad_of(f"{n.name}/bias") if n.attrs["bias"] else None
                     d.bwd_filter(s[t_in.id], dy, A.grad_of(f"{n.name}/kernel"), dbias=db, beta=param_beta, ws=ws,

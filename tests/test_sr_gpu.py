@@ -545,3 +545,22 @@ def test_sr_train_step_tuples():
         assert d.shape[-1] == 1
         if cls is Autoencoder:
             assert float(d.min()) >= 0.0 and float(d.max()) <= 1.0  # sigmoid output
+
+
+@gpu
+@pytest.mark.parametrize("kind", ["srgan", "fsrgan"])
+def test_sr_step_under_library_wide_f16x3(kind, monkeypatch):
+    """DG_CONV_MATH=f16x3 as the library-wide default (include/dgan.h): the SR generators' 64- /
+    32-channel convs then get fp16x3 input gradients whose dy comes from a BN / PReLU (no producer
+    bound: measured before the conv's backward, dgan/graph.py x3_measure_dy) and fp16x3 x planes
+    (measured by the op that splits them) -- the plans build and the step meets the same fp64 bars
+    as the default arithmetic (plan construction used to raise)."""
+    monkeypatch.setenv("DG_CONV_MATH", "f16x3")
+    from dgan import ops
+    assert ops.default_conv_math() == ops.MATH_F16X3
+    if kind == "srgan":
+        from srgan import SRGAN
+        _run_step_parity(SRGAN, "srgan", N=2, H=32, scale=4, conditioned=True)
+    else:
+        from fsrgan import FastSRGAN
+        _run_step_parity(FastSRGAN, "fsrgan", N=2, H=64, scale=4, content_loss=0)
