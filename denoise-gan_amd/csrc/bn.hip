@@ -393,8 +393,9 @@ __device__ __forceinline__ void load_z(const float *__restrict__ z, long off, fl
     }
 }
 
-// backward: partial sums of dbn and dbn*xhat per (chunk, channel)
-template <int V>
+// backward: partial sums of dbn and dbn*xhat per (chunk, channel); MX: also the maxima of the
+// fp16x3 dy bound (pd / pv set) -- without them the pass keeps round 3's register / LDS footprint
+template <int V, bool MX>
 __global__ void __launch_bounds__(256)
 k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict__ z, int ldz,
                  const float *__restrict__ y, int ldy, long M, int C, long rows, int cpb,
@@ -403,7 +404,7 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
                  float *__restrict__ bound) {
     // pd / pv (may be NULL): per chunk max |dbn| and max |y - mean|, the terms of the bound
     // on |dy| that scales its fp16x3 planes (k_bn_bwd_final); bound zeroed here for it
-    __shared__ float a1s[256 * V], a2s[256 * V], dms[256 * V], vms[256 * V];
+    __shared__ float a1s[256 * V], a2s[256 * V], dms[MX ? 256 * V : 1], vms[MX ? 256 * V : 1];
     if (bound && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x < X3_SHARDS)
         bound[threadIdx.x] = 0.f;
     const int slot = threadIdx.x % cpb, rl = threadIdx.x / cpb, RL = 256 / cpb;
@@ -430,8 +431,10 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
                 float dbn = dv[q] * act_grad_from_out(zv[q], act, alpha) * dscale;
                 a1[q] += dbn;
                 a2[q] += dbn * (yv[q] - mu[q]) * inv[q];
-                dm[q] = fmaxf(dm[q], fabsf(dbn));
-                vm[q] = fmaxf(vm[q], fabsf(yv[q] - mu[q]));
+                if constexpr (MX) {
+                    dm[q] = fmaxf(dm[q], fabsf(dbn));
+                    vm[q] = fmaxf(vm[q], fabsf(yv[q] - mu[q]));
+                }
             }
         };
         // U rows' loads in flight per lane, summed in row order (deterministic)
@@ -459,7 +462,7 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
 #pragma unroll
     for (int q = 0; q < V; ++q) {
         a1s[threadIdx.x * V + q] = a1[q]; a2s[threadIdx.x * V + q] = a2[q];
-        dms[threadIdx.x * V + q] = dm[q]; vms[threadIdx.x * V + q] = vm[q];
+        if constexpr (MX) { dms[threadIdx.x * V + q] = dm[q]; vms[threadIdx.x * V + q] = vm[q]; }
     }
     __syncthreads();
     if (rl != 0 || !cok) return;
@@ -468,7 +471,7 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
 #pragma unroll
         for (int q = 0; q < V; ++q) {
             a1[q] += a1s[t * V + q]; a2[q] += a2s[t * V + q];
-            dm[q] = fmaxf(dm[q], dms[t * V + q]); vm[q] = fmaxf(vm[q], vms[t * V + q]);
+            if constexpr (MX) { dm[q] = fmaxf(dm[q], dms[t * V + q]); vm[q] = fmaxf(vm[q], vms[t * V + q]); }
         }
     }
 #pragma unroll
@@ -476,7 +479,7 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
         const long o = (pbase + blockIdx.y) * C + c0 + q;
         p1[o] = a1[q];
         p2[o] = a2[q];
-        if (pd) { pd[o] = dm[q]; pv[o] = vm[q]; }
+        if constexpr (MX) { pd[o] = dm[q]; pv[o] = vm[q]; }
     }
 }
 
@@ -808,16 +811,17 @@ int dg_bn_bwd_seg_x(int S, int M, int C, const float *dz, int lddz, const float 
     float *p1 = w, *p2 = w + RC, *coef = w + 4 * RC;
     float *pd = x3 ? w + 2 * RC : nullptr, *pv = x3 ? w + 3 * RC : nullptr, *bnd = x3 ? dy_bound : nullptr;
     const bool v4 = dg::vec4_ok(C, {{dz, lddz}, {z, ldz}, {y, ldy}, {save_mean, 4}, {save_invstd, 4}});
-    if (v4) {
-        dg::PartGeom pg = dg::part_geom(C, 4);
-        hipLaunchKernelGGL(dg::k_bn_bwd_partial<4>, dim3(pg.cg, bp.R, S), dim3(256), 0, s, dz, lddz, z, ldz, y, ldy,
-                           (long)M, C, bp.rows, pg.cpb, save_mean, save_invstd, act, alpha, dscale, p1, p2, pd, pv,
-                           bnd);
-    } else {
-        dg::PartGeom pg = dg::part_geom(C, 1);
-        hipLaunchKernelGGL(dg::k_bn_bwd_partial<1>, dim3(pg.cg, bp.R, S), dim3(256), 0, s, dz, lddz, z, ldz, y, ldy,
-                           (long)M, C, bp.rows, pg.cpb, save_mean, save_invstd, act, alpha, dscale, p1, p2, pd, pv,
-                           bnd);
+    {
+        const dg::PartGeom pg = dg::part_geom(C, v4 ? 4 : 1);
+        const dim3 grid(pg.cg, bp.R, S);
+#define DG_BNP(V_, MX_)                                                                                          \
+    hipLaunchKernelGGL((dg::k_bn_bwd_partial<V_, MX_>), grid, dim3(256), 0, s, dz, lddz, z, ldz, y, ldy, (long)M, C, \
+                       bp.rows, pg.cpb, save_mean, save_invstd, act, alpha, dscale, p1, p2, pd, pv, bnd)
+        if (v4 && x3) DG_BNP(4, true);
+        else if (v4) DG_BNP(4, false);
+        else if (x3) DG_BNP(1, true);
+        else DG_BNP(1, false);
+#undef DG_BNP
     }
     DG_LAUNCHED("bn_bwd_partial");
     hipLaunchKernelGGL(dg::k_bn_bwd_final, dim3(dg_cdiv(C, dg::FIN_C)), dim3(256), 0, s, p1, p2, pd, pv, bp.R, C, S,

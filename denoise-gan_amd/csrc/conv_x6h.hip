@@ -54,13 +54,18 @@ constexpr bool kTapsColMajor = true;
 // Weight prefetch through a mid-K-tile barrier (as conv_x6.hip): once every wave
 // holds K-tile T's fragments in registers, its buffer takes tile T+NB, so a DMA
 // has NB K-tiles of MFMAs to land instead of NB-1.  DG_NO_MIDB builds the plain
-// pipelines, DG_MIDB_X3 the fp16x3-only form, for same-box A/B runs.
+// pipelines, DG_MIDB_X3 the fp16x3-only form, DG_MIDB_ALL every math, for same-box A/B runs.
+// Default: fp16x3 and fp16 (SRGAN 4208 -> 4271 img/s, profiles/r4/ab_halo_midb_all.txt); the
+// bf16x6 halo kernel keeps the plain pipeline (the autoencoder's 64^2 VGG19 forward ran 29 %
+// slower with it, profiles/r5/ab_ae_r3_r5.txt)
 #if defined(DG_NO_MIDB)
 constexpr int kMidb = 0;
 #elif defined(DG_MIDB_X3)
 constexpr int kMidb = 1;
-#else
+#elif defined(DG_MIDB_ALL)
 constexpr int kMidb = 2;
+#else
+constexpr int kMidb = 3;
 #endif
 // PACKED (fp16x3): the NPL plane images lie back to back (HPX * 32 bytes each) and
 // only the whole halo is rounded up to KiB DMAs -- 23 KiB instead of 24 for KT 3,
@@ -207,7 +212,16 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     constexpr int TL = (H_NJ - 1) / PPT;                    // the last tap position issuing halo pieces
     // mid-K-tile barrier form: needs the last NB-1 tap positions free of halo pieces
     // (the wait counts below), so not the KT 2 phases (4 taps, 4 buffers)
-    constexpr bool MIDB = (kMidb == 2 || (kMidb == 1 && X3)) && TL <= NTAP - NB;
+    constexpr bool MIDB = (kMidb == 2 || (kMidb == 1 && X3) || (kMidb == 3 && NI != 3)) && TL <= NTAP - NB;
+    // pipeline-tail DMAs (chunks past the split's range) out of range -- no traffic -- on the
+    // fp16x3 / fp16 instances; the bf16x6 kernel issues them in range (the autoencoder's 64^2
+    // VGG19 forward ran 23 % slower with the out-of-range form, profiles/r5/ab_ae_r3_r5.txt;
+    // DG_TAIL_OOB_ALL: out of range everywhere, for A/B runs)
+#if defined(DG_TAIL_OOB_ALL)
+    constexpr bool kTailAll = false;
+#else
+    constexpr bool kTailAll = NI == 3;
+#endif
     constexpr auto nh_of = [](int t) constexpr {   // halo pieces issued at tap position t (t < 0: t + NTAP)
         t = t < 0 ? t + NTAP : t;
         const int h0 = t * PPT, h1 = (t + 1) * PPT < H_NJ ? (t + 1) * PPT : H_NJ;
@@ -336,7 +350,8 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     auto issue_h = [&](int s, int chunk, char *hb) __attribute__((always_inline)) {
         // (chunks past the split's range -- the pipeline's tail -- out of range: no traffic)
         dma(rA, hb + hdst[s],
-            hoff[s] >= 0 && chunk < cend ? (unsigned)(hoff[s] + chunk * (NI == 3 ? 96 : (X3 ? 128 : 64))) : DG_OOB);
+            hoff[s] >= 0 && (kTailAll || chunk < cend) ? (unsigned)(hoff[s] + chunk * (NI == 3 ? 96 : (X3 ? 128 : 64)))
+                                                       : DG_OOB);
     };
 
     // ---- weight K-tile slots (as conv_x6.hip): FWD RC image [16 k][BN],
@@ -381,7 +396,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         else delta = (tap_w[T] * g.Ci * (LW * p.ldb) + chunk * (NI == 3 ? 48 : (X3 ? 64 : 32))) * 2;
 #pragma unroll
         for (int j = 0; j < B_NJ; ++j) {
-            dma(rB, bs + bdst[j], bok[j] && chunk < cend ? (unsigned)(bbase[j] + delta) : DG_OOB);
+            dma(rB, bs + bdst[j], bok[j] && (kTailAll || chunk < cend) ? (unsigned)(bbase[j] + delta) : DG_OOB);
         }
     };
     auto bbuf = [&](int i) __attribute__((always_inline)) -> char * {
