@@ -217,6 +217,7 @@ def main():
         torch.cuda.synchronize()
         graph = None
         if use_graph:
+            from dgan.dist import CAPTURE_MODE
             try:
                 s = torch.cuda.Stream()
                 s.wait_stream(torch.cuda.current_stream())
@@ -225,9 +226,10 @@ def main():
                 torch.cuda.current_stream().wait_stream(s)
                 torch.cuda.synchronize()
                 graph = torch.cuda.CUDAGraph()
-                # (collectives inside the capture go to a capture-only process group, dist.capture_group)
+                # (collectives inside the capture go to a capture-only process group, dist.capture_group;
+                # thread-local capture mode leaves the watchdog threads free to query eager events)
                 with (model.grad_sync.capturing() if distributed else contextlib.nullcontext()):
-                    with torch.cuda.graph(graph):
+                    with torch.cuda.graph(graph, capture_error_mode=CAPTURE_MODE):
                         trainer.step(x, y)
                 torch.cuda.synchronize()
             except Exception as e:  # report, fall back to eager launches

@@ -30,6 +30,15 @@ import torch.distributed as dist
 
 _CAPTURE_GROUPS = {}
 
+# Capture mode of every HIP-graph capture of a step.  Under the default ("global") mode the HIP
+# runtime refuses an event query from ANY thread while a capture is open
+# (hipErrorStreamCaptureUnsupported), so a process group's watchdog that is still retiring the
+# eager warm-up's all-reduces aborts the process (round 5: WorkNCCL::isCompleted on default_pg,
+# once D's parameter backward moved to a side stream changed the warm-up's timing).  Thread-local
+# mode restricts the check to the capturing thread; the watchdog's queries of events on the
+# default group's stream (which never joins a capture, see capture_group) are then legal.
+CAPTURE_MODE = "thread_local"
+
 
 def capture_group(device=None):
     """The process group that carries only collectives issued inside HIP-graph capture.

@@ -629,9 +629,11 @@ class DiscriminatorPlan:
             self.planes_half = (ops.plan_planes(self.desc_half, device, keep_x=False,
                                                 wbufs=[p.w for p in self.planes])
                                 if self.desc_half is not self.desc else self.planes)
-            # one dy bound per layer, shared by the full and the half-batch backward (in
-            # stream order, each BN backward rewrites it before its conv reads it)
+            # one dy bound per layer for the full backward; the half-batch backward (the G path
+            # through D(fake)) has its own bounds, dz and dy scratch, so the two backwards may run
+            # concurrently on two streams (trainer.Pix2PixTrainer overlap)
             self.gbound = grad_bounds(self.desc, self.planes, device)
+            self.gbound_h = list(self.gbound)
             # fp16x3 activation planes scaled from their producers' bounds (ActBounds): D.down1's
             # conv output from (max |input pair|, down1's weight bound), BN block i's output zb[i]
             self.ab = None
@@ -645,9 +647,10 @@ class DiscriminatorPlan:
             if self.desc_half is not self.desc:
                 for i, (d, P) in enumerate(zip(self.desc_half, self.planes_half)):
                     if FEED_DY and P is not None and P.dy is not None and P.dy.fmt == ops.PLANES_F16X3:
-                        if self.gbound[i] is None:
-                            self.gbound[i] = torch.zeros(8, dtype=torch.float32, device=device)
-                        d.set_grad_scale(dy_m=self.gbound[i])
+                        self.gbound_h[i] = torch.zeros(8, dtype=torch.float32, device=device)
+                        d.set_grad_scale(dy_m=self.gbound_h[i])
+                self.dz_h = [_empty(d.out_shape, device) for d in self.desc_half[:-1]]
+                self.dy_h = _empty((max(d.N * d.Ho * d.Wo * d.Cout for d in self.desc_half),), device)
         else:
             self.planes = self.planes_half = [None] * len(self.desc)
             self.ab = None
@@ -672,8 +675,9 @@ class DiscriminatorPlan:
     def _half(self, t, h):
         return t[h * self.N:(h + 1) * self.N]
 
-    def _dy(self, d):
-        return self.dy[: d.N * d.Ho * d.Wo * d.Cout].view(d.N, d.Ho, d.Wo, d.Cout)
+    def _dy(self, d, buf=None):
+        buf = self.dy if buf is None else buf
+        return buf[: d.N * d.Ho * d.Wo * d.Cout].view(d.N, d.Ho, d.Wo, d.Cout)
 
     def forward(self, slot=0, training=True, ws=None):
         A = self.arena
@@ -737,6 +741,12 @@ class DiscriminatorPlan:
             return t if half is None else self._half(t, half)
 
         planes = self.planes if half is None else self.planes_half
+        # (the half-batch pass has its own dz / dy scratch and dy bounds when built: it may run
+        # on another stream beside the full pass)
+        own = half is not None and getattr(self, "dz_h", None) is not None
+        dzs = self.dz_h if own else self.dz
+        dybuf = self.dy_h if own else None
+        gb = self.gbound_h if own else self.gbound
         dh = dlogits
         n = len(self.specs)
         for i in range(n - 1, -1, -1):
@@ -751,7 +761,7 @@ class DiscriminatorPlan:
                     d.bwd_filter(sub(self.z[i - 1]), dy, A.grad_of("last/kernel"), dbias=A.grad_of("last/bias"),
                                  beta=beta, ws=ws, planes=P)
             else:
-                dy = self._dy(d)
+                dy = self._dy(d, dybuf)
                 if bn:
                     feed = FEED_DY and P is not None and P.dy is not None
                     # all halves in one segmented call, or the one half's statistics
@@ -762,7 +772,7 @@ class DiscriminatorPlan:
                                A.grad_of(f"{name}/beta") if param_grads else None, act="lrelu", alpha=ALPHA,
                                beta=beta, ws=ws, dy_planes=plane_rows(P.dy, dy, 0) if feed else None,
                                segments=len(hs), dy_fp32=not (feed and DY_PLANES_ONLY),
-                               dy_bound=self.gbound[i] if feed else None)
+                               dy_bound=gb[i] if feed else None)
                     if feed:
                         P._filled(ops.TENSOR_DY)
                 else:
@@ -773,7 +783,7 @@ class DiscriminatorPlan:
             if param_grads and on_grads_ready:
                 on_grads_ready(name)
             if i > 0:
-                dz = sub(self.dz[i - 1])
+                dz = dzs[i - 1] if own else sub(self.dz[i - 1])
                 d.bwd_data(dy, A.param(f"{name}/kernel"), dz, ws=ws, planes=P)
                 dh = dz
             elif input_grad is not None and input_from == 3:

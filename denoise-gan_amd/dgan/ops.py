@@ -530,6 +530,12 @@ class ConvProfile:
         return out
 
 
+def profiling():
+    """A ConvProfile is recording: callers run their work on one stream (per-op events on two
+    concurrent streams would time the overlap, not the op)."""
+    return _PROF is not None
+
+
 def _prof_begin():
     if _PROF is None:
         return None

@@ -10,10 +10,18 @@ Both "tapes" see the same pre-update weights, as in the reference.
 Everything is enqueued on the current stream with pre-sized buffers and a
 pre-sized workspace, so a whole step can be captured in a HIP graph.
 """
+import os
+
 import torch
 
 from . import ops
 from .nets import DiscriminatorPlan, GeneratorPlan, DROP_RATE
+
+# D's parameter backward (both halves) on a second stream beside the G path (D(fake)'s input
+# gradient, the VGG19 backward, G's backward): the two are independent until Adam, and the D
+# pass's small grids, BN passes and tails fill the G path's idle CU slots.  DG_NO_OVERLAP: one
+# stream (same-box A/B)
+OVERLAP = not os.environ.get("DG_NO_OVERLAP")
 
 LOSS_NAMES = ("gen_total_loss", "gen_gan_loss", "gen_l1_loss", "gen_l2_loss", "content_loss", "disc_loss",
               "var_loss", "identity_loss")
@@ -72,6 +80,12 @@ class Pix2PixTrainer:
                        self.content.ws_bytes if self.content else 0)
         self.ws = ops.Workspace(device)
         self.ws.get(ws_bytes)
+        # the side stream of the overlapped D parameter backward, with its own workspace
+        self.side = None
+        if OVERLAP and getattr(self.D, "dz_h", None) is not None:
+            self.side = torch.cuda.Stream(device=device)
+            self.ws_side = ops.Workspace(device)
+            self.ws_side.get(self.D.ws_bytes)
 
     @property
     def gen_output(self):
@@ -114,9 +128,19 @@ class Pix2PixTrainer:
                      dlogit_fake_d=self.dlog[N:], dlogit_fake_g=self.dzf_g, ws=ws)
         sync = self.grad_sync
         # ---- disc_tape.gradient (train_pix2pix.py:65): both D calls in one pass
-        D.backward(self.dlog, param_grads=True, beta=0.0, ws=ws)
-        if sync:
-            sync.start("D")
+        side = self.side if not ops.profiling() else None
+        if side is not None:
+            # (on the side stream, forked after the losses; its all-reduce is issued from there)
+            main = torch.cuda.current_stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                D.backward(self.dlog, param_grads=True, beta=0.0, ws=self.ws_side)
+                if sync:
+                    sync.start("D")
+        else:
+            D.backward(self.dlog, param_grads=True, beta=0.0, ws=ws)
+            if sync:
+                sync.start("D")
         # ---- gen_tape.gradient (train_pix2pix.py:64): through D(fake) into G(x)
         if D.desc_g3 is not None:   # dL/dG(x) += channels 3..5 of dL/d D([x, G(x)])
             D.backward(self.dzf_g, half=1, param_grads=False, input_grad=dgen, input_beta=1.0, ws=ws, input_from=3)
@@ -128,6 +152,8 @@ class Pix2PixTrainer:
         # both generator calls (G(x), G(y)) in one backward: their gradients sum
         G.backward(self.dgout, beta=0.0, ws=ws, drop_rate=self.drop_rate,
                    on_grads_ready=(sync.ready_G if sync else None))
+        if side is not None:
+            torch.cuda.current_stream().wait_stream(side)   # (join: D's gradients before Adam)
         if sync:
             sync.finish()
         # ---- apply_gradients (train_pix2pix.py:68-69) ----------------------

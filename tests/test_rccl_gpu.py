@@ -76,9 +76,11 @@ def _run(kind, dp, bucket_bytes):
     cur.wait_stream(s)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    # (no settling delay: the captured all-reduces run on the capture-only group, dist.capture_group)
+    # (no settling delay: the captured all-reduces run on the capture-only group, dist.capture_group,
+    # and the capture is thread-local, dist.CAPTURE_MODE)
+    from dgan.dist import CAPTURE_MODE
     with (sync.capturing() if dp else contextlib.nullcontext()):
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode=CAPTURE_MODE):
             tr.step(x, y)                  # captured once: RCCL all-reduces + bucket hooks inside
     torch.cuda.synchronize()
     counts = (sync.last_mid_backward, sync.last_total) if sync else None
