@@ -1230,6 +1230,8 @@ struct OpPlan {
     // halo-tiled bf16x6 kernel (conv_x6h.hip): 1 = stride-1 3x3 FWD / DGRAD,
     // 2 = stride-2 4x4 DGRAD phases; cfg = its BN, tiles of 8 x 16 output pixels
     int halo, htx, hty;
+    // fp16x3 halo plans without split-K: patches per block (persistent blocks, conv_x6h.hip)
+    int ptiles;
     // small-Cin 4x4 stride-2 kernels (conv_small.hip); WGRAD: conv-view output rows per block
     int small, small_rows;
     // single-output-channel direct kernels (conv_co1.hip)
@@ -1558,6 +1560,24 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         pl.kchunk = (int)(cps * bkc * ntap);
         pl.splits = (int)((nch + cps - 1) / cps);
         if (hx3 || hx3p) pl.x6 = 3;
+        // fp16x3 plans with more patches than resident blocks (2 per CU): each block runs
+        // several patches back to back, the next patch's halo and weights fetched under the
+        // current patch's MFMAs, so a block waits for HBM once instead of once per patch.
+        // ~512 blocks (one per slot) for the stride-2 phases and for 3x3 layers of <= 4
+        // channel chunks per patch (VGG19 block1_conv2 fwd 0.959 -> 0.832 ms, bwd_data 1.000
+        // -> 0.830, G up7 fwd 0.351 -> 0.304, down2 bwd_data 0.220 -> 0.191 at bs32); deeper
+        // 3x3 layers amortise their prologue over >= 72 K-tiles and measured 1-2 % slower at
+        // 512, so ~2048 there (profiles/r5/ab_x3h_persistent.txt)
+        // (DG_X3H_PTILES: patches per block, DG_X3H_PDIV: the block target, for same-box A/B)
+        pl.ptiles = 1;
+        if ((hx3 || hx3p) && pl.splits == 1) {
+            const long tot = (long)pl.mtiles * pl.ntiles * pl.nphase;
+            long pdiv = hx3p || nch <= 4 ? 512 : 2048;
+            if (const char *e = getenv("DG_X3H_PDIV")) pdiv = std::max(1L, atol(e));
+            long pt = tot / pdiv;
+            if (const char *e = getenv("DG_X3H_PTILES")) pt = atol(e);
+            pl.ptiles = (int)std::max(1L, std::min(pt, 64L));
+        }
     }
     if (x3_gen && pl.x6 == 1 && 4.0 * ra * ca < 2.0e9 && 4.0 * rb * cb < 2.0e9) {
         pl.halo = 0; pl.htx = pl.hty = 0;
@@ -1713,6 +1733,7 @@ static GemmArgs make_args(const ConvGeom &g, const OpPlan &pl, const float *A, i
     a.mtiles = pl.mtiles; a.ntiles = pl.ntiles; a.nphase = pl.nphase;
     a.slab = (float *)slab;
     a.xcd_plain = plan_off("xcd_phase");
+    a.ptiles = pl.halo ? std::max(1, pl.ptiles) : 1;
     return a;
 }
 
@@ -2046,6 +2067,8 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
         a.B = (const float *)pb; a.ldb = pl.x6_cb; a.b_bytes = (unsigned)(4 * pl.x6_rb * pl.x6_cb);
         dim3 grid(pl.mtiles * pl.ntiles, pl.nphase * pl.splits);
         if (pl.halo) {
+            // (persistent blocks: patch row mt0 + j * gm, j < ptiles, of each of the gm * ntiles blocks)
+            grid.x = (unsigned)((pl.mtiles + a.ptiles - 1) / a.ptiles * pl.ntiles);
             launch_gemm_x6h(mode, pl.cfg, pl.halo == 2 ? 2 : 3, grid, a, pl.htx, pl.hty, s, 4);
             DG_LAUNCHED("conv_gemm_x3h");
         } else {

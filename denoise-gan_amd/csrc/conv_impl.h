@@ -58,6 +58,9 @@ struct GemmArgs {
     const unsigned short *mzp; int mzpC;
     // 1: DGRAD phase blocks in the plain XCD order (A/B switch DG_PLAN_DISABLE=xcd_phase)
     int xcd_plain;
+    // fp16x3 halo kernel: patches per block (blocks gm = gridDim.x / ntiles; block's patches
+    // mt0 + j * gm, j < ptiles); other kernels 1
+    int ptiles;
 };
 
 // the factor that undoes an fp16x3 GEMM's operand scales (powers of two: exact)
@@ -238,7 +241,8 @@ struct RowPix {
 template <int MODE, int TM, int TN, class RowMap>
 __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[TM][TN], int rbase, int cbase,
                                                 RowMap rowmap, int phase, int split, int lane, float *stage,
-                                                float ys_pre = 0.f) {
+                                                float ys_pre = 0.f, float *vacc = nullptr) {
+    // (vacc != NULL: max |output| folded into *vacc -- a persistent block's later atomic -- instead)
     // (ys_pre > 0: the output planes' scale, computed by the caller from loads issued at entry)
     constexpr int WTN = 16 * TN;
     constexpr int LD = WTN + 4;   // padded staging row (floats): conflict-free writes
@@ -333,7 +337,10 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
             }
         }
     }
-    if (p.ymax) block_atomic_absmax(p.ymax, vmax);
+    if (p.ymax) {
+        if (vacc) *vacc = fmaxf(*vacc, vmax);
+        else block_atomic_absmax(p.ymax, vmax);
+    }
 }
 
 // launcher of the bf16x6 kernels (conv_x6.hip); cfg indexes kX6Cfgs

@@ -97,7 +97,7 @@ struct HaloGeom {
 template <int TM, int TN>
 __device__ __forceinline__ void conv_epilogue16_pool(const GemmArgs &p, f32x4 (&acc)[TM][TN], int prow0, int cbase,
                                                      int ty, int tx, int nimg, int lane, float *stage,
-                                                     float ys_pre = 0.f) {
+                                                     float ys_pre = 0.f, float *vacc = nullptr) {
     constexpr int WTN = 16 * TN;
     constexpr int LD = WTN + 4;
     constexpr int C4 = WTN / 4;
@@ -165,7 +165,10 @@ __device__ __forceinline__ void conv_epilogue16_pool(const GemmArgs &p, f32x4 (&
             for (int q = 0; q < 4; ++q) vmax = fmaxf(vmax, fabsf(fv[q]));
         }
     }
-    if (p.ymax) block_atomic_absmax(p.ymax, vmax);
+    if (p.ymax) {
+        if (vacc) *vacc = fmaxf(*vacc, vmax);
+        else block_atomic_absmax(p.ymax, vmax);
+    }
 }
 
 // f(integral_constant<T>) for T = 0 .. NTAP-1, unrolled at compile time
@@ -256,31 +259,50 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     xcd_remap(zz, tile, MODE == MODE_DGRAD && p.nphase > 1 && !p.xcd_plain);
     const int phase = zz / p.splits;
     const int split = zz - phase * p.splits;
-    const int mt = tile / p.ntiles;
-    const int nt = tile - mt * p.ntiles;
+    const int mt0 = tile / p.ntiles;
+    const int nt = tile - mt0 * p.ntiles;
     const int n0 = nt * BN;
-    const int tx = mt % tiles_x;
-    const int t_ = mt / tiles_x;
-    const int ty = t_ % tiles_y;
-    const int nimg = t_ / tiles_y;
+    // persistent blocks (fp16x3): patches mt0, mt0 + gm, ... (p.ptiles of them) of one n-tile,
+    // phase and split run back to back -- the next patch's first halo and weight tiles are
+    // fetched during the current patch's last chunk, so only the first patch waits for them.
+    // The epilogue stages through the halo buffer just consumed (the other one is receiving).
+    constexpr bool PERS = X3;
+    const int PT = PERS ? max(1, p.ptiles) : 1;
+    const int gm = gridDim.x / p.ntiles;
     // A source (FWD: x; DGRAD: dy) extents and the output grid of this block
     // (DGRAD: the phase's sub-grid; stride 1: the whole dx)
     const int Hin = MODE == MODE_FWD ? g.H : g.Ho, Win = MODE == MODE_FWD ? g.W : g.Wo;
     PhaseInfo ph{};
-    int Hout, Wout, oy, ox;
+    int Hout, Wout, oh = 0, ow = 0;
     if constexpr (MODE == MODE_FWD) {
         Hout = g.Ho; Wout = g.Wo;
-        oy = ty * HX_PH - g.pt;
-        ox = tx * HX_PW - g.pl;
     } else {
         ph = phase_info(g, phase, g.N);
         Hout = ph.Hp; Wout = ph.Wp;
         // tap a of the phase reads dy row hh + oh - a (exact: ph + pt - i0h is a multiple of sh)
-        const int oh = (ph.ph + g.pt - ph.i0h) / g.sh, ow = (ph.pw + g.pl - ph.i0w) / g.sw;
-        oy = ty * HX_PH + oh - (KT - 1);
-        ox = tx * HX_PW + ow - (KT - 1);
+        oh = (ph.ph + g.pt - ph.i0h) / g.sh;
+        ow = (ph.pw + g.pl - ph.i0w) / g.sw;
     }
-    if (ty * HX_PH >= Hout || tx * HX_PW >= Wout) return;   // block-uniform: a smaller phase grid
+    struct HTile {
+        int tx, ty, nimg;
+    };
+    // the block's next patch from its j-th on (-1: none; a smaller phase grid skips patches)
+    auto next_tile = [&](int j, HTile &t) __attribute__((always_inline)) -> int {
+        for (; j < PT; ++j) {
+            const int mt = mt0 + j * gm;
+            if (mt >= p.mtiles) return -1;
+            t.tx = mt % tiles_x;
+            const int t_ = mt / tiles_x;
+            t.ty = t_ % tiles_y;
+            t.nimg = t_ / tiles_y;
+            if (t.ty * HX_PH < Hout && t.tx * HX_PW < Wout) return j;
+        }
+        return -1;
+    };
+    HTile cur, nxt;
+    const int jc = next_tile(0, cur);
+    if (jc < 0) return;   // block-uniform: a smaller phase grid
+    int jn = next_tile(jc + 1, nxt);
     // channel chunks of this split (kchunk is a multiple of NTAP taps x BK channels)
     const int nch = p.K / (NTAP * BK);
     const int cbeg = split * (p.kchunk / (NTAP * BK));
@@ -315,10 +337,11 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     // KiB) pieces (d >= HDMA repeats piece d - HDMA: same bytes, same data, and
     // every DMA provably targets the halo buffer); lane L of a piece fetches
     // the 16-byte half-row q = 64k + L of its plane image (halo pixel q/2,
-    // channel half q&1).  hoff: byte offset at chunk 0, or -1 outside the
-    // image / past the halo's pixels.
+    // channel half q&1).  hsrc: (halo row, halo column, element offset) of the
+    // piece, or -1 past the halo's pixels; hoff: byte offset at chunk 0 in the
+    // current patch (hoffn: the next one), or -1 outside the image.
     constexpr int PER = HG::HPL / 1024;
-    int hoff[H_NJ], hdst[H_NJ];
+    int hsrc[H_NJ], hdst[H_NJ];
 #pragma unroll
     for (int s = 0; s < H_NJ; ++s) {
         const int d = (wid + NW * s) % HG::HDMA;
@@ -334,24 +357,45 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
             hdst[s] = pl * HG::HPL + kk * 1024;
             q = kk * 64 + lane;
         }
-        hoff[s] = -1;
+        hsrc[s] = -1;
         const int hp = q >> 1, hh = q & 1;
         if (hp < HG::HPX && pl < NPL) {
             const int hr = hp / HG::HW, hc = hp - hr * HG::HW;
-            const int iy = oy + hr, ix = ox + hc;
-            // (bf16x6 pixel rows: per 16 channels 3 x 16 plane values; fp16: the
-            // channel row itself, plane image pl = channel half pl of the chunk;
-            // fp16x3: per 32 channels h[32] l[32], image pl = 16 values at 16 pl)
-            if ((unsigned)iy < (unsigned)Hin && (unsigned)ix < (unsigned)Win)
-                hoff[s] = ((((nimg * Hin + iy) * Win + ix) * (NI == 3 ? 3 * p.lda : (X3 ? 2 * p.lda : p.lda))) +
-                           16 * pl + 8 * hh) * 2;
+            hsrc[s] = (hr << 16) | (hc << 8) | (16 * pl + 8 * hh);
         }
     }
-    auto issue_h = [&](int s, int chunk, char *hb) __attribute__((always_inline)) {
+    // (bf16x6 pixel rows: per 16 channels 3 x 16 plane values; fp16: the channel row
+    // itself, plane image pl = channel half pl of the chunk; fp16x3: per 32 channels
+    // h[32] l[32], image pl = 16 values at 16 pl)
+    constexpr int PXS = NI == 3 ? 3 : (X3 ? 2 : 1);   // pixel stride in units of lda
+    auto halo_offsets = [&](const HTile &t, int (&ho)[H_NJ]) __attribute__((always_inline)) {
+        const int oy = MODE == MODE_FWD ? t.ty * HX_PH - g.pt : t.ty * HX_PH + oh - (KT - 1);
+        const int ox = MODE == MODE_FWD ? t.tx * HX_PW - g.pl : t.tx * HX_PW + ow - (KT - 1);
+#pragma unroll
+        for (int s = 0; s < H_NJ; ++s) {
+            ho[s] = -1;
+            if (hsrc[s] < 0) continue;
+            const int iy = oy + (hsrc[s] >> 16), ix = ox + ((hsrc[s] >> 8) & 255);
+            if ((unsigned)iy < (unsigned)Hin && (unsigned)ix < (unsigned)Win)
+                ho[s] = ((((t.nimg * Hin + iy) * Win + ix) * (PXS * p.lda)) + (hsrc[s] & 255)) * 2;
+        }
+    };
+    int hoff[H_NJ], hoffn[H_NJ];
+    halo_offsets(cur, hoff);
+    // (no next patch: the pipeline tail reads the current patch's pixels at chunk cend, as
+    // the one-patch kernel always did)
+    if (jn >= 0) halo_offsets(nxt, hoffn);
+    else {
+#pragma unroll
+        for (int s = 0; s < H_NJ; ++s) hoffn[s] = hoff[s];
+    }
+    // halo piece s of chunk `chunk` into hb; nxp: from the next patch's offsets
+    auto issue_h = [&](int s, int chunk, char *hb, bool nxp) __attribute__((always_inline)) {
         // (chunks past the split's range -- the pipeline's tail -- out of range: no traffic)
+        const int o = nxp ? hoffn[s] : hoff[s];
         dma(rA, hb + hdst[s],
-            hoff[s] >= 0 && (kTailAll || chunk < cend) ? (unsigned)(hoff[s] + chunk * (NI == 3 ? 96 : (X3 ? 128 : 64)))
-                                                       : DG_OOB);
+            o >= 0 && (kTailAll || chunk < cend) ? (unsigned)(o + chunk * (NI == 3 ? 96 : (X3 ? 128 : 64)))
+                                                 : DG_OOB);
     };
 
     // ---- weight K-tile slots (as conv_x6.hip): FWD RC image [16 k][BN],
@@ -411,14 +455,16 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // one K-tile: tap position T of chunk `chunk` from halo `hc`, weights in
-    // bs[T % NB]; issues halo pieces PPT*T .. of chunk+1 into `hn` and the
-    // weight tile two K-tiles ahead, then the MFMAs, then waits for the next
-    // weight tile (and, at the chunk's last tap, the whole next halo)
+    // bs[T % NB]; issues halo pieces PPT*T .. of chunk cn (the next one: chunk + 1, or the
+    // next patch's first -- nxp) into `hn` and the weight tile two K-tiles ahead, then the
+    // MFMAs, then waits for the next weight tile (and, at the chunk's last tap, the whole
+    // next halo)
     // A fragments of patch rows wm*TM + r (r = a + da, 0 <= r < TM + KT - 1) of the
     // current filter column: {hi|mid} and {hi|lo} of 16 halo pixels
     // (fp16x3: fm = [h0|h1], fl = [l0|l1])
     bf16x8 fm[TM + KT - 1], fl[TM + KT - 1];
-    auto ktile = [&](auto TT, auto PARc, int chunk, const char *hc, char *hn) __attribute__((always_inline)) {
+    auto ktile = [&](auto TT, auto PARc, int chunk, int cn, bool nxp, const char *hc, char *hn)
+                     __attribute__((always_inline)) {
         constexpr int T = decltype(TT)::value;
         constexpr int PAR = decltype(PARc)::value;   // (fp16x3) parity of the chunk's first K-tile in this block's sequence (NTAP even: 0)
         constexpr int ta = kTapsColMajor ? T % KT : T / KT, tb = kTapsColMajor ? T / KT : T % KT;
@@ -473,16 +519,16 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         if constexpr (MIDB) {   // every wave holds this tile's fragments: its buffer takes tile T+NB
             barrier();
             if constexpr (T + NB < NTAP) issue_b(T + NB, chunk, const_cast<char *>(bc));
-            else issue_b(T + NB - NTAP, chunk + 1, const_cast<char *>(bc));
+            else issue_b(T + NB - NTAP, cn, const_cast<char *>(bc));
         } else if constexpr (X3) {   // the next weight tile first: the wait below leaves only the halo pieces in flight
             if constexpr (T + 1 < NTAP) issue_b(T + 1, chunk, bn);
-            else issue_b(0, chunk + 1, bn);
+            else issue_b(0, cn, bn);
         }
 #pragma unroll
-        for (int s = H0P; s < H0P + NH; ++s) issue_h(s, chunk + 1, hn);
+        for (int s = H0P; s < H0P + NH; ++s) issue_h(s, cn, hn, nxp);
         if constexpr (!X3 && !MIDB) {
             if constexpr (T + 2 < NTAP) issue_b(T + 2, chunk, bn);
-            else issue_b(T + 2 - NTAP, chunk + 1, bn);
+            else issue_b(T + 2 - NTAP, cn, bn);
         }
         if constexpr (X3) {   // h.w_h, l.w_h, h.w_l
 #pragma unroll
@@ -536,15 +582,16 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         wait_dma_c<MIDB ? midb_wait_v(T) : (X3 ? NH : B_NJ + NH)>();
         barrier();
     };
-    auto chunk_tiles = [&](auto PARc, int chunk, const char *hc, char *hn) __attribute__((always_inline)) {
-        for_taps([&](auto TT) __attribute__((always_inline)) { ktile(TT, PARc, chunk, hc, hn); },
+    auto chunk_tiles = [&](auto PARc, int chunk, int cn, bool nxp, const char *hc, char *hn)
+                           __attribute__((always_inline)) {
+        for_taps([&](auto TT) __attribute__((always_inline)) { ktile(TT, PARc, chunk, cn, nxp, hc, hn); },
                  std::make_integer_sequence<int, NTAP>{});
     };
 
     // prologue: the whole halo of the first chunk and its first two weight tiles
     // (fp16x3: its first one)
 #pragma unroll
-    for (int s = 0; s < H_NJ; ++s) issue_h(s, cbeg, hal0);
+    for (int s = 0; s < H_NJ; ++s) issue_h(s, cbeg, hal0, false);
     issue_b(0, cbeg, bs0);
     if constexpr (MIDB) {   // one weight tile per buffer
         issue_b(1, cbeg, bs1);
@@ -558,46 +605,83 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         wait_dma_c<B_NJ>();
     }
     barrier();
-    int c = cbeg;
-    for (; c + 1 < cend; c += 2) {
-        chunk_tiles(std::integral_constant<int, 0>{}, c, hal0, hal1);
-        chunk_tiles(std::integral_constant<int, NTAP & 1>{}, c + 1, hal1, hal0);
-    }
-    if (c < cend) chunk_tiles(std::integral_constant<int, 0>{}, c, hal0, hal1);
-    // every wave's DMAs (including the harmless ones past the last chunk)
-    // have landed before the halo buffers become the epilogue's staging area
-    wait_dma_c<0>();
-    barrier();
 
     constexpr int STAGE = 16 * (WTN + 4);
-    static_assert(NW * STAGE * 4 <= 2 * HG::BYTES, "epilogue staging fits in the halo buffers");
-    float ys_pre = 0.f;
-    if constexpr (X3) {   // undo the operand scales (powers of two: exact)
-        const float osc = x3_out_scale(p, x3s);
+    static_assert(NW * STAGE * 4 <= (PERS ? 1 : 2) * HG::BYTES, "epilogue staging fits in the halo buffer(s)");
+    float osc = 1.f, ys_pre = 0.f, vacc = 0.f;
+    if constexpr (X3) {   // the operand scales to undo (powers of two: exact), the output planes' scale
+        osc = x3_out_scale(p, x3s);
         ys_pre = p.yp ? x3_raw_scale(x3s.y, F16X3_XS) : 0.f;
+    }
+    // after a patch's last chunk (its K-tiles consumed halo buffer HB): the epilogue, then the
+    // next patch (false: none)
+    auto patch_end = [&](auto HB) __attribute__((always_inline)) -> bool {
+        float *stage;
+        if constexpr (PERS) {
+            stage = reinterpret_cast<float *>(decltype(HB)::value ? hal1 : hal0) + wid * STAGE;
+        } else {
+            // every wave's DMAs (including the harmless ones past the last chunk)
+            // have landed before the halo buffers become the epilogue's staging area
+            wait_dma_c<0>();
+            barrier();
+            stage = reinterpret_cast<float *>(hal0) + wid * STAGE;
+        }
+        if constexpr (X3) {
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+                for (int b = 0; b < TN; ++b) acc[a][b] *= osc;
+        }
+        const int ty = cur.ty, tx = cur.tx, nimg = cur.nimg;
+        // patch row -> output pixel; slab rows: FWD / stride-1 DGRAD pixels, a
+        // phase's GEMM rows otherwise (as k_splitk_reduce maps them)
+        auto rowmap = [&](int row) __attribute__((always_inline)) -> RowPix {
+            const int ho = ty * HX_PH + (row >> 4), wo = tx * HX_PW + (row & 15);
+            if (ho >= Hout || wo >= Wout) return RowPix{-1, -1};
+            if constexpr (MODE == MODE_DGRAD && KT == 2) {
+                const long pix = ((long)nimg * g.H + ho * g.sh + ph.ph) * g.W + wo * g.sw + ph.pw;
+                return RowPix{((long)nimg * Hout + ho) * Wout + wo, pix};
+            } else {
+                const long pix = ((long)nimg * Hout + ho) * Wout + wo;
+                return RowPix{pix, pix};
+            }
+        };
+        float *va = PERS ? &vacc : nullptr;
+        if constexpr (POOL)
+            conv_epilogue16_pool<TM, TN>(p, acc, wm * TM, n0 + wn * WTN, ty, tx, nimg, lane, stage, ys_pre, va);
+        else
+            conv_epilogue16<MODE, TM, TN>(p, acc, wm * WTM, n0 + wn * WTN, rowmap, phase, split, lane, stage, ys_pre,
+                                          va);
+        if (jn < 0) return false;
+        // every wave has read its staging rows before the next patch's DMAs refill the buffer
+        barrier();
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
-            for (int b = 0; b < TN; ++b) acc[a][b] *= osc;
-    }
-    float *stage = reinterpret_cast<float *>(hal0) + wid * STAGE;
-    // patch row -> output pixel; slab rows: FWD / stride-1 DGRAD pixels, a
-    // phase's GEMM rows otherwise (as k_splitk_reduce maps them)
-    auto rowmap = [&](int row) __attribute__((always_inline)) -> RowPix {
-        const int ho = ty * HX_PH + (row >> 4), wo = tx * HX_PW + (row & 15);
-        if (ho >= Hout || wo >= Wout) return RowPix{-1, -1};
-        if constexpr (MODE == MODE_DGRAD && KT == 2) {
-            const long pix = ((long)nimg * g.H + ho * g.sh + ph.ph) * g.W + wo * g.sw + ph.pw;
-            return RowPix{((long)nimg * Hout + ho) * Wout + wo, pix};
-        } else {
-            const long pix = ((long)nimg * Hout + ho) * Wout + wo;
-            return RowPix{pix, pix};
-        }
+            for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+        cur = nxt;
+#pragma unroll
+        for (int s = 0; s < H_NJ; ++s) hoff[s] = hoffn[s];
+        jn = next_tile(jn + 1, nxt);
+        if (jn >= 0) halo_offsets(nxt, hoffn);
+        return true;
     };
-    if constexpr (POOL)
-        conv_epilogue16_pool<TM, TN>(p, acc, wm * TM, n0 + wn * WTN, ty, tx, nimg, lane, stage, ys_pre);
-    else
-        conv_epilogue16<MODE, TM, TN>(p, acc, wm * WTM, n0 + wn * WTN, rowmap, phase, split, lane, stage, ys_pre);
+    // chunk c of the current patch from halo buffer HB (the next chunk's halo into the other)
+    int c = cbeg;
+    auto step = [&](auto PARc, auto HB) __attribute__((always_inline)) -> bool {
+        const bool lastc = c + 1 == cend;
+        const int cn = lastc ? (jn >= 0 ? cbeg : cend) : c + 1;
+        chunk_tiles(PARc, c, cn, lastc, decltype(HB)::value ? hal1 : hal0, decltype(HB)::value ? hal0 : hal1);
+        c = lastc ? cbeg : cn;
+        return !lastc || patch_end(HB);
+    };
+    while (step(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}) &&
+           step(std::integral_constant<int, NTAP & 1>{}, std::integral_constant<int, 1>{})) {
+    }
+    if constexpr (PERS) {
+        if (p.ymax) block_atomic_absmax(p.ymax, vacc);
+        wait_dma_c<0>();   // (the pipeline tail's DMAs have landed before the block's LDS is released)
+    }
 }
 
 void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int tiles_x, int tiles_y, hipStream_t s,

@@ -85,6 +85,24 @@ def test_x3_layer_at_operand_scales(case, xs, gs, monkeypatch):
     test_conv_layer(case, "f16x3", xscale=xs, gscale=gs)
 
 
+# persistent halo blocks (conv_x6h.hip PERS: a block runs p.ptiles patches back to back, the
+# next patch's halo and weights fetched under the current one's MFMAs): forced to 3 and 5
+# patches per block on the halo cases -- patch counts that do not divide the grid, ragged
+# edge patches, Cout 48, the 4x4 stride-2 input-gradient / ConvT-forward phases -- at the
+# same fp64 bar (the planner applies it only to grids of >= 1024 patches, beyond these sizes)
+X3_PERS_CASES = [(c, pt) for c in (X3_CASES[0], X3_CASES[1], X3_CASES[2], X3_CASES[4], X3_CASES[5],
+                                   X3_CASES[6], X3_CASES[7], X3_CASES[8])
+                 for pt in (3, 5)]
+
+
+@gpu
+@pytest.mark.parametrize("case,pt", X3_PERS_CASES, ids=[f"{c[0]}-pt{pt}" for c, pt in X3_PERS_CASES])
+def test_x3_persistent_blocks_match_fp64(case, pt, monkeypatch):
+    monkeypatch.delenv("DG_PLAN_DISABLE", raising=False)
+    monkeypatch.setenv("DG_X3H_PTILES", str(pt))
+    test_conv_layer(case, "f16x3")
+
+
 @gpu
 def test_x3_shared_weight_planes_serve_bwd_data():
     """One weight PlaneBuf: the fp16x3 forward splits it; the (fp16x3) input gradient reading
@@ -146,10 +164,13 @@ def test_x3_producer_planes_equal_the_split(prod_math):
 
 
 @gpu
-def test_x3_fused_pool_planes_and_unfused_pool():
+@pytest.mark.parametrize("ptiles", ["1", "3"])
+def test_x3_fused_pool_planes_and_unfused_pool(ptiles, monkeypatch):
     """An fp16x3 conv with its 2x2 max pool fused (pool_fusable) writes the next fp16x3
     conv's x planes; so does the unfused pool (dg_maxpool2_fwd_plf).  Both equal the
-    consumer's own split, and the pooled values equal conv -> pool."""
+    consumer's own split, and the pooled values equal conv -> pool -- with one patch per
+    block and with persistent blocks of 3 patches (their max |pooled| folded across patches)."""
+    monkeypatch.setenv("DG_X3H_PTILES", ptiles)
     N, H, W, Ci, Co, Cn = 4, 32, 32, 64, 128, 128
     d = ops.ConvDesc(N, H, W, Ci, Co, 3, 1, "same", math="f16x3")
     nxt = ops.ConvDesc(N, H // 2, W // 2, Co, Cn, 3, 1, "same", math="f16x3")
