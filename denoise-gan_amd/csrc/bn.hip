@@ -38,10 +38,18 @@ static BnPlan bn_plan(long M, int C) {
 // statistics per segment: e.g. the G(x) and G(y) halves of one batched
 // generator pass, pix2pix.py:44 / :90):
 //   forward  [3*S*R*C partials (n, mean, M2)] [S*R*C unused] [4*S*C scale / shift]
-//   backward [4*S*R*C partials (sums, maxima)] [4*S*C coefficients]
+//   backward [4*S*R*C partials (sums, maxima)] [6*S*C coefficients]
 static size_t bn_ws_floats(long M, int C, int S = 1) {
     BnPlan p = bn_plan(M, C);
-    return (size_t)4 * S * p.R * C + (size_t)4 * S * C + 64;
+    return (size_t)4 * S * p.R * C + (size_t)6 * S * C + 64;
+}
+
+// the forward's per-channel scale / shift (z = act(y * scale + shift)), one rounding sequence
+// for the forward (k_bn_stats_final) and the backward passes that recompute act'(z) from y
+// (RZ): explicit fma, so both evaluate t = y * scale + shift to the same float
+__device__ __forceinline__ void bn_scale_shift(float g, float inv, float mu, float b, float &sc, float &sh) {
+    sc = g * inv;
+    sh = __builtin_fmaf(-mu, sc, b);
 }
 
 // segment of global row r (S is 1 or 2 in practice: a loop, no 64-bit divide)
@@ -276,8 +284,7 @@ k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, i
         if (save_invstd) save_invstd[sc] = inv;
         const float g = gamma ? gamma[c] : 1.f;
         const float b = beta ? beta[c] : 0.f;
-        scale[sc] = g * inv;
-        shift[sc] = b - mu * g * inv;
+        bn_scale_shift(g, inv, mu, b, scale[sc], shift[sc]);
         zbn = fmaxf(zbn, (fabsf(g * inv) * dmax + fabsf(b)) * keep_scale);
         mmc -= (mmc - mu) * (1.f - momentum);
         const float unb = n > 1.f ? m2 / (n - 1.f) : m2;
@@ -329,7 +336,7 @@ k_bn_apply(const float *__restrict__ y, int ld, long M, int S, int C, const floa
         const uint32_t sd = seed + (uint32_t)sg * seed_stride;
 #pragma unroll
         for (int q = 0; q < V; ++q) {
-            float t = v[q] * sc[q] + sh[q];
+            float t = __builtin_fmaf(v[q], sc[q], sh[q]);
             if (drop_rate > 0.f)
                 t = dropout_keep(sd, step, (uint32_t)(rr * C + c + q), drop_rate) ? t * keep_scale : 0.f;
             o[q] = act_fwd(t, act, alpha);
@@ -394,14 +401,17 @@ __device__ __forceinline__ void load_z(const float *__restrict__ z, long off, fl
 }
 
 // backward: partial sums of dbn and dbn*xhat per (chunk, channel); MX: also the maxima of the
-// fp16x3 dy bound (pd / pv set) -- without them the pass keeps round 3's register / LDS footprint
-template <int V, bool MX>
+// fp16x3 dy bound (pd / pv set) -- without them the pass keeps round 3's register / LDS footprint.
+// RZ: act'(z) from the sign of t = y * scale + shift (the forward's, bn_scale_shift from gamma,
+// offs, mean, invstd) instead of reading z -- ReLU / LeakyReLU without dropout, where
+// sign(z) = sign(t); one tensor fewer per element
+template <int V, bool MX, bool RZ = false>
 __global__ void __launch_bounds__(256)
 k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict__ z, int ldz,
                  const float *__restrict__ y, int ldy, long M, int C, long rows, int cpb,
                  const float *__restrict__ mean, const float *__restrict__ invstd, int act, float alpha, float dscale,
                  float *__restrict__ p1, float *__restrict__ p2, float *__restrict__ pd, float *__restrict__ pv,
-                 float *__restrict__ bound) {
+                 float *__restrict__ bound, const float *__restrict__ gamma, const float *__restrict__ offs) {
     // pd / pv (may be NULL): per chunk max |dbn| and max |y - mean|, the terms of the bound
     // on |dy| that scales its fp16x3 planes (k_bn_bwd_final); bound zeroed here for it
     __shared__ float a1s[256 * V], a2s[256 * V], dms[MX ? 256 * V : 1], vms[MX ? 256 * V : 1];
@@ -418,17 +428,23 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
     const long pbase = (long)blockIdx.z * gridDim.y;
     const long r0 = (long)blockIdx.y * rows;
     const long r1 = min(M, r0 + rows);
-    float a1[V], a2[V], dm[V], vm[V], mu[V], inv[V];
+    float a1[V], a2[V], dm[V], vm[V], mu[V], inv[V], fs[V], fh[V];
 #pragma unroll
     for (int q = 0; q < V; ++q) a1[q] = a2[q] = dm[q] = vm[q] = 0.f;
     const bool cok = c0 < C;
     if (cok) {
         loadv<V>(mean + c0, mu);
         loadv<V>(invstd + c0, inv);
+        if constexpr (RZ) {
+#pragma unroll
+            for (int q = 0; q < V; ++q)
+                bn_scale_shift(gamma ? gamma[c0 + q] : 1.f, inv[q], mu[q], offs ? offs[c0 + q] : 0.f, fs[q], fh[q]);
+        }
         auto acc_row = [&](const float (&dv)[V], const float (&zv)[V], const float (&yv)[V]) {
 #pragma unroll
             for (int q = 0; q < V; ++q) {
-                float dbn = dv[q] * act_grad_from_out(zv[q], act, alpha) * dscale;
+                const float zq = RZ ? __builtin_fmaf(yv[q], fs[q], fh[q]) : zv[q];
+                float dbn = dv[q] * act_grad_from_out(zq, act, alpha) * dscale;
                 a1[q] += dbn;
                 a2[q] += dbn * (yv[q] - mu[q]) * inv[q];
                 if constexpr (MX) {
@@ -445,7 +461,7 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 loadv<V>(dz + (r + u * RL) * lddz + c0, dv[u]);
-                load_z<V>(z, (r + u * RL) * ldz + c0, zv[u]);
+                load_z<V>(RZ ? nullptr : z, (r + u * RL) * ldz + c0, zv[u]);
                 loadv<V>(y + (r + u * RL) * ldy + c0, yv[u]);
             }
 #pragma unroll
@@ -454,7 +470,7 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
         for (; r < r1; r += RL) {
             float dv[V], zv[V], yv[V];
             loadv<V>(dz + r * lddz + c0, dv);
-            load_z<V>(z, r * ldz + c0, zv);
+            load_z<V>(RZ ? nullptr : z, r * ldz + c0, zv);
             loadv<V>(y + r * ldy + c0, yv);
             acc_row(dv, zv, yv);
         }
@@ -483,12 +499,14 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
     }
 }
 
-// per segment s: coef[s] = [A | B | D | mean] ([S][4][C]); dgamma / dbeta = the
+// per segment s: coef[s] = [A | B | D | mean | scale | shift] ([S][6][C]); dgamma / dbeta = the
 // sum over the segments (the reference's calls share the BN variables)
 __global__ void __launch_bounds__(256)
 k_bn_bwd_final(const float *p1, const float *p2, const float *pd, const float *pv, int R, int C, int S, long M,
                const float *gamma, const float *mean, const float *invstd, float *dgamma, float *dbeta, float beta,
-               float *coef, float *bound) {
+               float *coef, float *bound, int rz, const float *offs) {
+    // rz: also coef rows 4 / 5 = the forward's scale / shift (bn_scale_shift), for k_bn_bwd_apply's
+    // act'(z) recomputed from y
     // bound (pd, pv set): max over channels and segments of |A| max|dbn| + |B| max|y - mean| + |D|
     // >= max |dy|, into one of X3_SHARDS floats (zeroed by the partial pass)
     // one load round and one LDS round per segment: p1 / p2 (and pd / pv) together
@@ -527,11 +545,12 @@ k_bn_bwd_final(const float *p1, const float *p2, const float *pd, const float *p
         const float g = gamma ? gamma[c] : 1.f;
         const float k1 = g * invstd[sc];
         const float m1 = a1 / (float)M, m2 = a2 / (float)M;
-        float *cf = coef + (long)sg * 4 * C;
+        float *cf = coef + (long)sg * 6 * C;
         cf[c] = k1;
         cf[C + c] = -k1 * m2 * invstd[sc];
         cf[2 * C + c] = -k1 * m1;
         cf[3 * C + c] = mean[sc];
+        if (rz) bn_scale_shift(g, invstd[sc], mean[sc], offs ? offs[c] : 0.f, cf[4 * C + c], cf[5 * C + c]);
         bnd = fmaxf(bnd, fabsf(k1) * md + fabsf(cf[C + c]) * mv + fabsf(cf[2 * C + c]));
     }
     if (ln == 0 && c < C) {
@@ -549,7 +568,7 @@ k_bn_bwd_final(const float *p1, const float *p2, const float *pd, const float *p
     }
 }
 
-template <int V>
+template <int V, bool RZ = false>
 __global__ void __launch_bounds__(256)
 k_bn_bwd_apply(const float *__restrict__ dz, int lddz, const float *__restrict__ z, int ldz,
                const float *__restrict__ y, int ldy, long M, int S, int C, int act, float alpha, float dscale,
@@ -568,15 +587,22 @@ k_bn_bwd_apply(const float *__restrict__ dz, int lddz, const float *__restrict__
         const long r = e / CV;
         const int c = (int)(e - r * CV) * V;
         long rr = r;
-        const float *cf = coef + (long)seg_of(rr, M) * 4 * C;
+        const float *cf = coef + (long)seg_of(rr, M) * 6 * C;
         float dv[V], zv[V], yv[V], A[V], B[V], D[V], Mu[V], o[V];
         loadv<V>(dz + r * lddz + c, dv);
-        load_z<V>(z, r * ldz + c, zv);
+        load_z<V>(RZ ? nullptr : z, r * ldz + c, zv);
         loadv<V>(y + r * ldy + c, yv);
         loadv<V>(cf + c, A);
         loadv<V>(cf + C + c, B);
         loadv<V>(cf + 2 * C + c, D);
         loadv<V>(cf + 3 * C + c, Mu);
+        if constexpr (RZ) {   // act'(z) from t = y * scale + shift (the forward's rounding)
+            float fs[V], fh[V];
+            loadv<V>(cf + 4 * C + c, fs);
+            loadv<V>(cf + 5 * C + c, fh);
+#pragma unroll
+            for (int q = 0; q < V; ++q) zv[q] = __builtin_fmaf(yv[q], fs[q], fh[q]);
+        }
 #pragma unroll
         for (int q = 0; q < V; ++q)
             o[q] = A[q] * (dv[q] * act_grad_from_out(zv[q], act, alpha) * dscale) + B[q] * (yv[q] - Mu[q]) + D[q];
@@ -783,16 +809,22 @@ int dg_bn_bwd_seg_h(int S, int M, int C, const float *dz, int lddz, const float 
                            stream);
 }
 
-int dg_bn_bwd_seg_x(int S, int M, int C, const float *dz, int lddz, const float *z, int ldz, const float *y, int ldy,
-                    const float *gamma, const float *save_mean, const float *save_invstd, int act, float alpha,
-                    float drop_rate, float *dy, int lddy, void *dy_planes, int dy_planes_format, float *dy_bound,
-                    void *dy_f16, float *dgamma, float *dbeta, float beta, void *ws, size_t ws_bytes,
-                    dg_stream_t stream) {
+}  // extern "C"
+
+namespace dg {
+// rz: act'(z) from y and the forward's scale / shift (gamma, offs, save_mean, save_invstd) -- z
+// is not read (dg_bn_bwd_seg_r)
+static int bn_bwd_impl(int S, int M, int C, const float *dz, int lddz, const float *z, int ldz, const float *y,
+                       int ldy, const float *gamma, const float *offs, bool rz, const float *save_mean,
+                       const float *save_invstd, int act, float alpha, float drop_rate, float *dy, int lddy,
+                       void *dy_planes, int dy_planes_format, float *dy_bound, void *dy_f16, float *dgamma,
+                       float *dbeta, float beta, void *ws, size_t ws_bytes, dg_stream_t stream) {
     DG_ARG(!dy_f16 || (((uintptr_t)dy_f16) & 7) == 0, "fp16 copy must be 8-byte aligned");
     // dy NULL: only its planes are written (every consumer reads dy_planes)
-    // z NULL: allowed for a linear BN without dropout (act' = 1, z is not read)
-    DG_ARG(dz && (z || (act == DG_ACT_NONE && drop_rate == 0.f)) && y && save_mean && save_invstd &&
+    // z NULL: allowed for a linear BN without dropout (act' = 1, z is not read), and with rz
+    DG_ARG(dz && (z || rz || (act == DG_ACT_NONE && drop_rate == 0.f)) && y && save_mean && save_invstd &&
            (dy || dy_planes) && ws, "NULL tensor");
+    if (rz) z = nullptr;
     DG_ARG(dy_planes_format == DG_PLANES_BF16X6 || dy_planes_format == DG_PLANES_F16X3, "bad plane format");
     const bool x3 = dy_planes && dy_planes_format == DG_PLANES_F16X3;
     DG_ARG(!x3 || (dy_bound && C % 32 == 0), "fp16x3 dy planes need a bound buffer (8 floats) and C %% 32 == 0");
@@ -814,33 +846,68 @@ int dg_bn_bwd_seg_x(int S, int M, int C, const float *dz, int lddz, const float 
     {
         const dg::PartGeom pg = dg::part_geom(C, v4 ? 4 : 1);
         const dim3 grid(pg.cg, bp.R, S);
-#define DG_BNP(V_, MX_)                                                                                          \
-    hipLaunchKernelGGL((dg::k_bn_bwd_partial<V_, MX_>), grid, dim3(256), 0, s, dz, lddz, z, ldz, y, ldy, (long)M, C, \
-                       bp.rows, pg.cpb, save_mean, save_invstd, act, alpha, dscale, p1, p2, pd, pv, bnd)
-        if (v4 && x3) DG_BNP(4, true);
-        else if (v4) DG_BNP(4, false);
-        else if (x3) DG_BNP(1, true);
-        else DG_BNP(1, false);
+#define DG_BNP(V_, MX_, RZ_)                                                                                    \
+    hipLaunchKernelGGL((dg::k_bn_bwd_partial<V_, MX_, RZ_>), grid, dim3(256), 0, s, dz, lddz, z, ldz, y, ldy, (long)M, \
+                       C, bp.rows, pg.cpb, save_mean, save_invstd, act, alpha, dscale, p1, p2, pd, pv, bnd, gamma, offs)
+        if (rz) {
+            if (v4 && x3) DG_BNP(4, true, true);
+            else if (v4) DG_BNP(4, false, true);
+            else if (x3) DG_BNP(1, true, true);
+            else DG_BNP(1, false, true);
+        } else {
+            if (v4 && x3) DG_BNP(4, true, false);
+            else if (v4) DG_BNP(4, false, false);
+            else if (x3) DG_BNP(1, true, false);
+            else DG_BNP(1, false, false);
+        }
 #undef DG_BNP
     }
     DG_LAUNCHED("bn_bwd_partial");
     hipLaunchKernelGGL(dg::k_bn_bwd_final, dim3(dg_cdiv(C, dg::FIN_C)), dim3(256), 0, s, p1, p2, pd, pv, bp.R, C, S,
-                       (long)M, gamma, save_mean, save_invstd, dgamma, dbeta, beta, coef, bnd);
+                       (long)M, gamma, save_mean, save_invstd, dgamma, dbeta, beta, coef, bnd, rz ? 1 : 0, offs);
     DG_LAUNCHED("bn_bwd_final");
     const bool av4 = dg::vec4_ok(C, {{dz, lddz}, {z, ldz}, {y, ldy}, {dy, lddy}});
     unsigned short *dyp = (unsigned short *)dy_planes;
     DG_ARG(!dyp || (av4 && C % 16 == 0 && (((uintptr_t)dyp) & 15) == 0),
            "dy planes need C %% 16 == 0, float4-aligned tensors and a 16-byte aligned plane buffer");
     const long MT = (long)S * M;
-    if (av4)
-        hipLaunchKernelGGL(dg::k_bn_bwd_apply<4>, dim3(dg::ew_grid(MT * C / 4)), dim3(256), 0, s, dz, lddz, z, ldz, y,
-                           ldy, (long)M, S, C, act, alpha, dscale, coef, dy, lddy, dyp, (_Float16 *)dy_f16, bnd);
-    else
-        hipLaunchKernelGGL(dg::k_bn_bwd_apply<1>, dim3(dg::ew_grid(MT * C)), dim3(256), 0, s, dz, lddz, z, ldz, y,
-                           ldy, (long)M, S, C, act, alpha, dscale, coef, dy, lddy, dyp, (_Float16 *)dy_f16, bnd);
+#define DG_BNA(V_, RZ_)                                                                                    \
+    hipLaunchKernelGGL((dg::k_bn_bwd_apply<V_, RZ_>), dim3(dg::ew_grid(MT * C / V_)), dim3(256), 0, s, dz, lddz, z, \
+                       ldz, y, ldy, (long)M, S, C, act, alpha, dscale, coef, dy, lddy, dyp, (_Float16 *)dy_f16, bnd)
+    if (av4 && rz) DG_BNA(4, true);
+    else if (av4) DG_BNA(4, false);
+    else if (rz) DG_BNA(1, true);
+    else DG_BNA(1, false);
+#undef DG_BNA
     DG_LAUNCHED("bn_bwd_apply");
     return DG_OK;
 }
+}  // namespace dg
+
+extern "C" {
+
+int dg_bn_bwd_seg_x(int S, int M, int C, const float *dz, int lddz, const float *z, int ldz, const float *y, int ldy,
+                    const float *gamma, const float *save_mean, const float *save_invstd, int act, float alpha,
+                    float drop_rate, float *dy, int lddy, void *dy_planes, int dy_planes_format, float *dy_bound,
+                    void *dy_f16, float *dgamma, float *dbeta, float beta, void *ws, size_t ws_bytes,
+                    dg_stream_t stream) {
+    return dg::bn_bwd_impl(S, M, C, dz, lddz, z, ldz, y, ldy, gamma, nullptr, false, save_mean, save_invstd, act,
+                           alpha, drop_rate, dy, lddy, dy_planes, dy_planes_format, dy_bound, dy_f16, dgamma, dbeta,
+                           beta, ws, ws_bytes, stream);
+}
+
+int dg_bn_bwd_seg_r(int S, int M, int C, const float *dz, int lddz, const float *y, int ldy, const float *gamma,
+                    const float *bn_beta, const float *save_mean, const float *save_invstd, int act, float alpha,
+                    float *dy, int lddy, void *dy_planes, int dy_planes_format, float *dy_bound, void *dy_f16,
+                    float *dgamma, float *dbeta, float beta, void *ws, size_t ws_bytes, dg_stream_t stream) {
+    DG_ARG(act == DG_ACT_RELU || act == DG_ACT_LRELU || act == DG_ACT_NONE,
+           "act'(z) recomputed from y needs ReLU / LeakyReLU / linear (sign(z) = sign(y * scale + shift))");
+    return dg::bn_bwd_impl(S, M, C, dz, lddz, nullptr, C, y, ldy, gamma, bn_beta, true, save_mean, save_invstd, act,
+                           alpha, 0.f, dy, lddy, dy_planes, dy_planes_format, dy_bound, dy_f16, dgamma, dbeta, beta,
+                           ws, ws_bytes, stream);
+}
+
+
 
 int dg_act_bwd(int M, int C, const float *dz, int lddz, const float *z, int ldz, int act, float alpha, float *dy,
                int lddy, dg_stream_t stream) {

@@ -88,6 +88,8 @@ _SIGS = {
     "dg_conv_op_arith": (c_int, [_P, c_int, _P]),
     "dg_bn_bwd_seg_x": (c_int, [c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, _P, _P, _P, c_int, c_float,
                                 c_float, _P, c_int, _P, c_int, _P, _P, _P, _P, c_float, _P, c_size_t, _P]),
+    "dg_bn_bwd_seg_r": (c_int, [c_int, c_int, c_int, _P, c_int, _P, c_int, _P, _P, _P, _P, c_int, c_float,
+                                _P, c_int, _P, c_int, _P, _P, _P, _P, c_float, _P, c_size_t, _P]),
     "dg_accumulate": (c_int, [c_int64, c_int, _P, c_int, _P, c_int, c_float, _P]),
     "dg_act_fwd": (c_int, [c_int64, c_int, _P, c_int, c_int, c_float, _P, c_int, _P]),
     "dg_maxpool2_fwd": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P]),

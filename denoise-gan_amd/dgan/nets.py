@@ -35,6 +35,9 @@ DY_PLANES_ONLY = not os.environ.get("DG_DY_FP32")  # ... and then skips the fp32
 # fp16x3 activation planes scaled from their producers' bounds (ActBounds); DG_NO_ACT_BOUND: the
 # round-4 static 2^-4 (same-box A/B only: |x| < 2 then loses bits)
 ACT_BOUNDS = not os.environ.get("DG_NO_ACT_BOUND")
+# BN backward of the blocks without dropout takes act'(z) from y and the forward's scale / shift
+# (dg_bn_bwd_seg_r) instead of reading z; DG_BN_READ_Z: read z (same-box A/B)
+BN_RZ = not os.environ.get("DG_BN_READ_Z")
 
 
 def _eb(buf):
@@ -497,7 +500,8 @@ class GeneratorPlan:
         ops.bn_bwd(dz, z, y, A.param(f"{name}/gamma"), s["mean"][name], s["inv"][name], dy, A.grad_of(f"{name}/gamma"),
                    A.grad_of(f"{name}/beta"), act=act, alpha=ALPHA, drop_rate=drop_rate, beta=beta, ws=ws,
                    dy_planes=plane_rows(P.dy, dy, 0) if feed else None, segments=self.halves,
-                   dy_fp32=not (feed and DY_PLANES_ONLY), dy_bound=self.gbound[k] if feed else None)
+                   dy_fp32=not (feed and DY_PLANES_ONLY), dy_bound=self.gbound[k] if feed else None,
+                   offset=A.param(f"{name}/beta") if BN_RZ else None)
         if feed:
             P._filled(ops.TENSOR_DY)
 
@@ -772,7 +776,8 @@ class DiscriminatorPlan:
                                A.grad_of(f"{name}/beta") if param_grads else None, act="lrelu", alpha=ALPHA,
                                beta=beta, ws=ws, dy_planes=plane_rows(P.dy, dy, 0) if feed else None,
                                segments=len(hs), dy_fp32=not (feed and DY_PLANES_ONLY),
-                               dy_bound=gb[i] if feed else None)
+                               dy_bound=gb[i] if feed else None,
+                               offset=A.param(f"{name}/beta") if BN_RZ else None)
                     if feed:
                         P._filled(ops.TENSOR_DY)
                 else:

@@ -630,14 +630,16 @@ def bn_fwd_infer(y, gamma, beta, moving_mean, moving_var, z, act="none", alpha=0
 
 
 def bn_bwd(dz, z, y, gamma, save_mean, save_invstd, dy, dgamma, dbeta, act="none", alpha=0.3, drop_rate=0.0,
-           beta=0.0, ws=None, dy_planes=None, segments=1, dy_fp32=True, f16_out=None, dy_bound=None):
+           beta=0.0, ws=None, dy_planes=None, segments=1, dy_fp32=True, f16_out=None, dy_bound=None, offset=None):
     """dy_planes: a uint8 device tensor (e.g. a slice of a ConvPlanes' dy
     PlaneBuf) that also receives dy's bf16x6 planes -- or, with dy_bound (8 device
     floats, the consuming conv's dy scale source), its fp16x3 planes scaled from the
     bound written there (dg_bn_bwd_seg_x); dy_fp32=False then skips the fp32 dy (its
     consumers read the planes; dy only gives the shape).
     segments: see bn_fwd_train (dg_bn_bwd_seg; dgamma / dbeta summed over the
-    segments).  f16_out: the producing fp16 conv's dy PlaneBuf (dy's fp16 copy)."""
+    segments).  f16_out: the producing fp16 conv's dy PlaneBuf (dy's fp16 copy).
+    offset: the BN's beta (the forward's value): a ReLU / LeakyReLU block without dropout
+    then recomputes act'(z) from y (dg_bn_bwd_seg_r) and z is not read (may be None)."""
     C = y.shape[-1]
     M = _rows(y)
     if M % segments:
@@ -649,6 +651,14 @@ def bn_bwd(dz, z, y, gamma, save_mean, save_invstd, dy, dgamma, dbeta, act="none
         z = None   # a linear BN's backward does not read z (dg_bn_bwd_seg_h)
     if dy_bound is not None and dy_bound.numel() < 8:
         raise DGError("a gradient bound is 8 floats (per-workgroup shards)")
+    if offset is not None and act_id(act) in (ACT["relu"], ACT["lrelu"]) and drop_rate == 0.0:
+        call("dg_bn_bwd_seg_r", segments, M, C, _p(dz), pix_ld(dz, C), _p(y), pix_ld(y, C), _p(gamma), _p(offset),
+             _p(save_mean), _p(save_invstd), act_id(act), float(alpha),
+             _p(dy) if (dy_fp32 or dy_planes is None) else None, pix_ld(dy, C),
+             None if dy_planes is None else dy_planes.data_ptr(),
+             PLANES_F16X3 if dy_bound is not None else PLANES_BF16X6, _p(dy_bound), _f16(f16_out),
+             _p(dgamma), _p(dbeta), float(beta), _p(buf), n, _stream())
+        return dy
     call("dg_bn_bwd_seg_x", segments, M, C, _p(dz), pix_ld(dz, C), _p(z), pix_ld(z, C) if z is not None else C,
          _p(y), pix_ld(y, C),
          _p(gamma), _p(save_mean), _p(save_invstd), act_id(act), float(alpha), float(drop_rate),

@@ -366,6 +366,18 @@ int dg_bn_bwd_seg_x(int S, int M, int C, const float *dz, int lddz, const float 
                     int act, float alpha, float drop_rate,
                     float *dy, int lddy, void *dy_planes, int dy_planes_format, float *dy_bound, void *dy_f16,
                     float *dgamma, float *dbeta, float beta, void *ws, size_t ws_bytes, dg_stream_t stream);
+/* dg_bn_bwd_seg_x without z: act'(z) of a ReLU / LeakyReLU (or linear) BN block WITHOUT
+ * dropout recomputed from y as the sign of t = y * scale + shift, the forward's per-channel
+ * scale = gamma * invstd, shift = bn_beta - mean * scale (k_bn_stats_final's rounding, so t is
+ * the forward's pre-activation bit for bit and sign(z) = sign(t)) -- one tensor fewer read in
+ * both backward passes (pix2pix.py:119 / :135 / :211 BN sites, the down / up blocks' backward
+ * of Pix2Pix.train_step train_pix2pix.py:27-34).  bn_beta (the BN offset, may be NULL = 0) is
+ * the value the forward used (the gradients are taken before the optimizer step). */
+int dg_bn_bwd_seg_r(int S, int M, int C, const float *dz, int lddz,
+                    const float *y, int ldy, const float *gamma, const float *bn_beta,
+                    const float *save_mean, const float *save_invstd, int act, float alpha,
+                    float *dy, int lddy, void *dy_planes, int dy_planes_format, float *dy_bound, void *dy_f16,
+                    float *dgamma, float *dbeta, float beta, void *ws, size_t ws_bytes, dg_stream_t stream);
 /* dy = dz * act'(z)  for blocks without BN (pix2pix.py:118-121 with apply_batchnorm=False) */
 int dg_act_bwd(int M, int C, const float *dz, int lddz, const float *z, int ldz,
                int act, float alpha, float *dy, int lddy, dg_stream_t stream);

@@ -129,3 +129,44 @@ def test_bn_train_matches_fp64(case):
                         (dg, dg2, "dgamma"), (db, db2, "dbeta")):
         assert torch.equal(a, b_), f"{what} differs between two identical calls"
 
+
+
+@gpu
+@pytest.mark.parametrize("act", ["lrelu", "relu"])
+@pytest.mark.parametrize("planes", [False, True])
+def test_bn_bwd_act_from_y_equals_from_z(act, planes):
+    """dg_bn_bwd_seg_r (act'(z) from the sign of y * scale + shift, z not read) gives the bits
+    of dg_bn_bwd_seg_x reading the forward's z: dy, dgamma, dbeta and the fp16x3 dy planes with
+    their bound -- on two segments whose pre-activations crowd around 0 (beta 0, y within a
+    few ulps of the mean in a third of the channels), where a sign differing by one rounding
+    would show."""
+    from dgan import ops
+    torch.manual_seed(7 + planes)
+    S, M, C = 2, 3000, 96
+    R = S * M
+    y = torch.randn(R, C) * 1.3 + 0.2
+    y[:, ::3] = 0.5 + 1e-6 * torch.randn(R, (C + 2) // 3)   # t = (y - mean) * scale ~ rounding noise
+    y = y.to(DEV).view(1, 1, R, C)
+    g = (1 + 0.2 * torch.randn(C)).to(DEV)
+    b = torch.zeros(C, device=DEV)
+    b[1::3] = 0.1 * torch.randn((C + 1) // 3).to(DEV)
+    mm, mv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    mean, inv = torch.empty(S, C, device=DEV), torch.empty(S, C, device=DEV)
+    z = torch.empty(1, 1, R, C, device=DEV)
+    ops.bn_fwd_train(y, g, b, mean, inv, mm, mv, z, act=act, alpha=0.3, segments=S)
+    dz = torch.randn(1, 1, R, C).to(DEV)
+    out = []
+    for zz, off in ((z, None), (None, b)):
+        dy = torch.empty(1, 1, R, C, device=DEV)
+        dg, db = torch.full((C,), 0.5, device=DEV), torch.full((C,), -0.25, device=DEV)
+        pl = torch.zeros(R * C * 4, dtype=torch.uint8, device=DEV) if planes else None
+        bnd = torch.zeros(8, device=DEV) if planes else None
+        ops.bn_bwd(dz, zz, y, g, mean, inv, dy, dg, db, act=act, alpha=0.3, beta=1.0, segments=S,
+                   dy_planes=pl, dy_bound=bnd, offset=off)
+        out.append((dy, dg, db, pl, bnd))
+    torch.cuda.synchronize()
+    near0 = (z.view(R, C)[:, ::3].abs() < 1e-4).float().mean().item()
+    assert near0 > 0.5, f"the crowded channels sit near 0 ({near0:.2f})"
+    for a, b_, what in zip(out[0], out[1], ("dy", "dgamma", "dbeta", "dy planes", "dy bound")):
+        if a is not None:
+            assert torch.equal(a, b_), f"{what}: recomputed act' differs from the one read from z"
