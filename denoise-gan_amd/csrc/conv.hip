@@ -1547,14 +1547,21 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         // spends half its MFMAs on zero columns there)
         pl.cfg = pl.N > 64 && !h44 ? 128 : (h33 && pl.N <= 32 && !plan_off("halo32") ? 32 : 64);
         pl.mtiles = g.N * pl.htx * pl.hty;
-        pl.ntiles = (pl.N + pl.cfg - 1) / pl.cfg;
-        // split-K over channel chunks (at least two per split) until ~2 blocks per CU
-        const long nch = pl.K / (bkc * ntap), blocks = (long)pl.mtiles * pl.ntiles * pl.nphase;
-        long splits = 1;
         // (same-box A/B of the target: 256 -0.2%, 1024 -0.8% full step vs 512)
         long target = 512;
         // (diagnostic: DG_X3_TARGET sets the fp16x3 plans' block target for same-box sweeps)
         if (hx3 && getenv("DG_X3_TARGET")) target = atol(getenv("DG_X3_TARGET"));
+        // fp16x3 3x3 grids short of the target at BN 128: BN 64 tiles, twice the blocks, instead
+        // of (twice the) split-K, whose partial slabs and reduce launch cost more than the halved
+        // tile -- VGG19 block5 at bs32 0.148 -> 0.140 ms fwd, 0.152 -> 0.142 bwd_data, block4_conv1
+        // bwd_data 0.261 -> 0.255 (profiles/r5/ab_x3h_bn64.txt; DG_PLAN_DISABLE=x3h_bn64: BN 128)
+        if (hx3 && pl.cfg == 128 && (long)pl.mtiles * ((pl.N + 127) / 128) * pl.nphase < target &&
+            !plan_off("x3h_bn64"))
+            pl.cfg = 64;
+        pl.ntiles = (pl.N + pl.cfg - 1) / pl.cfg;
+        // split-K over channel chunks (at least two per split) until ~2 blocks per CU
+        const long nch = pl.K / (bkc * ntap), blocks = (long)pl.mtiles * pl.ntiles * pl.nphase;
+        long splits = 1;
         while (blocks * splits < target && splits * 4 <= nch) splits *= 2;
         const long cps = (nch + splits - 1) / splits;
         pl.kchunk = (int)(cps * bkc * ntap);
