@@ -38,6 +38,9 @@ ACT_BOUNDS = not os.environ.get("DG_NO_ACT_BOUND")
 # BN backward of the blocks without dropout takes act'(z) from y and the forward's scale / shift
 # (dg_bn_bwd_seg_r) instead of reading z; DG_BN_READ_Z: read z (same-box A/B)
 BN_RZ = not os.environ.get("DG_BN_READ_Z")
+# D's input gradient into a LeakyReLU block without BN masked in the conv epilogue; DG_NO_MASK_DZ:
+# a separate act_bwd pass (same-box A/B)
+MASK_DZ = not os.environ.get("DG_NO_MASK_DZ")
 
 
 def _eb(buf):
@@ -752,6 +755,7 @@ class DiscriminatorPlan:
         dybuf = self.dy_h if own else None
         gb = self.gbound_h if own else self.gbound
         dh = dlogits
+        masked = False   # dh already carries act'(z) of this layer's LeakyReLU (see bwd_data_masked below)
         n = len(self.specs)
         for i in range(n - 1, -1, -1):
             name, ci, co, bn = self.specs[i]
@@ -780,6 +784,8 @@ class DiscriminatorPlan:
                                offset=A.param(f"{name}/beta") if BN_RZ else None)
                     if feed:
                         P._filled(ops.TENSOR_DY)
+                elif masked:
+                    dy = dh
                 else:
                     ops.act_bwd(dh, sub(self.z[i]), dy, "lrelu", ALPHA)
                 if param_grads:
@@ -789,7 +795,14 @@ class DiscriminatorPlan:
                 on_grads_ready(name)
             if i > 0:
                 dz = dzs[i - 1] if own else sub(self.dz[i - 1])
-                d.bwd_data(dy, A.param(f"{name}/kernel"), dz, ws=ws, planes=P)
+                # a LeakyReLU block without BN below (down1, pix2pix.py:118-121): its act' applied
+                # in this input gradient's epilogue -- no separate act_bwd pass over dz
+                masked = MASK_DZ and not self.specs[i - 1][3]
+                if masked:
+                    d.bwd_data_masked(dy, A.param(f"{name}/kernel"), dz, sub(self.z[i - 1]), "lrelu", ALPHA, ws=ws,
+                                      planes=P)
+                else:
+                    d.bwd_data(dy, A.param(f"{name}/kernel"), dz, ws=ws, planes=P)
                 dh = dz
             elif input_grad is not None and input_from == 3:
                 co = self.specs[0][2]
