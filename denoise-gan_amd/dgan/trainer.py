@@ -22,6 +22,11 @@ from .nets import DiscriminatorPlan, GeneratorPlan, DROP_RATE
 # pass's small grids, BN passes and tails fill the G path's idle CU slots.  DG_NO_OVERLAP: one
 # stream (same-box A/B)
 OVERLAP = not os.environ.get("DG_NO_OVERLAP")
+# ... and D's forward beside the VGG19 content forward (DG_NO_OVERLAP_DF: in sequence)
+OVERLAP_DF = not os.environ.get("DG_NO_OVERLAP_DF")
+# ... and D(fake)'s input gradient (the G path through D) on a third stream beside the VGG19
+# backward, into its own buffer added to dL/dG(x) at the join (DG_NO_OVERLAP_DH: in sequence)
+OVERLAP_DH = not os.environ.get("DG_NO_OVERLAP_DH")
 
 LOSS_NAMES = ("gen_total_loss", "gen_gan_loss", "gen_l1_loss", "gen_l2_loss", "content_loss", "disc_loss",
               "var_loss", "identity_loss")
@@ -86,6 +91,12 @@ class Pix2PixTrainer:
             self.side = torch.cuda.Stream(device=device)
             self.ws_side = ops.Workspace(device)
             self.ws_side.get(self.D.ws_bytes)
+        self.side2 = None
+        if self.side is not None and OVERLAP_DH and self.content is not None and self.D.desc_g3 is not None:
+            self.side2 = torch.cuda.Stream(device=device)
+            self.ws_side2 = ops.Workspace(device)
+            self.ws_side2.get(self.D.ws_bytes)
+            self.dgen_d = e((N, H, W, 3))
 
     @property
     def gen_output(self):
@@ -115,12 +126,23 @@ class Pix2PixTrainer:
         gen = self.gout[:N]
         ident = self.gout[N:] if self.identity else None
         ops.strided_copy(gen, fake_in[..., 3:])
-        logits = D.forward(ws=ws)
-        zr, zf = logits[:N], logits[N:]
+        side = self.side if not ops.profiling() else None
+        main = torch.cuda.current_stream()
         content = None
-        if self.content is not None:
-            # content_loss(target, gen) = MSE(vgg(pre(y))/12.75, vgg(pre(G(x)))/12.75) (pix2pix.py:45-51)
+        if side is not None and OVERLAP_DF and self.content is not None:
+            # D's forward on the side stream beside the VGG19 forward (both read G(x) only; the
+            # losses join them)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                logits = D.forward(ws=self.ws_side)
             content = self.content.forward(gen, y, grad_weight=self.weights[5], ws=ws)
+            main.wait_stream(side)
+        else:
+            logits = D.forward(ws=ws)
+            if self.content is not None:
+                # content_loss(target, gen) = MSE(vgg(pre(y))/12.75, vgg(pre(G(x)))/12.75) (pix2pix.py:45-51)
+                content = self.content.forward(gen, y, grad_weight=self.weights[5], ws=ws)
+        zr, zf = logits[:N], logits[N:]
         # ---- losses + their gradients (pix2pix.py:74-103) ----------------
         dgen = self.dgout[:N]
         ops.p2p_loss(gen, y, zr, zf, self.loss, ident=ident, weights=self.weights, content=content,
@@ -128,10 +150,8 @@ class Pix2PixTrainer:
                      dlogit_fake_d=self.dlog[N:], dlogit_fake_g=self.dzf_g, ws=ws)
         sync = self.grad_sync
         # ---- disc_tape.gradient (train_pix2pix.py:65): both D calls in one pass
-        side = self.side if not ops.profiling() else None
         if side is not None:
             # (on the side stream, forked after the losses; its all-reduce is issued from there)
-            main = torch.cuda.current_stream()
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 D.backward(self.dlog, param_grads=True, beta=0.0, ws=self.ws_side)
@@ -142,13 +162,26 @@ class Pix2PixTrainer:
             if sync:
                 sync.start("D")
         # ---- gen_tape.gradient (train_pix2pix.py:64): through D(fake) into G(x)
-        if D.desc_g3 is not None:   # dL/dG(x) += channels 3..5 of dL/d D([x, G(x)])
-            D.backward(self.dzf_g, half=1, param_grads=False, input_grad=dgen, input_beta=1.0, ws=ws, input_from=3)
-        else:
-            D.backward(self.dzf_g, half=1, param_grads=False, input_grad=self.dinp, input_beta=0.0, ws=ws)
-            ops.accumulate(self.dinp[..., 3:], dgen, 1.0)
-        if self.content is not None:
+        side2 = self.side2 if side is not None else None
+        if side2 is not None:
+            # D(fake)'s input gradient beside the VGG19 backward (which accumulates into dgen
+            # meanwhile): into dgen_d, added at the join
+            side2.wait_stream(main)
+            with torch.cuda.stream(side2):
+                D.backward(self.dzf_g, half=1, param_grads=False, input_grad=self.dgen_d, input_beta=0.0,
+                           ws=self.ws_side2, input_from=3)
             self.content.backward(dgen, beta=1.0, ws=ws)
+            main.wait_stream(side2)
+            ops.accumulate(self.dgen_d, dgen, 1.0)
+        else:
+            if D.desc_g3 is not None:   # dL/dG(x) += channels 3..5 of dL/d D([x, G(x)])
+                D.backward(self.dzf_g, half=1, param_grads=False, input_grad=dgen, input_beta=1.0, ws=ws,
+                           input_from=3)
+            else:
+                D.backward(self.dzf_g, half=1, param_grads=False, input_grad=self.dinp, input_beta=0.0, ws=ws)
+                ops.accumulate(self.dinp[..., 3:], dgen, 1.0)
+            if self.content is not None:
+                self.content.backward(dgen, beta=1.0, ws=ws)
         # both generator calls (G(x), G(y)) in one backward: their gradients sum
         G.backward(self.dgout, beta=0.0, ws=ws, drop_rate=self.drop_rate,
                    on_grads_ready=(sync.ready_G if sync else None))
