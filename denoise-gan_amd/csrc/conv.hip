@@ -435,16 +435,17 @@ k_splitk_reduce(const GemmArgs p, int V4) {
                 pix = row;
             }
             const long off = pix * p.ldc;
-            f32x4 o;
+            f32x4 o, mf;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 float x = v[q];
                 if (p.bias) x += p.bias[col + q];
-                o[q] = epi_mask(p, pix, col + q, act_fwd(x, p.act, p.alpha));
+                mf[q] = epi_mask_factor(p, pix, col + q);
+                o[q] = act_fwd(x, p.act, p.alpha) * mf[q];
             }
             if (p.C) {
                 f32x4 *dst = reinterpret_cast<f32x4 *>(p.C + off + col);
-                if (p.beta != 0.f) o += p.beta * (*dst);
+                if (p.beta != 0.f) o += p.beta * (p.mask_acc ? (*dst) * mf : (*dst));
                 *dst = o;
             }
             if (p.yp) store_planes4(p.yp, p.ypC, pix, col, o, ys);
@@ -469,9 +470,10 @@ k_splitk_reduce(const GemmArgs p, int V4) {
         }
         const long off = pix * p.ldc;
         if (p.bias) v += p.bias[col];
-        v = epi_mask(p, pix, col, act_fwd(v, p.act, p.alpha));
+        const float mf = epi_mask_factor(p, pix, col);
+        v = act_fwd(v, p.act, p.alpha) * mf;
         if (p.C) {
-            if (p.beta != 0.f) v += p.beta * p.C[off + col];
+            if (p.beta != 0.f) v += p.beta * (p.mask_acc ? p.C[off + col] * mf : p.C[off + col]);
             p.C[off + col] = v;
         }
         if (p.yp) store_planes1(p.yp, p.ypC, pix, col, v, ys);
@@ -1831,6 +1833,12 @@ static int run_engine(const dg_conv_desc_s *d, int op, const float *A, int lda, 
     DG_ARG(ws_bytes >= need, "workspace too small: need %zu bytes, got %zu", need, ws_bytes);
     DG_ARG(need == 0 || ws != nullptr, "workspace pointer is NULL");
     GemmArgs a = make_args(d->g, pl, A, lda, B, ldb, C, ldc, bias, beta, act, alpha, ws);
+    // (mact | DG_MASK_SUM: the mask also multiplies beta*C -- the conv_epilogue16 / split-K reduce
+    // epilogues of the x6 / fp16x3 / fp16 plans implement it)
+    a.mask_acc = (mact & DG_MASK_SUM) ? 1 : 0;
+    mact &= ~DG_MASK_SUM;
+    DG_ARG(!a.mask_acc || (pl.x6 && !d->rc[op].on && (mz || mzp)),
+           "mask of the accumulated sum: only on the split-precision plans, with a mask");
     a.mz = mz; a.ldmz = ldmz; a.mact = mact; a.malpha = malpha;
     if (pl.x6 == 3) {
         // fp16x3 operand roles (op_tensors): A is x or dy, B is w, or, in a filter gradient,
@@ -2489,6 +2497,22 @@ int dg_conv_bwd_data_pl(dg_conv_t d, const float *dy, int lddy, const float *w, 
                           DG_ACT_NONE, 0.f, ws, ws_bytes, (hipStream_t)stream, z, z ? ldz : 0,
                           z ? act : DG_ACT_NONE, alpha, pr, planes ? (unsigned short *)planes->out : nullptr, nullptr,
                           nullptr, planes ? planes->out_format : DG_PLANES_BF16X6);
+}
+
+int dg_conv_bwd_data_masked_sum(dg_conv_t d, const float *dy, int lddy, const float *w, float *dx, int lddx,
+                                float beta, const float *z, int ldz, int act, float alpha,
+                                const dg_conv_planes_t *planes, void *ws, size_t ws_bytes, dg_stream_t stream) {
+    DG_ARG(d && dy && w && dx && z, "NULL tensor");
+    DG_ARG(lddy >= d->Cout && lddx >= d->Cin && ldz >= d->Cin, "pixel stride smaller than channels");
+    DG_ARG(act >= DG_ACT_NONE && act <= DG_ACT_SIGMOID, "unknown activation %d", act);
+    dg::PlaneRefs r{};
+    const dg::PlaneRefs *pr;
+    int e = dg::plane_refs(d, DG_OP_BWD_DATA, planes, r, pr);
+    if (e != DG_OK) return e;
+    return dg::run_engine(d, DG_OP_BWD_DATA, dy, lddy, w, d->transpose ? d->g.Co : 0, dx, lddx, nullptr, beta,
+                          DG_ACT_NONE, 0.f, ws, ws_bytes, (hipStream_t)stream, z, ldz, act | dg::DG_MASK_SUM, alpha,
+                          pr, planes ? (unsigned short *)planes->out : nullptr, nullptr, nullptr,
+                          planes ? planes->out_format : DG_PLANES_BF16X6);
 }
 
 int dg_conv_bwd_data_xmask(dg_conv_t d, const float *dy, int lddy, const float *w, float *dx, int lddx, float beta,

@@ -6,6 +6,8 @@
 namespace dg {
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+// run_engine's mask activation flag: the mask multiplies the accumulated sum (GemmArgs.mask_acc)
+constexpr int DG_MASK_SUM = 0x100;
 
 struct ConvGeom {
     int N, H, W, Ci;  // conv-view input
@@ -61,6 +63,9 @@ struct GemmArgs {
     // fp16x3 halo kernel: patches per block (blocks gm = gridDim.x / ntiles; block's patches
     // mt0 + j * gm, j < ptiles); other kernels 1
     int ptiles;
+    // 1: the gradient mask also multiplies the accumulated beta*C (dg_conv_bwd_data_masked_sum:
+    // C = act'(mz) * (result + beta*C), a fan-in whose other contribution arrived unmasked)
+    int mask_acc;
 };
 
 // the factor that undoes an fp16x3 GEMM's operand scales (powers of two: exact)
@@ -105,6 +110,11 @@ __device__ __forceinline__ float plane_scale(const GemmArgs &p) {
     return p.ys_m ? x3_grad_scale(p.ys_m, p.ys_g, p.ys_c) : F16X3_XS;
 }
 
+__device__ __forceinline__ float epi_mask_factor(const GemmArgs &p, long pix, int col) {
+    if (p.mz) return act_grad_from_out(p.mz[pix * p.ldmz + col], p.mact, p.malpha);
+    if (p.mzp) return act_grad_from_out(hi_plane(p.mzp, p.mzpC, pix, col), p.mact, p.malpha);
+    return 1.f;
+}
 __device__ __forceinline__ float epi_mask(const GemmArgs &p, long pix, int col, float v) {
     if (p.mz) return v * act_grad_from_out(p.mz[pix * p.ldmz + col], p.mact, p.malpha);
     if (p.mzp) return v * act_grad_from_out(hi_plane(p.mzp, p.mzpC, pix, col), p.mact, p.malpha);
@@ -289,6 +299,7 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q) o[q] = act_fwd(o[q], p.act, p.alpha);
+            f32x4 mf = {1.f, 1.f, 1.f, 1.f};   // the mask factors (p.mask_acc: beta*C's too)
             if (p.mz) {
                 const float *mz = p.mz + pix * p.ldmz + col;
                 f32x4 z;
@@ -299,7 +310,8 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
                     for (int q = 0; q < 4; ++q) z[q] = (col + q < p.N) ? mz[q] : 0.f;
                 }
 #pragma unroll
-                for (int q = 0; q < 4; ++q) o[q] *= act_grad_from_out(z[q], p.mact, p.malpha);
+                for (int q = 0; q < 4; ++q) mf[q] = act_grad_from_out(z[q], p.mact, p.malpha);
+                o *= mf;
             } else if (p.mzp) {
                 f32x4 z;
                 if (full) {
@@ -309,17 +321,22 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
                     for (int q = 0; q < 4; ++q) z[q] = (col + q < p.N) ? hi_plane(p.mzp, p.mzpC, pix, col + q) : 0.f;
                 }
 #pragma unroll
-                for (int q = 0; q < 4; ++q) o[q] *= act_grad_from_out(z[q], p.mact, p.malpha);
+                for (int q = 0; q < 4; ++q) mf[q] = act_grad_from_out(z[q], p.mact, p.malpha);
+                o *= mf;
             }
             if (!p.C) {
                 // planes-only output (dg_conv_fwd_pl with y == NULL, beta 0)
             } else if (cvec && full) {
-                if (p.beta != 0.f) o += p.beta * *reinterpret_cast<const f32x4 *>(dst);
+                if (p.beta != 0.f) {
+                    const f32x4 c = *reinterpret_cast<const f32x4 *>(dst);
+                    o += p.beta * (p.mask_acc ? c * mf : c);
+                }
                 *reinterpret_cast<f32x4 *>(dst) = o;
             } else {
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
-                    if (col + q < p.N) o[q] = dst[q] = p.beta != 0.f ? o[q] + p.beta * dst[q] : o[q];
+                    if (col + q < p.N)
+                        o[q] = dst[q] = p.beta != 0.f ? o[q] + p.beta * (p.mask_acc ? dst[q] * mf[q] : dst[q]) : o[q];
             }
             if (p.yp) {
                 if (full) {

@@ -678,10 +678,17 @@ __global__ void __launch_bounds__(256) k_absmax(const float *__restrict__ x, lon
     const long total = rows * C;
     if (ld == C && ((((uintptr_t)x) & 15) == 0)) {
         const long t4 = total >> 2;
-        for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < t4; e += (long)gridDim.x * blockDim.x) {
-            const f32x4 v = reinterpret_cast<const f32x4 *>(x)[e];
-            m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+        const long st = (long)gridDim.x * blockDim.x;
+        long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+        auto m4 = [](f32x4 v) { return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))); };
+        for (; e + 3 * st < t4; e += 4 * st) {   // (four loads in flight per lane)
+            f32x4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = reinterpret_cast<const f32x4 *>(x)[e + u * st];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) m = fmaxf(m, m4(v[u]));
         }
+        for (; e < t4; e += st) m = fmaxf(m, m4(reinterpret_cast<const f32x4 *>(x)[e]));
         for (long e = (t4 << 2) + (long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
              e += (long)gridDim.x * blockDim.x)
             m = fmaxf(m, fabsf(x[e]));

@@ -38,17 +38,42 @@ k_adam(float *__restrict__ p, const float *__restrict__ g, float *__restrict__ m
     const float lr_t = lr * sqrtf(1.f - powf(b2, t)) / (1.f - powf(b1, t));
     const long n4 = n >> 2;
     const long stride = (long)gridDim.x * blockDim.x;
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-        f32x4 gg = reinterpret_cast<const f32x4 *>(g)[i] * gscale;
-        f32x4 mm = reinterpret_cast<f32x4 *>(m)[i];
-        f32x4 vv = reinterpret_cast<f32x4 *>(v)[i];
-        f32x4 pp = reinterpret_cast<f32x4 *>(p)[i];
+    // U float4 groups per lane per round, all 4U loads issued before the first use (the
+    // single-group loop waited a full HBM latency per 64 B of the 28 B/element stream)
+    constexpr int U = 4;
+    auto upd = [&](f32x4 gg, f32x4 &mm, f32x4 &vv, f32x4 &pp) __attribute__((always_inline)) {
+        gg *= gscale;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             mm[q] += (gg[q] - mm[q]) * (1.f - b1);
             vv[q] += (gg[q] * gg[q] - vv[q]) * (1.f - b2);
             pp[q] -= (mm[q] * lr_t) / (sqrtf(vv[q]) + eps);
         }
+    };
+    long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+        f32x4 gg[U], mm[U], vv[U], pp[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            gg[u] = reinterpret_cast<const f32x4 *>(g)[i + u * stride];
+            mm[u] = reinterpret_cast<f32x4 *>(m)[i + u * stride];
+            vv[u] = reinterpret_cast<f32x4 *>(v)[i + u * stride];
+            pp[u] = reinterpret_cast<f32x4 *>(p)[i + u * stride];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            upd(gg[u], mm[u], vv[u], pp[u]);
+            reinterpret_cast<f32x4 *>(m)[i + u * stride] = mm[u];
+            reinterpret_cast<f32x4 *>(v)[i + u * stride] = vv[u];
+            reinterpret_cast<f32x4 *>(p)[i + u * stride] = pp[u];
+        }
+    }
+    for (; i < n4; i += stride) {
+        f32x4 gg = reinterpret_cast<const f32x4 *>(g)[i];
+        f32x4 mm = reinterpret_cast<f32x4 *>(m)[i];
+        f32x4 vv = reinterpret_cast<f32x4 *>(v)[i];
+        f32x4 pp = reinterpret_cast<f32x4 *>(p)[i];
+        upd(gg, mm, vv, pp);
         reinterpret_cast<f32x4 *>(m)[i] = mm;
         reinterpret_cast<f32x4 *>(v)[i] = vv;
         reinterpret_cast<f32x4 *>(p)[i] = pp;

@@ -114,6 +114,8 @@ _SIGS = {
     "dg_conv_fwd_pool_ok": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int)]),
     "dg_conv_bwd_data_xmask": (c_int, [c_void_p, _P, c_int, _P, _P, c_int, c_float, c_int, c_float, _P, _P, c_size_t,
                                        _P]),
+    "dg_conv_bwd_data_masked_sum": (c_int, [c_void_p, _P, c_int, _P, _P, c_int, c_float, _P, c_int, c_int, c_float,
+                                            _P, _P, c_size_t, _P]),
     "dg_conv_fwd_pool": (c_int, [c_void_p, _P, c_int, _P, _P, c_int, c_float, _P, c_int, _P, _P, _P, c_size_t, _P]),
     "dg_maxpool2_bwd_idx": (c_int, [c_int, c_int, c_int, c_int, _P, _P, c_int, _P, c_int, c_float, c_int, c_float, _P,
                                     _P]),

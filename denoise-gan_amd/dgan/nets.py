@@ -538,6 +538,7 @@ class GeneratorPlan:
             d.bwd_data(dy, A.param(f"{name}/kernel"), dhin, ws=ws, planes=P)
             if on_grads_ready:
                 on_grads_ready(name)
+        masked_sum = False
         for l in range(7, -1, -1):
             name, ci, co, bn = self.downs[l]
             d = self.ddesc[l]
@@ -547,13 +548,22 @@ class GeneratorPlan:
             P = self._bwd_planes(l)
             if bn:
                 self._bn_bwd(s, name, dz, z, s["yd"][l], dy, "lrelu", beta, ws, P=P if FEED_DY else None, k=l)
+            elif masked_sum:
+                dy = dz   # (down2's input gradient applied act' to the summed gradient)
             else:
                 ops.act_bwd(dz, z, dy, "lrelu", ALPHA)
             hin = s["x"] if l == 0 else self.z_view(s, l - 1)
             d.bwd_filter(hin, dy, A.grad_of(f"{name}/kernel"), beta=beta, ws=ws, planes=P)
+            masked_sum = False
             if l > 0:
-                # accumulate into the skip-gradient already sitting in the concat grad buffer
-                d.bwd_data(dy, A.param(f"{name}/kernel"), self.dz_view(l - 1), beta=1.0, ws=ws, planes=P)
+                # accumulate into the skip-gradient already sitting in the concat grad buffer; into
+                # a LeakyReLU block without BN (down1) with act' applied to the sum in the epilogue
+                if MASK_DZ and not self.downs[l - 1][3] and d.op_arith("bwd_data") != "fp32":
+                    d.bwd_data_masked_sum(dy, A.param(f"{name}/kernel"), self.dz_view(l - 1),
+                                          self.z_view(s, l - 1), "lrelu", ALPHA, beta=1.0, ws=ws, planes=P)
+                    masked_sum = True
+                else:
+                    d.bwd_data(dy, A.param(f"{name}/kernel"), self.dz_view(l - 1), beta=1.0, ws=ws, planes=P)
             if on_grads_ready:
                 on_grads_ready(name)
 

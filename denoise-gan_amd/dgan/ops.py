@@ -442,6 +442,22 @@ class ConvDesc:
         """dx = dL/dx * act'(z) + beta*dx, z = the activation output this conv read as input."""
         return self._bwd_data(dy, w, dx, z, act_id(act), alpha, beta, ws, planes)
 
+    def bwd_data_masked_sum(self, dy, w, dx, z, act, alpha=0.3, beta=1.0, ws=None, planes=None):
+        """dx = act'(z) * (dL/dx + beta*dx): the mask also covers the gradient already in dx
+        (dg_conv_bwd_data_masked_sum; split-precision plans only)."""
+        lddy, lddx = pix_ld(dy, self.Cout), pix_ld(dx, self.Cin)
+        wp, wn = self._ws(OP_BWD_DATA, ws)
+        pp, fills = self._pl(OP_BWD_DATA, planes)
+        ev = _prof_begin()
+        call("dg_conv_bwd_data_masked_sum", self._h, _p(dy), lddy, _p(w), _p(dx), lddx, float(beta), _p(z),
+             pix_ld(z, self.Cin), act_id(act), float(alpha), pp, wp, wn, _stream())
+        _prof_end(ev, self, "bwd_data")
+        if fills:
+            planes._filled(fills)
+        if planes is not None and planes.bwd_out is not None:
+            planes.bwd_out.ready = True
+        return dx
+
     def bwd_data_xmask(self, dy, w, dx, act, alpha=0.3, beta=0.0, ws=None, planes=None):
         """dx = dL/dx * act'(x) + beta*dx with act' from the sign of x's hi plane
         (planes.x, ready): the layer input need not exist in fp32."""

@@ -223,6 +223,14 @@ int dg_conv_bwd_filter_pl(dg_conv_t d, const float *x, int ldx, const float *dy,
 int dg_conv_bwd_data_xmask(dg_conv_t d, const float *dy, int lddy, const float *w, float *dx, int lddx,
                            float beta, int act, float alpha, const dg_conv_planes_t *planes,
                            void *ws, size_t ws_bytes, dg_stream_t stream);
+/* dg_conv_bwd_data_pl whose mask act'(z) multiplies the accumulated sum:
+ * dx = act'(z) * (dL/dx + beta*dx) -- the last contribution of a gradient fan-in into an
+ * activation without BN (the U-Net's down1 output reaches 'last' through the skip concat and
+ * down2, pix2pix.py:115-121 / :180-190), so no separate act' pass over the summed gradient.
+ * Split-precision plans only (DG_MATH_BF16X6 / F16X3 / FP16); others return DG_ERR_ARG. */
+int dg_conv_bwd_data_masked_sum(dg_conv_t d, const float *dy, int lddy, const float *w, float *dx, int lddx,
+                                float beta, const float *z, int ldz, int act, float alpha,
+                                const dg_conv_planes_t *planes, void *ws, size_t ws_bytes, dg_stream_t stream);
 /* Conv2D forward followed by MaxPool2D(2) on its activated output, fused into
  * the forward epilogue (VGG19 blockN_conv{2,4} -> blockN_pool, keras
  * applications VGG19 as built by pix2pix.py:53-67 / srgan.py:70-76; replaces

@@ -303,3 +303,31 @@ def test_x3_input_gradient_chain_with_scale_context():
     assert float(gmax[0].max()) == float(dzA.abs().max())
     assert float(gmax[1].max()) == float(dy.abs().max())
     _close(dx, xr.grad, 2 * 9 * max(C1, C2), "chain dx")
+
+
+@gpu
+@pytest.mark.parametrize("math", ["f16x3", "bf16x6"])
+@pytest.mark.parametrize("Co", [128, 512])
+def test_bwd_data_masked_sum(math, Co):
+    """dg_conv_bwd_data_masked_sum: dx = act'(z) * (dL/dx + beta dx) -- the U-Net's down1
+    gradient fan-in (skip + down2) masked once after the sum -- equals act'(z) applied in torch to
+    the unmasked input gradient plus the prior dx, on the halo phases kernel's epilogue and (the
+    K of 512 output channels splits) through the split-K reduce."""
+    N, H, W, Ci = 2, 32, 32, 64
+    d = ops.ConvDesc(N, H, W, Ci, Co, 4, 2, "same", math=math)
+    w, dy = _rand(d.weight_shape, 21, 0.05), _rand(d.out_shape, 22)
+    z = _rand((N, H, W, Ci), 23)
+    prior = _rand((N, H, W, Ci), 24)
+    dx = prior.clone()
+    if d.op_arith("bwd_data") == "fp32":   # (the planner kept this size on fp32 tiles: refused, loudly)
+        with pytest.raises(ops.DGError, match="split-precision"):
+            d.bwd_data_masked_sum(dy, w, dx, z, "lrelu", 0.3, beta=1.0)
+        return
+    dx_plain = torch.empty(N, H, W, Ci, device="cuda")
+    d.bwd_data(dy, w, dx_plain)
+    d.bwd_data_masked_sum(dy, w, dx, z, "lrelu", 0.3, beta=1.0)
+    torch.cuda.synchronize()
+    mask = torch.where(z > 0, torch.ones_like(z), torch.full_like(z, 0.3))
+    ref = mask * (dx_plain + prior)
+    err = (dx - ref).abs().max().item()
+    assert err <= 2e-6 * ref.abs().max().item(), err
