@@ -58,7 +58,7 @@ constexpr bool kTapsColMajor = true;
 // Default: fp16x3 and fp16 (SRGAN 4208 -> 4271 img/s, profiles/r4/ab_halo_midb_all.txt); the
 // bf16x6 halo kernel keeps the plain pipeline (the autoencoder's 64^2 VGG19 forward ran 29 %
 // slower with it, profiles/r5/ab_ae_r3_r5.txt)
-#if defined(DG_NO_MIDB)
+#if defined(DG_NO_MIDB) || defined(DG_X6H_NOB)
 constexpr int kMidb = 0;
 #elif defined(DG_MIDB_X3)
 constexpr int kMidb = 1;
@@ -434,6 +434,9 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     // tap position T of chunk c: FWD rows (tap*Ci + 16c) of w[(a,b,ci)][co];
     // DGRAD rows ci of w[i,j] at co-chunk c
     auto issue_b = [&](int T, int chunk, char *bs) __attribute__((always_inline)) {
+#ifdef DG_X6H_NOB
+        if constexpr (X3) return;   // (timing diagnostic only: no weight tiles move -- wrong results)
+#endif
         int delta;
         constexpr int LW = NI == 3 ? 3 : (X3 ? 2 : 1);   // weight row stride in units of ldb
         if constexpr (!B_KC) delta = ((tap_w[T] * g.Ci + chunk * BK) * (LW * p.ldb)) * 2;
