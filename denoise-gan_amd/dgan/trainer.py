@@ -27,6 +27,11 @@ OVERLAP_DF = not os.environ.get("DG_NO_OVERLAP_DF")
 # ... and D(fake)'s input gradient (the G path through D) on a third stream beside the VGG19
 # backward, into its own buffer added to dL/dG(x) at the join (DG_NO_OVERLAP_DH: in sequence)
 OVERLAP_DH = not os.environ.get("DG_NO_OVERLAP_DH")
+# ... and (one process, no all-reduce) G's Adam over the arena prefix of 'last' and the up blocks --
+# the backward-completion layout puts them first, final once up1's backward is enqueued -- on a
+# stream beside the down blocks' backward; the down blocks' suffix after it (DG_NO_EARLY_ADAM: one
+# Adam launch per network after the backward)
+EARLY_ADAM = not os.environ.get("DG_NO_EARLY_ADAM")
 
 LOSS_NAMES = ("gen_total_loss", "gen_gan_loss", "gen_l1_loss", "gen_l2_loss", "content_loss", "disc_loss",
               "var_loss", "identity_loss")
@@ -91,6 +96,14 @@ class Pix2PixTrainer:
             self.side = torch.cuda.Stream(device=device)
             self.ws_side = ops.Workspace(device)
             self.ws_side.get(self.D.ws_bytes)
+        # G arena prefix final after the up blocks' backward (layout = backward completion order)
+        downs = {n for n, *_ in self.G.downs}
+        self.g_split = min(g_arena.offsets[n] for n in g_arena.layout if n.split("/")[0] in downs)
+        assert all(g_arena.end_offset(n) <= self.g_split for n in g_arena.layout if n.split("/")[0] not in downs)
+        self.g_last_up = self.G.ups[0][0]   # (G.backward's last up block)
+        self.side3 = None
+        if self.side is not None and EARLY_ADAM:
+            self.side3 = torch.cuda.Stream(device=device)
         self.side2 = None
         if self.side is not None and OVERLAP_DH and self.content is not None and self.D.desc_g3 is not None:
             self.side2 = torch.cuda.Stream(device=device)
@@ -183,8 +196,21 @@ class Pix2PixTrainer:
             if self.content is not None:
                 self.content.backward(dgen, beta=1.0, ws=ws)
         # both generator calls (G(x), G(y)) in one backward: their gradients sum
-        G.backward(self.dgout, beta=0.0, ws=ws, drop_rate=self.drop_rate,
-                   on_grads_ready=(sync.ready_G if sync else None))
+        early = apply and sync is None and self.side3 is not None and side is not None
+        hook = sync.ready_G if sync else None
+        if early:
+            side3, gA, go = self.side3, self.gA, self.g_opt
+
+            def hook(name):
+                if name != self.g_last_up:
+                    return
+                # the up blocks' gradients are enqueued: their Adam beside the down blocks' backward
+                k = self.g_split
+                side3.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side3):
+                    ops.adam(gA.data[:k], gA.grad[:k], gA.m[:k], gA.v[:k], go.current_lr(), go.beta_1, go.beta_2,
+                             go.epsilon, gA.iterations)
+        G.backward(self.dgout, beta=0.0, ws=ws, drop_rate=self.drop_rate, on_grads_ready=hook)
         if side is not None:
             torch.cuda.current_stream().wait_stream(side)   # (join: D's gradients before Adam)
         if sync:
@@ -195,7 +221,13 @@ class Pix2PixTrainer:
             # the optimizers' hyper-parameters are read at every step (a changed or callable
             # learning_rate takes effect; a captured HIP graph keeps the values of its capture)
             for A, o in ((self.gA, self.g_opt), (self.dA, self.d_opt)):
-                ops.adam(A.data, A.grad, A.m, A.v, o.current_lr(), o.beta_1, o.beta_2, o.epsilon, A.iterations,
-                         grad_scale=scale)
+                if early and A is self.gA:   # (the prefix ran on side3; the suffix here, then the join)
+                    k = self.g_split
+                    ops.adam(A.data[k:], A.grad[k:], A.m[k:], A.v[k:], o.current_lr(), o.beta_1, o.beta_2,
+                             o.epsilon, A.iterations)
+                    torch.cuda.current_stream().wait_stream(self.side3)
+                else:
+                    ops.adam(A.data, A.grad, A.m, A.v, o.current_lr(), o.beta_1, o.beta_2, o.epsilon,
+                             A.iterations, grad_scale=scale)
                 ops.counter_add(A.iterations, 1)
         return self.loss
