@@ -1091,8 +1091,10 @@ class GraphNetwork:
         print_fn(f"Total params: {self.count_params():,d}")
         print_fn(f"Trainable params: {self.arena.count if self.trainable else 0:,d}")
 
-    def plan(self, N, H, W, slots=1, train=False, param_grads=True, alias=None):
-        key = (N, H, W, slots, train, param_grads, id(alias) if alias is not None else None, self.conv_math)
+    def plan(self, N, H, W, slots=1, train=False, param_grads=True, alias=None, tag=None):
+        """tag: a distinct plan (own buffers) of the same shape -- e.g. two forwards that run
+        concurrently on two streams."""
+        key = (N, H, W, slots, train, param_grads, id(alias) if alias is not None else None, self.conv_math, tag)
         if key not in self._plans:
             self._plans[key] = GraphPlan(self.graph, N, H, W, self.arena, self.bn, self.device, slots=slots,
                                          train=train, param_grads=param_grads, alias=alias, math=self.conv_math)

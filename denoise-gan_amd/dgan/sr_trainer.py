@@ -106,25 +106,72 @@ class ContentLoss:
     half only, on an N-image plan whose activations are views of the first
     half of the batched forward's buffers."""
 
-    def __init__(self, vgg, N, H, W, device, train=True):
+    def __init__(self, vgg, N, H, W, device, train=True, split=False):
+        """split: the target's VGG19 forward on its own N-image plan (forward_target, e.g. on a
+        second stream beside the generator's forward, whose output it does not need) and G(x)'s
+        on another; otherwise both in one 2N forward."""
         self.vgg = vgg
         self.N = N
-        self.fplan = vgg.plan(2 * N, H, W, slots=1, train=False, param_grads=False)
-        self.bplan = vgg.plan(N, H, W, slots=1, train=True, param_grads=False, alias=self.fplan) if train else None
+        self.split = split
         e = lambda s: torch.empty(s, dtype=torch.float32, device=device)
-        self.pre = e((2 * N, H, W, 3))                    # [pre(gen); pre(target)]
+        if split:
+            self.fplan = vgg.plan(N, H, W, slots=1, train=False, param_grads=False)
+            self.tplan = vgg.plan(N, H, W, slots=1, train=False, param_grads=False, tag="target")
+            self.pre = e((N, H, W, 3))                    # pre(gen)
+            self.pre_t = e((N, H, W, 3))                  # pre(target)
+            self.tfeat = None
+        else:
+            self.fplan = vgg.plan(2 * N, H, W, slots=1, train=False, param_grads=False)
+            self.tplan = None
+            self.pre = e((2 * N, H, W, 3))                # [pre(gen); pre(target)]
+        self.bplan = vgg.plan(N, H, W, slots=1, train=True, param_grads=False, alias=self.fplan) if train else None
         self.dpre = e((N, H, W, 3)) if train else None
         self.dfeat = e((N,) + tuple(self.fplan.out_shape[1:])) if train else None
         self.value = torch.zeros(1, dtype=torch.float32, device=device)
         self.ws_bytes = max(self.fplan.ws_bytes, self.bplan.ws_bytes if train else 0, ops.mse_workspace_bytes())
+        self.tws_bytes = self.tplan.ws_bytes if split else 0
 
-    def forward(self, gen, tgt, grad_weight=1.0, ws=None):
+    def forward_target(self, tgt, ws=None):
+        """(split) the target's features, read by the next forward()."""
+        ops.vgg_preprocess_fwd(tgt, self.pre_t)
+        self.tfeat = self.tplan.forward(self.pre_t, slot=0, training=False, ws=ws)
+        return self.tfeat
+
+    def feature_sources(self):
+        """((plan, rows) of G(x)'s VGG19 forward, (plan, rows) of the target's): where the
+        last step's activations of each live (one 2N plan, or the two N plans of split)."""
         N = self.N
-        ops.vgg_preprocess_fwd(gen, self.pre[:N])
-        ops.vgg_preprocess_fwd(tgt, self.pre[N:])
-        f = self.fplan.forward(self.pre, slot=0, training=False, ws=ws)
+        if self.split:
+            return (self.fplan, slice(0, N)), (self.tplan, slice(0, N))
+        return (self.fplan, slice(0, N)), (self.fplan, slice(N, 2 * N))
+
+    def settled(self):
+        """The shared frozen weight planes are split for the current VGG19 weights: the two
+        plans may then run on two streams (the first forward after a weight change splits them,
+        and the plans share the buffers -- that one runs in sequence)."""
+        return getattr(self, "_settled", None) == getattr(self.vgg.arena, "version", 0)
+
+    def mark_settled(self):
+        self._settled = getattr(self.vgg.arena, "version", 0)
+
+    def forward(self, gen, tgt, grad_weight=1.0, ws=None, tsync=None):
+        """tsync (split): called before the target's features are read (a stream join)."""
+        N = self.N
+        if self.split:
+            if self.tfeat is None:
+                raise RuntimeError("ContentLoss(split=True): forward_target first")
+            ops.vgg_preprocess_fwd(gen, self.pre)
+            fg = self.fplan.forward(self.pre, slot=0, training=False, ws=ws)
+            ft = self.tfeat
+            if tsync is not None:
+                tsync()
+        else:
+            ops.vgg_preprocess_fwd(gen, self.pre[:N])
+            ops.vgg_preprocess_fwd(tgt, self.pre[N:])
+            f = self.fplan.forward(self.pre, slot=0, training=False, ws=ws)
+            fg, ft = f[:N], f[N:]
         # MeanSquaredError()(target_features, gen_features): grad w.r.t. gen features
-        ops.mse(f[:N], f[N:], self.value, scale=FEAT_SCALE, da=self.dfeat, grad_weight=grad_weight, ws=ws)
+        ops.mse(fg, ft, self.value, scale=FEAT_SCALE, da=self.dfeat, grad_weight=grad_weight, ws=ws)
         return self.value
 
     def backward(self, dgen, beta=1.0, ws=None):

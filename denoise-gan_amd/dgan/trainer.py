@@ -32,6 +32,9 @@ OVERLAP_DH = not os.environ.get("DG_NO_OVERLAP_DH")
 # stream beside the down blocks' backward; the down blocks' suffix after it (DG_NO_EARLY_ADAM: one
 # Adam launch per network after the backward)
 EARLY_ADAM = not os.environ.get("DG_NO_EARLY_ADAM")
+# ... and the target's VGG19 forward (its own N-image plan) on a stream beside the generator's
+# forward from the start of the step (DG_NO_OVERLAP_VT: one 2N VGG19 forward after G)
+OVERLAP_VT = not os.environ.get("DG_NO_OVERLAP_VT")
 
 LOSS_NAMES = ("gen_total_loss", "gen_gan_loss", "gen_l1_loss", "gen_l2_loss", "content_loss", "disc_loss",
               "var_loss", "identity_loss")
@@ -82,9 +85,10 @@ class Pix2PixTrainer:
         self.loss = torch.zeros(8, dtype=torch.float32, device=device)
         # VGG19 content loss (pix2pix.py:45-51, :87): frozen feature extractor on G(x) and y
         self.content = None
+        vsplit = OVERLAP and OVERLAP_VT
         if vgg is not None and self.weights[5] != 0.0:
             from .sr_trainer import ContentLoss
-            self.content = ContentLoss(vgg, N, H, W, device)
+            self.content = ContentLoss(vgg, N, H, W, device, split=vsplit)
         ws_bytes = max(self.G.ws_bytes, self.D.ws_bytes,
                        ops.p2p_loss_workspace_bytes(N, H, W, 3, lshape[0] * lshape[1] * lshape[2]),
                        self.content.ws_bytes if self.content else 0)
@@ -101,6 +105,11 @@ class Pix2PixTrainer:
         self.g_split = min(g_arena.offsets[n] for n in g_arena.layout if n.split("/")[0] in downs)
         assert all(g_arena.end_offset(n) <= self.g_split for n in g_arena.layout if n.split("/")[0] not in downs)
         self.g_last_up = self.G.ups[0][0]   # (G.backward's last up block)
+        self.side4 = None
+        if self.side is not None and self.content is not None and self.content.split:
+            self.side4 = torch.cuda.Stream(device=device)
+            self.ws_vgg = ops.Workspace(device)
+            self.ws_vgg.get(self.content.tws_bytes)
         self.side3 = None
         if self.side is not None and EARLY_ADAM:
             self.side3 = torch.cuda.Stream(device=device)
@@ -126,6 +135,18 @@ class Pix2PixTrainer:
         inp = D.inp
         real_in, fake_in = inp[:N], inp[N:]
         step_dev = self.gA.iterations
+        main = torch.cuda.current_stream()
+        # the target's VGG19 features (pix2pix.py:45-51: vgg(pre(target))) need nothing of G:
+        # beside G's forward on side4 once the shared weight planes are settled
+        tfork = False
+        if self.content is not None and self.content.split:
+            tfork = self.side4 is not None and not ops.profiling() and self.content.settled()
+            if tfork:
+                self.side4.wait_stream(main)
+                with torch.cuda.stream(self.side4):
+                    self.content.forward_target(y, ws=self.ws_vgg)
+            else:
+                self.content.forward_target(y, ws=ws)
         # ---- forward (pix2pix.py:44-48 and the identity pass :90) -----------
         ops.channel_concat(x, y, real_in)                 # concatenate([inp, tar]) (pix2pix.py:200)
         ops.strided_copy(x, fake_in[..., :3])
@@ -140,21 +161,21 @@ class Pix2PixTrainer:
         ident = self.gout[N:] if self.identity else None
         ops.strided_copy(gen, fake_in[..., 3:])
         side = self.side if not ops.profiling() else None
-        main = torch.cuda.current_stream()
         content = None
+        tsync = (lambda: main.wait_stream(self.side4)) if tfork else None
         if side is not None and OVERLAP_DF and self.content is not None:
             # D's forward on the side stream beside the VGG19 forward (both read G(x) only; the
             # losses join them)
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 logits = D.forward(ws=self.ws_side)
-            content = self.content.forward(gen, y, grad_weight=self.weights[5], ws=ws)
+            content = self.content.forward(gen, y, grad_weight=self.weights[5], ws=ws, tsync=tsync)
             main.wait_stream(side)
         else:
             logits = D.forward(ws=ws)
             if self.content is not None:
                 # content_loss(target, gen) = MSE(vgg(pre(y))/12.75, vgg(pre(G(x)))/12.75) (pix2pix.py:45-51)
-                content = self.content.forward(gen, y, grad_weight=self.weights[5], ws=ws)
+                content = self.content.forward(gen, y, grad_weight=self.weights[5], ws=ws, tsync=tsync)
         zr, zf = logits[:N], logits[N:]
         # ---- losses + their gradients (pix2pix.py:74-103) ----------------
         dgen = self.dgout[:N]
@@ -216,6 +237,8 @@ class Pix2PixTrainer:
         if sync:
             sync.finish()
         # ---- apply_gradients (train_pix2pix.py:68-69) ----------------------
+        if self.content is not None and self.content.split:
+            self.content.mark_settled()
         if apply:
             scale = sync.grad_scale if sync else 1.0
             # the optimizers' hyper-parameters are read at every step (a changed or callable

@@ -22,6 +22,12 @@ import torch
 from oracle import p2p_oracle as O
 from oracle import sr_oracle as S
 
+
+def _vsrc(cl):
+    """(plan, slot, rows) of G(x)'s and of the target's VGG19 activations (ContentLoss)."""
+    (pg, rg), (pt, rt) = cl.feature_sources()
+    return (pg, 0, rg), (pt, 0, rt)
+
 gpu = pytest.mark.gpu
 DEV = "cuda"
 
@@ -92,8 +98,8 @@ def test_vgg19_planned_across_arithmetics_alternating():
         assert val == val_f, (step, N, H, val, val_f)
         assert np.array_equal(dg, dg_f), (step, N, H, float(np.abs(dg - dg_f).max()))
         PV = {k: torch.tensor(v.astype(np.float64)) for k, v in w.items()}
-        dec = {"Vsr": to_oracle(graph_decisions(cl.fplan, 0, rows=slice(0, N))),
-               "Vhr": to_oracle(graph_decisions(cl.fplan, 0, rows=slice(N, 2 * N)))}
+        dec = {"Vsr": to_oracle(graph_decisions(*_vsrc(cl)[0])),
+               "Vhr": to_oracle(graph_decisions(*_vsrc(cl)[1]))}
         gt = torch.tensor(gen.astype(np.float64), requires_grad=True)
         c = S.content_loss(PV, torch.tensor(y.astype(np.float64)), gt, dec["Vsr"], dec["Vhr"])
         d0 = torch.autograd.grad(c, gt)[0].numpy()

@@ -22,6 +22,12 @@ import torch
 
 from oracle import sr_oracle as S
 
+
+def _vsrc(cl):
+    """(plan, slot, rows) of G(x)'s and of the target's VGG19 activations (ContentLoss)."""
+    (pg, rg), (pt, rt) = cl.feature_sources()
+    return (pg, 0, rg), (pt, 0, rt)
+
 gpu = pytest.mark.gpu
 DEV = "cuda"
 
@@ -367,8 +373,8 @@ def _sr_decisions(tr):
     dec = {"G": graph_decisions(tr.Gp, 0), "Dr": graph_decisions(tr.Dp, 0), "Df": graph_decisions(tr.Dp, 1)}
     if tr.content is not None:
         N = tr.N
-        dec["Vsr"] = graph_decisions(tr.content.fplan, 0, rows=slice(0, N))
-        dec["Vhr"] = graph_decisions(tr.content.fplan, 0, rows=slice(N, 2 * N))
+        dec["Vsr"] = graph_decisions(*_vsrc(tr.content)[0])
+        dec["Vhr"] = graph_decisions(*_vsrc(tr.content)[1])
     return {k: to_oracle(v) for k, v in dec.items()}
 
 
@@ -481,8 +487,8 @@ def test_vgg_content_gradient_matches_oracle():
         v = cl.forward(torch.from_numpy(gen).to(DEV), torch.from_numpy(y).to(DEV), ws=ws)
         cl.backward(dg, beta=0.0, ws=ws)
         torch.cuda.synchronize()
-        dec = {"Vsr": to_oracle(graph_decisions(cl.fplan, 0, rows=slice(0, N))),
-               "Vhr": to_oracle(graph_decisions(cl.fplan, 0, rows=slice(N, 2 * N)))}
+        dec = {"Vsr": to_oracle(graph_decisions(*_vsrc(cl)[0])),
+               "Vhr": to_oracle(graph_decisions(*_vsrc(cl)[1]))}
         gt = torch.tensor(gen.astype(np.float64), requires_grad=True)
         c = S.content_loss(PV, torch.tensor(y.astype(np.float64)), gt, dec["Vsr"], dec["Vhr"])
         d0 = torch.autograd.grad(c, gt)[0]

@@ -17,6 +17,12 @@ import torch
 
 from oracle import p2p_oracle as O
 
+
+def _vsrc(cl):
+    """(plan, slot, rows) of G(x)'s and of the target's VGG19 activations (ContentLoss)."""
+    (pg, rg), (pt, rt) = cl.feature_sources()
+    return (pg, 0, rg), (pt, 0, rt)
+
 gpu = pytest.mark.gpu
 
 
@@ -243,8 +249,8 @@ def test_step_parity_with_vgg_content(case, monkeypatch):
     N = x.shape[0]
     dec = {"Gx": generator_decisions(tr.G, 0), "Gy": generator_decisions(tr.G, 1),
            "Dr": discriminator_decisions(tr.D, 0), "Df": discriminator_decisions(tr.D, 1),
-           "Vsr": graph_decisions(tr.content.fplan, 0, rows=slice(0, N)),
-           "Vhr": graph_decisions(tr.content.fplan, 0, rows=slice(N, 2 * N))}
+           "Vsr": graph_decisions(*_vsrc(tr.content)[0]),
+           "Vhr": graph_decisions(*_vsrc(tr.content)[1])}
     dec = {k: to_oracle(v) for k, v in dec.items()}
     vals, gG, gD, gen_ref = T.step_grads(G, D, x, y, width=width, drop_rate=drop, drop_seed=drop_seed, PV=PV,
                                          dec=dec)
