@@ -202,7 +202,14 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     constexpr int NTAP = HG::NTAP;
     // weight K-tile buffers: a tap position owns one (bf16x6 / fp16: two tiles in
     // flight); fp16x3: two buffers alternating by tap and chunk, one tile ahead
+    // (fp16x3 3x3 BN 64: three -- 72.8 KB with the halos, still two blocks per CU -- so a weight
+    // tile has two K-tiles of MFMAs to land; DG_X3H_NB2: two, for same-box A/B)
+#ifdef DG_X3H_NB2
     constexpr int NB = X3 ? 2 : (NTAP % 3 == 0 ? 3 : 4);
+#else
+    constexpr int NB = X3 ? ((KT == 3 && BN == 64) ? 3 : 2) : (NTAP % 3 == 0 ? 3 : 4);
+#endif
+    constexpr bool XPAR = X3 && NB == 2;   // buffers alternate by K-tile parity (NTAP odd: across chunks)
     static_assert(X3 || NTAP % NB == 0, "tap positions line up with the weight buffers across chunks");
     constexpr int BK = NI == 3 ? 16 : 32, NW = 4;   // channels per chunk
     constexpr int WTM = 64, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
@@ -216,6 +223,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     // mid-K-tile barrier form: needs the last NB-1 tap positions free of halo pieces
     // (the wait counts below), so not the KT 2 phases (4 taps, 4 buffers)
     constexpr bool MIDB = (kMidb == 2 || (kMidb == 1 && X3) || (kMidb == 3 && NI != 3)) && TL <= NTAP - NB;
+    static_assert(XPAR || !X3 || MIDB, "fp16x3 with three weight buffers: the mid-K-tile barrier pipeline");
     // pipeline-tail DMAs (chunks past the split's range) out of range -- no traffic -- on the
     // fp16x3 / fp16 instances; the bf16x6 kernel issues them in range (the autoencoder's 64^2
     // VGG19 forward ran 23 % slower with the out-of-range form, profiles/r5/ab_ae_r3_r5.txt;
@@ -475,8 +483,8 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         constexpr int db = MODE == MODE_FWD ? tb : KT - 1 - tb;
         constexpr int H0P = T * PPT, H1P = (T + 1) * PPT < H_NJ ? (T + 1) * PPT : H_NJ;
         constexpr int NH = H1P > H0P ? H1P - H0P : 0;   // halo pieces issued in this K-tile
-        const char *bc = X3 ? bbuf((T + PAR) & 1) : bbuf(T % NB);
-        char *bn = X3 ? bbuf((T + PAR + 1) & 1) : bbuf((T + 2) % NB);
+        const char *bc = XPAR ? bbuf((T + PAR) & 1) : bbuf(T % NB);
+        char *bn = XPAR ? bbuf((T + PAR + 1) & 1) : bbuf((T + 2) % NB);
         bf16x8 b1[TN], b2[TN], b3[TN];
         const char *H0 = hc, *H1 = hc + HIMG, *H2 = hc + 2 * HIMG, *H3 = hc + 3 * HIMG;
         auto load_row = [&](int r) __attribute__((always_inline)) {
