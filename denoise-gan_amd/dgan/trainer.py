@@ -35,6 +35,8 @@ EARLY_ADAM = not os.environ.get("DG_NO_EARLY_ADAM")
 # ... and the target's VGG19 forward (its own N-image plan) on a stream beside the generator's
 # forward from the start of the step (DG_NO_OVERLAP_VT: one 2N VGG19 forward after G)
 OVERLAP_VT = not os.environ.get("DG_NO_OVERLAP_VT")
+# D's parameter backward forked at the start of G's backward instead of after the losses
+DBWD_LATE = bool(os.environ.get("DG_DBWD_LATE"))
 
 LOSS_NAMES = ("gen_total_loss", "gen_gan_loss", "gen_l1_loss", "gen_l2_loss", "content_loss", "disc_loss",
               "var_loss", "identity_loss")
@@ -184,14 +186,17 @@ class Pix2PixTrainer:
                      dlogit_fake_d=self.dlog[N:], dlogit_fake_g=self.dzf_g, ws=ws)
         sync = self.grad_sync
         # ---- disc_tape.gradient (train_pix2pix.py:65): both D calls in one pass
-        if side is not None:
-            # (on the side stream, forked after the losses; its all-reduce is issued from there)
+        def d_param_backward():
+            # (on the side stream; its all-reduce is issued from there)
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 D.backward(self.dlog, param_grads=True, beta=0.0, ws=self.ws_side)
                 if sync:
                     sync.start("D")
-        else:
+        dlate = side is not None and DBWD_LATE
+        if side is not None and not dlate:
+            d_param_backward()   # (forked after the losses)
+        elif side is None:
             D.backward(self.dlog, param_grads=True, beta=0.0, ws=ws)
             if sync:
                 sync.start("D")
@@ -231,6 +236,8 @@ class Pix2PixTrainer:
                 with torch.cuda.stream(side3):
                     ops.adam(gA.data[:k], gA.grad[:k], gA.m[:k], gA.v[:k], go.current_lr(), go.beta_1, go.beta_2,
                              go.epsilon, gA.iterations)
+        if dlate:
+            d_param_backward()   # (forked at G's backward: its small layers leave CUs to fill)
         G.backward(self.dgout, beta=0.0, ws=ws, drop_rate=self.drop_rate, on_grads_ready=hook)
         if side is not None:
             torch.cuda.current_stream().wait_stream(side)   # (join: D's gradients before Adam)
