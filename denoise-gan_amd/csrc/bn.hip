@@ -46,10 +46,11 @@ static size_t bn_ws_floats(long M, int C, int S = 1) {
 
 // the forward's per-channel scale / shift (z = act(y * scale + shift)), one rounding sequence
 // for the forward (k_bn_stats_final) and the backward passes that recompute act'(z) from y
-// (RZ): explicit fma, so both evaluate t = y * scale + shift to the same float
+// (RZ), so both evaluate t = y * scale + shift to the same float.  shift keeps the rounding of
+// rounds 1-4 (b - mu*g*inv: the SR family's fp16 step tests sit on rounding ties of it)
 __device__ __forceinline__ void bn_scale_shift(float g, float inv, float mu, float b, float &sc, float &sh) {
     sc = g * inv;
-    sh = __builtin_fmaf(-mu, sc, b);
+    sh = b - mu * g * inv;
 }
 
 // segment of global row r (S is 1 or 2 in practice: a loop, no 64-bit divide)
