@@ -677,21 +677,31 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         if (jn >= 0) halo_offsets(nxt, hoffn);
         return true;
     };
-    // chunk c of the current patch from halo buffer HB (the next chunk's halo into the other)
-    int c = cbeg;
-    auto step = [&](auto PARc, auto HB) __attribute__((always_inline)) -> bool {
-        const bool lastc = c + 1 == cend;
-        const int cn = lastc ? (jn >= 0 ? cbeg : cend) : c + 1;
-        chunk_tiles(PARc, c, cn, lastc, decltype(HB)::value ? hal1 : hal0, decltype(HB)::value ? hal0 : hal1);
-        c = lastc ? cbeg : cn;
-        return !lastc || patch_end(HB);
-    };
-    while (step(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}) &&
-           step(std::integral_constant<int, NTAP & 1>{}, std::integral_constant<int, 1>{})) {
-    }
     if constexpr (PERS) {
+        // chunk c of the current patch from halo buffer HB (the next chunk's halo into the other)
+        int c = cbeg;
+        auto step = [&](auto PARc, auto HB) __attribute__((always_inline)) -> bool {
+            const bool lastc = c + 1 == cend;
+            const int cn = lastc ? (jn >= 0 ? cbeg : cend) : c + 1;
+            chunk_tiles(PARc, c, cn, lastc, decltype(HB)::value ? hal1 : hal0, decltype(HB)::value ? hal0 : hal1);
+            c = lastc ? cbeg : cn;
+            return !lastc || patch_end(HB);
+        };
+        while (step(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}) &&
+               step(std::integral_constant<int, NTAP & 1>{}, std::integral_constant<int, 1>{})) {
+        }
         if (p.ymax) block_atomic_absmax(p.ymax, vacc);
         wait_dma_c<0>();   // (the pipeline tail's DMAs have landed before the block's LDS is released)
+    } else {
+        // one patch: the chunk loop, then the epilogue outside it (in the loop body its registers
+        // would be live beside the bf16x6 / fp16 fragments: 150-580 VGPRs of spills measured)
+        int c = cbeg;
+        for (; c + 1 < cend; c += 2) {
+            chunk_tiles(std::integral_constant<int, 0>{}, c, c + 1, false, hal0, hal1);
+            chunk_tiles(std::integral_constant<int, NTAP & 1>{}, c + 1, c + 2, false, hal1, hal0);
+        }
+        if (c < cend) chunk_tiles(std::integral_constant<int, 0>{}, c, c + 1, false, hal0, hal1);
+        patch_end(std::integral_constant<int, 0>{});
     }
 }
 
