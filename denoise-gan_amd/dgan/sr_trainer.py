@@ -192,6 +192,13 @@ COEF = {
 }
 
 
+# the target's work (its VGG19 features and D(real)) on a second stream beside G's forward,
+# which it does not need -- for outputs of >= 256^2 pixels: FastSRGAN 512^2 +1.7 %, while the
+# 96^2 SRGAN (-2.5 %) and the 64^2 autoencoder (-7 %) lose more to the halved VGG19 batch than
+# the overlap returns (profiles/r5/ab_sr_overlap.txt; DG_SR_NO_OVERLAP: never)
+SR_OVERLAP = not os.environ.get("DG_SR_NO_OVERLAP")
+SR_OVERLAP_MIN_PIXELS = 256 * 256
+
 LOSS_SCALE_INIT = 2.0 ** 15     # tf.keras DynamicLossScale defaults (srgan.py:64-67)
 LOSS_SCALE_PERIOD = 2000
 LOSS_SCALE_MULT = 2.0
@@ -230,12 +237,19 @@ class SRTrainer:
         self.dzr, self.dzf_d, self.dzf_g = e(ls), e(ls), e(ls)
         self.dgen = e((N, H, W, 3))
         self.loss = torch.zeros(7, dtype=torch.float32, device=device)
-        self.content = ContentLoss(vgg, N, H, W, device) if vgg is not None else None
+        dev = torch.device(device)
+        ov = SR_OVERLAP and dev.type == "cuda" and H * W >= SR_OVERLAP_MIN_PIXELS
+        self.content = ContentLoss(vgg, N, H, W, device, split=ov) if vgg is not None else None
         wsb = [self.Gp.ws_bytes, self.Dp.ws_bytes, ops.gan_loss_workspace_bytes()]
         if self.content:
             wsb.append(self.content.ws_bytes)
         self.ws = ops.Workspace(device)
         self.ws.get(max(wsb))
+        self.side = None
+        if ov:
+            self.side = torch.cuda.Stream(device=dev)
+            self.ws_side = ops.Workspace(device)
+            self.ws_side.get(max(self.Dp.ws_bytes, self.content.tws_bytes if self.content else 0))
 
     @property
     def gen_output(self):
@@ -249,8 +263,26 @@ class SRTrainer:
         ws = self.ws
         Gp, Dp = self.Gp, self.Dp
         # ---- forward (train_srgan.py:76-80) ---------------------------------
+        # (the target's VGG19 features and D(real) beside G's forward once the frozen VGG19's
+        # shared weight planes are settled; D(fake) follows D(real) on the joined stream -- the
+        # two slots of D's plan share its per-plan state)
+        main = torch.cuda.current_stream() if self.side is not None else None
+        ov = (self.side is not None and not ops.profiling() and
+              (self.content is None or self.content.settled()))
+        zr = None
+        if ov:
+            self.side.wait_stream(main)
+            with torch.cuda.stream(self.side):
+                if self.content is not None:
+                    self.content.forward_target(y, ws=self.ws_side)
+                zr = Dp.forward(y, slot=0, training=True, ws=self.ws_side)
+        elif self.content is not None and self.content.split:
+            self.content.forward_target(y, ws=ws)
         gen = Gp.forward(x, slot=0, training=True, ws=ws)
-        zr = Dp.forward(y, slot=0, training=True, ws=ws)
+        if ov:
+            main.wait_stream(self.side)
+        else:
+            zr = Dp.forward(y, slot=0, training=True, ws=ws)
         zf = Dp.forward(gen, slot=1, training=True, ws=ws)
         content = None
         if self.content is not None:
@@ -287,6 +319,8 @@ class SRTrainer:
             ops.check_finite(self.G.arena.grad, self.ls_g)
             ops.check_finite(self.D.arena.grad, self.ls_d)
         # ---- apply_gradients (train_srgan.py:113-114) -----------------------
+        if self.content is not None and self.content.split:
+            self.content.mark_settled()
         if apply:
             scale = sync.grad_scale if sync else 1.0
             apply_adam(self.G.arena, self.g_opt, scale, self.ls_g)
