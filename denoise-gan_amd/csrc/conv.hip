@@ -1532,22 +1532,28 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     // input gradients of G / D) where the implicit-GEMM fp16x3 plan applies (32-channel chunks)
     const bool hx3p = x3_gen && pl.x6 == 1 && h22 && pl.K % 128 == 0 && 4.0 * ra * ca < 2.0e9 &&
                       4.0 * rb * cb < 2.0e9 && !plan_off("x3h2");
-    if ((pl.x6 == 1 && (h33 || h22 || h44) || hf16) && !plan_off("halo")) {
+    // fp16x3 stride-1 4x4 (the PatchGAN's 512-channel conv, forward and input gradient) on the
+    // halo kernel: 11 x 19 halo, BN 64 (72.4 KB, two blocks per CU) -- full step 982 vs 972 img/s
+    // on the implicit-GEMM fp16x3 tiles (profiles/r5/ab_x3h_kt4.txt; DG_PLAN_DISABLE=x3h4)
+    const bool f44 = mode == MODE_FWD && g.kh == 4 && g.kw == 4 && g.sh == 1 && g.sw == 1;
+    const bool hx3q = x3_gen && pl.x6 == 1 && (h44 || f44) && pl.K % 512 == 0 && 4.0 * ra * ca < 2.0e9 &&
+                      4.0 * rb * cb < 2.0e9 && !plan_off("x3h4");
+    if ((pl.x6 == 1 && (h33 || h22 || h44 || hx3q) || hf16) && !plan_off("halo")) {
         // each input pixel staged once per channel chunk instead of once per tap
-        const int ntap = h33 ? 9 : (h44 ? 16 : 4);
-        const int bkc = (pl.x6 == 2 || hx3 || hx3p) ? 32 : 16;   // channels per chunk
+        const int ntap = h33 ? 9 : (h44 || f44 ? 16 : 4);
+        const int bkc = (pl.x6 == 2 || hx3 || hx3p || hx3q) ? 32 : 16;   // channels per chunk
         int Hout, Wout;
         if (mode == MODE_FWD) { Hout = g.Ho; Wout = g.Wo; }
         else if (h33 || h44) { Hout = g.H; Wout = g.W; }
         else { Hout = (g.H + 1) / 2; Wout = (g.W + 1) / 2; }   // phase 0's grid, the largest
-        pl.halo = h33 ? 1 : (h44 ? 4 : 2);
+        pl.halo = h33 ? 1 : (h44 || f44 ? 4 : 2);
         pl.htx = (Wout + 15) / 16;
         pl.hty = (Hout + 7) / 8;
         // (4x4: BN 128 needs 93 KB of LDS -- one block per CU -- and measured 0.685 vs
         // 0.666 ms for BN 64, which keeps two)
         // (32 output columns, 3x3: BN 32 -- the SR family's 32-channel layers; a 64-wide tile
         // spends half its MFMAs on zero columns there)
-        pl.cfg = pl.N > 64 && !h44 ? 128 : (h33 && pl.N <= 32 && !plan_off("halo32") ? 32 : 64);
+        pl.cfg = pl.N > 64 && !h44 && !f44 ? 128 : (h33 && pl.N <= 32 && !plan_off("halo32") ? 32 : 64);
         pl.mtiles = g.N * pl.htx * pl.hty;
         // (same-box A/B of the target: 256 -0.2%, 1024 -0.8% full step vs 512)
         long target = 512;
@@ -1568,7 +1574,7 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         const long cps = (nch + splits - 1) / splits;
         pl.kchunk = (int)(cps * bkc * ntap);
         pl.splits = (int)((nch + cps - 1) / cps);
-        if (hx3 || hx3p) pl.x6 = 3;
+        if (hx3 || hx3p || hx3q) pl.x6 = 3;
         // fp16x3 plans with more patches than resident blocks (2 per CU): each block runs
         // several patches back to back, the next patch's halo and weights fetched under the
         // current patch's MFMAs, so a block waits for HBM once instead of once per patch.
@@ -1579,7 +1585,7 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         // 512, so ~2048 there (profiles/r5/ab_x3h_persistent.txt)
         // (DG_X3H_PTILES: patches per block, DG_X3H_PDIV: the block target, for same-box A/B)
         pl.ptiles = 1;
-        if ((hx3 || hx3p) && pl.splits == 1) {
+        if ((hx3 || hx3p || hx3q) && pl.splits == 1) {
             const long tot = (long)pl.mtiles * pl.ntiles * pl.nphase;
             long pdiv = hx3p || nch <= 4 ? 512 : 2048;
             if (const char *e = getenv("DG_X3H_PDIV")) pdiv = std::max(1L, atol(e));
@@ -2084,7 +2090,7 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
         if (pl.halo) {
             // (persistent blocks: patch row mt0 + j * gm, j < ptiles, of each of the gm * ntiles blocks)
             grid.x = (unsigned)((pl.mtiles + a.ptiles - 1) / a.ptiles * pl.ntiles);
-            launch_gemm_x6h(mode, pl.cfg, pl.halo == 2 ? 2 : 3, grid, a, pl.htx, pl.hty, s, 4);
+            launch_gemm_x6h(mode, pl.cfg, pl.halo == 2 ? 2 : (pl.halo == 4 ? 4 : 3), grid, a, pl.htx, pl.hty, s, 4);
             DG_LAUNCHED("conv_gemm_x3h");
         } else {
             fastdiv_magic((unsigned)a.g.Wo, a.mg_wo, a.sh_wo);

@@ -364,7 +364,8 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
 void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t s);
 // the halo-tiled bf16x6 kernel (conv_x6h.hip): kt 3 = stride-1 3x3 FWD / DGRAD, kt 2 = the
 // sub-pixel phases of a stride-2 4x4 DGRAD (grid y = phase * splits + split); bn = 64 | 128.
-// ni 3 bf16x6, 2 fp16 (DG_MATH_FP16), 4 fp16x3 (DG_MATH_F16X3 forward, kt 3, bn 64 | 128).
+// ni 3 bf16x6, 2 fp16 (DG_MATH_FP16), 4 fp16x3 (kt 3, bn 64 | 128; kt 2 phases; kt 4 stride-1 4x4
+// forward / input gradient, bn 64).
 // a.pidx != NULL selects the fused max-pool epilogue (FWD, one split, output Ho % 8 == 0, Wo % 16 == 0)
 void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int tiles_x, int tiles_y, hipStream_t s,
                      int ni = 3);

@@ -192,9 +192,9 @@ __global__ void __launch_bounds__(256, 2)
 k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "forward or input gradient");
     static_assert(!POOL || MODE == MODE_FWD, "the pool epilogue is a forward epilogue");
-    static_assert(KT == 3 || (KT != 3 && MODE == MODE_DGRAD),
-                  "3x3 stride 1, or a stride-1 4x4 / stride-2 4x4-phase input gradient");
-    static_assert(NI == 3 || (NI == 2 && KT == 3 && !POOL) || (NI == 4 && (KT == 3 || (KT == 2 && MODE == MODE_DGRAD))),
+    static_assert(KT == 3 || MODE == MODE_DGRAD || (KT == 4 && NI == 4),
+                  "3x3 stride 1, a stride-1 4x4 / stride-2 4x4-phase input gradient, or an fp16x3 4x4 stride-1 forward");
+    static_assert(NI == 3 || (NI == 2 && KT == 3 && !POOL) || (NI == 4 && (KT == 3 || KT == 4 || (KT == 2 && MODE == MODE_DGRAD))),
                   "fp16: 3x3 stride 1, no pool epilogue; fp16x3: 3x3 stride 1, or the stride-2 4x4 input-gradient phases");
     constexpr bool X3 = NI == 4;
     constexpr int NPL = NI == 3 ? 3 : (X3 ? 4 : 2);   // plane images per chunk
@@ -210,7 +210,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     constexpr int NB = X3 ? ((KT == 3 && BN == 64) ? 3 : 2) : (NTAP % 3 == 0 ? 3 : 4);
 #endif
     constexpr bool XPAR = X3 && NB == 2;   // buffers alternate by K-tile parity (NTAP odd: across chunks)
-    static_assert(X3 || NTAP % NB == 0, "tap positions line up with the weight buffers across chunks");
+    static_assert(XPAR || NTAP % NB == 0, "tap positions line up with the weight buffers across chunks");
     constexpr int BK = NI == 3 ? 16 : 32, NW = 4;   // channels per chunk
     constexpr int WTM = 64, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
     constexpr bool B_KC = MODE == MODE_DGRAD;
@@ -713,7 +713,10 @@ void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int
 #define DG_X3H(B_, P_) hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_FWD, B_, P_, 3, 4>), grid, blk, 0, s, a, tiles_x, tiles_y)
     // (bn 32: the SR discriminators' / FastSRGAN's 32-channel 3x3 layers, stride 1; a
     // 64-wide tile computes half zeros there)
-    if (ni == 4 && mode == MODE_DGRAD && kt == 2) {   // fp16x3 stride-2 4x4 input-gradient phases (bn 64 | 128)
+    if (ni == 4 && kt == 4) {   // fp16x3 stride-1 4x4 forward / input gradient (BN 64)
+        if (mode == MODE_FWD) hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_FWD, 64, false, 4, 4>), grid, blk, 0, s, a, tiles_x, tiles_y);
+        else hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_DGRAD, 64, false, 4, 4>), grid, blk, 0, s, a, tiles_x, tiles_y);
+    } else if (ni == 4 && mode == MODE_DGRAD && kt == 2) {   // fp16x3 stride-2 4x4 input-gradient phases (bn 64 | 128)
         if (bn == 128) hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_DGRAD, 128, false, 2, 4>), grid, blk, 0, s, a, tiles_x, tiles_y);
         else hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_DGRAD, 64, false, 2, 4>), grid, blk, 0, s, a, tiles_x, tiles_y);
     } else if (ni == 4 && mode == MODE_DGRAD) {   // fp16x3 input gradient (3x3 stride 1, bn 64 | 128)

@@ -51,6 +51,10 @@ X3_CASES = [
     ("x3.deep", 4, 4, 4, 512, 512, 4, 2, "same", False, False),
     ("x3.deep.up", 4, 2, 2, 1024, 512, 4, 2, "same", True, False),
     ("x3.patch", 2, 18, 21, 64, 128, 4, 1, (1, 1, 1, 1), False, False),
+    # the PatchGAN's stride-1 4x4 on the fp16x3 halo kernel (KT 4, forward and input gradient):
+    # 'valid' on a zero-padded map as pix2pix.py:205-208 builds it, 8 channel chunks, ragged
+    # patches, Cout 96 (a ragged BN 64 column block)
+    ("x3.patch.valid", 2, 34, 27, 256, 96, 4, 1, "valid", False, True),
 ]
 
 
@@ -91,7 +95,7 @@ def test_x3_layer_at_operand_scales(case, xs, gs, monkeypatch):
 # edge patches, Cout 48, the 4x4 stride-2 input-gradient / ConvT-forward phases -- at the
 # same fp64 bar (the planner applies it only to grids of >= 1024 patches, beyond these sizes)
 X3_PERS_CASES = [(c, pt) for c in (X3_CASES[0], X3_CASES[1], X3_CASES[2], X3_CASES[4], X3_CASES[5],
-                                   X3_CASES[6], X3_CASES[7], X3_CASES[8])
+                                   X3_CASES[6], X3_CASES[7], X3_CASES[8], X3_CASES[12], X3_CASES[13])
                  for pt in (3, 5)]
 
 
