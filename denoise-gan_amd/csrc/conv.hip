@@ -1315,10 +1315,11 @@ static bool plan_off(const char *feature) {
     return false;
 }
 
-static double choose_tiles(OpPlan &pl, const TileCfg *cfgs, int ncfg, double peak, const char *force_env, void *) {
+static double choose_tiles(OpPlan &pl, const TileCfg *cfgs, int ncfg, double peak, const char *force_env,
+                           int rule = -1) {
     const double cu_flops = peak / 256.0;
     static const double occ_eff[] = {0.0, 0.62, 0.80, 0.88, 0.92};
-    int forced = -1;
+    int forced = rule;   // (a measured per-shape rule of the caller; the environment overrides it)
     if (const char *f = getenv(force_env)) forced = atoi(f);
     // DG_FORCE_SPLITS: split-K count for sweeps (scripts/diag/deep_sweep.py); unset in production
     long fsplits = 0;
@@ -1443,7 +1444,7 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     }
     // Tile + split-K choice: the cheaper of the fp32 kernel and (math mode
     // BF16X6, eligible shapes) the bf16x6 kernel plus its two split passes.
-    double t32 = choose_tiles(pl, kCfgs, kNumCfgs, 157.3e12, "DG_FORCE_CFG", nullptr);
+    double t32 = choose_tiles(pl, kCfgs, kNumCfgs, 157.3e12, "DG_FORCE_CFG");
     int x6_ok = 0;
     long ra = 0, ca = 0, rb = 0, cb = 0;
     if (mode == MODE_FWD) {
@@ -1477,7 +1478,7 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
                          (mode == MODE_WGRAD && g.Ci % 32 == 0 && g.Co % 32 == 0));
     if (x6_ok) {
         OpPlan p6 = pl;
-        double t6 = choose_tiles(p6, kX6Cfgs, kNumX6Cfgs, 2516.6e12 / 6.0, "DG_FORCE_X6CFG", nullptr);
+        double t6 = choose_tiles(p6, kX6Cfgs, kNumX6Cfgs, 2516.6e12 / 6.0, "DG_FORCE_X6CFG");
         t6 += (double)(ra * ca + rb * cb) * 10.0 / 4.0e12 + 4e-6;  // split passes: read 4 B, write 6 B
         // (the implicit-GEMM fp16x3 ops where the split path beats the fp32 tiles at all: on
         // pix2pix's deepest layers (M 32..128 rows) the fp32 tiles win; DG_FORCE_X3: every
@@ -1500,12 +1501,12 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         ok = ok && 2.0 * ra * ca < 2.0e9 && 2.0 * rb * cb < 2.0e9 && g.kh * g.kw <= 32;
         if (ok) {
             pl.x6 = 0;
-            choose_tiles(pl, kF16Cfgs, kNumF16Cfgs, 2516.6e12, "DG_FORCE_F16CFG", nullptr);
+            choose_tiles(pl, kF16Cfgs, kNumF16Cfgs, 2516.6e12, "DG_FORCE_F16CFG");
             pl.x6 = 2;
             pl.x6_ra = ra; pl.x6_ca = (int)ca; pl.x6_rb = rb; pl.x6_cb = (int)cb;
         }
     }
-    if (!pl.x6) choose_tiles(pl, kCfgs, kNumCfgs, 157.3e12, "DG_FORCE_CFG", nullptr);
+    if (!pl.x6) choose_tiles(pl, kCfgs, kNumCfgs, 157.3e12, "DG_FORCE_CFG");
     // halo-tiled kernel: 3x3 stride-1 FWD / DGRAD (kt 3), and the sub-pixel
     // phases of a 4x4 stride-2 DGRAD (kt 2: ConvT forwards, down-block input gradients)
     const bool h33 = (mode == MODE_FWD || mode == MODE_DGRAD) && g.kh == 3 && g.kw == 3 && g.sh == 1 && g.sw == 1 &&
@@ -1596,7 +1597,15 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     }
     if (x3_gen && pl.x6 == 1 && 4.0 * ra * ca < 2.0e9 && 4.0 * rb * cb < 2.0e9) {
         pl.halo = 0; pl.htx = pl.hty = 0;
-        choose_tiles(pl, kX3Cfgs, kNumX3Cfgs, 2516.6e12 / 3.0, "DG_FORCE_X3CFG", nullptr);
+        // short-K forward / input-gradient GEMMs (K = 16 taps x 64..128 channels: G / D down2-3
+        // forwards, the up6 / up7 input gradients): the 64 x 128 tile at K 1024 and 128 x 128 at
+        // K 2048 -- the MFMA-time model's 128 x 256 pick loses there to its prologue / epilogue
+        // share (bs32 sweep: up7 bwd_data 0.406 -> 0.323 ms, D down2 fwd 0.238 -> 0.210, G down3
+        // fwd 0.182 -> 0.167, up6 bwd_data 0.282 -> 0.263; profiles/r5/x3cfg_sweep.txt;
+        // DG_PLAN_DISABLE=x3shortk: the model's pick)
+        const int rule = mode == MODE_WGRAD || pl.N <= 64 || plan_off("x3shortk") ? -1
+                         : (pl.K <= 1024 ? 2 : (pl.K <= 2048 ? 0 : -1));
+        choose_tiles(pl, kX3Cfgs, kNumX3Cfgs, 2516.6e12 / 3.0, "DG_FORCE_X3CFG", rule);
         pl.x6 = 3;
     }
     pl.vec = pl.x6 ? 1 : cfg_vec(g, mode, kCfgs[pl.cfg].bk);

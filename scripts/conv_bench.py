@@ -13,6 +13,7 @@ import torch  # noqa: E402
 from dgan.ops import ConvDesc, Workspace  # noqa: E402
 
 B = int(os.environ.get("DG_BS", "16"))
+MATH = os.environ.get("DG_MATH")   # conv arithmetic ("f16x3", "bf16x6", ...); unset: the planner's default
 # (name, H, W, Cin, Cout, k, s, pad, transpose, calls fwd, bwd_data, bwd_filter per train step)
 LAYERS = [
     ("G.down1", 256, 256, 3, 64, 4, 2, "same", False, (2, 0, 2)),
@@ -59,7 +60,7 @@ def main():
     for name, H, W, ci, co, k, s, pad, tr, calls in LAYERS:
         if only and name not in only.split(","):
             continue
-        d = ConvDesc(B, H, W, ci, co, k, s, pad, tr)
+        d = ConvDesc(B, H, W, ci, co, k, s, pad, tr, **({"math": MATH} if MATH else {}))
         x = torch.randn(B, H, W, ci, device=dev)
         w = torch.randn(*d.weight_shape, device=dev) * 0.02
         y = torch.empty(d.out_shape, device=dev)
