@@ -187,11 +187,14 @@ def main():
     x_np, y_np = synthetic_batch(wl, batch, seed=1000 + rank)
     x = torch.from_numpy(x_np).to(dev)
     y = torch.from_numpy(y_np).to(dev)
-    # N=1: the step is captured once into a HIP graph and replayed (eager
-    # launches if capture fails).  N>1 launches eagerly: measured at N=1, eager
-    # runs at the graph's rate (598.7 vs 599.0 img/s), so no rank needs to rely
-    # on multi-rank RCCL graph capture (a world-size-1 RCCL group does capture)
-    use_graph = not args.no_graph and world == 1
+    # The step is captured once into a HIP graph and replayed, at every N: with the five-stream
+    # step of round 5 eager launches lost 3.7 % at world 1 through RCCL (939 / 941 vs 974 / 977
+    # img/s, profiles/r6/dist_graph_eager.txt).  The captured all-reduces go to a capture-only
+    # process group (dgan.dist.capture_group).  Every rank must take the same path: the ranks
+    # agree on the capture's success (an all-reduce MIN on the default group) and all fall back
+    # to eager launches if any rank's capture failed.  (A gloo rehearsal, DG_DIST_BACKEND=gloo, has
+    # no capturable collectives: eager at N>1.)
+    use_graph = not args.no_graph and (world == 1 or os.environ.get("DG_DIST_BACKEND", "nccl") == "nccl")
 
     def trainer_of(model):
         return model.trainer(x.shape) if args.model == "pix2pix" else model.trainer(x.shape, y.shape)
@@ -235,6 +238,15 @@ def main():
             except Exception as e:  # report, fall back to eager launches
                 print(f"[bench] graph capture failed ({e}); eager launches", file=sys.stderr)
                 graph = None
+            if distributed and world > 1:
+                ok = torch.tensor([1 if graph is not None else 0], dtype=torch.int32, device=dev)
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+                if int(ok.item()) == 0 and graph is not None:
+                    print("[bench] another rank's capture failed; eager launches on every rank", file=sys.stderr)
+                    graph = None
+        check = None
+        if graph is not None:
+            check = graph_vs_eager(trainer, graph, x, y, strict=world == 1)
 
         def step():
             if graph is not None:
@@ -260,10 +272,12 @@ def main():
             t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
+        measure.check = check
         return model, trainer, graph, elapsed
 
     content = not args.no_content
     model, trainer, graph, elapsed = measure(content)
+    graph_check = measure.check
     hip_graph = graph is not None
     conv_math = "fp16" if fp16 else ("bf16x6" if ops.default_conv_math() == ops.MATH_BF16X6 else "fp32")
     if not fp16 and args.model != "pix2pix" and content:
@@ -400,6 +414,7 @@ def main():
                        "conv_gflop_per_image": round(step_flops / batch / 1e9, 2) if step_flops else None},
             "lib": _lib_build_info(),
             "losses": [round(float(v), 6) for v in losses],
+            "graph_equals_eager": graph_check,
             "core": core,
             "fp32_exact": twin,
             "roofline": roofline,
@@ -408,6 +423,34 @@ def main():
         print(json.dumps(out), file=json_out, flush=True)
     if distributed:
         dist.destroy_process_group()
+
+
+def graph_vs_eager(trainer, graph, x, y, strict=True):
+    """The timed work is the tested work: from one snapshot of every tensor the step carries
+    (both networks' parameters, gradients, Adam slots and counters, BN moving statistics, the
+    losses), one eager step and one replay of the captured graph must end bit-identical.  The
+    eager step is the launch sequence the -m gpu parity tests check against the fp64 oracle.
+    strict (N=1): a difference ends the run; N>1: reported (the eager and the captured
+    all-reduces run on two RCCL communicators).  The snapshot is restored afterwards."""
+    from dgan.trainer import restore, snapshot, state_diff
+    torch.cuda.synchronize()
+    s0 = snapshot(trainer)
+    trainer.step(x, y)
+    eager = snapshot(trainer)
+    restore(trainer, s0)
+    graph.replay()
+    replay = snapshot(trainer)
+    torch.cuda.synchronize()
+    bad = state_diff(eager, replay)
+    restore(trainer, s0)
+    torch.cuda.synchronize()
+    if bad and strict:
+        sys.exit(f"bench.py: the graph replay differs from the eager step in {bad[:8]} ({len(bad)} tensors)")
+    if bad:
+        print(f"[bench] graph replay != eager step in {len(bad)} tensors: {bad[:8]}", file=sys.stderr)
+    return {"equal": not bad, "tensors": len(eager), "differing": bad[:8],
+            "what": "one eager step and one graph replay from the same snapshot of parameters, gradients, Adam "
+                    "slots, iteration counters, BN moving statistics and losses (G and D)"}
 
 
 def _lib_build_info():

@@ -2419,6 +2419,14 @@ int dg_weight_bound(const float *w, int64_t K, int Co, const float *bias, float 
     return DG_OK;
 }
 
+int dg_weight_bound_in(const float *w, int taps, int Ci, int Co, float *g_out, dg_stream_t stream) {
+    DG_ARG(w && g_out, "NULL tensor");
+    DG_ARG(taps > 0 && Ci > 0 && Co > 0, "bad shape");
+    dg::launch_weight_bound_in(w, taps, Ci, Co, g_out, (hipStream_t)stream);
+    DG_LAUNCHED("weight_bound_in");
+    return DG_OK;
+}
+
 int dg_conv_set_grad_scale(dg_conv_t d, const float *dy_m, const float *dy_g, const float *dx_m, const float *dx_g,
                            float *dx_max) {
     DG_ARG(d != nullptr, "descriptor is NULL");

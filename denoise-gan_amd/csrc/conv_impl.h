@@ -381,6 +381,9 @@ void launch_absmax(const float *x, long rows, int C, int ld, float *out, hipStre
 // max over columns of sum_k |w[k][co]| into gout[0], max |bias| into cout[0] (dg_weight_bound)
 void launch_weight_bound(const float *w, long K, int Co, const float *bias, float *gout, float *cout, hipStream_t s,
                          float *zero8 = nullptr);
+// max over input channels of sum over taps and output channels of |w[tap][ci][co]| into gout[0]
+// (dg_weight_bound_in)
+void launch_weight_bound_in(const float *w, int taps, int Ci, int Co, float *gout, hipStream_t s);
 // the fp16 conv math (DG_MATH_FP16): one fp16 plane [rows][C] and its GEMM (kF16Cfgs)
 void launch_split_f16(const float *src, int ld, long rows, int C, void *dst, hipStream_t s);
 void launch_split_f16_pair(const float *a, int lda, long ra, int ca, void *da, const float *b, int ldb, long rb,

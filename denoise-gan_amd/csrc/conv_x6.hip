@@ -748,9 +748,92 @@ __global__ void __launch_bounds__(256) k_weight_bound(const float *__restrict__ 
     }
 }
 
+// The same bound over a large kernel (the frozen VGG19's 3x3 layers, once per weight version:
+// up to 627 us as one workgroup): workgroup b sums the 16 columns 16b.. over all K rows (16 row
+// lanes per column, four loads in flight, the lanes combined in a fixed order), and its max goes
+// to gout[0] by an integer atomicMax -- non-negative floats order as their bits, so the result is
+// exact and independent of the order the workgroups finish in.  gout[0] is zeroed before the launch
+// (launch_weight_bound); workgroup 0 also writes cout and zeroes zero8.
+__global__ void __launch_bounds__(256) k_weight_bound_cols(const float *__restrict__ w, long K, int Co,
+                                                          const float *__restrict__ bias, float *gout, float *cout,
+                                                          float *zero8) {
+    __shared__ float red[256];
+    if (blockIdx.x == 0 && zero8 && threadIdx.x < X3_SHARDS) zero8[threadIdx.x] = 0.f;
+    const int cl = threadIdx.x & 15, rl = threadIdx.x >> 4;
+    const int co = blockIdx.x * 16 + cl;
+    float sum = 0.f;
+    if (co < Co) {
+        long k = rl;
+        for (; k + 48 < K; k += 64) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = w[(k + 16 * u) * Co + co];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) sum += fabsf(v[u]);
+        }
+        for (; k < K; k += 16) sum += fabsf(w[k * Co + co]);
+    }
+    red[threadIdx.x] = sum;
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        float s = 0.f;
+        for (int r = 0; r < 16; ++r) s += red[16 * r + threadIdx.x];
+        red[threadIdx.x] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float g = 0.f;
+        for (int i = 0; i < 16; ++i) g = fmaxf(g, red[i]);
+        atomicMax(reinterpret_cast<unsigned *>(gout), __float_as_uint(g));
+        if (blockIdx.x == 0 && cout) {
+            float c = 0.f;
+            if (bias)
+                for (int i = 0; i < Co; ++i) c = fmaxf(c, fabsf(bias[i]));
+            cout[0] = c;
+        }
+    }
+}
+
+// The input-gradient bound of a conv (dg_weight_bound_in): gout[0] = max over input channels ci of
+// sum over taps and output channels of |w[tap][ci][co]| (HWIO), >= max |dx| / max |dy|.  One
+// workgroup per ci, a fixed-order LDS tree per workgroup, the workgroups' maxima by integer
+// atomicMax into gout[0] (zeroed before the launch).
+__global__ void __launch_bounds__(256) k_weight_bound_in(const float *__restrict__ w, int taps, int Ci, int Co,
+                                                        float *gout) {
+    __shared__ float red[256];
+    const int ci = blockIdx.x;
+    float s = 0.f;
+    for (int t = 0; t < taps; ++t) {
+        const float *row = w + ((long)t * Ci + ci) * Co;
+        for (int co = threadIdx.x; co < Co; co += 256) s += fabsf(row[co]);
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+#pragma unroll
+    for (int h = 128; h > 0; h >>= 1) {
+        if (threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicMax(reinterpret_cast<unsigned *>(gout), __float_as_uint(red[0]));
+}
+
+// one workgroup while the kernel is small (the trainable down1 layers' per-step bounds: K 48 / 96,
+// Co 64 -- a memset node would cost more than the read), the column-parallel form beyond
+constexpr long WBOUND_ONE_BLOCK_MAX = 1 << 16;
+
 void launch_weight_bound(const float *w, long K, int Co, const float *bias, float *gout, float *cout, hipStream_t s,
                          float *zero8) {
-    hipLaunchKernelGGL(k_weight_bound, dim3(1), dim3(256), 0, s, w, K, Co, bias, gout, cout, zero8);
+    if (K * Co <= WBOUND_ONE_BLOCK_MAX) {
+        hipLaunchKernelGGL(k_weight_bound, dim3(1), dim3(256), 0, s, w, K, Co, bias, gout, cout, zero8);
+        return;
+    }
+    hipMemsetAsync(gout, 0, sizeof(float), s);
+    hipLaunchKernelGGL(k_weight_bound_cols, dim3((Co + 15) / 16), dim3(256), 0, s, w, K, Co, bias, gout, cout, zero8);
+}
+
+void launch_weight_bound_in(const float *w, int taps, int Ci, int Co, float *gout, hipStream_t s) {
+    hipMemsetAsync(gout, 0, sizeof(float), s);
+    hipLaunchKernelGGL(k_weight_bound_in, dim3(Ci), dim3(256), 0, s, w, taps, Ci, Co, gout);
 }
 
 void launch_absmax(const float *x, long rows, int C, int ld, float *out, hipStream_t s) {

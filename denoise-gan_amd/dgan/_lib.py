@@ -125,6 +125,7 @@ _SIGS = {
     "dg_absmax": (c_int, [_P, ctypes.c_int64, c_int, c_int, _P, _P]),
     "dg_absmax_set": (c_int, [_P, ctypes.c_int64, c_int, c_int, _P, _P]),
     "dg_weight_bound": (c_int, [_P, ctypes.c_int64, c_int, _P, _P, _P, _P, _P]),
+    "dg_weight_bound_in": (c_int, [_P, c_int, c_int, c_int, _P, _P]),
     "dg_conv_set_act_scale": (c_int, [c_void_p, _P, _P, _P, _P, _P, _P, _P]),
     "dg_upsample2_relu_fwd": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P]),
     "dg_upsample2_relu_bwd": (c_int, [c_int, c_int, c_int, c_int, _P, c_int, _P, c_int, _P, c_int, c_float, _P]),

@@ -598,14 +598,22 @@ class GraphPlan:
         # output| (the consumer's input) in the same epilogue.  Every other fp16x3 x operand is
         # measured by the op that splits it (a plain max slot).  VGG19's activations (a
         # preprocessed image of +-128 onwards) thus keep 22 bits down to 2^-17 of each bound.
+        # The measured maxima are per slot (amax[slot]): a slot's forward re-measures them, and its
+        # kept x planes must be read back (bwd_filter) with the scale of the slot that wrote them --
+        # D(real) and D(fake) of the SR discriminator are two slots of one plan whose inputs may
+        # sit in different binades.  The descriptors are shared by the slots, so each slot's scale
+        # context is set on them before that slot's forward and backward (_use_act_slot; host-side
+        # pointers, baked into the launches).
         self.act_feeds = {}      # producer conv idx -> (consumer conv node, unfused pool node or None)
         self.act_measure = []    # convs whose input max is measured before them (input not a conv's output)
-        self.pool_scale = {}     # unfused maxpool node idx -> scale source of the planes it writes
+        self.pool_scale = [dict() for _ in range(slots)]   # unfused maxpool idx -> its planes' scale source
         self.amax = self.awb = None
         self._awb_ver = None
+        self._act_ctx = None     # per slot: [(desc, x source, y source, y_max)]
+        self._act_slot = None
         if alias is None and any(self.desc[n.idx].plane_format(ops.TENSOR_X) == ops.PLANES_F16X3 for n in conv_nodes):
             ci = {n.idx: i for i, n in enumerate(conv_nodes)}
-            self.amax = torch.zeros(len(conv_nodes), 8, dtype=torch.float32, device=device)
+            self.amax = torch.zeros(slots, len(conv_nodes), 8, dtype=torch.float32, device=device)
             self.awb = torch.zeros(len(conv_nodes), 2, dtype=torch.float32, device=device)
             feeds = {}   # producer conv idx -> (consumer conv, unfused pool or None, planes it writes or None)
             for n in conv_nodes:
@@ -625,32 +633,34 @@ class GraphPlan:
                               if buf is not None and buf.fmt == ops.PLANES_F16X3}
             producer = {c.idx: i for i, (c, _, _) in feeds.items()}
 
-            def ysrc(n):
+            def ysrc(n, k):
                 i = ci[n.idx]
-                return (self.amax[i], self.awb[i, 0:1], self.awb[i, 1:2] if n.attrs["bias"] else None)
+                return (self.amax[k, i], self.awb[i, 0:1], self.awb[i, 1:2] if n.attrs["bias"] else None)
 
-            ctx = {n.idx: [None, None, None] for n in conv_nodes}   # x source, y source, y_max
-            for i, (c, m) in self.act_feeds.items():
-                n = nodes[i]
-                ctx[i][1] = ysrc(n)
-                if m is not None:
-                    self.pool_scale[m.idx] = ysrc(n)
+            for i in self.act_feeds:
                 # the producer's output bound needs max |its input|: measured by the epilogue of the
                 # conv producing that input (any arithmetic), else by an absmax pass before it
-                if i in producer:
-                    ctx[producer[i]][2] = self.amax[ci[i]]
-                else:
+                if i not in producer:
                     self.act_measure.append(i)
-            for n in conv_nodes:
-                if self.desc[n.idx].plane_format(ops.TENSOR_X) != ops.PLANES_F16X3:
-                    continue
-                p = producer.get(n.idx)
-                ctx[n.idx][0] = ysrc(nodes[p]) if p in self.act_feeds else (self.amax[ci[n.idx]],)
-            for n in conv_nodes:
-                x, y, ymax = ctx[n.idx]
-                if x is not None or y is not None or ymax is not None:
-                    self.desc[n.idx].set_act_scale(x=x, y=y, y_max=ymax)
+            self._act_ctx = []
+            for k in range(slots):
+                ctx = {n.idx: [None, None, None] for n in conv_nodes}   # x source, y source, y_max
+                for i, (c, m) in self.act_feeds.items():
+                    n = nodes[i]
+                    ctx[i][1] = ysrc(n, k)
+                    if m is not None:
+                        self.pool_scale[k][m.idx] = ysrc(n, k)
+                    if i in producer:
+                        ctx[producer[i]][2] = self.amax[k, ci[i]]
+                for n in conv_nodes:
+                    if self.desc[n.idx].plane_format(ops.TENSOR_X) != ops.PLANES_F16X3:
+                        continue
+                    p = producer.get(n.idx)
+                    ctx[n.idx][0] = ysrc(nodes[p], k) if p in self.act_feeds else (self.amax[k, ci[n.idx]],)
+                self._act_ctx.append([(self.desc[i], x, y, ymax) for i, (x, y, ymax) in ctx.items()
+                                      if x is not None or y is not None or ymax is not None])
             self._act_ci = ci
+            self._use_act_slot(0)
         # ---- workspace ----
         ws = [0]
         for n in nodes[1:]:
@@ -665,6 +675,14 @@ class GraphPlan:
             elif n.kind == "dwconv":
                 ws.append(ops.dwconv3_workspace_bytes(*sx))
         self.ws_bytes = max(ws)
+
+    def _use_act_slot(self, slot):
+        """Point the shared descriptors' fp16x3 activation scale context at slot's sources."""
+        if self._act_ctx is None or self._act_slot == slot:
+            return
+        for d, x, y, ymax in self._act_ctx[slot]:
+            d.set_act_scale(x=x, y=y, y_max=ymax)
+        self._act_slot = slot
 
     def _alloc_set(self, nodes, shp):
         """tensor id -> NHWC view (graph input excluded: supplied per call)."""
@@ -747,6 +765,8 @@ class GraphPlan:
         # weight planes: re-split every forward, except for a frozen network
         # (VGG19 content loss) whose buffer holds the planes of the current weights
         frozen = getattr(A, "frozen", False)
+        if self.amax is not None:
+            self._use_act_slot(slot)
         if self.act_feeds:
             # fp16x3 activation scales: the output bounds' weight terms (frozen weights: once per
             # version) and this pass's measured maxima
@@ -758,7 +778,7 @@ class GraphPlan:
                                      bias=A.param(f"{n.name}/bias") if n.attrs["bias"] else None,
                                      c_out=self.awb[j, 1:2])
                 self._awb_ver = A.version
-            self.amax.zero_()
+            ops.fill(self.amax[slot], 0.0)
         if self.half_w:
             # every fp16 conv's weight copy of this network in one launch
             ops.to_f16(A.data, A.half)
@@ -793,7 +813,7 @@ class GraphPlan:
                 else:
                     P.invalidate((self._stale_w(P, frozen)) | (0 if fed else ops.TENSOR_X))
                 if n.idx in self.act_measure:
-                    ops.absmax(xin, self.amax[self._act_ci[n.idx]])   # (zeroed above)
+                    ops.absmax(xin, self.amax[slot, self._act_ci[n.idx]])   # (zeroed above)
                 mp = self.fused_conv.get(n.idx)
                 if mp is not None:
                     d.fwd_pool(xin, A.param(f"{n.name}/kernel"), self.pool_idx[slot][mp.idx], bias=bias,
@@ -834,7 +854,7 @@ class GraphPlan:
             elif k == "maxpool":
                 if n.idx not in self.fused_pool:   # (else done by its conv's epilogue)
                     ops.maxpool2_fwd(xin, y, planes_out=self.pool_out[slot].get(n.idx),
-                                     scale=self.pool_scale.get(n.idx))
+                                     scale=self.pool_scale[slot].get(n.idx))
             elif k == "upsample":
                 ops.upsample2_relu_fwd(xin, y)
             elif k == "dwconv":
@@ -865,10 +885,9 @@ class GraphPlan:
     # --------------------------------------------------------------- backward
     def _update_weight_bounds(self):
         """gwb[conv] = max over input channels of sum |w| over taps and output channels
-        (a bound of |dx| / max |dy| of the layer's input gradient)."""
+        (a bound of |dx| / max |dy| of the layer's input gradient; dg_weight_bound_in)."""
         for i, n in enumerate(m for m in self.g.nodes if m.kind == "conv"):
-            w = self.arena.param(f"{n.name}/kernel")   # HWIO
-            self.gwb[i:i + 1].copy_(w.abs().sum(dim=(0, 1, 3)).amax().reshape(1))
+            ops.weight_bound_in(self.arena.param(f"{n.name}/kernel"), self.gwb[i:i + 1])   # HWIO
 
     def _scratch(self, shape):
         N, H, W, C = shape
@@ -887,13 +906,15 @@ class GraphPlan:
         s = self.slots[slot]
         gr = dict(self.grad)
         gr[g.output.id] = dout
+        if self.amax is not None:
+            self._use_act_slot(slot)   # (the kept x planes of this slot: its scale sources)
         if getattr(self, "x3_convs", None):
             # fp16x3 input gradients: weight bounds (frozen weights: once per version), the
             # per-step max slots, and the measured max of the gradient entering the graph
             if not getattr(A, "frozen", False) or self._gwb_ver != A.version:   # (trainable: every step)
                 self._update_weight_bounds()
                 self._gwb_ver = A.version
-            self.gmax.zero_()
+            ops.fill(self.gmax, 0.0)
             if self.x3_top is not None:
                 i = [n.idx for n in g.nodes if n.kind == "conv"].index(self.x3_top.idx)
                 ops.absmax(dout, self.gmax[i])

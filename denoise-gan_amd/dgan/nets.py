@@ -643,8 +643,14 @@ class DiscriminatorPlan:
             # D.down1 (conv + LeakyReLU, no BN) writes D.down2's x planes in its epilogue
             if FEED_X and self.planes[1].x is not None:
                 self.planes[0].fwd_out = self.planes[1].x
-            self.planes_half = (ops.plan_planes(self.desc_half, device, keep_x=False,
-                                                wbufs=[p.w for p in self.planes])
+            # (the half-batch pass runs on another stream beside the full backward and reads its
+            # weight planes with no event wait: it shares a layer's buffer only when the full
+            # pass's FORWARD splits the weights -- ready before either backward is enqueued; a
+            # layer whose weights the full pass splits first in a backward op gets a buffer of its
+            # own, split by the half pass itself)
+            wshare = [p.w if (p.w is not None and d.plane_mask[ops.OP_FWD] & ops.TENSOR_W) else None
+                      for p, d in zip(self.planes, self.desc)]
+            self.planes_half = (ops.plan_planes(self.desc_half, device, keep_x=False, wbufs=wshare)
                                 if self.desc_half is not self.desc else self.planes)
             # one dy bound per layer for the full backward; the half-batch backward (the G path
             # through D(fake)) has its own bounds, dz and dy scratch, so the two backwards may run

@@ -594,6 +594,9 @@ def bn_fwd_train(y, gamma, beta, save_mean, save_invstd, moving_mean, moving_var
     -- a second tensor's planes into z_planes[0] at that column with the same scale (the
     U-Net skip half of a concatenation)."""
     if z_bound is not None or copy is not None:
+        if res is not None or f16_out is not None:
+            # (dg_bn_fwd_train_seg_x rejects a residual with a z bound; the fp16 copy is not routed)
+            raise DGError("bn_fwd_train: z_bound / copy cannot be combined with res or f16_out")
         return _bn_fwd_train_x(y, gamma, beta, save_mean, save_invstd, moving_mean, moving_var, z, act, alpha,
                                momentum, eps, drop_rate, drop_seed, step_dev, ws, z_planes, segments,
                                drop_seed_stride, z_bound, copy)
@@ -915,6 +918,13 @@ def weight_bound(w, g_out, bias=None, c_out=None, zero=None):
     max |bias| (dg_weight_bound): a conv output's bound terms; zero: 8 floats zeroed on the way."""
     Co = w.shape[-1]
     call("dg_weight_bound", _p(w), w.numel() // Co, Co, _p(bias), _p(g_out), _p(c_out), _p(zero), _stream())
+
+
+def weight_bound_in(w, g_out):
+    """g_out[0] = max over input channels of sum |w| over the taps and output channels (HWIO w,
+    dg_weight_bound_in): the weight term of an input gradient's bound."""
+    kh, kw, Ci, Co = w.shape
+    call("dg_weight_bound_in", _p(w), kh * kw, Ci, Co, _p(g_out), _stream())
 
 
 def upsample2_relu_fwd(x, z):

@@ -42,6 +42,45 @@ LOSS_NAMES = ("gen_total_loss", "gen_gan_loss", "gen_l1_loss", "gen_l2_loss", "c
               "var_loss", "identity_loss")
 
 
+def state_tensors(tr):
+    """name -> device tensor of everything a training step carries to the next one or returns:
+    both networks' parameter, gradient and Adam arenas and iteration counters, the BN moving
+    statistics, the loss vector and (mixed_float16) the loss-scale states.  Works on a
+    Pix2PixTrainer and on an SRTrainer (dgan.sr_trainer): for comparing two ways of running the
+    same step (graph replay vs eager launches, one stream vs several) from one starting state."""
+    nets = (("G", tr.gA, tr.G.bn), ("D", tr.dA, tr.D.bn)) if hasattr(tr, "gA") else \
+        (("G", tr.G.arena, tr.G.bn), ("D", tr.D.arena, tr.D.bn))
+    out = {}
+    for tag, A, bn in nets:
+        for k in ("data", "grad", "m", "v", "iterations"):
+            out[f"{tag}.{k}"] = getattr(A, k)
+        for k in bn.mean:
+            out[f"{tag}.bn.{k}.mean"] = bn.mean[k]
+            out[f"{tag}.bn.{k}.var"] = bn.var[k]
+    out["loss"] = tr.loss
+    for k in ("ls_g", "ls_d"):
+        if getattr(tr, k, None) is not None:
+            out[k] = getattr(tr, k)
+    return out
+
+
+def snapshot(tr):
+    """Copies of state_tensors(tr) (enqueued on the current stream)."""
+    return {k: t.clone() for k, t in state_tensors(tr).items()}
+
+
+def restore(tr, snap):
+    """Write a snapshot back into the trainer's own tensors (addresses unchanged: a captured
+    graph of the step stays valid)."""
+    for k, t in state_tensors(tr).items():
+        t.copy_(snap[k])
+
+
+def state_diff(a, b):
+    """Names whose tensors differ in any bit between two snapshots."""
+    return [k for k in a if not torch.equal(a[k], b[k])]
+
+
 class AdamConfig:
     def __init__(self, lr=2e-4, beta_1=0.5, beta_2=0.999, epsilon=1e-7):
         self.lr, self.beta_1, self.beta_2, self.epsilon = lr, beta_1, beta_2, epsilon
@@ -87,7 +126,10 @@ class Pix2PixTrainer:
         self.loss = torch.zeros(8, dtype=torch.float32, device=device)
         # VGG19 content loss (pix2pix.py:45-51, :87): frozen feature extractor on G(x) and y
         self.content = None
-        vsplit = OVERLAP and OVERLAP_VT
+        # (the split VGG19 plans also when the step runs on one stream -- profiling, DG_NO_OVERLAP --
+        # so the one-stream step runs the overlapped step's kernels: the two are bit-identical,
+        # tests/test_overlap_gpu.py)
+        vsplit = OVERLAP_VT
         if vgg is not None and self.weights[5] != 0.0:
             from .sr_trainer import ContentLoss
             self.content = ContentLoss(vgg, N, H, W, device, split=vsplit)
@@ -116,11 +158,16 @@ class Pix2PixTrainer:
         if self.side is not None and EARLY_ADAM:
             self.side3 = torch.cuda.Stream(device=device)
         self.side2 = None
-        if self.side is not None and OVERLAP_DH and self.content is not None and self.D.desc_g3 is not None:
-            self.side2 = torch.cuda.Stream(device=device)
-            self.ws_side2 = ops.Workspace(device)
-            self.ws_side2.get(self.D.ws_bytes)
+        # D(fake)'s input gradient into its own buffer, added to dL/dG(x) after the VGG19 backward
+        # -- on side2 beside that backward, or in sequence on one stream (the same additions in the
+        # same order either way)
+        self.dgen_d = None
+        if OVERLAP_DH and self.content is not None and self.D.desc_g3 is not None:
             self.dgen_d = e((N, H, W, 3))
+            if self.side is not None:
+                self.side2 = torch.cuda.Stream(device=device)
+                self.ws_side2 = ops.Workspace(device)
+                self.ws_side2.get(self.D.ws_bytes)
 
     @property
     def gen_output(self):
@@ -211,6 +258,11 @@ class Pix2PixTrainer:
                            ws=self.ws_side2, input_from=3)
             self.content.backward(dgen, beta=1.0, ws=ws)
             main.wait_stream(side2)
+            ops.accumulate(self.dgen_d, dgen, 1.0)
+        elif self.dgen_d is not None:   # (the same on one stream)
+            D.backward(self.dzf_g, half=1, param_grads=False, input_grad=self.dgen_d, input_beta=0.0, ws=ws,
+                       input_from=3)
+            self.content.backward(dgen, beta=1.0, ws=ws)
             ops.accumulate(self.dgen_d, dgen, 1.0)
         else:
             if D.desc_g3 is not None:   # dL/dG(x) += channels 3..5 of dL/d D([x, G(x)])

@@ -197,6 +197,10 @@ int dg_absmax_set(const float *x, int64_t rows, int C, int ld, float *out, dg_st
  * 8 floats zeroed on the way (the measured-max slot a following dg_absmax fills). */
 int dg_weight_bound(const float *w, int64_t K, int Co, const float *bias, float *g_out, float *c_out,
                     float *zero8, dg_stream_t stream);
+/* g_out[0] = max over input channels ci of sum over taps and output channels of |w[tap][ci][co]|
+ * (an HWIO kernel, taps = kh*kw): the weight term of an fp16x3 input gradient's bound, |dx| <=
+ * g_out[0] * max |dy| (dg_conv_set_grad_scale dx_g / dy_g of the graph executor's plans). */
+int dg_weight_bound_in(const float *w, int taps, int Ci, int Co, float *g_out, dg_stream_t stream);
 /* the arithmetic op's GEMM runs in (DG_MATH_*: fp32 for the exact direct kernels -- Co 1,
  * narrow, small-Cin -- and fp32 MFMA tiles; bf16x6, fp16 or fp16x3 for the split kernels):
  * per-op peaks for a roofline */

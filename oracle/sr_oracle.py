@@ -78,17 +78,26 @@ FP16 = None
 
 def _q16(t):
     r = t.to(torch.float16)
-    tau = FP16.get("flip_tau") if FP16 is not None else None
-    if tau:
-        r = _flip_near_ties(t, r, tau)
+    ft = FP16.get("flip_tau") if FP16 is not None else None
+    if ft:
+        tau, seed = ft if isinstance(ft, tuple) else (ft, 0)
+        sel = None
+        if seed:
+            # (a seeded half of the near-tie elements: one more realisation of the flips an fp32
+            # value may take; the n-th rounded operand of the step draws from seed and n)
+            FP16["flip_n"] = n = FP16.get("flip_n", 0) + 1
+            g = torch.Generator().manual_seed(int(seed) * 1000003 + n)
+            sel = torch.rand(t.shape, generator=g, dtype=torch.float64) < 0.5
+        r = _flip_near_ties(t, r, tau, sel)
     return r.to(t.dtype)
 
 
-def _flip_near_ties(t, r, tau):
+def _flip_near_ties(t, r, tau, sel=None):
     """Tie sensitivity (test diagnostics only): the elements of t whose fp64 value lies
     within tau fp16 ulps of the midpoint between its two fp16 neighbours -- where an
     fp32 value of the same quantity may round to the other neighbour -- take the OTHER
-    neighbour.  r: t rounded to fp16 (RNE)."""
+    neighbour (only where sel, a boolean mask of t's shape, is set, when given).  r: t
+    rounded to fp16 (RNE)."""
     mag = r.abs().view(torch.int16).to(torch.int32)      # fp16 magnitude bits
     up = t.abs() > r.abs().to(t.dtype)                   # the other neighbour is further from 0
     other_mag = torch.where(up, mag + 1, torch.clamp(mag - 1, min=0))
@@ -97,6 +106,8 @@ def _flip_near_ties(t, r, tau):
     mid = (rd + other) / 2
     near = (t - mid).abs() < tau * (rd - other).abs()
     near &= torch.isfinite(other) & (other_mag != mag)
+    if sel is not None:
+        near &= sel
     return torch.where(near, other.to(torch.float16), r)
 
 
@@ -401,7 +412,8 @@ def train_step(st, x, y, apply=True, dec=None, flip_tau=None):
     (any subset) -- the activation decisions of G(x), D(y), D(G(x)) and VGG19
     on G(x) and on y (mask-conditioned parity).  flip_tau (fp16 only, test diagnostics):
     every GEMM operand within flip_tau fp16 ulps of a rounding tie takes the other fp16
-    neighbour (_flip_near_ties) -- the tie sensitivity of the mixed_float16 step."""
+    neighbour (_flip_near_ties) -- the tie sensitivity of the mixed_float16 step; a
+    (tau, seed) pair with seed > 0 flips a seeded half of those operands instead."""
     global FP16
     dec = dec or {}
     FP16 = {"scale": st.ls["G"][0], "flip_tau": flip_tau} if st.fp16 else None

@@ -164,3 +164,15 @@ def test_pix2pix_networks_planned_at_several_shapes_alternating():
             f.generator.bn.load(states)
             want = f.generator(x, training=False).cpu().numpy()
             assert np.array_equal(out, want), (step, what, n)
+
+    # the sequence really alternates arithmetics, not only shapes: at width 4
+    # the 2N = 4 and 2N = 6 training plans run G up5 / up6 in different arithmetics (fp32 tiles at
+    # 4 images, fp16x3 at 6), so the alternation above switches plans of both kinds on one network
+    def ariths(n):
+        tr = m.trainer(xs[n][0].shape)
+        return [(d.label, o, d.op_arith(o)) for d in tr.G.ddesc + tr.G.udesc + [tr.G.ldesc] + tr.D.desc
+                for o in ("fwd", "bwd_data", "bwd_filter")]
+    a2, a3 = ariths(2), ariths(3)
+    moved = [(l, o, p, q) for (l, o, p), (_, _, q) in zip(a2, a3) if p != q]
+    assert moved, "the alternating training plans run every op in one arithmetic"
+    assert any(q == "f16x3" for *_, q in moved) and any(p == "fp32" for *_, p, _ in moved), moved

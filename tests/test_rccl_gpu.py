@@ -162,6 +162,9 @@ def test_bench_dist_world1_uses_rccl():
     out = json.loads(lines[0])
     assert out["config"]["parallelism"] == "dp1" and out["config"]["process_group"] == "nccl", out["config"]
     assert out["config"]["hip_graph"] is True
+    # (the data-parallel path replays the captured graph at every N since round 6; its replay equals
+    # the eager step with its RCCL all-reduces, bit for bit)
+    assert out["graph_equals_eager"]["equal"] is True, out["graph_equals_eager"]
     assert out["value"] > 0
 
 

@@ -570,3 +570,43 @@ def test_sr_step_under_library_wide_f16x3(kind, monkeypatch):
     else:
         from fsrgan import FastSRGAN
         _run_step_parity(FastSRGAN, "fsrgan", N=2, H=64, scale=4, content_loss=0)
+
+
+@gpu
+def test_two_slot_plan_keeps_per_slot_activation_scales(monkeypatch):
+    """D(real) and D(fake) are two slots of one GraphPlan sharing its conv
+    descriptors.  Under fp16x3 activation planes each slot's kept x planes carry the scale of the
+    maxima measured in THAT slot's forward; slot 1's forward must not change the scale slot 0's
+    filter gradient reads them back with.  Slot inputs 40x apart (five binades): both forwards then
+    both backwards (the SR trainer's order) must give the parameter gradients of two one-slot passes,
+    bit for bit."""
+    monkeypatch.setenv("DG_CONV_MATH", "f16x3")
+    from dgan import ops, zoo
+    from dgan.graph import GraphNetwork
+    D = GraphNetwork(zoo.sr_discriminator(), seed=5)
+    N, H = 2, 32
+    two = D.plan(N, H, H, slots=2, train=True)
+    one = D.plan(N, H, H, slots=1, train=True)
+    assert two.amax is not None and two.amax.shape[0] == 2 and two.act_feeds, "fp16x3 activation planes in play"
+    g = torch.Generator().manual_seed(3)
+    x0 = (torch.rand(N, H, H, 3, generator=g) * 2 - 1).to(DEV)
+    x1 = (40.0 * (torch.rand(N, H, H, 3, generator=g) * 2 - 1)).to(DEV)
+    dl0 = (torch.randn(two.out_shape, generator=g) * 1e-2).to(DEV)
+    dl1 = (torch.randn(two.out_shape, generator=g) * 1e-2).to(DEV)
+    ws = ops.Workspace(DEV)
+    ws.get(max(two.ws_bytes, one.ws_bytes))
+    two.forward(x0, slot=0, training=True, ws=ws)
+    two.forward(x1, slot=1, training=True, ws=ws)
+    two.backward(dl0, slot=0, param_beta=0.0, ws=ws)
+    two.backward(dl1, slot=1, param_beta=1.0, ws=ws)
+    g_two = D.arena.grad.clone()
+    one.forward(x0, slot=0, training=True, ws=ws)
+    one.backward(dl0, slot=0, param_beta=0.0, ws=ws)
+    one.forward(x1, slot=0, training=True, ws=ws)
+    one.backward(dl1, slot=0, param_beta=1.0, ws=ws)
+    g_one = D.arena.grad.clone()
+    torch.cuda.synchronize()
+    assert torch.isfinite(g_two).all()
+    bad = [n for n, _ in D.arena.var_list
+           if not torch.equal(D.arena._v(g_two, n), D.arena._v(g_one, n))]
+    assert not bad, f"two-slot gradients differ from the one-slot passes: {bad}"
