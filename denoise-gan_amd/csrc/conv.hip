@@ -1758,6 +1758,19 @@ static GemmArgs make_args(const ConvGeom &g, const OpPlan &pl, const float *A, i
     a.slab = (float *)slab;
     a.xcd_plain = plan_off("xcd_phase");
     a.ptiles = pl.halo ? std::max(1, pl.ptiles) : 1;
+    // n-grouped XCD raster (xcd_group_tile) for the stride-1 4x4 halo plans (the PatchGAN's conv:
+    // 8 n-tiles of 64 columns over 256 patches at bs16 x 2): with every XCD running all 8 n-tiles
+    // its L2 streams the whole 8.4 MB fp16x3 filter per round of patches -- the forward read 562 MB
+    // for 105 MB of operands (profiles/r5/r5_final_pmc_layers.md); in groups of NG the XCD keeps
+    // ntiles / NG column blocks.  DG_XCD_NG: the group count (0: off), for same-box A/B
+    if (pl.halo == 4 && pl.ptiles <= 1 && pl.splits == 1 && pl.nphase == 1) {
+        int ng = 4;
+        if (const char *e = getenv("DG_XCD_NG")) ng = atoi(e);
+        const long tot = (long)pl.mtiles * pl.ntiles;
+        if ((ng == 1 || ng == 2 || ng == 4 || ng == 8) && tot % 8 == 0 && pl.ntiles % ng == 0 &&
+            pl.mtiles % (8 / ng) == 0)
+            a.xcd_ng = ng;
+    }
     return a;
 }
 

@@ -66,7 +66,26 @@ struct GemmArgs {
     // 1: the gradient mask also multiplies the accumulated beta*C (dg_conv_bwd_data_masked_sum:
     // C = act'(mz) * (result + beta*C), a fan-in whose other contribution arrived unmasked)
     int mask_acc;
+    // halo kernel, one patch per block, one phase, no split: > 0 = the n-tiles are dealt to the
+    // XCDs in xcd_ng groups (XCD x runs the n-tiles of group x % xcd_ng over patches of part
+    // x / xcd_ng), so an XCD's L2 keeps its weight columns instead of streaming every column of
+    // the filter (xcd_group_tile); 0: the plain XCD order
+    int xcd_ng;
 };
+
+// (mt, nt) of this block under the n-grouped XCD raster (GemmArgs.xcd_ng = NG > 0): blocks are
+// dealt round-robin to the 8 XCDs (lin & 7 labels the XCD, lin >> 3 the dispatch order on it);
+// XCD x takes n-tiles [g TPG, (g+1) TPG) of group g = x % NG and patches [h MPH, (h+1) MPH) of
+// part h = x / NG, TPG = ntiles / NG, MPH = mtiles / (8 / NG).  A bijection when the grid is
+// mtiles x ntiles with both divisible as stated (the planner checks); speed only, any placement
+// is correct.
+__device__ __forceinline__ void xcd_group_tile(int ng, int mtiles, int ntiles, int &mt, int &nt) {
+    const int lin = blockIdx.y * gridDim.x + blockIdx.x;
+    const int x = lin & 7, idx = lin >> 3;
+    const int tpg = ntiles / ng, mph = mtiles / (8 / ng);
+    nt = (x % ng) * tpg + idx % tpg;
+    mt = (x / ng) * mph + idx / tpg;
+}
 
 // the factor that undoes an fp16x3 GEMM's operand scales (powers of two: exact)
 __device__ __forceinline__ float x3_out_scale(const GemmArgs &p) {

@@ -87,9 +87,18 @@ __device__ __forceinline__ rsrc4_t make_rsrc4(const void *base, unsigned bytes) 
     const unsigned n = (unsigned)__builtin_amdgcn_readfirstlane((int)bytes);
     return make_rsrc((const float *)(uintptr_t)(((unsigned long long)hi << 32) | lo), n);
 }
+// The asm opens with `s_nop 4`: hipcc pads no hazard into an asm statement
+// (cdna_hip_programming.md §5.7 item 2), and two reach this one -- a VALU write of
+// a descriptor SGPR (the spill restore `v_readlane_b32 s7, ...` hipcc places
+// among the DMAs of these SGPR-spilling kernels) needs 5 wait states before a
+// VMEM instruction reads it, and the compiler's `s_mov_b32 m0` one before an
+// LDS-DMA.  Without the pad (round 5 and before) a regalloc change put such a
+// restore 1-3 instructions ahead of a DMA in k_conv_gemm_x6h<DGRAD, 128, .., 2, 4>
+// (G up5 / up6 forward): run-to-run different outputs, one memory-access fault
+// (round 6, scripts/diag/determinism.py; profiles/r6/dma_hazard.txt).
 __device__ __forceinline__ void dma16(rsrc4_t r, char *lds, unsigned off) {
     const unsigned la = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char *)lds;
-    asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(off), "s"(r), "{m0}"(la) : "memory");
+    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(off), "s"(r), "{m0}"(la) : "memory");
 }
 
 }  // namespace dg

