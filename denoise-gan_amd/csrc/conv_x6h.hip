@@ -659,10 +659,20 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
             }
         };
         float *va = PERS ? &vacc : nullptr;
+#ifdef DG_X6H_LAUNDER
+        // the epilogue's arguments re-read from the kernarg segment here (scalar loads), instead of
+        // held in SGPRs -- spilled to VGPR lanes -- across the whole patch loop
+        const __attribute__((address_space(4))) GemmArgs *pq =
+            (const __attribute__((address_space(4))) GemmArgs *)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(pq));
+        const GemmArgs &pe = *(const GemmArgs *)pq;
+#else
+        const GemmArgs &pe = p;
+#endif
         if constexpr (POOL)
-            conv_epilogue16_pool<TM, TN>(p, acc, wm * TM, n0 + wn * WTN, ty, tx, nimg, lane, stage, ys_pre, va);
+            conv_epilogue16_pool<TM, TN>(pe, acc, wm * TM, n0 + wn * WTN, ty, tx, nimg, lane, stage, ys_pre, va);
         else
-            conv_epilogue16<MODE, TM, TN>(p, acc, wm * WTM, n0 + wn * WTN, rowmap, phase, split, lane, stage, ys_pre,
+            conv_epilogue16<MODE, TM, TN>(pe, acc, wm * WTM, n0 + wn * WTN, rowmap, phase, split, lane, stage, ys_pre,
                                           va);
         if (jn < 0) return false;
         // every wave has read its staging rows before the next patch's DMAs refill the buffer
