@@ -105,7 +105,7 @@ k_bn_stats_partial(const float *__restrict__ y, int ld, long M, int C, long rows
     // term of the output bound that scales fp16x3 z planes (k_bn_stats_final); zbound zeroed here
     __shared__ float s1s[256 * V], s2s[256 * V], dms[256 * V];
     if (zbound && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x < X3_SHARDS)
-        zbound[threadIdx.x] = 0.f;
+        zbound[threadIdx.x * X3_SHARD_STRIDE] = 0.f;
     const int slot = threadIdx.x % cpb, rl = threadIdx.x / cpb, RL = 256 / cpb;
     const int c0 = (blockIdx.x * cpb + slot) * V;
     y += (long)blockIdx.z * M * ld;
@@ -227,7 +227,7 @@ k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, i
                  const float *cp_bound) {
     // zbound (pbd set): max over channels and segments of (|scale| max |y - mean| + |beta|) x the
     // dropout keep scale >= max |z| (ReLU / LeakyReLU do not grow |t|), and the bound of the
-    // tensor copied beside z (cp_bound, 8 shards), into one of X3_SHARDS floats (zeroed by the
+    // tensor copied beside z (cp_bound, a max slot), into one of X3_SHARDS floats (zeroed by the
     // partial pass): the scale of the z planes (k_bn_apply)
     __shared__ float sh[2 * 256];
     const int cl = threadIdx.x % FIN_C, ln = threadIdx.x / FIN_C;
@@ -302,8 +302,9 @@ k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, i
             float b = 0.f;
             for (int i = 0; i < FIN_C; ++i) b = fmaxf(b, sh[i]);
             if (cp_bound && blockIdx.x == 0)
-                for (int i = 0; i < X3_SHARDS; ++i) b = fmaxf(b, cp_bound[i]);
-            atomicMax(reinterpret_cast<unsigned *>(zbound) + (blockIdx.x & (X3_SHARDS - 1)), __float_as_uint(b));
+                for (int i = 0; i < X3_SHARDS; ++i) b = fmaxf(b, cp_bound[i * X3_SHARD_STRIDE]);
+            atomicMax(reinterpret_cast<unsigned *>(zbound) + (blockIdx.x & (X3_SHARDS - 1)) * X3_SHARD_STRIDE,
+                      __float_as_uint(b));
         }
     }
 }
@@ -417,7 +418,7 @@ k_bn_bwd_partial(const float *__restrict__ dz, int lddz, const float *__restrict
     // on |dy| that scales its fp16x3 planes (k_bn_bwd_final); bound zeroed here for it
     __shared__ float a1s[256 * V], a2s[256 * V], dms[MX ? 256 * V : 1], vms[MX ? 256 * V : 1];
     if (bound && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x < X3_SHARDS)
-        bound[threadIdx.x] = 0.f;
+        bound[threadIdx.x * X3_SHARD_STRIDE] = 0.f;
     const int slot = threadIdx.x % cpb, rl = threadIdx.x / cpb, RL = 256 / cpb;
     const int c0 = (blockIdx.x * cpb + slot) * V;
     {   // segment blockIdx.z: its rows and its saved statistics
@@ -564,7 +565,8 @@ k_bn_bwd_final(const float *p1, const float *p2, const float *pd, const float *p
         if (threadIdx.x == 0) {
             float b = 0.f;
             for (int i = 0; i < FIN_C; ++i) b = fmaxf(b, sh[i]);
-            atomicMax(reinterpret_cast<unsigned *>(bound) + (blockIdx.x & (X3_SHARDS - 1)), __float_as_uint(b));
+            atomicMax(reinterpret_cast<unsigned *>(bound) + (blockIdx.x & (X3_SHARDS - 1)) * X3_SHARD_STRIDE,
+                      __float_as_uint(b));
         }
     }
 }

@@ -94,10 +94,15 @@ __device__ __forceinline__ void split_x3(float x, float s, _Float16 &h, _Float16
 // measured max |value| (atomicMax by the producer of the previous gradient), g a weight
 // bound (max over input channels of sum |w|, NULL = 1) -- so the scaled values stay below
 // 2^14 (fp16 max 65504) while values down to 2^-28 of the bound keep 22 bits
-// A measured max is kept as X3_SHARDS floats (one per workgroup shard, so the atomics of a
-// grid spread over that many words: one word takes about one atomic per 11 ns,
-// MI355X_MICROARCH.md 'fanin'); its value is their max.
+// A measured max is kept as X3_SHARDS floats (one per workgroup shard) X3_SHARD_STRIDE floats
+// apart -- a 128-byte line each -- in an X3_SLOT-float slot; its value is their max.  Device-wide
+// atomics to one line serialize at about 10 ns each whatever word they hit: with the 8 shards in
+// one 32-byte run (round 5) a 2048-workgroup split-K reduce spent 20 us of its 30 on them; one
+// line per shard costs nothing measurable (round 6, scripts/diag/atomic_bench.hip,
+// profiles/r6/atomic_bench.txt).
 constexpr int X3_SHARDS = 8;
+constexpr int X3_SHARD_STRIDE = 32;
+constexpr int X3_SLOT = X3_SHARDS * X3_SHARD_STRIDE;
 // Activations use the same form when a scale source is given (dg_conv_set_act_scale,
 // dg_bn_fwd_train_seg_x): a BN forward's bound of its output, a measured max, or a conv
 // output's bound m * g + c (m: measured max |input|, g: max over output channels of sum |w|,
@@ -112,7 +117,7 @@ __device__ __forceinline__ float x3_bound_scale(float b) {
 __device__ __forceinline__ float x3_grad_scale(const float *m, const float *g, const float *c = nullptr) {
     float mm = m[0];
 #pragma unroll
-    for (int i = 1; i < X3_SHARDS; ++i) mm = fmaxf(mm, m[i]);
+    for (int i = 1; i < X3_SHARDS; ++i) mm = fmaxf(mm, m[i * X3_SHARD_STRIDE]);
     return x3_bound_scale(mm * (g ? *g : 1.f) + (c ? *c : 0.f));
 }
 // the raw terms of a scale source, loaded at kernel entry and combined in the epilogue (the
@@ -126,7 +131,7 @@ __device__ __forceinline__ X3Raw x3_raw(const float *m, const float *g, const fl
     X3Raw r;
     r.on = m != nullptr;
 #pragma unroll
-    for (int i = 0; i < X3_SHARDS; ++i) r.m[i] = m ? m[i] : 0.f;
+    for (int i = 0; i < X3_SHARDS; ++i) r.m[i] = m ? m[i * X3_SHARD_STRIDE] : 0.f;
     r.g = g ? *g : 1.f;
     r.c = c ? *c : 0.f;
     return r;
@@ -139,9 +144,9 @@ __device__ __forceinline__ float x3_raw_scale(const X3Raw &r, float dflt) {
     return x3_bound_scale(mm * r.g + r.c);
 }
 // |v| into a sharded device max (non-negative floats order as their bit patterns): a
-// butterfly over each wave's lanes, the waves' maxima through LDS, then one lane reads the
-// workgroup's shard and adds one vector atomic only when its value is larger (most
-// workgroups of a grid then add none).  Every thread of the workgroup must call it.
+// butterfly over each wave's lanes, the waves' maxima through LDS, then one vector atomic into
+// the workgroup's shard (a read-before-atomic test measured slower once the shards sit on their
+// own lines).  Every thread of the workgroup must call it.
 __device__ __forceinline__ void block_atomic_absmax(float *dst, float v) {
     __shared__ float red[16];
 #pragma unroll
@@ -151,9 +156,9 @@ __device__ __forceinline__ void block_atomic_absmax(float *dst, float v) {
     if (threadIdx.x == 0) {
         const int nw = (blockDim.x + 63) >> 6;
         for (int i = 1; i < nw; ++i) v = fmaxf(v, red[i]);
-        unsigned *w = reinterpret_cast<unsigned *>(dst) + ((blockIdx.x + blockIdx.y * gridDim.x) & (X3_SHARDS - 1));
-        const unsigned u = __float_as_uint(v);
-        if (u > __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(w, u);
+        unsigned *w = reinterpret_cast<unsigned *>(dst) +
+                      ((blockIdx.x + blockIdx.y * gridDim.x) & (X3_SHARDS - 1)) * X3_SHARD_STRIDE;
+        atomicMax(w, __float_as_uint(v));
     }
 }
 

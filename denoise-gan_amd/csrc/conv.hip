@@ -1243,7 +1243,7 @@ struct OpPlan {
     // narrow stride-1 filter gradient on row segments (k_narrow_wgrad_tile): partial blocks
     int ntile;
     // fp16x3 input gradient: workspace offset of the max |dy| float (no scale source set)
-    size_t x3_max_off;   // (+256: max |x| when the x operand has no scale source)
+    size_t x3_max_off;   // (+X3_SLOT floats: max |x| when the x operand has no scale source)
 };
 
 // A narrow op (GEMM N <= 8) recast as a 1x1-geometry MFMA GEMM plus a gather:
@@ -1620,7 +1620,7 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         pl.ws_bytes = pl.x6_b_off + eb * rb * cb;
         if (pl.x6 == 3) {   // (max |dy| and max |x| when no scale source is set: any mode may read dy / x)
             pl.x3_max_off = (pl.ws_bytes + 255) & ~(size_t)255;
-            pl.ws_bytes = pl.x3_max_off + 512;
+            pl.ws_bytes = pl.x3_max_off + 2 * X3_SLOT * sizeof(float);
         }
     }
     pl.gemm_bytes = pl.ws_bytes;
@@ -2074,12 +2074,12 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
             if (!m) {
                 DG_ARG(!grad || !ready, "fp16x3 dy planes given without their scale source (dg_conv_set_grad_scale)");
                 if (!grad && held) continue;
-                meas = (float *)(ws + pl.x3_max_off + (grad ? 0 : 256));
+                meas = (float *)(ws + pl.x3_max_off + (grad ? 0 : X3_SLOT * sizeof(float)));
             } else if (!ready && (is_a ? !a.as_g && !a.as_c : !a.bs_g && !a.bs_c) && !grad) {
                 meas = const_cast<float *>(m);   // an x source that is a plain max slot: measured by this split
             }
             if (!meas) continue;
-            if (hipMemsetAsync(meas, 0, X3_SHARDS * sizeof(float), s) != hipSuccess) {
+            if (hipMemsetAsync(meas, 0, X3_SLOT * sizeof(float), s) != hipSuccess) {
                 dg::set_error("hipMemsetAsync failed");
                 return DG_ERR_HIP;
             }
@@ -2212,6 +2212,11 @@ static int finish_splitk(int mode, const OpPlan &pl, const GemmArgs &a, hipStrea
         const int v4 = tpo;
         long total = tpo ? (long)pl.M * pl.N / 4 * tpo : (long)pl.M * pl.N;
         dim3 rg((unsigned)std::min<long>(dg_cdiv(total, 256), 4096), pl.nphase);
+        static const bool trace = getenv("DG_TRACE_REDUCE") != nullptr;
+        if (trace)
+            fprintf(stderr, "[reduce] mode %d M %ld N %d splits %d nphase %d tpo %d grid %u C %d beta %g bias %d yp %d ymax %d mz %d mzp %d ys_m %d\n",
+                    mode, (long)pl.M, pl.N, pl.splits, pl.nphase, tpo, rg.x, a.C != nullptr, a.beta, a.bias != nullptr,
+                    a.yp != nullptr, a.ymax != nullptr, a.mz != nullptr, a.mzp != nullptr, a.ys_m != nullptr);
         switch (mode) {
         case MODE_FWD: hipLaunchKernelGGL(k_splitk_reduce<MODE_FWD>, rg, dim3(256), 0, s, a, v4); break;
         case MODE_DGRAD: hipLaunchKernelGGL(k_splitk_reduce<MODE_DGRAD>, rg, dim3(256), 0, s, a, v4); break;
@@ -2416,7 +2421,7 @@ int dg_absmax(const float *x, int64_t rows, int C, int ld, float *out, dg_stream
 
 int dg_absmax_set(const float *x, int64_t rows, int C, int ld, float *out, dg_stream_t stream) {
     DG_ARG(out, "NULL tensor");
-    if (hipMemsetAsync(out, 0, dg::X3_SHARDS * sizeof(float), (hipStream_t)stream) != hipSuccess) {
+    if (hipMemsetAsync(out, 0, dg::X3_SLOT * sizeof(float), (hipStream_t)stream) != hipSuccess) {
         dg::set_error("hipMemsetAsync failed");
         return DG_ERR_HIP;
     }

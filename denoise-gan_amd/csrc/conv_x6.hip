@@ -710,7 +710,7 @@ __global__ void __launch_bounds__(256) k_weight_bound(const float *__restrict__ 
                                                      const float *__restrict__ bias, float *gout, float *cout,
                                                      float *zero8) {
     __shared__ float red[256];
-    if (zero8 && threadIdx.x < X3_SHARDS) zero8[threadIdx.x] = 0.f;
+    if (zero8 && threadIdx.x < X3_SHARDS) zero8[threadIdx.x * X3_SHARD_STRIDE] = 0.f;
     const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
     float g = 0.f, c = 0.f;
     for (int c0 = 0; c0 < Co; c0 += 64) {
@@ -758,7 +758,7 @@ __global__ void __launch_bounds__(256) k_weight_bound_cols(const float *__restri
                                                           const float *__restrict__ bias, float *gout, float *cout,
                                                           float *zero8) {
     __shared__ float red[256];
-    if (blockIdx.x == 0 && zero8 && threadIdx.x < X3_SHARDS) zero8[threadIdx.x] = 0.f;
+    if (blockIdx.x == 0 && zero8 && threadIdx.x < X3_SHARDS) zero8[threadIdx.x * X3_SHARD_STRIDE] = 0.f;
     const int cl = threadIdx.x & 15, rl = threadIdx.x >> 4;
     const int co = blockIdx.x * 16 + cl;
     float sum = 0.f;

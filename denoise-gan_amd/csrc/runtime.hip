@@ -164,6 +164,8 @@ extern "C" {
 
 const char *dg_last_error_string(void) { return dg::g_err; }
 int dg_version(void) { return 1; }
+static_assert(dg::X3_SLOT == DG_MAX_SLOT, "include/dgan.h DG_MAX_SLOT is the library's max-slot size");
+int dg_max_slot_floats(void) { return dg::X3_SLOT; }
 
 #ifndef DG_SOURCE_SHA
 #define DG_SOURCE_SHA "unknown"

@@ -22,6 +22,7 @@ _P = c_void_p  # device pointer
 _SIGS = {
     "dg_last_error_string": (c_char_p, []),
     "dg_version": (c_int, []),
+    "dg_max_slot_floats": (c_int, []),
     "dg_build_info": (c_char_p, []),
     "dg_conv_desc_create": (c_int, [ctypes.POINTER(c_void_p)] + [c_int] * 14),
     "dg_conv_desc_destroy": (c_int, [c_void_p]),

@@ -551,7 +551,7 @@ class GraphPlan:
         if x3g:
             slot_of = {n.idx: i for i, n in enumerate(conv_nodes)}
             self._x3_slot = slot_of
-            self.gmax = torch.zeros(len(conv_nodes), 8, dtype=torch.float32, device=device)   # 8 atomic shards
+            self.gmax = ops.max_slot(len(conv_nodes), device=device)
             self.gwb = torch.zeros(len(conv_nodes), dtype=torch.float32, device=device)
             self._gwb_ver = None
             self.x3_convs = [n for n in x3g]
@@ -613,7 +613,7 @@ class GraphPlan:
         self._act_slot = None
         if alias is None and any(self.desc[n.idx].plane_format(ops.TENSOR_X) == ops.PLANES_F16X3 for n in conv_nodes):
             ci = {n.idx: i for i, n in enumerate(conv_nodes)}
-            self.amax = torch.zeros(slots, len(conv_nodes), 8, dtype=torch.float32, device=device)
+            self.amax = ops.max_slot(slots, len(conv_nodes), device=device)
             self.awb = torch.zeros(len(conv_nodes), 2, dtype=torch.float32, device=device)
             feeds = {}   # producer conv idx -> (consumer conv, unfused pool or None, planes it writes or None)
             for n in conv_nodes:

@@ -77,14 +77,14 @@ P2P_MATH = os.environ.get("DG_P2P_MATH", "f16x3")
 
 
 def grad_bounds(descs, planes, device):
-    """One 8-float dy bound per conv whose dy planes are fp16x3 (written by the BN backward
+    """One dy bound (a max slot) per conv whose dy planes are fp16x3 (written by the BN backward
     producing that dy, dg_bn_bwd_seg_x), set as the conv's dy scale source; None elsewhere
     (the conv measures max |dy| itself where it splits dy)."""
     out = []
     for d, P in zip(descs, planes):
         b = None
         if FEED_DY and P is not None and P.dy is not None and P.dy.fmt == ops.PLANES_F16X3:
-            b = torch.zeros(8, dtype=torch.float32, device=device)
+            b = ops.max_slot(device=device)
             d.set_grad_scale(dy_m=b)
         out.append(b)
     return out
@@ -97,7 +97,7 @@ def x3_planes(P):
 
 class ActBounds:
     """Scale sources of a network's fp16x3 activation planes (include/dgan.h
-    dg_conv_set_act_scale): `zb[i]` (8 floats) the bound of BN block i's output written by its
+    dg_conv_set_act_scale): `zb[i]` (a max slot) the bound of BN block i's output written by its
     statistics (dg_bn_fwd_train_seg_x), `in_max` the measured max |input| and `w1[0]` the
     forward weight bound of the first conv (no BN after it: its output planes are scaled from
     in_max x w1).  Each conv whose x planes are fp16x3 reads the source its producer wrote
@@ -105,8 +105,8 @@ class ActBounds:
     scale left |x| < 2 -- most of a BN output -- with a subnormal low piece)."""
 
     def __init__(self, n, device):
-        self.zb = torch.zeros(n, 8, dtype=torch.float32, device=device)
-        self.in_max = torch.zeros(8, dtype=torch.float32, device=device)
+        self.zb = ops.max_slot(n, device=device)
+        self.in_max = ops.max_slot(device=device)
         self.w1 = torch.zeros(2, dtype=torch.float32, device=device)
 
     def first_conv(self, x, w):
@@ -670,7 +670,7 @@ class DiscriminatorPlan:
             if self.desc_half is not self.desc:
                 for i, (d, P) in enumerate(zip(self.desc_half, self.planes_half)):
                     if FEED_DY and P is not None and P.dy is not None and P.dy.fmt == ops.PLANES_F16X3:
-                        self.gbound_h[i] = torch.zeros(8, dtype=torch.float32, device=device)
+                        self.gbound_h[i] = ops.max_slot(device=device)
                         d.set_grad_scale(dy_m=self.gbound_h[i])
                 self.dz_h = [_empty(d.out_shape, device) for d in self.desc_half[:-1]]
                 self.dy_h = _empty((max(d.N * d.Ho * d.Wo * d.Cout for d in self.desc_half),), device)

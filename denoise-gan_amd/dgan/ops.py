@@ -11,6 +11,16 @@ import torch
 
 from ._lib import call, lib, DGError
 
+# floats of a measured-max slot (include/dgan.h DG_MAX_SLOT: 8 atomic shards on their own
+# 128-byte lines; tests/test_lib.py checks it against dg_max_slot_floats)
+MAX_SLOT = 256
+
+
+def max_slot(*lead, device=None):
+    """A zeroed measured-max slot (or [*lead] of them): the fp16x3 scale sources' form."""
+    return torch.zeros(*lead, MAX_SLOT, dtype=torch.float32, device=device)
+
+
 ACT = {"none": 0, "linear": 0, None: 0, "lrelu": 1, "leaky_relu": 1, "relu": 2, "tanh": 3, "sigmoid": 4}
 OP_FWD, OP_BWD_DATA, OP_BWD_FILTER = 0, 1, 2
 
@@ -303,24 +313,24 @@ class ConvDesc:
     def set_grad_scale(self, dy_m=None, dy_g=None, dx_m=None, dx_g=None, dx_max=None):
         """The fp16x3 input-gradient scale context (include/dgan.h dg_conv_set_grad_scale):
         device floats (views that stay alive with the plan; the measured maxima dy_m, dx_m and
-        dx_max 8 floats each), None = unset."""
+        dx_max max slots), None = unset."""
         for t in (dy_m, dx_m, dx_max):
-            if t is not None and t.numel() < 8:
-                raise DGError("a measured gradient max is 8 floats (per-workgroup shards)")
+            if t is not None and t.numel() < MAX_SLOT:
+                raise DGError(f"a measured gradient max is a max slot of {MAX_SLOT} floats (per-workgroup shards)")
         self._gs = (dy_m, dy_g, dx_m, dx_g, dx_max)   # (keeps the views referenced)
         call("dg_conv_set_grad_scale", self._h, _p(dy_m), _p(dy_g), _p(dx_m), _p(dx_g), _p(dx_max))
 
     def set_act_scale(self, x=None, y=None, y_max=None):
         """The fp16x3 activation scale context (include/dgan.h dg_conv_set_act_scale): x, y = (m, g, c)
         scale sources of the input planes and of the output planes the forward writes (device
-        floats: m 8 shards, g and c one float or None), y_max 8 floats receiving max |y|."""
-        def src(v):   # a tensor alone = (m,): a plain 8-float slot
+        floats: m a max slot, g and c one float or None), y_max a max slot receiving max |y|."""
+        def src(v):   # a tensor alone = (m,): a plain max slot
             v = (v,) if isinstance(v, torch.Tensor) else tuple(v or ())
             return v + (None,) * (3 - len(v))
         xs, ys = src(x), src(y)
         for t in (xs[0], ys[0], y_max):
-            if t is not None and t.numel() < 8:
-                raise DGError("a measured max / bound slot is 8 floats (per-workgroup shards)")
+            if t is not None and t.numel() < MAX_SLOT:
+                raise DGError(f"a measured max / bound slot is {MAX_SLOT} floats (per-workgroup shards)")
         self._as = (xs, ys, y_max)   # (keeps the views referenced)
         call("dg_conv_set_act_scale", self._h, *(_p(t) for t in xs), *(_p(t) for t in ys), _p(y_max))
 
@@ -624,8 +634,8 @@ def _bn_fwd_train_x(y, gamma, beta, save_mean, save_invstd, moving_mean, moving_
     if M % segments:
         raise DGError(f"{M} rows do not split into {segments} segments")
     M //= segments
-    if z_bound is None or z_bound.numel() < 8:
-        raise DGError("a z bound is 8 device floats (per-workgroup shards)")
+    if z_bound is None or z_bound.numel() < MAX_SLOT:
+        raise DGError(f"a z bound is a max slot of {MAX_SLOT} device floats (per-workgroup shards)")
     ws = ws or default_workspace()
     buf, n = ws.get(bn_workspace_bytes(M, C, segments))
     zp = [(t.data_ptr(), int(pc), int(col)) for t, pc, col in z_planes] + [(None, 0, 0)] * (2 - len(z_planes))
@@ -668,8 +678,8 @@ def bn_bwd(dz, z, y, gamma, save_mean, save_invstd, dy, dgamma, dbeta, act="none
     buf, n = ws.get(bn_workspace_bytes(M, C, segments))
     if act_id(act) == 0 and drop_rate == 0.0:
         z = None   # a linear BN's backward does not read z (dg_bn_bwd_seg_h)
-    if dy_bound is not None and dy_bound.numel() < 8:
-        raise DGError("a gradient bound is 8 floats (per-workgroup shards)")
+    if dy_bound is not None and dy_bound.numel() < MAX_SLOT:
+        raise DGError(f"a gradient bound is a max slot of {MAX_SLOT} floats (per-workgroup shards)")
     if offset is not None and act_id(act) in (ACT["relu"], ACT["lrelu"]) and drop_rate == 0.0:
         call("dg_bn_bwd_seg_r", segments, M, C, _p(dz), pix_ld(dz, C), _p(y), pix_ld(y, C), _p(gamma), _p(offset),
              _p(save_mean), _p(save_invstd), act_id(act), float(alpha),
@@ -897,8 +907,8 @@ def maxpool2_bwd_idx(idx, dy, dx, C, H, W, beta=0.0, act="none", alpha=0.3, plan
 def absmax(t, out):
     """out (8 device floats, zeroed by the caller; the max is their max) = max(out, max |t|)
     (dg_absmax)."""
-    if out.numel() < 8:
-        raise DGError("absmax needs 8 floats (per-workgroup shards)")
+    if out.numel() < MAX_SLOT:
+        raise DGError(f"absmax needs a max slot of {MAX_SLOT} floats (per-workgroup shards)")
     C = t.shape[-1]
     call("dg_absmax", _p(t), _rows(t), C, pix_ld(t, C), _p(out), _stream())
     return out
@@ -906,8 +916,8 @@ def absmax(t, out):
 
 def absmax_set(t, out):
     """out (8 device floats) = max |t| (zeroed first, dg_absmax_set): a measured max."""
-    if out.numel() < 8:
-        raise DGError("absmax needs 8 floats (per-workgroup shards)")
+    if out.numel() < MAX_SLOT:
+        raise DGError(f"absmax needs a max slot of {MAX_SLOT} floats (per-workgroup shards)")
     C = t.shape[-1]
     call("dg_absmax_set", _p(t), _rows(t), C, pix_ld(t, C), _p(out), _stream())
     return out
@@ -915,7 +925,7 @@ def absmax_set(t, out):
 
 def weight_bound(w, g_out, bias=None, c_out=None, zero=None):
     """g_out[0] = max over output channels of sum |w| over the other axes (HWIO w), c_out[0] =
-    max |bias| (dg_weight_bound): a conv output's bound terms; zero: 8 floats zeroed on the way."""
+    max |bias| (dg_weight_bound): a conv output's bound terms; zero: a max slot zeroed on the way."""
     Co = w.shape[-1]
     call("dg_weight_bound", _p(w), w.numel() // Co, Co, _p(bias), _p(g_out), _p(c_out), _p(zero), _stream())
 

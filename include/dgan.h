@@ -51,6 +51,12 @@ const char *dg_build_info(void);
 /* an empty kernel dispatch on `stream`: a mark in the dispatch sequence for profiling
  * (per-dispatch rocprofv3 PMC counters attributed to the calls between marks) */
 int dg_mark(int id, dg_stream_t stream);
+/* A measured max |value| (the fp16x3 scale sources below) is kept in a max slot of
+ * DG_MAX_SLOT device floats: 8 per-workgroup shards of the producers' atomics, 32 floats (a
+ * 128-byte line) apart, at slot[0], slot[32], ..., slot[224]; its value is their max and the
+ * floats between them stay 0.  (Atomics to one line serialize: round 6 spread the shards.) */
+#define DG_MAX_SLOT 256
+int dg_max_slot_floats(void);
 
 /* ------------------------------------------------------------------------
  * Convolution layers: Conv2D (pix2pix.py:115-116, :207-209, :217-218) and
@@ -159,42 +165,42 @@ int dg_conv_planes_format(dg_conv_t d, int tensor, int *format);
 /* fp16x3 input gradients (DG_MATH_F16X3 bwd_data of a layer whose forward runs fp16x3;
  * VGG19's backward, pix2pix.py:45-51): a gradient has no static range, so its fp16x3 planes
  * are scaled by 2^(14 - e), bound = m * *g < 2^e (g NULL = 1) -- m a measured max |value|
- * kept as 8 floats (per-workgroup shards of the atomics; m = their max), g a weight bound
+ * kept in a max slot (DG_MAX_SLOT floats; m = the max of its shards), g a weight bound
  * max_ci sum_{taps, co} |w| -- which keeps every scaled value below 2^14.
  * dy_m / dy_g: the source of the dy planes' scale (the producer's: dx_m / dx_g of the
  * consuming layer, or dg_maxpool2_bwd_idx_x3's); NULL dy_m: bwd_data measures max |dy| of
  * its fp32 dy itself (dy planes must then not be ready).  dx_m / dx_g: the source of the
  * scale of the dx planes this op writes (planes->out with out_format DG_PLANES_F16X3),
- * normally (max |dy| of this layer, its weight bound).  dx_max: 8 floats receiving max |dx|
+ * normally (max |dy| of this layer, its weight bound).  dx_max: a max slot receiving max |dx|
  * by atomicMax (the caller zeroes them per step).  All device pointers, kept by the descriptor. */
 int dg_conv_set_grad_scale(dg_conv_t d, const float *dy_m, const float *dy_g, const float *dx_m, const float *dx_g,
                            float *dx_max);
 /* fp16x3 activation scale context (round 5).  An activation's fp16x3 planes are scaled by
- * 2^(14 - e) from a bound b = max(m[0..7]) * (g ? *g : 1) + (c ? *c : 0) < 2^e, like a gradient's,
+ * 2^(14 - e) from a bound b = max(shards of m) * (g ? *g : 1) + (c ? *c : 0) < 2^e, like a gradient's,
  * so every |x| >= 2^-17 b keeps 22 bits (a static 2^-4 leaves |x| < 2 with a subnormal low piece).
  *   x_m / x_g / x_c: the source of the layer input's planes (the one their producer wrote them
  *     with: a BN forward's bound -- dg_bn_fwd_train_seg_x -- or a producing conv's output source
- *     below); a plain 8-float slot (x_g, x_c NULL) is also measured into (max |x|) by any op of
+ *     below); a plain max slot (x_g, x_c NULL) is also measured into (max |x|) by any op of
  *     this descriptor that splits x itself.  NULL x_m: x planes in the workspace are measured per
  *     op; caller-held x planes keep the static 2^-4.
  *   y_m / y_g / y_c: the source of the output planes the forward writes for its consumer
  *     (planes->out, any arithmetic): normally (max |x| measured, max over output channels of
  *     sum |w| over taps and input channels, max |bias|) -- a bound of |y| after a ReLU /
- *     LeakyReLU / linear activation.  y_max: 8 floats receiving max |y| of the forward (the
+ *     LeakyReLU / linear activation.  y_max: a max slot receiving max |y| of the forward (the
  *     16x16-tile, split-K reduce and small-Cin epilogues), the caller zeroes them.
  * All device pointers, kept by the descriptor. */
 int dg_conv_set_act_scale(dg_conv_t d, const float *x_m, const float *x_g, const float *x_c, const float *y_m,
                           const float *y_g, const float *y_c, float *y_max);
-/* max |x| over [rows][ld] (first C columns) into out[0..7] by atomicMax (the caller zeroes
- * them; the max is their max): the measured max of a gradient entering an fp16x3 input
+/* max |x| over [rows][ld] (first C columns) into the max slot out by atomicMax (the caller
+ * zeroes it): the measured max of a gradient entering an fp16x3 input
  * gradient from fp32 */
 int dg_absmax(const float *x, int64_t rows, int C, int ld, float *out, dg_stream_t stream);
-/* the same into freshly zeroed out[0..7] (a measured max of one tensor) */
+/* the same into the freshly zeroed max slot out (a measured max of one tensor) */
 int dg_absmax_set(const float *x, int64_t rows, int C, int ld, float *out, dg_stream_t stream);
 /* g_out[0] = max over output channels co of sum over k of |w[k][co]| (w as [K][Co]: an HWIO
  * kernel with K = kh*kw*Cin), c_out[0] (may be NULL) = max |bias| (0 for bias NULL): the
  * terms of a conv output's bound for dg_conv_set_act_scale (y_g, y_c).  zero8 (may be NULL):
- * 8 floats zeroed on the way (the measured-max slot a following dg_absmax fills). */
+ * a max slot zeroed on the way (the measured-max slot a following dg_absmax fills). */
 int dg_weight_bound(const float *w, int64_t K, int Co, const float *bias, float *g_out, float *c_out,
                     float *zero8, dg_stream_t stream);
 /* g_out[0] = max over input channels ci of sum over taps and output channels of |w[tap][ci][co]|
@@ -341,13 +347,13 @@ int dg_bn_fwd_train_seg_h(int S, int M, int C, const float *y, int ldy, const fl
                           void *zp0, int zp0C, int zp0col, void *zp1, int zp1C, int zp1col,
                           const float *res, int ldres, void *z_f16,
                           void *ws, size_t ws_bytes, dg_stream_t stream);
-/* dg_bn_fwd_train_seg_h with bound-scaled fp16x3 z planes (round 5).  z_bound (8 floats,
+/* dg_bn_fwd_train_seg_h with bound-scaled fp16x3 z planes (round 5).  z_bound (a max slot,
  * zeroed and filled here; NULL: the static 2^-4): max over channels of (|gamma| invstd
  * max |y - mean| + |beta|) x the dropout keep scale >= max |z|, from per-chunk maxima of the
  * statistics pass -- the planes' scale source the consuming conv reads
  * (dg_conv_set_act_scale x_m = z_bound).  cp (may be NULL): cpC channels ([S*M rows], pixel
  * stride ldcp) of a second tensor whose planes go to zp0 at column cpcol with the same scale,
- * and cp_bound their bound (8 floats, merged into z_bound): the U-Net skip half of the
+ * and cp_bound their bound (a max slot, merged into z_bound): the U-Net skip half of the
  * concatenation the next ConvT reads (pix2pix.py:188), so one scale covers its whole operand. */
 int dg_bn_fwd_train_seg_x(int S, int M, int C, const float *y, int ldy, const float *gamma, const float *beta,
                           float *save_mean, float *save_invstd,
@@ -367,7 +373,7 @@ int dg_bn_bwd_seg_h(int S, int M, int C, const float *dz, int lddz, const float 
 /* dg_bn_bwd_seg_h with the format of the dy planes: DG_PLANES_F16X3 writes the consuming
  * DG_MATH_F16X3 conv's fp16x3 dy planes (C % 32 == 0), scaled by x3 scale 2^(14 - e) from
  * dy's bound b < 2^e -- b = max over channels of |A| max|dbn| + |B| max|y - mean| + |D|
- * >= max |dy| (dy = A dbn + B (y - mean) + D per channel), written into dy_bound (8 floats:
+ * >= max |dy| (dy = A dbn + B (y - mean) + D per channel), written into dy_bound (a max slot:
  * the bound's per-workgroup shards, their max is b) -- the buffer to pass that conv as its dy
  * scale source (dg_conv_set_grad_scale dy_m, dy_g NULL).  In the forward calls above a
  * NEGATIVE zp*C names the consumer's fp16x3 x planes of -zp*C channels (column and C

@@ -36,7 +36,7 @@ def run():
                      ("db", db))})
         if C % 32 == 0:
             planes = torch.zeros(S * M * C * 4, dtype=torch.uint8, device=dev)
-            bound = torch.zeros(8, device=dev)
+            bound = ops.max_slot(device=dev)
             dg2, db2 = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
             ops.bn_bwd(dz, z, y, gm, mean, inv, dy, dg2, db2, act="leaky_relu", alpha=0.3, segments=S,
                        dy_planes=planes, dy_bound=bound)

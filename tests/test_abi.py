@@ -64,6 +64,8 @@ def test_library_loads_without_gpu_and_reports_errors():
     from dgan import _lib
     L = _lib.lib()
     assert L.dg_version() == 1
+    from dgan import ops
+    assert L.dg_max_slot_floats() == ops.MAX_SLOT == 256   # include/dgan.h DG_MAX_SLOT
     h = ctypes.c_void_p()
     rc = L.dg_conv_desc_create(ctypes.byref(h), 0, 8, 8, 4, 4, 3, 3, 1, 1, 1, 1, 1, 1, 0)
     assert rc != 0

@@ -160,7 +160,7 @@ def test_bn_bwd_act_from_y_equals_from_z(act, planes):
         dy = torch.empty(1, 1, R, C, device=DEV)
         dg, db = torch.full((C,), 0.5, device=DEV), torch.full((C,), -0.25, device=DEV)
         pl = torch.zeros(R * C * 4, dtype=torch.uint8, device=DEV) if planes else None
-        bnd = torch.zeros(8, device=DEV) if planes else None
+        bnd = ops.max_slot(device=DEV) if planes else None
         ops.bn_bwd(dz, zz, y, g, mean, inv, dy, dg, db, act=act, alpha=0.3, beta=1.0, segments=S,
                    dy_planes=pl, dy_bound=bnd, offset=off)
         out.append((dy, dg, db, pl, bnd))

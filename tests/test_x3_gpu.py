@@ -114,7 +114,7 @@ def test_x3_shared_weight_planes_serve_bwd_data():
     holds no bf16x6 part (tensor_plane_bytes)."""
     N, H, W, Ci, Co = 2, 24, 32, 64, 128
     d = ops.ConvDesc(N, H, W, Ci, Co, 3, 1, "same", math="f16x3")
-    d.set_act_scale(x=(torch.zeros(8, device="cuda"),))   # held x planes: a plain max slot, measured
+    d.set_act_scale(x=(ops.max_slot(device="cuda"),))   # held x planes: a plain max slot, measured
     x, w, dy = _rand((N, H, W, Ci), 1), _rand(d.weight_shape, 2, 0.05), _rand((N, H, W, Co), 3)
     P = ops.ConvPlanes.for_desc(d, x=True, dy=True, w=True)
     assert P.w is not None and 4 * 9 * Ci * Co <= P.w.buf.numel() < 10 * 9 * Ci * Co
@@ -143,7 +143,7 @@ def test_x3_producer_planes_equal_the_split(prod_math):
     x = _rand((N, H, W, C0), 4)
     wa, wb = _rand(a.weight_shape, 5, 0.08), _rand(b.weight_shape, 6, 0.05)
     ba = _rand((C1,), 7, 0.1)
-    mx, wbd, ymx = torch.zeros(8, device="cuda"), torch.zeros(2, device="cuda"), torch.zeros(8, device="cuda")
+    mx, wbd, ymx = ops.max_slot(device="cuda"), torch.zeros(2, device="cuda"), ops.max_slot(device="cuda")
     ops.absmax_set(x, mx)
     ops.weight_bound(wa, wbd[0:1], bias=ba, c_out=wbd[1:2])
     src = (mx, wbd[0:1], wbd[1:2])
@@ -182,11 +182,11 @@ def test_x3_fused_pool_planes_and_unfused_pool(ptiles, monkeypatch):
     x, w, b = _rand((N, H, W, Ci), 8), _rand(d.weight_shape, 9, 0.06), _rand((Co,), 10, 0.1)
     wn = _rand(nxt.weight_shape, 11, 0.05)
     # the pooled planes' scale source: d's output bound (max |x|, d's weight bound, max |b|)
-    mx, wbd, pmx = torch.zeros(8, device="cuda"), torch.zeros(2, device="cuda"), torch.zeros(8, device="cuda")
+    mx, wbd, pmx = ops.max_slot(device="cuda"), torch.zeros(2, device="cuda"), ops.max_slot(device="cuda")
     ops.absmax_set(x, mx)
     ops.weight_bound(w, wbd[0:1], bias=b, c_out=wbd[1:2])
     src = (mx, wbd[0:1], wbd[1:2])
-    d.set_act_scale(x=(torch.zeros(8, device="cuda"),), y=src, y_max=pmx)
+    d.set_act_scale(x=(ops.max_slot(device="cuda"),), y=src, y_max=pmx)
     nxt.set_act_scale(x=src)
     y = torch.empty(N, H, W, Co, device="cuda")
     d.fwd(x, w, y, bias=b, act="relu")
@@ -290,7 +290,7 @@ def test_x3_input_gradient_chain_with_scale_context():
     za = conv2d_ref(xr, wa64, 1, a.pads, None) * mask
     yb = conv2d_ref(za, wb64, 1, b.pads, None)
     yb.backward(dy64)
-    gmax = torch.zeros(2, 8, device=dev)   # [A, B] x 8 atomic shards
+    gmax = ops.max_slot(2, device=dev)   # [A, B] max slots
     gwb = torch.stack([wa.abs().sum(dim=(0, 1, 3)).amax(), wb.abs().sum(dim=(0, 1, 3)).amax()])
     b.set_grad_scale(dy_m=gmax[1], dx_m=gmax[1], dx_g=gwb[1:2], dx_max=gmax[0])
     a.set_grad_scale(dy_m=gmax[1], dy_g=gwb[1:2])
