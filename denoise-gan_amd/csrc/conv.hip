@@ -1230,8 +1230,9 @@ struct OpPlan {
     int x6_ca, x6_cb;
     size_t x6_a_off, x6_b_off;
     // halo-tiled bf16x6 kernel (conv_x6h.hip): 1 = stride-1 3x3 FWD / DGRAD,
-    // 2 = stride-2 4x4 DGRAD phases; cfg = its BN, tiles of 8 x 16 output pixels
-    int halo, htx, hty;
+    // 2 = stride-2 4x4 DGRAD phases; cfg = its BN, tiles of hph x 16 output pixels
+    // (hph 8, or 16: the fp16x3 3x3 16 x 16 patch on 8 waves)
+    int halo, htx, hty, hph;
     // fp16x3 halo plans without split-K: patches per block (persistent blocks, conv_x6h.hip)
     int ptiles;
     // small-Cin 4x4 stride-2 kernels (conv_small.hip); WGRAD: conv-view output rows per block
@@ -1370,7 +1371,9 @@ static double choose_tiles(OpPlan &pl, const TileCfg *cfgs, int ncfg, double pea
     return best_t;
 }
 
-static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
+// x6_extra: seconds the split-precision path costs beyond its GEMM and split passes (plan_all:
+// a filter gradient whose operands no other op of the layer splits measures and splits both)
+static OpPlan make_plan(const ConvGeom &g, int mode, int math, double x6_extra = 0.0) {
     OpPlan pl{};
     if (mode == MODE_FWD) {
         pl.M = g.N * g.Ho * g.Wo; pl.N = g.Co; pl.K = g.kh * g.kw * g.Ci; pl.nphase = 1;
@@ -1479,7 +1482,7 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     if (x6_ok) {
         OpPlan p6 = pl;
         double t6 = choose_tiles(p6, kX6Cfgs, kNumX6Cfgs, 2516.6e12 / 6.0, "DG_FORCE_X6CFG");
-        t6 += (double)(ra * ca + rb * cb) * 10.0 / 4.0e12 + 4e-6;  // split passes: read 4 B, write 6 B
+        t6 += (double)(ra * ca + rb * cb) * 10.0 / 4.0e12 + 4e-6 + x6_extra;  // split passes: read 4 B, write 6 B
         // (the implicit-GEMM fp16x3 ops where the split path beats the fp32 tiles at all: on
         // pix2pix's deepest layers (M 32..128 rows) the fp32 tiles win; DG_FORCE_X3: every
         // eligible op, for the kernel tests at small sizes.  The halo kernel's fp16x3 3x3 layers
@@ -1548,8 +1551,20 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         else if (h33 || h44) { Hout = g.H; Wout = g.W; }
         else { Hout = (g.H + 1) / 2; Wout = (g.W + 1) / 2; }   // phase 0's grid, the largest
         pl.halo = h33 ? 1 : (h44 || f44 ? 4 : 2);
+        // fp16x3 3x3 on 16 x 16 patches (8 waves, one block per CU): the K >= 4096 layers (512
+        // reduction channels: VGG19 block4_conv2-4 forward and input gradient, 4-6 % faster, one
+        // stream) where the grid still fills the chip at one block per CU; the shorter-K layers ran
+        // 2-11 % slower on it (profiles/r6/ab_x3h_ph16.txt).  DG_X3H_PH=8|16 forces,
+        // DG_PLAN_DISABLE=x3h16: 8 x 16 everywhere
+        pl.hph = 8;
+        if (hx3 && Hout >= 16 && pl.K >= 4096 && !plan_off("x3h16")) {
+            const long t16 = (long)g.N * ((Wout + 15) / 16) * ((Hout + 15) / 16) * ((pl.N + 127) / 128);
+            pl.hph = t16 >= 256 ? 16 : 8;
+        }
+        if (hx3)
+            if (const char *e = getenv("DG_X3H_PH")) pl.hph = atoi(e) == 16 && Hout >= 16 ? 16 : 8;
         pl.htx = (Wout + 15) / 16;
-        pl.hty = (Hout + 7) / 8;
+        pl.hty = (Hout + pl.hph - 1) / pl.hph;
         // (4x4: BN 128 needs 93 KB of LDS -- one block per CU -- and measured 0.685 vs
         // 0.666 ms for BN 64, which keeps two)
         // (32 output columns, 3x3: BN 32 -- the SR family's 32-channel layers; a 64-wide tile
@@ -1564,6 +1579,7 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         // of (twice the) split-K, whose partial slabs and reduce launch cost more than the halved
         // tile -- VGG19 block5 at bs32 0.148 -> 0.140 ms fwd, 0.152 -> 0.142 bwd_data, block4_conv1
         // bwd_data 0.261 -> 0.255 (profiles/r5/ab_x3h_bn64.txt; DG_PLAN_DISABLE=x3h_bn64: BN 128)
+        if (pl.hph == 16) target /= 2;   // (one block per CU)
         if (hx3 && pl.cfg == 128 && (long)pl.mtiles * ((pl.N + 127) / 128) * pl.nphase < target &&
             !plan_off("x3h_bn64"))
             pl.cfg = 64;
@@ -1589,6 +1605,7 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
         if ((hx3 || hx3p || hx3q) && pl.splits == 1) {
             const long tot = (long)pl.mtiles * pl.ntiles * pl.nphase;
             long pdiv = hx3p || nch <= 4 ? 512 : 2048;
+            if (pl.hph == 16) pdiv /= 2;   // (one block per CU)
             if (const char *e = getenv("DG_X3H_PDIV")) pdiv = std::max(1L, atol(e));
             long pt = tot / pdiv;
             if (const char *e = getenv("DG_X3H_PTILES")) pt = atol(e);
@@ -1625,9 +1642,9 @@ static OpPlan make_plan(const ConvGeom &g, int mode, int math) {
     }
     pl.gemm_bytes = pl.ws_bytes;
     if (getenv("DG_PLAN_DEBUG"))
-        fprintf(stderr, "[dg plan] mode %d M=%d N=%d K=%d -> %s cfg %d splits %d\n", mode, pl.M, pl.N, pl.K,
+        fprintf(stderr, "[dg plan] mode %d M=%d N=%d K=%d -> %s cfg %d splits %d ph %d ptiles %d\n", mode, pl.M, pl.N, pl.K,
                 pl.halo == 2 ? (pl.x6 == 3 ? "x3h2" : "x6h2") : pl.halo == 4 ? "x6h4" : pl.halo ? (pl.x6 == 2 ? "f16h" : (pl.x6 == 3 ? "x3h" : "x6h")) : (pl.x6 == 2 ? "f16" : (pl.x6 == 3 ? "x3" : (pl.x6 ? "x6" : "fp32"))),
-                pl.cfg, pl.splits);
+                pl.cfg, pl.splits, pl.halo ? std::max(8, pl.hph) : 0, pl.ptiles);
     return pl;
 }
 
@@ -1704,7 +1721,18 @@ static size_t colsum_ws(long M, int C);
 static void plan_all(dg_conv_desc_s *d) {
     for (int op = 0; op < 3; ++op) {
         // (DG_MATH_F16X3: fp16x3 wherever make_plan finds the op eligible, bf16x6 elsewhere)
-        d->plan[op] = make_plan(d->g, engine_mode(d, op), d->math);
+        // A filter gradient reads the layer's input and output gradient, whose fp16x3 planes exist
+        // only where the forward / input gradient of the layer runs fp16x3 (the producers write
+        // them for those ops); otherwise its split path also zeroes a max slot and measures the
+        // operand (memset + absmax launches and a read) before splitting it -- G down7 / up2
+        // filter gradients: 37 us of passes around a 27-42 us GEMM (round 6, profiles/r6/calls.txt)
+        double extra = 0.0;
+        if (op == DG_OP_BWD_FILTER && d->math == DG_MATH_F16X3) {
+            const double xin = (double)d->N * d->H * d->W * d->Cin, gout = (double)d->N * d->Ho * d->Wo * d->Cout;
+            if (d->plan[DG_OP_FWD].x6 != 3) extra += 8e-6 + xin * 4.0 / 4.0e12;
+            if (d->plan[DG_OP_BWD_DATA].x6 != 3) extra += 8e-6 + gout * 4.0 / 4.0e12;
+        }
+        d->plan[op] = make_plan(d->g, engine_mode(d, op), d->math, plan_off("wgrad_extra") ? 0.0 : extra);
         plan_recast(d, op);
         if (d->rc[op].on) d->plan[op].ws_bytes = d->rc[op].bytes;
         if (op == DG_OP_BWD_FILTER) {
@@ -1844,7 +1872,7 @@ static bool pool_fusable(const dg_conv_desc_s *d, int act) {
     const OpPlan &pl = d->plan[DG_OP_FWD];
     return !d->transpose && (pl.x6 == 1 || pl.x6 == 3) && pl.halo == 1 && pl.cfg != 32 && pl.splits == 1 &&
            !d->rc[DG_OP_FWD].on &&
-           d->g.Ho % 8 == 0 &&
+           d->g.Ho % (pl.hph == 16 ? 16 : 8) == 0 &&
            d->g.Wo % 16 == 0 && d->g.Co % 16 == 0 &&
            (act == DG_ACT_NONE || act == DG_ACT_RELU || act == DG_ACT_LRELU);
 }
@@ -2112,7 +2140,8 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
         if (pl.halo) {
             // (persistent blocks: patch row mt0 + j * gm, j < ptiles, of each of the gm * ntiles blocks)
             grid.x = (unsigned)((pl.mtiles + a.ptiles - 1) / a.ptiles * pl.ntiles);
-            launch_gemm_x6h(mode, pl.cfg, pl.halo == 2 ? 2 : (pl.halo == 4 ? 4 : 3), grid, a, pl.htx, pl.hty, s, 4);
+            launch_gemm_x6h(mode, pl.cfg, pl.halo == 2 ? 2 : (pl.halo == 4 ? 4 : 3), grid, a, pl.htx, pl.hty, s, 4,
+                            pl.hph == 16 ? 16 : 8);
             DG_LAUNCHED("conv_gemm_x3h");
         } else {
             fastdiv_magic((unsigned)a.g.Wo, a.mg_wo, a.sh_wo);

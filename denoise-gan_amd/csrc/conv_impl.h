@@ -386,8 +386,9 @@ void launch_gemm_x6(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t
 // ni 3 bf16x6, 2 fp16 (DG_MATH_FP16), 4 fp16x3 (kt 3, bn 64 | 128; kt 2 phases; kt 4 stride-1 4x4
 // forward / input gradient, bn 64).
 // a.pidx != NULL selects the fused max-pool epilogue (FWD, one split, output Ho % 8 == 0, Wo % 16 == 0)
+// ph 16: the 16 x 16 patch on 8 waves (fp16x3 kt 3, bn 64 | 128)
 void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int tiles_x, int tiles_y, hipStream_t s,
-                     int ni = 3);
+                     int ni = 3, int ph = 8);
 // fp32 [rows][ld] (first C columns, C % 8 == 0) -> bf16 hi/mid/lo planes [rows][C]
 void launch_split3(const float *src, int ld, long rows, int C, unsigned short *dst, hipStream_t s);
 // fp32 [rows][ld] -> fp16x3 planes (common.h): per group of G columns (32: activations,

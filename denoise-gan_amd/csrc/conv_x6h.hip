@@ -70,9 +70,9 @@ constexpr int kMidb = 3;
 // PACKED (fp16x3): the NPL plane images lie back to back (HPX * 32 bytes each) and
 // only the whole halo is rounded up to KiB DMAs -- 23 KiB instead of 24 for KT 3,
 // which keeps two fp16x3 blocks (two halo buffers, two weight buffers) per CU
-template <int KT, int NPL = 3, bool PACKED = false>
+template <int KT, int NPL = 3, bool PACKED = false, int PH = HX_PH>
 struct HaloGeom {
-    static constexpr int HH = HX_PH + KT - 1, HW = HX_PW + KT - 1;
+    static constexpr int HH = PH + KT - 1, HW = HX_PW + KT - 1;
     static constexpr int HPX = HH * HW;
     static constexpr int HPL = PACKED ? HPX * 32 : (HPX * 32 + 1023) / 1024 * 1024;  // bytes per plane image
     static constexpr int BYTES = (NPL * HPL + 1023) / 1024 * 1024;                   // bytes per halo buffer
@@ -94,7 +94,7 @@ struct HaloGeom {
 // element: its bf16x6 planes (the next conv's x operand), optionally its
 // fp32 value, and one byte {argmax, value > 0} for the backward -- the
 // full-size activation is never written.
-template <int TM, int TN>
+template <int TM, int TN, int PH = HX_PH>
 __device__ __forceinline__ void conv_epilogue16_pool(const GemmArgs &p, f32x4 (&acc)[TM][TN], int prow0, int cbase,
                                                      int ty, int tx, int nimg, int lane, float *stage,
                                                      float ys_pre = 0.f, float *vacc = nullptr) {
@@ -156,7 +156,7 @@ __device__ __forceinline__ void conv_epilogue16_pool(const GemmArgs &p, f32x4 (&
                 fi |= (id | (fv[q] > 0.f ? 4u : 0u)) << (8 * q);
             }
             if (!lead || !colok) continue;
-            const int ho2 = (ty * HX_PH + prow0 + a) >> 1, wo2 = (tx * HX_PW + rl) >> 1;
+            const int ho2 = (ty * PH + prow0 + a) >> 1, wo2 = (tx * HX_PW + rl) >> 1;
             const long pp = ((long)nimg * Ho2 + ho2) * Wo2 + wo2;
             *reinterpret_cast<unsigned *>(p.pidx + pp * p.N + col) = fi;
             if (p.pool_y) *reinterpret_cast<f32x4 *>(p.pool_y + pp * p.ldpy + col) = fv;
@@ -187,8 +187,14 @@ __device__ __forceinline__ void for_taps(F &&f, std::integer_sequence<int, T...>
 // (= h.w_h + l.w_h + h.w_l) -- two A and two B fragment reads per K-tile.  Two
 // weight buffers and packed halo images keep two blocks per CU; a K-tile's buffer
 // takes tile T+2 once every wave holds its fragments (MIDB).
-template <int MODE, int BN, bool POOL, int KT, int NI = 3>
-__global__ void __launch_bounds__(256, 2)
+//
+// PH = 16 (fp16x3 3x3 only): a 16 x 16 patch -- 256 GEMM rows -- on 8 waves (4 x 2), one block per
+// CU: every weight K-tile staged in LDS feeds twice the rows, halving the weight traffic per MFMA
+// that the 8 x 16 patch's two blocks per CU each stream (no weight DMAs ran the deep VGG19 layers
+// 13-35 % faster, profiles/r5/pmc_x6h_waits.txt), and the halo overhead drops from 180 to 162
+// pixels per 128 outputs.
+template <int MODE, int BN, bool POOL, int KT, int NI = 3, int PH = HX_PH>
+__global__ void __launch_bounds__(32 * PH, PH == HX_PH ? 2 : 1)
 k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     static_assert(MODE == MODE_FWD || MODE == MODE_DGRAD, "forward or input gradient");
     static_assert(!POOL || MODE == MODE_FWD, "the pool epilogue is a forward epilogue");
@@ -197,8 +203,9 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     static_assert(NI == 3 || (NI == 2 && KT == 3 && !POOL) || (NI == 4 && (KT == 3 || KT == 4 || (KT == 2 && MODE == MODE_DGRAD))),
                   "fp16: 3x3 stride 1, no pool epilogue; fp16x3: 3x3 stride 1, or the stride-2 4x4 input-gradient phases");
     constexpr bool X3 = NI == 4;
+    static_assert(PH == HX_PH || (PH == 16 && X3 && KT == 3), "the 16 x 16 patch: fp16x3 3x3 only");
     constexpr int NPL = NI == 3 ? 3 : (X3 ? 4 : 2);   // plane images per chunk
-    using HG = HaloGeom<KT, NPL, X3>;
+    using HG = HaloGeom<KT, NPL, X3, PH>;
     constexpr int NTAP = HG::NTAP;
     // weight K-tile buffers: a tap position owns one (bf16x6 / fp16: two tiles in
     // flight); fp16x3: two buffers alternating by tap and chunk, one tile ahead
@@ -206,12 +213,14 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     // tile has two K-tiles of MFMAs to land; DG_X3H_NB2: two, for same-box A/B)
 #ifdef DG_X3H_NB2
     constexpr int NB = X3 ? 2 : (NTAP % 3 == 0 ? 3 : 4);
+#elif defined(DG_X3H16_NB)   // (the 16 x 16 patch's weight buffers, for same-box A/B)
+    constexpr int NB = X3 ? (PH == 16 ? DG_X3H16_NB : ((KT == 3 && BN == 64) ? 3 : 2)) : (NTAP % 3 == 0 ? 3 : 4);
 #else
     constexpr int NB = X3 ? ((KT == 3 && BN == 64) ? 3 : 2) : (NTAP % 3 == 0 ? 3 : 4);
 #endif
     constexpr bool XPAR = X3 && NB == 2;   // buffers alternate by K-tile parity (NTAP odd: across chunks)
     static_assert(XPAR || NTAP % NB == 0, "tap positions line up with the weight buffers across chunks");
-    constexpr int BK = NI == 3 ? 16 : 32, NW = 4;   // channels per chunk
+    constexpr int BK = NI == 3 ? 16 : 32, NW = PH / 2;   // channels per chunk; waves
     constexpr int WTM = 64, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
     constexpr bool B_KC = MODE == MODE_DGRAD;
     constexpr int BPL = BN * 32 + 96, BBUF = NPL * BPL;
@@ -304,7 +313,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
             const int t_ = mt / tiles_x;
             t.ty = t_ % tiles_y;
             t.nimg = t_ / tiles_y;
-            if (t.ty * HX_PH < Hout && t.tx * HX_PW < Wout) return j;
+            if (t.ty * PH < Hout && t.tx * HX_PW < Wout) return j;
         }
         return -1;
     };
@@ -378,7 +387,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
     // h[32] l[32], image pl = 16 values at 16 pl)
     constexpr int PXS = NI == 3 ? 3 : (X3 ? 2 : 1);   // pixel stride in units of lda
     auto halo_offsets = [&](const HTile &t, int (&ho)[H_NJ]) __attribute__((always_inline)) {
-        const int oy = MODE == MODE_FWD ? t.ty * HX_PH - g.pt : t.ty * HX_PH + oh - (KT - 1);
+        const int oy = MODE == MODE_FWD ? t.ty * PH - g.pt : t.ty * PH + oh - (KT - 1);
         const int ox = MODE == MODE_FWD ? t.tx * HX_PW - g.pl : t.tx * HX_PW + ow - (KT - 1);
 #pragma unroll
         for (int s = 0; s < H_NJ; ++s) {
@@ -648,7 +657,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         // patch row -> output pixel; slab rows: FWD / stride-1 DGRAD pixels, a
         // phase's GEMM rows otherwise (as k_splitk_reduce maps them)
         auto rowmap = [&](int row) __attribute__((always_inline)) -> RowPix {
-            const int ho = ty * HX_PH + (row >> 4), wo = tx * HX_PW + (row & 15);
+            const int ho = ty * PH + (row >> 4), wo = tx * HX_PW + (row & 15);
             if (ho >= Hout || wo >= Wout) return RowPix{-1, -1};
             if constexpr (MODE == MODE_DGRAD && KT == 2) {
                 const long pix = ((long)nimg * g.H + ho * g.sh + ph.ph) * g.W + wo * g.sw + ph.pw;
@@ -670,7 +679,7 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
         const GemmArgs &pe = p;
 #endif
         if constexpr (POOL)
-            conv_epilogue16_pool<TM, TN>(pe, acc, wm * TM, n0 + wn * WTN, ty, tx, nimg, lane, stage, ys_pre, va);
+            conv_epilogue16_pool<TM, TN, PH>(pe, acc, wm * TM, n0 + wn * WTN, ty, tx, nimg, lane, stage, ys_pre, va);
         else
             conv_epilogue16<MODE, TM, TN>(pe, acc, wm * WTM, n0 + wn * WTN, rowmap, phase, split, lane, stage, ys_pre,
                                           va);
@@ -717,8 +726,24 @@ k_conv_gemm_x6h(const GemmArgs p, int tiles_x, int tiles_y) {
 }
 
 void launch_gemm_x6h(int mode, int bn, int kt, dim3 grid, const GemmArgs &a, int tiles_x, int tiles_y, hipStream_t s,
-                     int ni) {
+                     int ni, int ph) {
     const dim3 blk(256);
+    if (ph == 16) {   // fp16x3 3x3 on the 16 x 16 patch (8 waves)
+        const dim3 b16(512);
+#define DG_X3H16(M_, B_, P_) hipLaunchKernelGGL((k_conv_gemm_x6h<M_, B_, P_, 3, 4, 16>), grid, b16, 0, s, a, tiles_x, tiles_y)
+        if (mode == MODE_FWD && a.pidx) {
+            if (bn == 128) DG_X3H16(MODE_FWD, 128, true);
+            else DG_X3H16(MODE_FWD, 64, true);
+        } else if (mode == MODE_FWD) {
+            if (bn == 128) DG_X3H16(MODE_FWD, 128, false);
+            else DG_X3H16(MODE_FWD, 64, false);
+        } else {
+            if (bn == 128) DG_X3H16(MODE_DGRAD, 128, false);
+            else DG_X3H16(MODE_DGRAD, 64, false);
+        }
+#undef DG_X3H16
+        return;
+    }
 #define DG_X6H(M_, B_, P_, K_) hipLaunchKernelGGL((k_conv_gemm_x6h<M_, B_, P_, K_>), grid, blk, 0, s, a, tiles_x, tiles_y)
 #define DG_F16H(M_, B_) hipLaunchKernelGGL((k_conv_gemm_x6h<M_, B_, false, 3, 2>), grid, blk, 0, s, a, tiles_x, tiles_y)
 #define DG_X3H(B_, P_) hipLaunchKernelGGL((k_conv_gemm_x6h<MODE_FWD, B_, P_, 3, 4>), grid, blk, 0, s, a, tiles_x, tiles_y)

@@ -107,6 +107,41 @@ def test_x3_persistent_blocks_match_fp64(case, pt, monkeypatch):
     test_conv_layer(case, "f16x3")
 
 
+# the 16 x 16 patch on 8 waves (conv_x6h.hip PH 16, round 6): forced on the 3x3 halo cases
+# (ragged 21 x 37 and 'valid' 20 x 22 images, BN 64 / 128, Cout 48; x3.splitk's 8 x 8 image
+# keeps the 8 x 16 patch), one patch per block and 3 per block; the fp64 bar, and bit-identity
+# with the 8 x 16 patch -- each output's K-tiles and MFMAs run in the same order on both
+X3_PH16_CASES = [(c, pt) for c in X3_CASES[:6] for pt in (None, 3)]
+
+
+@gpu
+@pytest.mark.parametrize("case,pt", X3_PH16_CASES, ids=[f"{c[0]}-pt{pt}" for c, pt in X3_PH16_CASES])
+def test_x3_16x16_patch_matches_fp64_and_the_8x16_patch(case, pt, monkeypatch, capfd):
+    monkeypatch.delenv("DG_PLAN_DISABLE", raising=False)
+    if pt:
+        monkeypatch.setenv("DG_X3H_PTILES", str(pt))
+    monkeypatch.setenv("DG_X3H_PH", "16")
+    monkeypatch.setenv("DG_PLAN_DEBUG", "1")
+    test_conv_layer(case, "f16x3")
+    name, N, H, W, Cin, Cout, k, s, padding, transpose, bias = case
+    d16 = ops.ConvDesc(N, H, W, Cin, Cout, k, s, padding, transpose, math="f16x3")
+    err = capfd.readouterr().err
+    fwd_plan = [l for l in err.splitlines() if l.startswith("[dg plan] mode 0") and "x3h" in l][-1]
+    assert (" ph 16 " in fwd_plan) == (H >= 16), fwd_plan
+    monkeypatch.setenv("DG_X3H_PH", "8")
+    d8 = ops.ConvDesc(N, H, W, Cin, Cout, k, s, padding, transpose, math="f16x3")
+    x, w = _rand((N, H, W, Cin), 11), _rand(d16.weight_shape, 12, 0.05)
+    dy = _rand(d16.out_shape, 13)
+    ys = [torch.empty(d16.out_shape, device="cuda") for _ in range(2)]
+    dxs = [torch.empty_like(x) for _ in range(2)]
+    for d, y, dx in zip((d16, d8), ys, dxs):
+        d.fwd(x, w, y)
+        d.bwd_data(dy, w, dx)
+    torch.cuda.synchronize()
+    assert torch.equal(ys[0], ys[1]), f"{name}: forward differs between the 16x16 and 8x16 patches"
+    assert torch.equal(dxs[0], dxs[1]), f"{name}: input gradient differs between the 16x16 and 8x16 patches"
+
+
 @gpu
 def test_x3_shared_weight_planes_serve_bwd_data():
     """One weight PlaneBuf: the fp16x3 forward splits it; the (fp16x3) input gradient reading
@@ -168,13 +203,15 @@ def test_x3_producer_planes_equal_the_split(prod_math):
 
 
 @gpu
-@pytest.mark.parametrize("ptiles", ["1", "3"])
-def test_x3_fused_pool_planes_and_unfused_pool(ptiles, monkeypatch):
+@pytest.mark.parametrize("ptiles,ph", [("1", "8"), ("3", "8"), ("1", "16"), ("3", "16")])
+def test_x3_fused_pool_planes_and_unfused_pool(ptiles, ph, monkeypatch):
     """An fp16x3 conv with its 2x2 max pool fused (pool_fusable) writes the next fp16x3
     conv's x planes; so does the unfused pool (dg_maxpool2_fwd_plf).  Both equal the
     consumer's own split, and the pooled values equal conv -> pool -- with one patch per
-    block and with persistent blocks of 3 patches (their max |pooled| folded across patches)."""
+    block and with persistent blocks of 3 patches (their max |pooled| folded across patches),
+    on the 8 x 16 and the 16 x 16 patch."""
     monkeypatch.setenv("DG_X3H_PTILES", ptiles)
+    monkeypatch.setenv("DG_X3H_PH", ph)
     N, H, W, Ci, Co, Cn = 4, 32, 32, 64, 128, 128
     d = ops.ConvDesc(N, H, W, Ci, Co, 3, 1, "same", math="f16x3")
     nxt = ops.ConvDesc(N, H // 2, W // 2, Co, Cn, 3, 1, "same", math="f16x3")
