@@ -411,22 +411,47 @@ k_splitk_reduce(const GemmArgs p, int V4) {
     const float ys = p.yp ? plane_scale(p) : 0.f;
     float vmax = 0.f;   // max |output| of this lane (p.ymax)
     if (V4) {  // N % 4 == 0, ldc % 4 == 0, 16-byte aligned C: float4 outputs, V4 lanes per output
-        const int tpo = V4;  // power of two <= 16: lane j sums slabs j, j+tpo, ...; fixed butterfly after
-        const int lane = threadIdx.x & (tpo - 1);
+        // tpo = V4 (a power of two <= 64) lanes per output: the block's 256 threads are opb = 256 / tpo
+        // consecutive outputs x tpo split lanes, lane j summing slabs j, j + tpo, ... in order (four
+        // loads in flight) -- a wave's 64 lanes read opb consecutive float4 of one slab -- then lane 0
+        // adds the lanes' sums in lane order through LDS.  (Round 5 interleaved the tpo lanes of one
+        // output inside a wave: 16 scattered 64-byte pieces per load, one load in flight per lane --
+        // 2.3 TB/s on the filter gradients' 32 MB of partials, profiles/r6/reduce_args.txt.)
+        const int tpo = V4, opb = 256 / tpo;
+        const int o = threadIdx.x % opb, j = threadIdx.x / opb;
+        __shared__ f32x4 red[256];
         const int N4 = p.N >> 2;
         const long total = (long)Mrows * N4;
-        const long stride = ((long)gridDim.x * blockDim.x) / tpo;
-        for (long e = ((long)blockIdx.x * blockDim.x + threadIdx.x) / tpo; e < total; e += stride) {
-            const int row = (int)(e / N4);
-            const int col = (int)(e - (long)row * N4) * 4;
-            const float *src = base + (long)row * p.N + col;
+        const long step = (long)tpo * plane;
+        for (long e0 = (long)blockIdx.x * opb; e0 < total; e0 += (long)gridDim.x * opb) {   // (block-uniform)
+            const long e = e0 + o;
             f32x4 v = {0.f, 0.f, 0.f, 0.f};
-            for (int s = lane; s < p.splits; s += tpo) v += *reinterpret_cast<const f32x4 *>(src + s * plane);
-            for (int o = tpo >> 1; o >= 1; o >>= 1) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] += __shfl_xor(v[q], o);
+            int row = 0, col = 0;
+            if (e < total) {
+                row = (int)(e / N4);
+                col = (int)(e - (long)row * N4) * 4;
+                const float *src = base + (long)row * p.N + col + (long)j * plane;
+                int s = j;
+                for (; s + 3 * tpo < p.splits; s += 4 * tpo, src += 4 * step) {
+                    const f32x4 a0 = *reinterpret_cast<const f32x4 *>(src);
+                    const f32x4 a1 = *reinterpret_cast<const f32x4 *>(src + step);
+                    const f32x4 a2 = *reinterpret_cast<const f32x4 *>(src + 2 * step);
+                    const f32x4 a3 = *reinterpret_cast<const f32x4 *>(src + 3 * step);
+                    v += a0;
+                    v += a1;
+                    v += a2;
+                    v += a3;
+                }
+                for (; s < p.splits; s += tpo, src += step) v += *reinterpret_cast<const f32x4 *>(src);
             }
-            if (lane != 0) continue;
+            if (tpo > 1) {
+                red[threadIdx.x] = v;
+                __syncthreads();
+                if (j == 0)
+                    for (int k = 1; k < tpo; ++k) v += red[k * opb + o];
+                __syncthreads();
+            }
+            if (j != 0 || e >= total) continue;
             long pix;
             if constexpr (MODE == MODE_DGRAD) {
                 int ww = row % ph.Wp; int t = row / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
@@ -435,22 +460,22 @@ k_splitk_reduce(const GemmArgs p, int V4) {
                 pix = row;
             }
             const long off = pix * p.ldc;
-            f32x4 o, mf;
+            f32x4 ov, mf;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 float x = v[q];
                 if (p.bias) x += p.bias[col + q];
                 mf[q] = epi_mask_factor(p, pix, col + q);
-                o[q] = act_fwd(x, p.act, p.alpha) * mf[q];
+                ov[q] = act_fwd(x, p.act, p.alpha) * mf[q];
             }
             if (p.C) {
                 f32x4 *dst = reinterpret_cast<f32x4 *>(p.C + off + col);
-                if (p.beta != 0.f) o += p.beta * (p.mask_acc ? (*dst) * mf : (*dst));
-                *dst = o;
+                if (p.beta != 0.f) ov += p.beta * (p.mask_acc ? (*dst) * mf : (*dst));
+                *dst = ov;
             }
-            if (p.yp) store_planes4(p.yp, p.ypC, pix, col, o, ys);
+            if (p.yp) store_planes4(p.yp, p.ypC, pix, col, ov, ys);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) vmax = fmaxf(vmax, fabsf(o[q]));
+            for (int q = 0; q < 4; ++q) vmax = fmaxf(vmax, fabsf(ov[q]));
         }
         if (p.ymax) block_atomic_absmax(p.ymax, vmax);
         return;
@@ -2233,10 +2258,12 @@ static int run_gemm(int mode, const OpPlan &pl, const GemmArgs &a_in, hipStream_
 static int finish_splitk(int mode, const OpPlan &pl, const GemmArgs &a, hipStream_t s) {
     if (pl.splits > 1) {
         // float4 outputs with tpo lanes per output (tpo = 0 -> scalar path)
+        // (tpo lanes per float4 output until ~256K threads read the slabs, each lane summing >= 4)
         int tpo = 0;
         if ((pl.N % 4 == 0) && (a.ldc % 4 == 0) && ((((uintptr_t)a.C) | ((uintptr_t)a.slab)) & 15) == 0) {
             tpo = 1;
-            while (tpo < 16 && tpo * 4 <= pl.splits) tpo <<= 1;
+            const long E = (long)pl.M * pl.N / 4 * pl.nphase;
+            while (tpo < 64 && tpo * 4 <= pl.splits && E * tpo < 262144) tpo <<= 1;
         }
         const int v4 = tpo;
         long total = tpo ? (long)pl.M * pl.N / 4 * tpo : (long)pl.M * pl.N;

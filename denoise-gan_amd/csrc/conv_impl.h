@@ -292,7 +292,16 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
         for (int b = 0; b < TN; ++b)
 #pragma unroll
             for (int r = 0; r < 4; ++r) stage[(4 * (lane >> 4) + r) * LD + b * 16 + (lane & 15)] = acc[a][b][r];
+        // (the passes read the staged rows back from LDS, so they need no unrolling: one pass body
+        // per accumulator row block keeps the epilogue's code -- inlined once or twice per kernel,
+        // executed once per tile -- a quarter of the fully unrolled form's, which ran to ~100 KB of the
+        // 250 KB fp16x3 halo kernels against a 64 KB instruction cache.  DG_EPI_UNROLL_PASSES: the
+        // unrolled form, for same-box A/B)
+#ifdef DG_EPI_UNROLL_PASSES
 #pragma clang loop unroll(full)
+#else
+#pragma clang loop unroll(disable)
+#endif
         for (int pass = 0; pass < 16 / RPP; ++pass) {
             const int rl = pass * RPP + lane / C4;
             const f32x4 v = *reinterpret_cast<const f32x4 *>(stage + rl * LD + c4 * 4);
