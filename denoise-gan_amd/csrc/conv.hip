@@ -391,7 +391,18 @@ k_conv_gemm(const GemmArgs p) {
         __syncthreads();
     }
 
-    conv_epilogue<MODE, TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, Mrows, ph, phase, split, l32, h2);
+    // (the loop's last barrier: every wave is done with smem, which now stages the epilogue)
+    static_assert(4 * 32 * 36 <= 2 * (ASZ + BSZ), "epilogue staging fits in the operand tiles");
+    auto rowmap = [&](int row) __attribute__((always_inline)) -> RowPix {
+        if (row >= Mrows) return RowPix{-1, -1};
+        if constexpr (MODE == MODE_DGRAD) {
+            int ww = row % ph.Wp; int t = row / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
+            return RowPix{row, (long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw};
+        } else {
+            return RowPix{row, row};
+        }
+    };
+    conv_epilogue32<MODE, TM, TN>(p, acc, m0 + wm * WTM, n0 + wn * WTN, rowmap, phase, split, lane, smem + wid * 32 * 36);
 }
 
 // split-K reduction + epilogue (deterministic: slabs summed in split order)

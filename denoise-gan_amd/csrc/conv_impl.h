@@ -206,59 +206,113 @@ __device__ __forceinline__ PhaseInfo phase_info(const ConvGeom &g, int phase, in
     return q;
 }
 
-// Shared epilogue of the GEMM kernels: a wave's TM x TN 32x32 accumulator
-// tiles (MFMA C layout: col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5))
-// written either to its split-K slab or through bias + activation + beta
-// accumulation into C (DGRAD rows scattered back to their phase pixels).
-template <int MODE, int TM, int TN>
-__device__ __forceinline__ void conv_epilogue(const GemmArgs &p, f32x16 (&acc)[TM][TN], int rbase, int cbase,
-                                              int Mrows, const PhaseInfo &ph, int phase, int split, int l32, int h2) {
-    const ConvGeom &g = p.g;
-    float vmax = 0.f;   // max |output| of this lane (p.ymax)
-    const float ys = p.yp ? plane_scale(p) : 0.f;
-#pragma clang loop unroll(full)
-    for (int a = 0; a < TM; ++a) {
-#pragma clang loop unroll(full)
-        for (int b = 0; b < TN; ++b) {
-            const int col = cbase + b * 32 + l32;
-            if (col >= p.N) continue;
-#pragma clang loop unroll(full)
-            for (int r = 0; r < 16; ++r) {
-                const int row = rbase + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h2;
-                if (row >= Mrows) continue;
-                float v = acc[a][b][r];
-                if (p.splits > 1) {
-                    p.slab[((long)(phase * p.splits + split) * p.M + row) * p.N + col] = v;
-                } else {
-                    long pix;
-                    if constexpr (MODE == MODE_DGRAD) {
-                        int ww = row % ph.Wp; int t = row / ph.Wp; int hh = t % ph.Hp; int n = t / ph.Hp;
-                        pix = (long)(n * g.H + hh * g.sh + ph.ph) * g.W + ww * g.sw + ph.pw;
-                    } else {
-                        pix = row;
-                    }
-                    const long off = pix * p.ldc;
-                    if (p.bias) v += p.bias[col];
-                    v = act_fwd(v, p.act, p.alpha);
-                    v = epi_mask(p, pix, col, v);
-                    if (p.C) {
-                        if (p.beta != 0.f) v += p.beta * p.C[off + col];
-                        p.C[off + col] = v;
-                    }
-                    if (p.yp) store_planes1(p.yp, p.ypC, pix, col, v, ys);
-                    vmax = fmaxf(vmax, fabsf(v));
-                }
-            }
-        }
-    }
-    if (p.ymax) block_atomic_absmax(p.ymax, vmax);
-}
-
 // Row of a GEMM tile -> (row of the split-K slab, output pixel); slab < 0
 // marks a row outside the output.
 struct RowPix {
     long slab, pix;
 };
+
+// The same for 16x16 accumulator tiles (v_mfma_f32_16x16x32_bf16 C layout:
+// col = lane&15, row = 4(lane>>4) + r), staged through LDS: the wave writes
+// 16 rows of its tile at a time into `stage` (16 x (16*TN + 4) floats, its
+// own region) and reads them back row-contiguous, so every global access is
+// 16 bytes per lane (C, the split-K slab, beta*C and the gradient mask) and
+// the row -> pixel map (`rowmap(rbase + local row)` -> RowPix) is evaluated
+// once per row per lane.
+// What the GEMM epilogues hoist per call (epi_out4)
+struct EpiCtx {
+    bool cvec, mvec, svec;   // 16-byte C / gradient mask / split-K slab access possible
+    float ys;                // the output planes' scale
+};
+__device__ __forceinline__ EpiCtx epi_ctx(const GemmArgs &p, float ys_pre) {
+    EpiCtx e;
+    e.cvec = ((p.ldc & 3) == 0) && ((((uintptr_t)p.C) & 15) == 0);
+    e.mvec = ((p.ldmz & 3) == 0) && ((((uintptr_t)p.mz) & 15) == 0);
+    e.svec = ((p.N & 3) == 0) && ((((uintptr_t)p.slab) & 15) == 0);
+    e.ys = p.yp ? (ys_pre > 0.f ? ys_pre : plane_scale(p)) : 0.f;
+    return e;
+}
+
+// Output columns col .. col+3 of GEMM row rp (staged accumulators v): the split-K slab, or bias +
+// activation + gradient mask + beta*C into C, the consumer's planes and the max |output|.
+__device__ __forceinline__ void epi_out4(const GemmArgs &p, const EpiCtx &e, const RowPix &rp, int col, const f32x4 &v,
+                                         int phase, int split, float &vmax) {
+    if (rp.slab < 0 || col >= p.N) return;
+    const bool full = col + 3 < p.N;
+    if (p.splits > 1) {
+        float *dst = p.slab + ((long)(phase * p.splits + split) * p.M + rp.slab) * p.N + col;
+        if (e.svec && full) {
+            *reinterpret_cast<f32x4 *>(dst) = v;
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (col + q < p.N) dst[q] = v[q];
+        }
+        return;
+    }
+    const long pix = rp.pix;
+    float *dst = p.C + pix * p.ldc + col;
+    f32x4 o = v;
+    if (p.bias) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] += (col + q < p.N) ? p.bias[col + q] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = act_fwd(o[q], p.act, p.alpha);
+    f32x4 mf = {1.f, 1.f, 1.f, 1.f};   // the mask factors (p.mask_acc: beta*C's too)
+    if (p.mz) {
+        const float *mz = p.mz + pix * p.ldmz + col;
+        f32x4 z;
+        if (e.mvec && full) {
+            z = *reinterpret_cast<const f32x4 *>(mz);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) z[q] = (col + q < p.N) ? mz[q] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) mf[q] = act_grad_from_out(z[q], p.mact, p.malpha);
+        o *= mf;
+    } else if (p.mzp) {
+        f32x4 z;
+        if (full) {
+            z = hi_plane4(p.mzp, p.mzpC, pix, col);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) z[q] = (col + q < p.N) ? hi_plane(p.mzp, p.mzpC, pix, col + q) : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) mf[q] = act_grad_from_out(z[q], p.mact, p.malpha);
+        o *= mf;
+    }
+    if (!p.C) {
+        // planes-only output (dg_conv_fwd_pl with y == NULL, beta 0)
+    } else if (e.cvec && full) {
+        if (p.beta != 0.f) {
+            const f32x4 c = *reinterpret_cast<const f32x4 *>(dst);
+            o += p.beta * (p.mask_acc ? c * mf : c);
+        }
+        *reinterpret_cast<f32x4 *>(dst) = o;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (col + q < p.N)
+                o[q] = dst[q] = p.beta != 0.f ? o[q] + p.beta * (p.mask_acc ? dst[q] * mf[q] : dst[q]) : o[q];
+    }
+    if (p.yp) {
+        if (full) {
+            store_planes4(p.yp, p.ypC, pix, col, o, e.ys);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (col + q < p.N) store_planes1(p.yp, p.ypC, pix, col + q, o[q], e.ys);
+        }
+    }
+    if (p.ymax) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (col + q < p.N) vmax = fmaxf(vmax, fabsf(o[q]));
+    }
+}
 
 // The same for 16x16 accumulator tiles (v_mfma_f32_16x16x32_bf16 C layout:
 // col = lane&15, row = 4(lane>>4) + r), staged through LDS: the wave writes
@@ -278,13 +332,9 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
     constexpr int C4 = WTN / 4;   // float4 per row
     constexpr int RPP = 64 / C4;  // rows per pass of the wave
     static_assert(64 % C4 == 0 && 16 % RPP == 0, "wave tile width");
-    const bool cvec = ((p.ldc & 3) == 0) && ((((uintptr_t)p.C) & 15) == 0);
-    const bool mvec = ((p.ldmz & 3) == 0) && ((((uintptr_t)p.mz) & 15) == 0);
-    const bool svec = ((p.N & 3) == 0) && ((((uintptr_t)p.slab) & 15) == 0);
+    const EpiCtx e = epi_ctx(p, ys_pre);
     const int c4 = lane % C4;
     const int col = cbase + c4 * 4;
-    const bool full = col + 3 < p.N;
-    const float ys = p.yp ? (ys_pre > 0.f ? ys_pre : plane_scale(p)) : 0.f;
     float vmax = 0.f;   // max |output| of this lane (p.ymax)
 #pragma clang loop unroll(full)
     for (int a = 0; a < TM; ++a) {
@@ -305,87 +355,42 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
         for (int pass = 0; pass < 16 / RPP; ++pass) {
             const int rl = pass * RPP + lane / C4;
             const f32x4 v = *reinterpret_cast<const f32x4 *>(stage + rl * LD + c4 * 4);
-            const RowPix rp = rowmap(rbase + a * 16 + rl);
-            if (rp.slab < 0 || col >= p.N) continue;
-            if (p.splits > 1) {
-                float *dst = p.slab + ((long)(phase * p.splits + split) * p.M + rp.slab) * p.N + col;
-                if (svec && full) {
-                    *reinterpret_cast<f32x4 *>(dst) = v;
-                } else {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        if (col + q < p.N) dst[q] = v[q];
-                }
-                continue;
-            }
-            const long pix = rp.pix;
-            float *dst = p.C + pix * p.ldc + col;
-            f32x4 o = v;
-            if (p.bias) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) o[q] += (col + q < p.N) ? p.bias[col + q] : 0.f;
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] = act_fwd(o[q], p.act, p.alpha);
-            f32x4 mf = {1.f, 1.f, 1.f, 1.f};   // the mask factors (p.mask_acc: beta*C's too)
-            if (p.mz) {
-                const float *mz = p.mz + pix * p.ldmz + col;
-                f32x4 z;
-                if (mvec && full) {
-                    z = *reinterpret_cast<const f32x4 *>(mz);
-                } else {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) z[q] = (col + q < p.N) ? mz[q] : 0.f;
-                }
-#pragma unroll
-                for (int q = 0; q < 4; ++q) mf[q] = act_grad_from_out(z[q], p.mact, p.malpha);
-                o *= mf;
-            } else if (p.mzp) {
-                f32x4 z;
-                if (full) {
-                    z = hi_plane4(p.mzp, p.mzpC, pix, col);
-                } else {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) z[q] = (col + q < p.N) ? hi_plane(p.mzp, p.mzpC, pix, col + q) : 0.f;
-                }
-#pragma unroll
-                for (int q = 0; q < 4; ++q) mf[q] = act_grad_from_out(z[q], p.mact, p.malpha);
-                o *= mf;
-            }
-            if (!p.C) {
-                // planes-only output (dg_conv_fwd_pl with y == NULL, beta 0)
-            } else if (cvec && full) {
-                if (p.beta != 0.f) {
-                    const f32x4 c = *reinterpret_cast<const f32x4 *>(dst);
-                    o += p.beta * (p.mask_acc ? c * mf : c);
-                }
-                *reinterpret_cast<f32x4 *>(dst) = o;
-            } else {
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    if (col + q < p.N)
-                        o[q] = dst[q] = p.beta != 0.f ? o[q] + p.beta * (p.mask_acc ? dst[q] * mf[q] : dst[q]) : o[q];
-            }
-            if (p.yp) {
-                if (full) {
-                    store_planes4(p.yp, p.ypC, pix, col, o, ys);
-                } else {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        if (col + q < p.N) store_planes1(p.yp, p.ypC, pix, col + q, o[q], ys);
-                }
-            }
-            if (p.ymax) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    if (col + q < p.N) vmax = fmaxf(vmax, fabsf(o[q]));
-            }
+            epi_out4(p, e, rowmap(rbase + a * 16 + rl), col, v, phase, split, vmax);
         }
     }
     if (p.ymax) {
         if (vacc) *vacc = fmaxf(*vacc, vmax);
         else block_atomic_absmax(p.ymax, vmax);
     }
+}
+
+// The fp32 kernel's epilogue (k_conv_gemm: 32x32 accumulator tiles, MFMA C layout col = lane&31,
+// row = (r&3) + 8(r>>2) + 4(lane>>5)) staged through LDS the same way: a wave writes one 32x32
+// tile into `stage` (32 x 36 floats, its own region) and reads it back as 8 float4 per row, 8 rows
+// per pass of the wave (epi_out4).  Round 5 wrote each of the TM x TN x 16 accumulators with its own
+// runtime-branched store -- a fully unrolled epilogue of up to ~150 KB of code in a ~200 KB kernel.
+template <int MODE, int TM, int TN, class RowMap>
+__device__ __forceinline__ void conv_epilogue32(const GemmArgs &p, f32x16 (&acc)[TM][TN], int rbase, int cbase,
+                                                RowMap rowmap, int phase, int split, int lane, float *stage) {
+    constexpr int LD = 36;
+    const EpiCtx e = epi_ctx(p, 0.f);
+    const int l32 = lane & 31, h2 = lane >> 5, c4 = lane & 7;
+    float vmax = 0.f;
+#pragma clang loop unroll(full)
+    for (int a = 0; a < TM; ++a) {
+#pragma clang loop unroll(full)
+        for (int b = 0; b < TN; ++b) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) stage[((r & 3) + 8 * (r >> 2) + 4 * h2) * LD + l32] = acc[a][b][r];
+#pragma clang loop unroll(disable)
+            for (int pass = 0; pass < 4; ++pass) {
+                const int rl = pass * 8 + (lane >> 3);
+                const f32x4 v = *reinterpret_cast<const f32x4 *>(stage + rl * LD + c4 * 4);
+                epi_out4(p, e, rowmap(rbase + a * 32 + rl), cbase + b * 32 + c4 * 4, v, phase, split, vmax);
+            }
+        }
+    }
+    if (p.ymax) block_atomic_absmax(p.ymax, vmax);
 }
 
 // launcher of the bf16x6 kernels (conv_x6.hip); cfg indexes kX6Cfgs
