@@ -336,12 +336,28 @@ __device__ __forceinline__ void conv_epilogue16(const GemmArgs &p, f32x4 (&acc)[
     const int c4 = lane % C4;
     const int col = cbase + c4 * 4;
     float vmax = 0.f;   // max |output| of this lane (p.ymax)
-#pragma clang loop unroll(full)
-    for (int a = 0; a < TM; ++a) {
+    // accumulator row block a into the stage: compile-time indices into acc in each case of a
+    // switch, so the row-block loop itself need not unroll (one epi_out4 body per epilogue)
+    auto stage_rows = [&](auto A) __attribute__((always_inline)) {
 #pragma unroll
         for (int b = 0; b < TN; ++b)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) stage[(4 * (lane >> 4) + r) * LD + b * 16 + (lane & 15)] = acc[a][b][r];
+            for (int r = 0; r < 4; ++r)
+                stage[(4 * (lane >> 4) + r) * LD + b * 16 + (lane & 15)] = acc[decltype(A)::value][b][r];
+    };
+#ifdef DG_EPI_UNROLL_ROWS
+#pragma clang loop unroll(full)
+#else
+#pragma clang loop unroll(disable)
+#endif
+    for (int a = 0; a < TM; ++a) {
+        static_assert(TM <= 4, "row blocks");
+        switch (a) {
+        case 0: stage_rows(std::integral_constant<int, 0>{}); break;
+        case 1: if constexpr (TM > 1) stage_rows(std::integral_constant<int, (TM > 1 ? 1 : 0)>{}); break;
+        case 2: if constexpr (TM > 2) stage_rows(std::integral_constant<int, (TM > 2 ? 2 : 0)>{}); break;
+        default: if constexpr (TM > 3) stage_rows(std::integral_constant<int, (TM > 3 ? 3 : 0)>{}); break;
+        }
         // (the passes read the staged rows back from LDS, so they need no unrolling: one pass body
         // per accumulator row block keeps the epilogue's code -- inlined once or twice per kernel,
         // executed once per tile -- a quarter of the fully unrolled form's, which ran to ~100 KB of the

@@ -116,12 +116,29 @@ __device__ __forceinline__ void conv_epilogue16_pool(const GemmArgs &p, f32x4 (&
     unsigned hix[NP];
     float vmax = 0.f;   // max |pooled value| of this lane (p.ymax: the consumer's measured input)
     const float ys = p.yp ? (ys_pre > 0.f ? ys_pre : plane_scale(p)) : 0.f;
-#pragma unroll
-    for (int a = 0; a < TM; ++a) {
+    // (row blocks in pairs -- a window's two rows -- with the pair loop not unrolled: the staging
+    // takes compile-time acc indices in each case of a switch, as conv_epilogue16's, so one pair
+    // body is the pool epilogue's code instead of TM / 2)
+    auto stage_rows = [&](auto A) __attribute__((always_inline)) {
 #pragma unroll
         for (int b = 0; b < TN; ++b)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) stage[(4 * (lane >> 4) + r) * LD + b * 16 + (lane & 15)] = acc[a][b][r];
+            for (int r = 0; r < 4; ++r)
+                stage[(4 * (lane >> 4) + r) * LD + b * 16 + (lane & 15)] = acc[decltype(A)::value][b][r];
+    };
+    static_assert(TM == 2 || TM == 4, "row-block pairs");
+#pragma clang loop unroll(disable)
+    for (int a2 = 0; a2 < TM; a2 += 2)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int a = a2 + h;
+        if (h == 0) {
+            if (a2 == 0) stage_rows(std::integral_constant<int, 0>{});
+            else stage_rows(std::integral_constant<int, (TM > 2 ? 2 : 0)>{});
+        } else {
+            if (a2 == 0) stage_rows(std::integral_constant<int, 1>{});
+            else stage_rows(std::integral_constant<int, (TM > 2 ? 3 : 1)>{});
+        }
 #pragma unroll
         for (int pass = 0; pass < NP; ++pass) {
             const int rl = pass * RPP + rsub;
@@ -141,7 +158,7 @@ __device__ __forceinline__ void conv_epilogue16_pool(const GemmArgs &p, f32x4 (&
                 hvv[q] = t ? po[q] : o[q];
                 hi |= (t ? 1u : 0u) << (8 * q);
             }
-            if ((a & 1) == 0) {
+            if (h == 0) {
                 hv[pass] = hvv;
                 hix[pass] = hi;
                 continue;

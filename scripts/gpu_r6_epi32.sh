@@ -1,4 +1,4 @@
-# Round 6: the fp32 kernel's LDS-staged epilogue (k_conv_gemm: 196 -> 57 KB of code): the -m gpu suite,
+# Round 6: an epilogue change (the fp32 kernel LDS-staged epilogue; then the row-block loops not unrolled): the -m gpu suite,
 # then a same-box A/B against the previous commit's library (libdgan_head.so).
 set -o pipefail
 mkdir -p gpurun_out/r6
@@ -7,4 +7,4 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 600 --timeout
     -rf > gpurun_out/r6/epi32_tests.log 2>&1; rc=$?
 tail -n 3 gpurun_out/r6/epi32_tests.log
 [ $rc -ne 0 ] && exit $rc
-TAG=epi32 bash scripts/gpu_r6_ab.sh "new" "head|DG_LIB=@L/libdgan_head.so"
+TAG=${T:-epi32} bash scripts/gpu_r6_ab.sh "new" "head|DG_LIB=@L/libdgan_head.so"
