@@ -245,7 +245,10 @@ def main():
                     print("[bench] another rank's capture failed; eager launches on every rank", file=sys.stderr)
                     graph = None
         check = None
-        if graph is not None:
+        # (--profile-only: the check's snapshot copies and comparisons would land in the profiled
+        # window as non-step kernels -- at::native compares, rocclr copies -- so it runs only in
+        # the measured bench)
+        if graph is not None and not args.profile_only:
             check = graph_vs_eager(trainer, graph, x, y, strict=world == 1)
 
         def step():
