@@ -944,16 +944,13 @@ void launch_gemm_x3(int mode, int cfg, dim3 grid, const GemmArgs &a, hipStream_t
 #ifndef DG_X3_NB12
 #define DG_X3_NB12 2
 #endif
-#ifndef DG_X3_NB45
-#define DG_X3_NB45 2
-#endif
     switch (cfg) {
         DG_X3(0, 128, 128, 2, 2, 2, DG_X3_NB0)
         DG_X3(1, 128, 64, 2, 2, 2, DG_X3_NB12)
         DG_X3(2, 64, 128, 2, 2, 2, DG_X3_NB12)
         DG_X3(3, 64, 64, 2, 2, 3, 3)
-        DG_X3(4, 256, 128, 4, 2, 1, DG_X3_NB45)
-        DG_X3(5, 128, 256, 2, 4, 1, DG_X3_NB45)
+        DG_X3(4, 256, 128, 4, 2, 1, 2)
+        DG_X3(5, 128, 256, 2, 4, 1, 2)
         DG_X3(6, 128, 32, 4, 1, 3, 3)
     }
 #undef DG_X3
