@@ -234,9 +234,12 @@ k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, i
     const int c = blockIdx.x * FIN_C + cl;
     const bool cok = c < C;
     float mmc = 0.f, mvc = 0.f, zbn = 0.f;
+    float gpar = 1.f, bpar = 0.f;   // (gamma / beta with the partials' load round, not after the reductions)
     if (ln == 0 && cok) {
         if (mm) mmc = mm[c];
         if (mv) mvc = mv[c];
+        if (gamma) gpar = gamma[c];
+        if (beta) bpar = beta[c];
     }
     for (int sg = 0; sg < S; ++sg) {
         const long o = (long)sg * R * C;
@@ -283,10 +286,8 @@ k_bn_stats_final(const float *pn, const float *pmean, const float *pm2, int R, i
         const int sc = sg * C + c;
         if (save_mean) save_mean[sc] = mu;
         if (save_invstd) save_invstd[sc] = inv;
-        const float g = gamma ? gamma[c] : 1.f;
-        const float b = beta ? beta[c] : 0.f;
-        bn_scale_shift(g, inv, mu, b, scale[sc], shift[sc]);
-        zbn = fmaxf(zbn, (fabsf(g * inv) * dmax + fabsf(b)) * keep_scale);
+        bn_scale_shift(gpar, inv, mu, bpar, scale[sc], shift[sc]);
+        zbn = fmaxf(zbn, (fabsf(gpar * inv) * dmax + fabsf(bpar)) * keep_scale);
         mmc -= (mmc - mu) * (1.f - momentum);
         const float unb = n > 1.f ? m2 / (n - 1.f) : m2;
         mvc -= (mvc - unb) * (1.f - momentum);
@@ -516,6 +517,15 @@ k_bn_bwd_final(const float *p1, const float *p2, const float *pd, const float *p
     const int cl = threadIdx.x % FIN_C, ln = threadIdx.x / FIN_C;
     const int c = blockIdx.x * FIN_C + cl;
     float t1 = 0.f, t2 = 0.f, bnd = 0.f;
+    // the per-channel operands with the partials' load round (S <= 2 segments: the forward's
+    // statistics of both), not after the reductions
+    float g = 1.f, off = 0.f, inv0 = 0.f, mu0 = 0.f, inv1 = 0.f, mu1 = 0.f;
+    if (ln == 0 && c < C) {
+        if (gamma) g = gamma[c];
+        if (rz && offs) off = offs[c];
+        inv0 = invstd[c]; mu0 = mean[c];
+        if (S > 1) { inv1 = invstd[C + c]; mu1 = mean[C + c]; }
+    }
     for (int sg = 0; sg < S; ++sg) {
         const long o = (long)sg * R * C;
         float v1[FIN_K], v2[FIN_K], vd[FIN_K], vv[FIN_K];
@@ -544,15 +554,16 @@ k_bn_bwd_final(const float *p1, const float *p2, const float *pd, const float *p
         t2 += a2;
         // dy = k1 (dbn - m1 - xhat m2), xhat = (y - mean) invstd  ==>  dy = A dbn + B (y - mean) + D
         const int sc = sg * C + c;
-        const float g = gamma ? gamma[c] : 1.f;
-        const float k1 = g * invstd[sc];
+        const float inv = sg == 0 ? inv0 : (sg == 1 ? inv1 : invstd[sc]);
+        const float mu = sg == 0 ? mu0 : (sg == 1 ? mu1 : mean[sc]);
+        const float k1 = g * inv;
         const float m1 = a1 / (float)M, m2 = a2 / (float)M;
         float *cf = coef + (long)sg * 6 * C;
         cf[c] = k1;
-        cf[C + c] = -k1 * m2 * invstd[sc];
+        cf[C + c] = -k1 * m2 * inv;
         cf[2 * C + c] = -k1 * m1;
-        cf[3 * C + c] = mean[sc];
-        if (rz) bn_scale_shift(g, invstd[sc], mean[sc], offs ? offs[c] : 0.f, cf[4 * C + c], cf[5 * C + c]);
+        cf[3 * C + c] = mu;
+        if (rz) bn_scale_shift(g, inv, mu, off, cf[4 * C + c], cf[5 * C + c]);
         bnd = fmaxf(bnd, fabsf(k1) * md + fabsf(cf[C + c]) * mv + fabsf(cf[2 * C + c]));
     }
     if (ln == 0 && c < C) {

@@ -139,11 +139,39 @@ k_channel_concat(long npix, const float *a, int lda, int ca, const float *b, int
 
 __global__ void __launch_bounds__(256)
 k_strided_copy(long npix, int C, const float *src, int lds, float *dst, int ldd) {
+    if (C <= 4) {   // (a few channels: one pixel per lane, no per-element index division)
+        for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += (long)gridDim.x * blockDim.x)
+            for (int c = 0; c < C; ++c) dst[p * ldd + c] = src[p * lds + c];
+        return;
+    }
     const long total = npix * C;
     for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long)gridDim.x * blockDim.x) {
         long pix = e / C;
         int c = (int)(e - pix * C);
         dst[pix * ldd + c] = src[pix * lds + c];
+    }
+}
+
+// the pix2pix step's input staging in one pass over the pixels (trainer.Pix2PixTrainer.step):
+// cat = [x | y] (D(real)'s input, pix2pix.py:200), catx[:, 0:C] = x (D(fake)'s input, whose other
+// half G(x) fills), gx / gy = x / y (the 2N-image G batch of the identity pass, pix2pix.py:44,90)
+__global__ void __launch_bounds__(256)
+k_stage_pair(long npix, int C, const float *__restrict__ x, const float *__restrict__ y, float *__restrict__ cat,
+             int ldcat, float *__restrict__ catx, int ldcatx, float *__restrict__ gx, float *__restrict__ gy) {
+    for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += (long)gridDim.x * blockDim.x) {
+        float xv[4], yv[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            if (c < C) { xv[c] = x[p * C + c]; yv[c] = y[p * C + c]; }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (c >= C) break;
+            cat[p * ldcat + c] = xv[c];
+            cat[p * ldcat + C + c] = yv[c];
+            if (catx) catx[p * ldcatx + c] = xv[c];
+            if (gx) gx[p * C + c] = xv[c];
+            if (gy) gy[p * C + c] = yv[c];
+        }
     }
 }
 
@@ -277,12 +305,24 @@ int dg_channel_concat(int64_t npix, const float *a, int lda, int ca, const float
     return DG_OK;
 }
 
+int dg_stage_pair(int64_t npix, int C, const float *x, const float *y, float *cat, int ldcat, float *catx, int ldcatx,
+                  float *gx, float *gy, dg_stream_t stream) {
+    DG_ARG(x && y && cat, "NULL tensor");
+    DG_ARG(C >= 1 && C <= 4, "1 to 4 channels");
+    DG_ARG(ldcat >= 2 * C && (!catx || ldcatx >= C), "bad strides");
+    if (npix == 0) return DG_OK;
+    hipLaunchKernelGGL(dg::k_stage_pair, dim3(dg::grid_for(npix)), dim3(256), 0, (hipStream_t)stream, (long)npix, C, x,
+                       y, cat, ldcat, catx, ldcatx, gx, gy);
+    DG_LAUNCHED("stage_pair");
+    return DG_OK;
+}
+
 int dg_strided_copy(int64_t npix, int C, const float *src, int lds, float *dst, int ldd, dg_stream_t stream) {
     DG_ARG(src && dst, "NULL tensor");
     DG_ARG(lds >= C && ldd >= C, "bad strides");
     long total = (long)npix * C;
     if (total == 0) return DG_OK;
-    hipLaunchKernelGGL(dg::k_strided_copy, dim3(dg::grid_for(total)), dim3(256), 0, (hipStream_t)stream, (long)npix, C,
+    hipLaunchKernelGGL(dg::k_strided_copy, dim3(dg::grid_for(C <= 4 ? (long)npix : total)), dim3(256), 0, (hipStream_t)stream, (long)npix, C,
                        src, lds, dst, ldd);
     DG_LAUNCHED("strided_copy");
     return DG_OK;

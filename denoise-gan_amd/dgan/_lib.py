@@ -66,6 +66,7 @@ _SIGS = {
     "dg_fill": (c_int, [_P, c_int64, c_float, _P]),
     "dg_to_f16": (c_int, [c_int64, _P, _P, _P]),
     "dg_strided_copy": (c_int, [c_int64, c_int, _P, c_int, _P, c_int, _P]),
+    "dg_stage_pair": (c_int, [c_int64, c_int, _P, _P, _P, c_int, _P, c_int, _P, _P, _P]),
     "dg_adam_sched": (c_int, [_P, _P, _P, _P, c_int64, c_float, c_int64, c_float, c_int, c_float, c_float, c_float,
                               c_float, _P, _P]),
     "dg_prelu_workspace_size": (c_int, [c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_size_t)]),

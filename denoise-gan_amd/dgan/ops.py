@@ -787,6 +787,23 @@ def fill(t, value):
     return t
 
 
+def stage_pair(x, y, cat, catx=None, gx=None, gy=None):
+    """One launch: cat = [x | y] along channels, catx[..., :C] = x, gx = x, gy = y (dg_stage_pair;
+    x, y dense NHWC, gx / gy dense, catx / gx / gy optional)."""
+    C = x.shape[-1]
+    if y.shape != x.shape or not (x.is_contiguous() and y.is_contiguous()):
+        raise DGError("stage_pair: x and y are dense tensors of one shape")
+    pix_ld(x, C), pix_ld(y, C)
+    for t, c in ((cat, 2 * C), (catx, C)):
+        if t is not None and (_rows(t) != _rows(x) or t.shape[-1] < c):
+            raise DGError("stage_pair: cat / catx have x's pixels and at least 2C / C channels")
+    for t in (gx, gy):
+        if t is not None and (t.shape != x.shape or not t.is_contiguous()):
+            raise DGError("stage_pair: gx / gy are dense tensors of x's shape")
+    call("dg_stage_pair", _rows(x), C, _p(x), _p(y), _p(cat), pix_ld(cat, 2 * C), _p(catx),
+         pix_ld(catx, C) if catx is not None else 0, _p(gx), _p(gy), _stream())
+
+
 def strided_copy(src, dst):
     C = src.shape[-1]
     call("dg_strided_copy", _rows(src), C, _p(src), pix_ld(src, C), _p(dst), pix_ld(dst, C), _stream())

@@ -37,6 +37,9 @@ EARLY_ADAM = not os.environ.get("DG_NO_EARLY_ADAM")
 OVERLAP_VT = not os.environ.get("DG_NO_OVERLAP_VT")
 # D's parameter backward forked at the start of G's backward instead of after the losses
 DBWD_LATE = bool(os.environ.get("DG_DBWD_LATE"))
+# the step's input staging in one launch (dg_stage_pair) instead of a concat and three copies;
+# DG_STAGE_SPLIT=1: the four launches (same-box A/B)
+STAGE_SPLIT = bool(os.environ.get("DG_STAGE_SPLIT"))
 
 LOSS_NAMES = ("gen_total_loss", "gen_gan_loss", "gen_l1_loss", "gen_l2_loss", "content_loss", "disc_loss",
               "var_loss", "identity_loss")
@@ -197,13 +200,20 @@ class Pix2PixTrainer:
             else:
                 self.content.forward_target(y, ws=ws)
         # ---- forward (pix2pix.py:44-48 and the identity pass :90) -----------
-        ops.channel_concat(x, y, real_in)                 # concatenate([inp, tar]) (pix2pix.py:200)
-        ops.strided_copy(x, fake_in[..., :3])
-        if self.identity:
-            ops.strided_copy(x, self.gin[:N])
-            ops.strided_copy(y, self.gin[N:])
+        # concatenate([inp, tar]) (pix2pix.py:200), D(fake)'s x half, and the identity pass's
+        # [x; y] G batch (pix2pix.py:44,90): one staging launch
+        if STAGE_SPLIT:
+            ops.channel_concat(x, y, real_in)
+            ops.strided_copy(x, fake_in[..., :3])
+            if self.identity:
+                ops.strided_copy(x, self.gin[:N])
+                ops.strided_copy(y, self.gin[N:])
+            gin = self.gin if self.identity else x
+        elif self.identity:
+            ops.stage_pair(x, y, real_in, fake_in[..., :3], self.gin[:N], self.gin[N:])
             gin = self.gin
         else:
+            ops.stage_pair(x, y, real_in, fake_in[..., :3])
             gin = x
         G.forward(gin, self.gout, ws=ws, drop_rate=self.drop_rate, drop_seed=self.drop_seed, step_dev=step_dev)
         gen = self.gout[:N]

@@ -471,6 +471,13 @@ int dg_fill(float *p, int64_t n, float value, dg_stream_t stream);
  * (dg_conv_planes_t.w views into dst, passed ready) instead of one conversion per conv */
 int dg_to_f16(int64_t n, const float *src, void *dst, dg_stream_t stream);
 int dg_strided_copy(int64_t npix, int C, const float *src, int lds, float *dst, int ldd, dg_stream_t stream);
+/* dg_stage_pair: the pix2pix step's input staging in one launch -- cat[p, 0:C] = x[p],
+ * cat[p, C:2C] = y[p] (concatenate([inp, tar]), pix2pix.py:200); catx[p, 0:C] = x[p] (D(fake)'s
+ * input, its channels C..2C are G(x)); gx[p] = x[p], gy[p] = y[p] (dense: the G(x) / G(y) halves
+ * of the identity pass's 2N-image batch, pix2pix.py:44,90).  x, y dense [npix, C], C <= 4;
+ * catx, gx, gy may be NULL.  Replaces dg_channel_concat + three dg_strided_copy calls. */
+int dg_stage_pair(int64_t npix, int C, const float *x, const float *y, float *cat, int ldcat, float *catx,
+                  int ldcatx, float *gx, float *gy, dg_stream_t stream);
 
 /* ------------------------------------------------------------------------
  * Layers of the SRGAN / FastSRGAN / Autoencoder models and of the frozen

@@ -115,3 +115,28 @@ def test_main_checkpoint_resume_is_bit_identical(tmp_path):
             assert np.array_equal(v, nb.bn.export()[k]), k
     assert (tmp_path / "b" / "models" / "pix2pix.npz").exists()
     assert (tmp_path / "a" / "logs" / "train_1" / "events.jsonl").exists()
+
+
+@gpu
+@pytest.mark.parametrize("C", [1, 3, 4])
+def test_stage_pair_and_strided_copy_are_exact_copies(C):
+    """dg_stage_pair (the step's input staging: concatenate([inp, tar]) at pix2pix.py:200, D(fake)'s
+    x half, the identity pass's [x; y] batch) and dg_strided_copy's few-channel path move bits."""
+    from dgan import ops
+    g = torch.Generator().manual_seed(C)
+    x = torch.randn(3, 17, 19, C, generator=g).cuda()
+    y = torch.randn(3, 17, 19, C, generator=g).cuda()
+    cat = torch.full((3, 17, 19, 2 * C + 1), 7.0, device="cuda")
+    catx = torch.full((3, 17, 19, 2 * C), 7.0, device="cuda")
+    gin = torch.full((6, 17, 19, C), 7.0, device="cuda")
+    ops.stage_pair(x, y, cat[..., :2 * C], catx[..., :C], gin[:3], gin[3:])
+    ops.strided_copy(y, catx[..., C:])
+    torch.cuda.synchronize()
+    assert torch.equal(cat[..., :C], x) and torch.equal(cat[..., C:2 * C], y)
+    assert torch.equal(cat[..., 2 * C], torch.full_like(cat[..., 2 * C], 7.0))   # untouched column
+    assert torch.equal(catx, torch.cat([x, y], -1))
+    assert torch.equal(gin, torch.cat([x, y], 0))
+    cat2 = torch.zeros(3, 17, 19, 2 * C, device="cuda")
+    ops.stage_pair(x, y, cat2)   # optional outputs absent
+    torch.cuda.synchronize()
+    assert torch.equal(cat2, torch.cat([x, y], -1))
