@@ -151,10 +151,11 @@ def test_rccl_world1_graph_captured_step_bit_identical():
 @gpu
 def test_bench_dist_world1_uses_rccl():
     """`bench.py --dist` at world size 1: the process group + RCCL path with the
-    step graph-captured; one JSON line, dp1."""
+    step graph-captured; one JSON line, dp1.  (Not --profile-only: that mode skips the
+    graph-vs-eager check, whose snapshot kernels would land in a profile.)"""
     env = dict(os.environ, MASTER_PORT=str(_free_port()))
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--dist", "--steps", "3", "--warmup", "2",
-                        "--batch", "4", "--no-cpu-baseline", "--no-pmc-leg", "--no-core", "--profile-only"],
+                        "--batch", "4", "--no-cpu-baseline", "--no-pmc-leg", "--no-core", "--no-twin"],
                        cwd=REPO, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
